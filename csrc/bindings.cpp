@@ -1,0 +1,64 @@
+// pybind11 bindings of the gfx950 kernels.  Device pointers and HIP streams cross
+// the boundary as integers (tensor.data_ptr(), torch.cuda.Stream.cuda_stream), so the
+// extension does not depend on libtorch's C++ ABI and launches onto whatever stream
+// python (or a hipGraph capture) is using.
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels/launchers.h"
+
+
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+template <typename T>
+static T* P(u x) { return reinterpret_cast<T*>(x); }
+static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
+
+PYBIND11_MODULE(_dnn_hip, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
+  m.def("layout", []() {
+    py::dict d;
+    d["conv1.weight"] = dnn::OFF_C1W; d["conv1.bias"] = dnn::OFF_C1B;
+    d["conv2.weight"] = dnn::OFF_C2W; d["conv2.bias"] = dnn::OFF_C2B;
+    d["fc1.weight"] = dnn::OFF_F1W; d["fc1.bias"] = dnn::OFF_F1B;
+    d["fc2.weight"] = dnn::OFF_F2W; d["fc2.bias"] = dnn::OFF_F2B;
+    d["fc3.weight"] = dnn::OFF_F3W; d["fc3.bias"] = dnn::OFF_F3B;
+    d["arena"] = dnn::ARENA; d["slab"] = dnn::SLAB;
+    return d;
+  });
+  m.def("fused_train",
+        [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
+           u z1, u z2, u z3, u slab, u loss, u correct, u stream) {
+          dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order),
+                                  order_len, batch, P<int32_t>(state), P<const float>(master),
+                                  P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
+                                  P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
+                                  S(stream));
+        });
+  m.def("fused_eval", [](u images, u labels, u order, int n, int base, int count, u master, u shadow, u loss,
+                         u correct, u stream) {
+    dnn::launch_fused_eval(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), n, base,
+                           count, P<const float>(master), P<const bf16>(shadow), P<float>(loss), P<int32_t>(correct),
+                           S(stream));
+  });
+  m.def("grad_reduce", [](u a0, u h1, u h2, u z1, u z2, u z3, u slab, u loss, u correct, int batch, u master,
+                          u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
+                          int fuse_sgd, int lo, int hi, int bookkeeping, u stream) {
+    dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
+                      P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
+                      P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
+                      P<bf16>(shadow), P<int32_t>(state), P<double>(stats), lr, momentum, grad_scale, fuse_sgd,
+                      lo, hi, bookkeeping};
+    dnn::launch_grad_reduce(a, S(stream));
+  });
+  m.def("init", []() { dnn::init_kernels(); });
+  m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
+                        int pack_only, u stream) {
+    dnn::launch_sgd_apply(P<float>(master), P<const float>(grad), P<float>(mom), P<bf16>(shadow), n, lr, momentum,
+                          grad_scale, pack_only, S(stream));
+  });
+}

@@ -1,0 +1,69 @@
+// Shared definitions for the gfx950 (CDNA4) kernels of the LeNet/CIFAR-10 engine.
+//
+// Layout contract with python (distributed_neural_network_amd/models/network.py,
+// ArenaLayout): every parameter lives in one flat fp32 arena, each tensor on a
+// 64-element (256 B) boundary, in reference state_dict order
+// (reference models/model.py:13-18).  ops/native.py asserts these constants
+// against ArenaLayout at import time.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace dnn {
+
+// ---- arena offsets (fp32 elements) -------------------------------------------------
+constexpr int OFF_C1W = 0;      // [6][3][5][5]   450
+constexpr int OFF_C1B = 512;    // [6]
+constexpr int OFF_C2W = 576;    // [16][6][5][5] 2400
+constexpr int OFF_C2B = 3008;   // [16]
+constexpr int OFF_F1W = 3072;   // [120][400]   48000
+constexpr int OFF_F1B = 51072;  // [120]
+constexpr int OFF_F2W = 51200;  // [84][120]    10080
+constexpr int OFF_F2B = 61312;  // [84]
+constexpr int OFF_F3W = 61440;  // [10][84]       840
+constexpr int OFF_F3B = 62336;  // [10]
+constexpr int ARENA = 62400;    // padded length
+constexpr int NUM_PARAMS = 62006;
+
+// ---- per-sample conv weight-gradient slab (fp32) -----------------------------------
+// [dW1 450][db1 6][dW2 2400][db2 16]
+constexpr int SLAB_C1W = 0;
+constexpr int SLAB_C1B = 450;
+constexpr int SLAB_C2W = 456;
+constexpr int SLAB_C2B = 2856;
+constexpr int SLAB = 2872;
+
+// ---- per-sample activation rows written by the fused kernel --------------------------
+constexpr int A0_LD = 400;  // pooled conv2 output (fc1 input)
+constexpr int H1_LD = 120;  // relu(fc1)
+constexpr int H2_LD = 84;   // relu(fc2)
+constexpr int Z1_LD = 120;  // dL/d(fc1 pre-activation)
+constexpr int Z2_LD = 84;   // dL/d(fc2 pre-activation)
+constexpr int Z3_LD = 16;   // dL/dlogits (10 used)
+
+constexpr int IMG = 3 * 32 * 32;
+
+// ---- device step state (int32 words) -------------------------------------------------
+// [0] cursor: step index within the epoch (advanced by the reduce kernel)
+// [1] bvalid: valid samples of the current batch (written by the fused kernel)
+constexpr int ST_CURSOR = 0;
+constexpr int ST_BVALID = 1;
+// device stats (fp64): [0] sum of batch-mean losses, [1] batches, [2] correct, [3] samples
+constexpr int STAT_LOSS = 0, STAT_BATCHES = 1, STAT_CORRECT = 2, STAT_SAMPLES = 3;
+
+}  // namespace dnn
+
+#define HIP_CHECK(x)                                                                      \
+  do {                                                                                    \
+    hipError_t err__ = (x);                                                               \
+    if (err__ != hipSuccess) {                                                            \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(err__) +    \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));       \
+    }                                                                                     \
+  } while (0)

@@ -1,0 +1,139 @@
+"""fp32 PyTorch oracle of every quantity the HIP kernels produce.
+
+Used (1) by the numerics tests, which compare each kernel output against the same
+quantity computed here in fp32, and (2) by the CPU engine (``CpuEngine``), the
+explicit CPU-only execution path ("a pure-PyTorch CPU path
+used only as the test oracle and for config #1").
+
+All functions address parameters through views of the flat arena, so the oracle and
+the kernels share one parameter layout.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+import torch.nn.functional as F
+
+from ..models.network import LAYOUT
+
+SLAB = 2872
+
+
+def normalize_u8(x: torch.Tensor) -> torch.Tensor:
+    """ToTensor + Normalize((.5,.5,.5),(.5,.5,.5)) of data_parallelism_train.py:24-27."""
+    return (x.float() / 255.0 - 0.5) / 0.5
+
+
+def forward(arena: torch.Tensor, x: torch.Tensor, return_acts: bool = False):
+    p = LAYOUT.views(arena)
+    c1 = F.conv2d(x, p["conv1.weight"], p["conv1.bias"])
+    p1 = F.max_pool2d(F.relu(c1), 2, 2)
+    c2 = F.conv2d(p1, p["conv2.weight"], p["conv2.bias"])
+    p2 = F.max_pool2d(F.relu(c2), 2, 2)
+    a0 = p2.flatten(1)
+    h1 = F.relu(F.linear(a0, p["fc1.weight"], p["fc1.bias"]))
+    h2 = F.relu(F.linear(h1, p["fc2.weight"], p["fc2.bias"]))
+    logits = F.linear(h2, p["fc3.weight"], p["fc3.bias"])
+    if return_acts:
+        return logits, {"a0": a0, "h1": h1, "h2": h2}
+    return logits
+
+
+def per_sample_outputs(arena: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor,
+                       bvalid: int | None = None) -> Dict[str, torch.Tensor]:
+    """Exactly the rows the fused kernel writes for a batch (fp32, CPU).
+
+    ``z3`` includes the 1/bvalid of CrossEntropy(reduction='mean');  ``slab`` is the
+    per-sample conv weight/bias gradient [dW1 450 | db1 6 | dW2 2400 | db2 16].
+    """
+    arena = arena.detach().float().cpu()
+    x = normalize_u8(images_u8.cpu())
+    y = labels.cpu().long()
+    B = x.shape[0]
+    bvalid = B if bvalid is None else bvalid
+    logits, acts = forward(arena, x, return_acts=True)
+    loss = F.cross_entropy(logits, y, reduction="none")
+    correct = (logits.argmax(1) == y).int()
+    p = LAYOUT.views(arena)
+    z3 = (torch.softmax(logits, 1) - F.one_hot(y, 10).float()) / bvalid
+    z2 = (z3 @ p["fc3.weight"]) * (acts["h2"] > 0).float()
+    z1 = (z2 @ p["fc2.weight"]) * (acts["h1"] > 0).float()
+    slabs = torch.zeros(B, SLAB)
+    conv_keys = ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"]
+    for b in range(B):
+        a = arena.clone().requires_grad_(True)
+        out = forward(a, x[b:b + 1])
+        (F.cross_entropy(out, y[b:b + 1]) / bvalid).backward()
+        g = LAYOUT.views(a.grad)
+        slabs[b] = torch.cat([g[k].flatten() for k in conv_keys])
+    z3p = torch.zeros(B, 16)
+    z3p[:, :10] = z3
+    return {"a0": acts["a0"], "h1": acts["h1"], "h2": acts["h2"], "z1": z1, "z2": z2, "z3": z3p,
+            "slab": slabs, "loss": loss, "correct": correct, "logits": logits}
+
+
+def batch_grad(arena: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor) -> tuple[torch.Tensor, float]:
+    """Flat-arena gradient of mean CrossEntropy over the batch (zeros in padding)."""
+    a = arena.detach().float().cpu().clone().requires_grad_(True)
+    loss = F.cross_entropy(forward(a, normalize_u8(images_u8.cpu())), labels.cpu().long())
+    loss.backward()
+    return a.grad.detach(), float(loss)
+
+
+def sgd_momentum_(params: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor, lr: float, momentum: float) -> None:
+    """torch.optim.SGD(lr, momentum, dampening=0) on flat tensors; zero buffer == fresh optimizer."""
+    mom.mul_(momentum).add_(grad)
+    params.sub_(lr * mom)
+
+
+def _bf(t: torch.Tensor) -> torch.Tensor:
+    return t.bfloat16().float()
+
+
+def per_sample_outputs_bf16(shadow: torch.Tensor, master: torch.Tensor, images_u8: torch.Tensor,
+                            labels: torch.Tensor, bvalid: int | None = None) -> Dict[str, torch.Tensor]:
+    """The fused kernel's math with bf16 rounding at exactly the kernel's rounding points.
+
+    Weights come from the bf16 shadow, biases from the fp32 master; the image, the
+    pooled conv1 output (conv2 input), dY2 and dY1 are rounded to bf16 because they
+    are MFMA operands; everything else (accumulators, MLP, loss, bias grads) is fp32.
+    A correct kernel matches this to accumulation-order noise.
+    """
+    w = LAYOUT.views(shadow.detach().float().cpu())
+    bm = LAYOUT.views(master.detach().float().cpu())
+    x = _bf(normalize_u8(images_u8.cpu()))
+    y = labels.cpu().long()
+    B = x.shape[0]
+    bvalid = B if bvalid is None else bvalid
+    W1, W2 = w["conv1.weight"], w["conv2.weight"]
+    c1 = F.conv2d(x, W1, bm["conv1.bias"])
+    p1, i1 = F.max_pool2d_with_indices(F.relu(c1), 2, 2)
+    p1b = _bf(p1)
+    c2 = F.conv2d(p1b, W2, bm["conv2.bias"])
+    p2, i2 = F.max_pool2d_with_indices(F.relu(c2), 2, 2)
+    a0 = p2.flatten(1)
+    h1 = F.relu(F.linear(a0, w["fc1.weight"], bm["fc1.bias"]))
+    h2 = F.relu(F.linear(h1, w["fc2.weight"], bm["fc2.bias"]))
+    logits = F.linear(h2, w["fc3.weight"], bm["fc3.bias"])
+    loss = F.cross_entropy(logits, y, reduction="none")
+    correct = (logits.argmax(1) == y).int()
+    z3 = (torch.softmax(logits, 1) - F.one_hot(y, 10).float()) / bvalid
+    z2 = (z3 @ w["fc3.weight"]) * (h2 > 0).float()
+    z1 = (z2 @ w["fc2.weight"]) * (h1 > 0).float()
+    da0 = z1 @ w["fc1.weight"]
+    dp2 = da0.view(B, 16, 5, 5) * (p2 > 0).float()
+    dy2 = F.max_unpool2d(dp2, i2, 2, 2, output_size=c2.shape[-2:])
+    db2 = dy2.sum((2, 3))
+    dy2b = _bf(dy2)
+    dW2 = torch.stack([torch.nn.grad.conv2d_weight(p1b[b:b + 1], W2.shape, dy2b[b:b + 1]) for b in range(B)])
+    dp1 = torch.nn.grad.conv2d_input(p1.shape, W2, dy2b) * (p1 > 0).float()
+    dy1 = F.max_unpool2d(dp1, i1, 2, 2, output_size=c1.shape[-2:])
+    db1 = dy1.sum((2, 3))
+    dy1b = _bf(dy1)
+    dW1 = torch.stack([torch.nn.grad.conv2d_weight(x[b:b + 1], W1.shape, dy1b[b:b + 1]) for b in range(B)])
+    slab = torch.cat([dW1.flatten(1), db1, dW2.flatten(1), db2], 1)
+    z3p = torch.zeros(B, 16)
+    z3p[:, :10] = z3
+    return {"a0": a0, "h1": h1, "h2": h2, "z1": z1, "z2": z2, "z3": z3p, "slab": slab, "loss": loss,
+            "correct": correct, "logits": logits}

@@ -1,0 +1,348 @@
+"""Training engines: the MI355X HIP engine and the CPU oracle engine.
+
+Both expose one interface used by the trainer / sync policies:
+
+* ``attach(train_split)`` - make the training split resident on the device,
+* ``begin_epoch(order)``  - this rank's sample order for the epoch (cursor <- 0),
+* ``run_steps(n)``        - n optimizer steps (fwd + bwd + [grad sync] + SGD),
+* ``epoch_stats()``       - device-accumulated loss/accuracy of the epoch,
+* ``evaluate(split, bs)`` - per-sample test loss/correct (reference eval semantics),
+* ``master`` / ``mom``    - flat fp32 parameter / momentum arenas (state_dict views).
+
+Capability parity: ``run_child``'s hot loop (data_parallelism_train.py:185-213,
+model_replication_train.py:96-114, single_proc_train.py:61-74) and ``eval``
+(data_parallelism_train.py:157-183).
+
+HipEngine design (MI355X): a step is 2 kernels (fused per-sample fwd/bwd, batch
+reduce + SGD) or, with a per-step gradient all-reduce, 2 + 1 kernels around
+bucketed RCCL all-reduces.  Steps are captured into hipGraphs (through
+torch.cuda.CUDAGraph) in chunks of ``graph_chunk`` steps; the step cursor, the
+tail-batch size and the epoch loss/accuracy accumulators live on the device, so a
+chunk replays with zero host work per step and no host<->device sync until the
+epoch ends.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional, Protocol
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..data.datasets import Split
+from ..models.network import LAYOUT, arena_state_dict, init_arena, load_state_dict_into
+from ..ops import native, reference
+
+
+class GradSync(Protocol):
+    """Per-step gradient synchronisation (the step-allreduce policy implements it)."""
+
+    def allreduce_grads(self, grad: torch.Tensor, buckets: list[tuple[int, int]],
+                        before_last: Optional[Callable[[], None]] = None) -> None: ...
+
+
+@dataclass
+class StepStats:
+    loss_sum: float      # sum over batches of the batch-mean loss
+    batches: int
+    correct: int
+    samples: int
+
+    @property
+    def mean_loss(self) -> float:
+        return self.loss_sum / max(self.batches, 1)
+
+    @property
+    def accuracy(self) -> float:
+        return 100.0 * self.correct / max(self.samples, 1)
+
+
+def eval_metrics(loss: torch.Tensor, correct: torch.Tensor, batch_size: int) -> tuple[float, float]:
+    """Reference eval metrics from per-sample values.
+
+    val loss = mean over test batches of the batch-mean loss (np.mean(losses),
+    data_parallelism_train.py:176); accuracy = 100 * correct / total (:177).
+    """
+    loss = loss.double().cpu()
+    n = loss.numel()
+    nb = (n + batch_size - 1) // batch_size
+    sums = torch.zeros(nb, dtype=torch.float64).index_add_(0, torch.arange(n) // batch_size, loss)
+    counts = torch.full((nb,), float(batch_size), dtype=torch.float64)
+    counts[-1] = n - (nb - 1) * batch_size
+    return float((sums / counts).mean()), 100.0 * float(correct.sum()) / max(n, 1)
+
+
+class Engine:
+    device: torch.device
+    batch: int
+
+    def __init__(self, batch: int, lr: float, momentum: float, arena: torch.Tensor | None, seed: int | None) -> None:
+        self.batch = int(batch)
+        self.lr = float(lr)
+        self.momentum = float(momentum)
+        self._init_arena = arena if arena is not None else init_arena(seed)
+        self.grad_sync: GradSync | None = None
+        self.train: Split | None = None
+        self.order_len = 0
+
+    # -- parameters --------------------------------------------------------------------
+    def state_dict(self):
+        return arena_state_dict(self.master)
+
+    def load_state_dict(self, sd) -> None:
+        with torch.no_grad():
+            host = torch.zeros(LAYOUT.total)
+            load_state_dict_into(host, sd)
+            self.master.copy_(host.to(self.master.device))
+        self.params_changed()
+
+    def params_changed(self) -> None:
+        """Call after writing ``master`` from outside (all-reduce, load)."""
+
+    def reset_momentum(self) -> None:
+        self.mom.zero_()
+
+    def steps_per_epoch(self) -> int:
+        return (self.order_len + self.batch - 1) // self.batch
+
+    def synchronize(self) -> None:
+        pass
+
+
+class CpuEngine(Engine):
+    """fp32 PyTorch execution on the CPU (oracle / CPU-only hosts), same arena layout."""
+
+    def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
+                 seed: int | None = None) -> None:
+        super().__init__(batch, lr, momentum, arena, seed)
+        self.device = torch.device("cpu")
+        self.master = self._init_arena.clone().float()
+        self.grad = torch.zeros_like(self.master)
+        self.mom = torch.zeros_like(self.master)
+        self._stats = [0.0, 0, 0, 0]
+        self._order = np.zeros(0, dtype=np.int32)
+        self._cursor = 0
+
+    def attach(self, train: Split) -> None:
+        self.train = train.to("cpu")
+
+    def begin_epoch(self, order: np.ndarray) -> None:
+        self._order = np.asarray(order, dtype=np.int32)
+        self.order_len = int(self._order.shape[0])
+        self._cursor = 0
+
+    def run_steps(self, n: int) -> None:
+        assert self.train is not None
+        for _ in range(n):
+            lo = self._cursor * self.batch
+            idx = torch.from_numpy(self._order[lo:lo + self.batch].astype(np.int64))
+            self._cursor += 1
+            if idx.numel() == 0:
+                continue
+            x = self.train.images[idx]
+            y = self.train.labels[idx]
+            g, loss = reference.batch_grad(self.master, x, y)
+            with torch.no_grad():
+                logits = reference.forward(self.master, reference.normalize_u8(x))
+                correct = int((logits.argmax(1) == y.long()).sum())
+            self.grad.copy_(g)
+            if self.grad_sync is not None:
+                self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])
+            reference.sgd_momentum_(self.master, self.grad, self.mom, self.lr, self.momentum)
+            self._stats[0] += loss
+            self._stats[1] += 1
+            self._stats[2] += correct
+            self._stats[3] += int(idx.numel())
+
+    def epoch_stats(self, reset: bool = True) -> StepStats:
+        s = StepStats(float(self._stats[0]), int(self._stats[1]), int(self._stats[2]), int(self._stats[3]))
+        if reset:
+            self._stats = [0.0, 0, 0, 0]
+        return s
+
+    def evaluate_samples(self, split: Split, lo: int = 0, hi: int | None = None, chunk: int = 1000):
+        hi = len(split) if hi is None else hi
+        losses, corrects = [], []
+        with torch.no_grad():
+            for s in range(lo, hi, chunk):
+                e = min(hi, s + chunk)
+                x = reference.normalize_u8(split.images[s:e])
+                y = split.labels[s:e].long()
+                logits = reference.forward(self.master, x)
+                losses.append(F.cross_entropy(logits, y, reduction="none"))
+                corrects.append((logits.argmax(1) == y).int())
+        if not losses:
+            return torch.zeros(0), torch.zeros(0, dtype=torch.int32)
+        return torch.cat(losses), torch.cat(corrects)
+
+
+class HipEngine(Engine):
+    """MI355X engine: hand-written gfx950 kernels + hipGraph-captured step chunks."""
+
+    def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
+                 seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
+                 use_graphs: bool = True, overlap: bool = True) -> None:
+        super().__init__(batch, lr, momentum, arena, seed)
+        if not torch.cuda.is_available():
+            raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.ext = native.hip()
+        self.ext.init()
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        dev = self.device
+        B = self.batch
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.master = self._init_arena.to(**f32).contiguous()
+        self.grad = torch.zeros(LAYOUT.total, **f32)
+        self.mom = torch.zeros(LAYOUT.total, **f32)
+        self.shadow = torch.zeros(LAYOUT.total, device=dev, dtype=torch.bfloat16)
+        self.state = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.stats = torch.zeros(4, device=dev, dtype=torch.float64)
+        self.a0 = torch.zeros(B, 400, **f32)
+        self.h1 = torch.zeros(B, 120, **f32)
+        self.h2 = torch.zeros(B, 84, **f32)
+        self.z1 = torch.zeros(B, 120, **f32)
+        self.z2 = torch.zeros(B, 84, **f32)
+        self.z3 = torch.zeros(B, 16, **f32)
+        self.slab = torch.zeros(B, native.SLAB, **f32)
+        self.loss = torch.zeros(B, **f32)
+        self.correct = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.order = torch.zeros(0, device=dev, dtype=torch.int32)
+        self.graph_chunk = max(1, int(graph_chunk))
+        self.use_graphs = use_graphs
+        self.overlap = overlap
+        self.stream = torch.cuda.Stream(dev)
+        self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.params_changed()
+        torch.cuda.synchronize(dev)
+
+    # -- helpers ------------------------------------------------------------------------
+    @staticmethod
+    def _p(t: torch.Tensor) -> int:
+        return t.data_ptr()
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def synchronize(self) -> None:
+        torch.cuda.synchronize(self.device)
+
+    def params_changed(self) -> None:
+        with torch.cuda.device(self.device):
+            self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
+                               LAYOUT.total, 0.0, 0.0, 1.0, 1, self._stream())
+
+    def invalidate_graphs(self) -> None:
+        self._graphs.clear()
+
+    # -- data ---------------------------------------------------------------------------
+    def attach(self, train: Split) -> None:
+        self.train = train.to(self.device)
+        self.invalidate_graphs()
+
+    def begin_epoch(self, order: np.ndarray) -> None:
+        order = np.ascontiguousarray(order, dtype=np.int32)
+        n = int(order.shape[0])
+        if self.order.numel() < n:
+            self.order = torch.zeros(n, device=self.device, dtype=torch.int32)
+            self.invalidate_graphs()
+        if n != self.order_len:
+            self.invalidate_graphs()  # order_len is a baked kernel argument
+        self.order_len = n
+        if n:
+            self.order[:n].copy_(torch.from_numpy(order), non_blocking=False)
+        self.state[0] = 0
+
+    # -- one step (launch sequence; also what graphs capture) ---------------------------
+    def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int) -> None:
+        self.ext.grad_reduce(self._p(self.a0), self._p(self.h1), self._p(self.h2), self._p(self.z1),
+                             self._p(self.z2), self._p(self.z3), self._p(self.slab), self._p(self.loss),
+                             self._p(self.correct), self.batch, self._p(self.master), self._p(self.grad),
+                             self._p(self.mom), self._p(self.shadow), self._p(self.state), self._p(self.stats),
+                             self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, s)
+
+    def _launch_step(self) -> None:
+        assert self.train is not None
+        s = self._stream()
+        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.order),
+                             self.order_len, self.batch, self._p(self.state), self._p(self.master),
+                             self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
+                             self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
+                             self._p(self.loss), self._p(self.correct), s)
+        if self.grad_sync is None:
+            self._reduce(1, 0, LAYOUT.total, 1, s)
+            return
+        mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
+        if self.overlap:
+            # MLP bucket (95% of the bytes) is reduced first; its all-reduce runs on the
+            # comm stream while the conv bucket is being reduced on the compute stream.
+            self._reduce(0, mlp[0], mlp[1], 1, s)
+            self.grad_sync.allreduce_grads(self.grad, [mlp, conv],
+                                           before_last=lambda: self._reduce(0, conv[0], conv[1], 0, self._stream()))
+        else:
+            self._reduce(0, 0, LAYOUT.total, 1, s)
+            self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])
+        self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
+                           LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
+
+    def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
+        key = (nsteps, self.grad_sync is not None, self.overlap, self.order_len)
+        g = self._graphs.get(key)
+        if g is None:
+            # Capture advances nothing: kernels are recorded, not run.
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                for _ in range(nsteps):
+                    self._launch_step()
+            torch.cuda.synchronize(self.device)
+            self._graphs[key] = g
+        return g
+
+    def run_steps(self, n: int) -> None:
+        if n <= 0:
+            return
+        if not self.use_graphs:
+            with torch.cuda.device(self.device):
+                for _ in range(n):
+                    self._launch_step()
+            return
+        full, rem = divmod(n, self.graph_chunk)
+        if full:
+            g = self._graph(self.graph_chunk)
+            for _ in range(full):
+                g.replay()
+        if rem:
+            g = self._graph(1)
+            for _ in range(rem):
+                g.replay()
+
+    def epoch_stats(self, reset: bool = True) -> StepStats:
+        v = self.stats.cpu().tolist()
+        if reset:
+            self.stats.zero_()
+        return StepStats(v[0], int(round(v[1])), int(round(v[2])), int(round(v[3])))
+
+    # -- evaluation -----------------------------------------------------------------------
+    def evaluate_samples(self, split: Split, lo: int = 0, hi: int | None = None):
+        """Per-sample test loss/correct for samples [lo, hi) of ``split`` (one launch)."""
+        split = split.to(self.device)
+        hi = len(split) if hi is None else hi
+        n = max(0, hi - lo)
+        loss = torch.zeros(n, device=self.device, dtype=torch.float32)
+        corr = torch.zeros(n, device=self.device, dtype=torch.int32)
+        if n:
+            with torch.cuda.device(self.device):
+                self.ext.fused_eval(self._p(split.images), self._p(split.labels), 0, hi, lo, n,
+                                    self._p(self.master), self._p(self.shadow), self._p(loss), self._p(corr),
+                                    self._stream())
+        return loss, corr
+
+
+def make_engine(device: str, batch: int, lr: float, momentum: float, arena: torch.Tensor | None = None,
+                seed: int | None = None, **kw) -> Engine:
+    if device == "cpu":
+        return CpuEngine(batch, lr, momentum, arena, seed)
+    return HipEngine(batch, lr, momentum, arena, seed, device=device, **kw)

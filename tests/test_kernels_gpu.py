@@ -1,0 +1,93 @@
+"""Numerics of the gfx950 kernels against the fp32 PyTorch oracle (ops/reference.py).
+
+bf16 MFMA operands with fp32 accumulation: tolerances are relative to the
+magnitude of each tensor (asymmetric random data, odd batch sizes, tail batch).
+"""
+import numpy as np
+import pytest
+import torch
+
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.models.network import LAYOUT, init_arena
+from distributed_neural_network_amd.ops import reference
+from distributed_neural_network_amd.runtime.engine import CpuEngine, HipEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize("B,n", [(4, 4), (16, 13), (64, 64)])
+def test_fused_rows_match_oracle(B, n):
+    split = synthetic(97, seed=3)
+    eng = HipEngine(batch=B, seed=1, use_graphs=False)
+    eng.attach(split)
+    order = np.arange(5, 5 + n, dtype=np.int32)
+    eng.begin_epoch(order)
+    s = eng._stream()
+    ext = eng.ext
+    with torch.cuda.device(eng.device):
+        ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.order), eng.order_len,
+                        eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
+                        eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
+                        eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), s)
+    torch.cuda.synchronize()
+    bvalid = min(B, n)
+    assert int(eng.state[1]) == bvalid
+    idx = torch.from_numpy(order[:bvalid].astype(np.int64))
+    # oracle on the bf16-rounded weights the kernel sees
+    ref = reference.per_sample_outputs(eng.shadow.float().cpu(), split.images[idx], split.labels[idx], bvalid)
+    got = {k: getattr(eng, k)[:bvalid].float().cpu() for k in ["a0", "h1", "h2", "z1", "z2", "z3", "slab", "loss"]}
+    errs = {k: _rel(got[k], ref[k]) for k in got}
+    for lo, hi, name in [(0, 450, "dW1"), (450, 456, "db1"), (456, 2856, "dW2"), (2856, 2872, "db2")]:
+        errs[name] = _rel(got["slab"][:, lo:hi], ref["slab"][:, lo:hi])
+    # (1) bit-level structure: the bf16-emulating oracle rounds where the kernel rounds
+    emu = reference.per_sample_outputs_bf16(eng.shadow, eng.master, split.images[idx], split.labels[idx], bvalid)
+    eerrs = {k: _rel(got[k], emu[k]) for k in got}
+    for lo, hi, name in [(0, 450, "dW1"), (450, 456, "db1"), (456, 2856, "dW2"), (2856, 2872, "db2")]:
+        eerrs[name] = _rel(got["slab"][:, lo:hi], emu["slab"][:, lo:hi])
+    print("vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
+    print("vs bf16-emulating oracle:", {k: f"{v:.2e}" for k, v in eerrs.items()})
+    for k, v in eerrs.items():
+        assert v < 1e-3, f"{k}: rel err vs bf16 emulation {v:.3e}"
+    # (2) end-to-end precision vs the pure fp32 oracle
+    #     (bf16 operands: ReLU-mask / argmax flips make small batches noisy)
+    for k, tol in [("a0", 1e-2), ("h1", 1e-2), ("h2", 1e-2), ("loss", 1e-2), ("z3", 1e-2), ("z2", 0.15),
+                   ("z1", 0.15), ("dW2", 0.15), ("dW1", 0.2)]:
+        assert errs[k] < tol, f"{k}: rel err {errs[k]:.3e}"
+    if B > n:  # tail rows must be zero
+        assert float(eng.a0[bvalid:].abs().sum()) == 0.0
+        assert float(eng.slab[bvalid:].abs().sum()) == 0.0
+
+
+def test_train_steps_track_cpu_oracle():
+    split = synthetic(640, seed=5)
+    arena = init_arena(seed=7)
+    B = 64
+    hip = HipEngine(batch=B, arena=arena, use_graphs=True, graph_chunk=4)
+    cpu = CpuEngine(batch=B, arena=arena)
+    for e in (hip, cpu):
+        e.attach(split)
+        e.begin_epoch(np.arange(640, dtype=np.int32))
+    hip.run_steps(10)
+    cpu.run_steps(10)
+    hs, cs = hip.epoch_stats(), cpu.epoch_stats()
+    assert hs.batches == cs.batches == 10 and hs.samples == cs.samples == 640
+    assert abs(hs.mean_loss - cs.mean_loss) < 2e-2 * abs(cs.mean_loss)
+    r = _rel(hip.master.cpu() - arena, cpu.master - arena)
+    assert r < 8e-2, f"parameter update rel err {r:.3e}"
+
+
+def test_eval_matches_oracle():
+    split = synthetic(1000, seed=9, train=False)
+    eng = HipEngine(batch=64, seed=2)
+    loss, corr = eng.evaluate_samples(split, 0, 1000)
+    logits = reference.forward(eng.shadow.float().cpu(), reference.normalize_u8(split.images))
+    ref_loss = torch.nn.functional.cross_entropy(logits, split.labels.long(), reduction="none")
+    assert _rel(loss, ref_loss) < 2e-2
+    agree = (corr.cpu() == (logits.argmax(1) == split.labels.long()).int()).float().mean()
+    assert agree > 0.98
