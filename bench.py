@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training images/sec + epoch time (BASELINE.json).
+
+Config: reference CIFAR-10 CNN (models/model.py Network, 62,006 params), batch 64
+per GPU (weak scaling), synthetic CIFAR-shaped data (50,000 train / 10,000 test,
+3x32x32 uint8 -> normalised in-kernel), random-init weights, bf16 MFMA operands
+with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sync step-allreduce|epoch-avg]
+
+For N > 1 run under torchrun (one rank per GPU, RCCL over xGMI).  W untimed warmup
+steps, then EXACTLY K timed optimizer steps bracketed by barrier + device sync;
+epoch boundaries inside the window re-shuffle and continue (no step is skipped).
+The max over ranks is reported.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
+from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
+from distributed_neural_network_amd.runtime import HipEngine, eval_metrics  # noqa: E402
+
+BASELINE_IMG_S = 1261.0  # BASELINE.md headline: bs64, "4 procs", training-phase whole-node img/s
+METRIC = "images/sec (whole node) + epoch time, CIFAR-10 CNN bs=64 at 1/2/4/8 MI355X"
+
+
+class EpochCursor:
+    """Feeds K steps to the engine, starting a new shuffled epoch whenever one ends."""
+
+    def __init__(self, engine, sampler, policy, batch):
+        self.engine, self.sampler, self.policy, self.batch = engine, sampler, policy, batch
+        self.epoch = -1
+        self.left = 0
+        self.steps_per_epoch = sampler.steps(batch)
+
+    def _next_epoch(self):
+        if self.epoch >= 0:
+            self.policy.epoch_end(self.engine, self.epoch)
+        self.epoch += 1
+        self.policy.epoch_start(self.engine, self.epoch)
+        self.engine.begin_epoch(self.sampler.order(self.epoch))
+        self.left = self.steps_per_epoch
+
+    def run(self, k):
+        while k > 0:
+            if self.left == 0:
+                self._next_epoch()
+            n = min(k, self.left)
+            self.engine.run_steps(n)
+            self.left -= n
+            k -= n
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5000)
+    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--batch-size", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--sync", default="step-allreduce", choices=["step-allreduce", "epoch-avg"])
+    ap.add_argument("--graph-chunk", type=int, default=64)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    env = detect()
+    if env.world != args.gpus:
+        if env.world == 1 and args.gpus > 1:
+            sys.exit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks (found WORLD_SIZE=1)")
+    torch.cuda.set_device(env.local_rank)
+    device = torch.device("cuda", env.local_rank)
+    comm = Communicator(env, device)
+    B = args.batch_size
+
+    train, test = synthetic(50_000, args.seed, True), synthetic(10_000, args.seed, False)
+    sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
+    engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
+                       overlap=not args.no_overlap)
+    engine.attach(train)
+    test_dev = test.to(device)
+    policy = make_policy(args.sync, comm)
+    policy.attach(engine)
+    policy.initial_broadcast(engine)
+    cur = EpochCursor(engine, sampler, policy, B)
+
+    # warmup: captures every chunk graph, runs W real steps
+    cur._next_epoch()
+    engine.prepare_graphs()
+    cur.run(args.warmup)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+
+    t0 = time.perf_counter()
+    cur.run(args.steps)
+    torch.cuda.synchronize(device)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    dt = comm.reduce_scalar(dt, "max")
+    ms_per_step = 1000.0 * dt / args.steps
+    value = comm.world * B * args.steps / dt
+
+    # one complete epoch from its first step: train + averaging/sync + full test-set eval
+    epoch = {}
+    if not args.no_epoch:
+        cur.left = 0
+        cur._next_epoch()
+        engine.epoch_stats(reset=True)
+        comm.barrier()
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        engine.run_steps(cur.steps_per_epoch)
+        cur.left = 0
+        policy.epoch_end(engine, cur.epoch)
+        stats = engine.epoch_stats(reset=True)
+        torch.cuda.synchronize(device)
+        t2 = time.perf_counter()
+        lo = comm.rank * len(test) // comm.world
+        hi = (comm.rank + 1) * len(test) // comm.world
+        loss, corr = engine.evaluate_samples(test_dev, lo, hi)
+        full_l = torch.zeros(len(test), device=device)
+        full_c = torch.zeros(len(test), device=device, dtype=torch.float32)
+        full_l[lo:hi] = loss
+        full_c[lo:hi] = corr.float()
+        comm.allreduce_(full_l, "sum")
+        comm.allreduce_(full_c, "sum")
+        val_loss, val_acc = eval_metrics(full_l, full_c, B)
+        torch.cuda.synchronize(device)
+        t3 = time.perf_counter()
+        epoch_s = comm.reduce_scalar(t3 - t1, "max")
+        epoch = {"epoch_s": round(epoch_s, 6), "epoch_train_s": round(comm.reduce_scalar(t2 - t1, "max"), 6),
+                 "eval_s": round(comm.reduce_scalar(t3 - t2, "max"), 6),
+                 "epoch_images": int(len(sampler) * comm.world),
+                 "train_loss": round(stats.mean_loss, 5), "val_loss": round(val_loss, 5),
+                 "val_acc": round(val_acc, 3)}
+
+    if comm.rank == 0:
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": comm.world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 6),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
+               "dtype": "bf16", "data": "synthetic (CIFAR-10-shaped 3x32x32 uint8, 50k train / 10k test), "
+                                        "random-init weights",
+               "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)",
+                          "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
+                          "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
+                          "optimizer": "SGD lr=0.001 momentum=0.9, every step"},
+               **epoch}
+        print(json.dumps(out), flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

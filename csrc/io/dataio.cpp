@@ -88,7 +88,7 @@ py::tuple read_cifar_bin(const std::vector<std::string>& paths) {
 
 // Learnable CIFAR-shaped data: each class has a fixed colour/gradient template and
 // every image is template + uniform noise, so the CNN's loss actually falls.
-py::tuple synthetic(int64_t n, uint64_t seed, int noise) {
+py::tuple synthetic(int64_t n, uint64_t seed, int noise, uint64_t split) {
   if (n < 0) throw std::runtime_error("n must be >= 0");
   py::array_t<uint8_t> images({(py::ssize_t)n, (py::ssize_t)3, (py::ssize_t)32, (py::ssize_t)32});
   py::array_t<int32_t> labels((py::ssize_t)n);
@@ -98,7 +98,7 @@ py::tuple synthetic(int64_t n, uint64_t seed, int noise) {
   std::vector<float> tmpl(10 * kImg);
   SplitMix64 tr(mix_key(seed, 0xC1A55, 7));
   for (int k = 0; k < 10; ++k) {
-    const float base[3] = {(float)(tr.below(160) + 48), (float)(tr.below(160) + 48), (float)(tr.below(160) + 48)};
+    const float base[3] = {(float)(tr.below(96) + 80), (float)(tr.below(96) + 80), (float)(tr.below(96) + 80)};
     const float gy = ((float)tr.below(81) - 40.f) / 31.f, gx = ((float)tr.below(81) - 40.f) / 31.f;
     for (int c = 0; c < 3; ++c)
       for (int y = 0; y < 32; ++y)
@@ -107,7 +107,7 @@ py::tuple synthetic(int64_t n, uint64_t seed, int noise) {
   }
   {
   py::gil_scoped_release nogil;
-  SplitMix64 r(mix_key(seed, 0xDA7A, 11));
+  SplitMix64 r(mix_key(seed, 0xDA7A + split, 11));  // per-split sample stream, shared templates
   const int span = 2 * noise + 1;
   for (int64_t i = 0; i < n; ++i) {
     const int k = (int)r.below(10);
@@ -148,6 +148,6 @@ py::array_t<int32_t> shuffled(py::array_t<int32_t, py::array::c_style | py::arra
 PYBIND11_MODULE(_dnn_io, m) {
   m.doc() = "native data runtime: CIFAR-10 binary reader, synthetic data, seeded permutations";
   m.def("read_cifar_bin", &read_cifar_bin, py::arg("paths"));
-  m.def("synthetic", &synthetic, py::arg("n"), py::arg("seed"), py::arg("noise") = 48);
+  m.def("synthetic", &synthetic, py::arg("n"), py::arg("seed"), py::arg("noise") = 96, py::arg("split") = 0);
   m.def("shuffled", &shuffled, py::arg("indices"), py::arg("seed"), py::arg("epoch"), py::arg("stream") = 0);
 }

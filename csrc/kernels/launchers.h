@@ -7,7 +7,7 @@ namespace dnn {
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
-                        int32_t* correct, hipStream_t stream);
+                        int32_t* correct, long long* stamps, hipStream_t stream);
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);

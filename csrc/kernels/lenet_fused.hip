@@ -50,8 +50,9 @@ constexpr int L_DZ1 = L_DZ2 + 384;          // f32 [128]
 constexpr int L_DA0 = L_DZ1 + 512;          // f32 [400]
 constexpr int L_W1S = L_DA0 + 1600;         // bf16 [6][75] (+pad)
 constexpr int L_W2S = L_W1S + 912;          // bf16 [16][150]
-constexpr int L_MISC = L_W2S + 4800;        // scalars
-constexpr int LDS_TOTAL = L_MISC + 64;      // 160,000 B
+constexpr int L_IMG = L_W2S + 4800;         // u8 [3][32][32] raw image (re-used by phase F)
+constexpr int L_MISC = L_IMG + 3072;        // scalars
+constexpr int LDS_TOTAL = L_MISC + 64;      // 163,072 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 
 // REGA sub-layout during the conv backward
@@ -68,6 +69,32 @@ __device__ __forceinline__ float u8norm(uint32_t u) {
   return ((float)u / 255.0f - 0.5f) / 0.5f;
 }
 
+// Barrier for LDS hand-offs only: waits for this wave's LDS ops, not for vmcnt, so an
+// in-flight LDS-DMA (global_load_lds) keeps streaming across it.  __syncthreads()
+// would emit s_waitcnt vmcnt(0) and drain the DMA.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from per-lane global addresses into
+// LDS [lds_base, lds_base + 1 KB).  Inline asm on purpose: hipcc's waitcnt pass does
+// not see it, so it neither drains it at unrelated ds_reads (it cannot disprove LDS
+// aliasing inside the single dynamic LDS array) nor at later plain-load uses.  The
+// caller owns completion: s_waitcnt vmcnt(0) + a barrier before reading the bytes,
+// and every plain global load issued before a DMA is consumed before the DMA.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
+
 __device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -77,8 +104,8 @@ __device__ __forceinline__ short bf16_bits(float f) {
   return __builtin_bit_cast(short, h);
 }
 
-// Build the 29 window records of one input row (c, y) straight from the u8 image.
-__device__ __forceinline__ void build_r1_row(const uint8_t* __restrict__ img, bf16x8* R1, int row) {
+// Build the 29 window records of one input row (c, y) from the u8 image staged in LDS.
+__device__ __forceinline__ void build_r1_row(const uint8_t* img, bf16x8* R1, int row) {
   const uint4* src = reinterpret_cast<const uint4*>(img + row * 32);
   uint4 lo = src[0], hi = src[1];
   uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -97,7 +124,7 @@ __device__ __forceinline__ void build_r1_row(const uint8_t* __restrict__ img, bf
 }
 
 template <bool TRAIN>
-__global__ void __launch_bounds__(NT) lenet_fused_kernel(
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
     const int32_t* __restrict__ order,    // [order_len] sample ids (nullptr: identity)
@@ -107,8 +134,13 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
     const bf16* __restrict__ shadow,      // bf16 arena (weights)
     float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
-    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out) {
+    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
+    long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // diagnostic phase timeline (block 0, thread 0): s_memrealtime ticks (100 MHz)
+  const bool stamp = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+#define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+  STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -159,21 +191,39 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
   bf16* W2S = reinterpret_cast<bf16*>(smem + L_W2S);
 
   // ============ phase A: ingest + weight staging ======================================
-  if (tid < 96) build_r1_row(img, R1, tid);
+  // Loads are issued before any is consumed, in order of use: image + conv weights and
+  // biases (needed now), then fc1 (96 KB) by LDS-DMA straight into its LDS region; the
+  // DMA stays in flight through both convolutions (phases B-C synchronise with
+  // LDS-only barriers, which do not drain vmcnt) and is waited for before phase D.
+  uint8_t* IMGS = smem + L_IMG;
+  const uint4 im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
+  const uint4 w1v = reinterpret_cast<const uint4*>(shadow + OFF_C1W)[min(tid, 56)];  // 450 bf16 + zero pad
+  const uint4 w2v = reinterpret_cast<const uint4*>(shadow + OFF_C2W)[max(tid - 212, 0)];
+  const float bias_c1 = master[OFF_C1B + min(lane & 15, 5)];
+  const float bias_c2 = master[OFF_C2B + (lane & 15)];
+  for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = 0.f;
+  if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  if (tid < 57) reinterpret_cast<uint4*>(smem + L_W1S)[tid] = w1v;
+  if (tid >= 212) reinterpret_cast<uint4*>(smem + L_W2S)[tid - 212] = w2v;
+  // (hipcc waits vmcnt(0) for a plain load consumed while an LDS-DMA is in flight, so the
+  //  loads above are consumed first and the DMA is issued after them)
+  float bc1 = bias_c1, bc2 = bias_c2;
+  asm volatile("" : "+v"(bc1), "+v"(bc2));  // consume (wait for) the bias loads before the DMA
   {
-    // fc1 weights (bf16, 96,000 B) -> LDS; conv weights -> LDS.
-    const uint4* src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
-    uint4* dst = reinterpret_cast<uint4*>(smem + L_REGA);
-    for (int i = tid; i < 6000; i += NT) dst[i] = src[i];
-    const uint4* s1 = reinterpret_cast<const uint4*>(shadow + OFF_C1W);
-    uint4* d1 = reinterpret_cast<uint4*>(smem + L_W1S);
-    if (tid < 57) d1[tid] = s1[tid];  // 450 bf16 (+ zero pad of the arena)
-    const uint4* s2 = reinterpret_cast<const uint4*>(shadow + OFF_C2W);
-    uint4* d2 = reinterpret_cast<uint4*>(smem + L_W2S);
-    if (tid < 300) d2[tid] = s2[tid];
-    for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = 0.f;
+    // 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all in-arena).
+    // 12 per wave with the index clamped: a duplicate copies identical bytes.
+    const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const int i = min(wave + 8 * k, 93);
+      dma16(f1src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
+    }
   }
-  __syncthreads();
+  lds_barrier();
+  if (tid < 96) build_r1_row(IMGS, R1, tid);
+  lds_barrier();
+  STAMP(1);
 
   const int fr = lane & 15;   // MFMA fragment row/col within the 16-tile
   const int fg = lane >> 4;   // MFMA k-group (0..3)
@@ -188,7 +238,7 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
       for (int j = 0; j < 8; ++j)
         bw[s][j] = (fr < 6 && pr < 15 && j < 5) ? W1S[fr * 75 + pr * 5 + j] : (bf16)0.f;
     }
-    const float bias = fr < 6 ? master[OFF_C1B + fr] : 0.f;
+    const float bias = fr < 6 ? bc1 : 0.f;
     const int wi = fr >> 2, pi = fr & 3;  // A-operand row -> (window, pixel)
     for (int t = wave; t < 49; t += 8) {
       const int q = 4 * t + wi;
@@ -221,9 +271,29 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
 
+  STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============
+  // MLP operands each lane needs in phase D, loaded now so conv2 hides their latency.
+  const int mo = tid >> 2, mp = tid & 3;   // MLP lane roles: output (or input) index, quarter
+  bf16x8 w2f[4];                           // fc2 forward: row mo, chunks mp + 4k
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w2f[k] = reinterpret_cast<const bf16x8*>(shadow + OFF_F2W + min(mo, 83) * 120)[min(mp + 4 * k, 14)];
+  bf16x4 w3f[6];                           // fc3 forward: row mo, chunks mp + 4k
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    w3f[k] = reinterpret_cast<const bf16x4*>(shadow + OFF_F3W + min(mo, 9) * 84)[min(mp + 4 * k, 20)];
+  bf16 w3d[10];                            // fc3 dgrad: column tid
+#pragma unroll
+  for (int o = 0; o < 10; ++o) w3d[o] = shadow[OFF_F3W + o * 84 + min(tid, 83)];
+  bf16 w2d[21];                            // fc2 dgrad: column mo, rows mp*21 + k
+#pragma unroll
+  for (int k = 0; k < 21; ++k) w2d[k] = shadow[OFF_F2W + (mp * 21 + k) * 120 + min(mo, 119)];
+  const float bias_f1 = master[OFF_F1B + min(mo, 119)];
+  const float bias_f2 = master[OFF_F2B + min(mo, 83)];
+  const float bias_f3 = master[OFF_F3B + min(mo, 9)];
   if (tid < 84) {  // window records of P1 rows (overwrite R1: dead until phase F)
     const int row = tid;  // c*14 + y
     float v[20];
@@ -237,7 +307,7 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
       R2[row * 13 + x] = r;
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (wave < 7) {
     const int t = wave;
     const int wi = fr >> 2, pi = fr & 3;
@@ -262,7 +332,7 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
     }
     const int qo = 4 * t + fg;
     if (qo < 25) {
-      const float bias = master[OFF_C2B + fr];
+      const float bias = bc2;
       float best = acc[0] + bias;
       int arg = 0;
 #pragma unroll
@@ -274,8 +344,10 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
       CODE2[fr * 25 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // fc1 LDS-DMA (and MLP prefetch) landed
   __syncthreads();
 
+  STAMP(3);
   // ============ phase D: MLP forward, cross-entropy, MLP data-backward ==================
   {  // fc1: 120 x 400, 4 lanes per output
     const int o = tid >> 2, p = tid & 3;
@@ -292,39 +364,41 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
     }
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
-    if (o < 120 && p == 0) H1[o] = fmaxf(acc + master[OFF_F1B + o], 0.f);
+    if (o < 120 && p == 0) H1[o] = fmaxf(acc + bias_f1, 0.f);
   }
   __syncthreads();
-  {  // fc2: 84 x 120 (weights straight from L2)
-    const int o = tid >> 2, p = tid & 3;
+  {  // fc2: 84 x 120 (prefetched fragments)
     float acc = 0.f;
-    if (o < 84) {
-      const bf16x8* wrow = reinterpret_cast<const bf16x8*>(shadow + OFF_F2W + o * 120);
-      for (int c8 = p; c8 < 15; c8 += 4) {
-        const bf16x8 w = wrow[c8];
+    if (mo < 84) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += (float)w[j] * H1[c8 * 8 + j];
+      for (int k = 0; k < 4; ++k) {
+        const int c8 = mp + 4 * k;
+        if (c8 < 15) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += (float)w2f[k][j] * H1[c8 * 8 + j];
+        }
       }
     }
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
-    if (o < 84 && p == 0) H2[o] = fmaxf(acc + master[OFF_F2B + o], 0.f);
+    if (mo < 84 && mp == 0) H2[mo] = fmaxf(acc + bias_f2, 0.f);
   }
   __syncthreads();
-  {  // fc3: 10 x 84
-    const int o = tid >> 2, p = tid & 3;
+  {  // fc3: 10 x 84 (prefetched fragments)
     float acc = 0.f;
-    if (o < 10) {
-      const bf16x4* wrow = reinterpret_cast<const bf16x4*>(shadow + OFF_F3W + o * 84);
-      for (int c4 = p; c4 < 21; c4 += 4) {
-        const bf16x4 w = wrow[c4];
+    if (mo < 10) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc += (float)w[j] * H2[c4 * 4 + j];
+      for (int k = 0; k < 6; ++k) {
+        const int c4 = mp + 4 * k;
+        if (c4 < 21) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc += (float)w3f[k][j] * H2[c4 * 4 + j];
+        }
       }
     }
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
-    if (o < 10 && p == 0) LOG[o] = acc + master[OFF_F3B + o];
+    if (mo < 10 && mp == 0) LOG[mo] = acc + bias_f3;
   }
   __syncthreads();
   if (tid == 0) {  // CrossEntropy (mean over the valid batch) + accuracy
@@ -347,21 +421,28 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
   }
   if (!TRAIN) return;
   __syncthreads();
-  if (tid < 84) {  // fc3 dgrad + ReLU mask
+  STAMP(4);
+  if (tid < 84) {  // fc3 dgrad + ReLU mask (prefetched column)
     float acc = 0.f;
 #pragma unroll
-    for (int o = 0; o < 10; ++o) acc += DZ3[o] * (float)shadow[OFF_F3W + o * 84 + tid];
+    for (int o = 0; o < 10; ++o) acc += DZ3[o] * (float)w3d[o];
     DZ2[tid] = H2[tid] > 0.f ? acc : 0.f;
   }
   __syncthreads();
-  if (tid < 120) {  // fc2 dgrad + ReLU mask
+  {  // fc2 dgrad + ReLU mask: 4 lanes per input, 21 prefetched rows each
     float acc = 0.f;
-    for (int o = 0; o < 84; ++o) acc += DZ2[o] * (float)shadow[OFF_F2W + o * 120 + tid];
-    DZ1[tid] = H1[tid] > 0.f ? acc : 0.f;
+    if (mo < 120) {
+#pragma unroll
+      for (int k = 0; k < 21; ++k) acc += DZ2[mp * 21 + k] * (float)w2d[k];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (mo < 120 && mp == 0) DZ1[mo] = H1[mo] > 0.f ? acc : 0.f;
   }
   __syncthreads();
   if (tid < 400) {  // fc1 dgrad (mask applied through CODE2 below)
     float acc = 0.f;
+#pragma unroll 8
     for (int o = 0; o < 120; ++o) acc += DZ1[o] * (float)fc1s[o * 400 + tid];
     DA0[tid] = acc;
   }
@@ -372,28 +453,33 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
   if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
   __syncthreads();
 
+  STAMP(5);
   // ============ phase E: conv2 backward =================================================
   float* slab = slab_out + (size_t)b * SLAB;
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);     // [16][10][16]
   bf16* DY2T = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2T);   // [112][16]
   float* DCOLS = reinterpret_cast<float*>(smem + L_REGA + A_DCOLS);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
-  for (int e = tid; e < 16 * 160; e += NT) {  // unpool + ReLU mask -> dY2 (two layouts)
-    const int o = e / 160, r = e % 160, y = r >> 4, x = r & 15;
-    float v = 0.f;
-    if (x < 10) {
-      const int q = (y >> 1) * 5 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
-      if (CODE2[o * 25 + q] == i) v = DA0[o * 25 + q];
-      DY2T[(y * 10 + x) * 16 + o] = (bf16)v;
+  // unpool + ReLU mask -> dY2 (two layouts); wave w owns channels w and w+8 and
+  // reduces their bias gradient with shuffles (fixed order: deterministic)
+  for (int o = wave; o < 16; o += 8) {
+    float bsum = 0.f;
+    for (int r = lane; r < 160; r += 64) {
+      const int y = r >> 4, x = r & 15;
+      float v = 0.f;
+      if (x < 10) {
+        const int q = (y >> 1) * 5 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
+        if (CODE2[o * 25 + q] == i) v = DA0[o * 25 + q];
+        DY2T[(y * 10 + x) * 16 + o] = (bf16)v;
+      }
+      DY2[o * 160 + r] = (bf16)v;
+      bsum += v;
     }
-    DY2[e] = (bf16)v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_xor(bsum, off);
+    if (lane == 0) slab[SLAB_C2B + o] = bsum;
   }
   for (int e = tid; e < 12 * 16; e += NT) DY2T[100 * 16 + e] = (bf16)0.f;
-  if (tid < 16) {  // conv2 bias grad (fp32, fixed order)
-    float s = 0.f;
-    for (int q = 0; q < 25; ++q) if (CODE2[tid * 25 + q] < 4) s += DA0[tid * 25 + q];
-    slab[SLAB_C2B + tid] = s;
-  }
   __syncthreads();
   // conv2 wgrad: dW2[o][(c,ky,kx)] = sum_pix dY2[o][pix] * P1[c][y+ky][x+kx]
   for (int nt = wave; nt < 10; nt += 8) {
@@ -451,23 +537,29 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
   }
   __syncthreads();
 
+  STAMP(6);
   // ============ phase F: conv1 weight gradient ==========================================
   bf16* DY1 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY1);  // [6][28][32]
-  for (int e = tid; e < 6 * 28 * 32; e += NT) {  // unpool + ReLU mask -> dY1
-    const int c = e / 896, r = e % 896, y = r >> 5, x = r & 31;
-    float v = 0.f;
-    if (x < 28) {
-      const int q = (y >> 1) * 14 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
-      if (CODE1[c * 196 + q] == i) v = DP1[c * 196 + q];
+  if (wave < 6) {  // wave c: unpool + ReLU mask -> dY1[c], and the conv1 bias gradient
+    const int c = wave;
+    float bsum = 0.f;
+#pragma unroll 2
+    for (int r = lane; r < 896; r += 64) {
+      const int y = r >> 5, x = r & 31;
+      float v = 0.f;
+      if (x < 28) {
+        const int q = (y >> 1) * 14 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
+        if (CODE1[c * 196 + q] == i) v = DP1[c * 196 + q];
+      }
+      DY1[c * 896 + r] = (bf16)v;
+      bsum += v;
     }
-    DY1[e] = (bf16)v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_xor(bsum, off);
+    if (lane == 0) slab[SLAB_C1B + c] = bsum;
+  } else if (tid - 384 < 96) {
+    build_r1_row(IMGS, R1, tid - 384);  // R2 is dead: rebuild R1
   }
-  if (tid < 6) {
-    float s = 0.f;
-    for (int q = 0; q < 196; ++q) if (CODE1[tid * 196 + q] < 4) s += DP1[tid * 196 + q];
-    slab[SLAB_C1B + tid] = s;
-  }
-  if (tid >= 128 && tid < 224) build_r1_row(img, R1, tid - 128);  // R2 is dead: rebuild R1
   __syncthreads();
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
     const int nt = wave;
@@ -498,6 +590,11 @@ __global__ void __launch_bounds__(NT) lenet_fused_kernel(
       }
     }
   }
+  if (stamp) {
+    __builtin_amdgcn_s_waitcnt(0);
+    STAMP(7);
+  }
+#undef STAMP
 }
 
 }  // namespace dnn
@@ -518,11 +615,11 @@ void init_kernels() {
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
-                        int32_t* correct, hipStream_t stream) {
+                        int32_t* correct, long long* stamps, hipStream_t stream) {
   init_kernels();
   hipLaunchKernelGGL(lenet_fused_kernel<true>, dim3(batch), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, order_len, batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss,
-                     correct);
+                     correct, stamps);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -533,7 +630,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL(lenet_fused_kernel<false>, dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct);
+                     nullptr, nullptr, nullptr, loss, correct, nullptr);
   HIP_CHECK(hipGetLastError());
 }
 

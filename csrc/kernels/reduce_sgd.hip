@@ -20,20 +20,7 @@ constexpr int RT = 256;
 
 
 
-__device__ __forceinline__ float dot_batch(const float* __restrict__ z, int zld, int o,
-                                           const float* __restrict__ x, int xld, int i, int batch) {
-  float s = 0.f;
-  for (int b = 0; b < batch; ++b) s += z[(size_t)b * zld + o] * x[(size_t)b * xld + i];
-  return s;
-}
-
-__device__ __forceinline__ float sum_batch(const float* __restrict__ z, int zld, int o, int batch) {
-  float s = 0.f;
-  for (int b = 0; b < batch; ++b) s += z[(size_t)b * zld + o];
-  return s;
-}
-
-__device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs& a) {
+__device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs a) {
   g *= a.grad_scale;
   if (a.fuse_sgd) {
     const float m = a.momentum * a.mom[e] + g;
@@ -46,60 +33,124 @@ __device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs& a) 
   }
 }
 
-__global__ void __launch_bounds__(RT) grad_reduce_kernel(ReduceArgs a) {
-  const int nblk = gridDim.x - a.bookkeeping;
-  if ((int)blockIdx.x == nblk) {
-    // bookkeeping block: epoch statistics + cursor advance (one wave, fixed order)
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      float ls = 0.f;
-      int cs = 0;
-      for (int b = lane; b < a.batch; b += 64) { ls += a.loss[b]; cs += a.correct[b]; }
+// fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
+// output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).
+struct FcLayer { int O, I, IT, tiles, arena_off, zld, xld, which; };
+__constant__ FcLayer kFc[3] = {
+    {120, 400, 25, 8 * 25, OFF_F1W, Z1_LD, A0_LD, 0},
+    {84, 120, 8, 6 * 8, OFF_F2W, Z2_LD, H1_LD, 1},
+    {10, 84, 6, 1 * 6, OFF_F3W, Z3_LD, H2_LD, 2},
+};
+constexpr int FC_TILES = 200 + 48 + 6;        // 254 wave-tiles
+constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
+
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
+  int l = 0;
+  while (l < 2 && t >= kFc[l].tiles) { t -= kFc[l].tiles; ++l; }
+  const FcLayer L = kFc[l];
+  const float* z = L.which == 0 ? a.z1 : (L.which == 1 ? a.z2 : a.z3);
+  const float* x = L.which == 0 ? a.a0 : (L.which == 1 ? a.h1 : a.h2);
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15, kq = lane >> 4;
+  const int o0 = (t / L.IT) * 16, i0 = (t % L.IT) * 16;
+  const int om = o0 + col, in = i0 + col;
+  const bool ov = om < L.O, iv = in < L.I;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = 0; b0 < a.batch; b0 += 64) {
+    float av[16], bv[16];
+    // every operand load is unconditional (clamped address) and issued before the first
+    // MFMA; out-of-range operands are zeroed by a select afterwards
+    const int omc = ov ? om : 0, inc = iv ? in : 0;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
-      if (lane == 0) {
-        const int bv = a.state[ST_BVALID];
-        if (bv > 0) {
-          a.stats[STAT_LOSS] += (double)ls / (double)bv;
-          a.stats[STAT_BATCHES] += 1.0;
-          a.stats[STAT_CORRECT] += (double)cs;
-          a.stats[STAT_SAMPLES] += (double)bv;
-        }
-        a.state[ST_CURSOR] += 1;
-      }
+    for (int s = 0; s < 16; ++s) {
+      const int b = min(b0 + 4 * s + kq, a.batch - 1);
+      av[s] = z[(size_t)b * L.zld + omc];
+      bv[s] = x[(size_t)b * L.xld + inc];
     }
-    return;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool bvld = b0 + 4 * s + kq < a.batch;
+      av[s] = (bvld && ov) ? av[s] : 0.f;
+      bv[s] = (bvld && iv) ? bv[s] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
   }
-  for (int e = a.lo + blockIdx.x * RT + threadIdx.x; e < a.hi; e += nblk * RT) {
-    float g = 0.f;
-    bool real = true;
-    if (e >= OFF_F1W && e < OFF_F1W + 48000) {
-      const int r = e - OFF_F1W;
-      g = dot_batch(a.z1, Z1_LD, r / 400, a.a0, A0_LD, r % 400, a.batch);
-    } else if (e >= OFF_F1B && e < OFF_F1B + 120) {
-      g = sum_batch(a.z1, Z1_LD, e - OFF_F1B, a.batch);
-    } else if (e >= OFF_F2W && e < OFF_F2W + 10080) {
-      const int r = e - OFF_F2W;
-      g = dot_batch(a.z2, Z2_LD, r / 120, a.h1, H1_LD, r % 120, a.batch);
-    } else if (e >= OFF_F2B && e < OFF_F2B + 84) {
-      g = sum_batch(a.z2, Z2_LD, e - OFF_F2B, a.batch);
-    } else if (e >= OFF_F3W && e < OFF_F3W + 840) {
-      const int r = e - OFF_F3W;
-      g = dot_batch(a.z3, Z3_LD, r / 84, a.h2, H2_LD, r % 84, a.batch);
-    } else if (e >= OFF_F3B && e < OFF_F3B + 10) {
-      g = sum_batch(a.z3, Z3_LD, e - OFF_F3B, a.batch);
-    } else if (e >= OFF_C1W && e < OFF_C1W + 450) {
-      g = sum_batch(a.slab, SLAB, SLAB_C1W + (e - OFF_C1W), a.batch);
-    } else if (e >= OFF_C1B && e < OFF_C1B + 6) {
-      g = sum_batch(a.slab, SLAB, SLAB_C1B + (e - OFF_C1B), a.batch);
-    } else if (e >= OFF_C2W && e < OFF_C2W + 2400) {
-      g = sum_batch(a.slab, SLAB, SLAB_C2W + (e - OFF_C2W), a.batch);
-    } else if (e >= OFF_C2B && e < OFF_C2B + 16) {
-      g = sum_batch(a.slab, SLAB, SLAB_C2B + (e - OFF_C2B), a.batch);
-    } else {
-      real = false;  // arena padding
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = o0 + 4 * kq + j;
+    if (o < L.O && iv) sgd_update(L.arena_off + o * L.I + in, acc[j], a);
+  }
+}
+
+// element tasks: fc biases (sum_b z[b][o]) and conv slab columns (sum_b slab[b][j])
+constexpr int FCB_ELEMS = 120 + 84 + 10;
+constexpr int CONV_ELEMS = SLAB;
+__device__ __forceinline__ void elem_task(int e, bool mlp_part, const ReduceArgs a) {
+  const float* src;
+  int ld, col, dst;
+  if (mlp_part) {
+    if (e >= FCB_ELEMS) return;
+    if (e < 120) { src = a.z1; ld = Z1_LD; col = e; dst = OFF_F1B + e; }
+    else if (e < 204) { src = a.z2; ld = Z2_LD; col = e - 120; dst = OFF_F2B + e - 120; }
+    else { src = a.z3; ld = Z3_LD; col = e - 204; dst = OFF_F3B + e - 204; }
+  } else {
+    if (e >= CONV_ELEMS) return;
+    src = a.slab; ld = SLAB; col = e;
+    if (e < SLAB_C1B) dst = OFF_C1W + e;
+    else if (e < SLAB_C2W) dst = OFF_C1B + (e - SLAB_C1B);
+    else if (e < SLAB_C2B) dst = OFF_C2W + (e - SLAB_C2W);
+    else dst = OFF_C2B + (e - SLAB_C2B);
+  }
+  float g = 0.f;
+  for (int b0 = 0; b0 < a.batch; b0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = src[(size_t)min(b0 + k, a.batch - 1) * ld + col];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) g += (b0 + k < a.batch) ? v[k] : 0.f;
+  }
+  sgd_update(dst, g, a);
+}
+
+__global__ void __launch_bounds__(RT) grad_reduce_kernel(ReduceArgs a) {
+  // block roles: [MLP tile blocks][MLP bias block][conv element blocks][bookkeeping]
+  const bool mlp = a.hi > OFF_F1W;
+  const bool conv = a.lo < OFF_F1W;
+  int blk = blockIdx.x;
+  if (mlp) {
+    if (blk < TILE_BLOCKS) {
+      const int t = blk * 4 + (threadIdx.x >> 6);
+      if (t < FC_TILES) fc_tile(t, a);
+      return;
     }
-    if (real) sgd_update(e, g, a);
+    blk -= TILE_BLOCKS;
+    if (blk < 1) { elem_task(threadIdx.x, true, a); return; }
+    blk -= 1;
+  }
+  if (conv) {
+    constexpr int CB = (CONV_ELEMS + RT - 1) / RT;
+    if (blk < CB) { elem_task(blk * RT + threadIdx.x, false, a); return; }
+    blk -= CB;
+  }
+  if (a.bookkeeping && blk == 0 && threadIdx.x < 64) {
+    // epoch statistics + cursor advance (one wave, fixed order)
+    const int lane = threadIdx.x;
+    float ls = 0.f;
+    int cs = 0;
+    for (int b = lane; b < a.batch; b += 64) { ls += a.loss[b]; cs += a.correct[b]; }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
+    if (lane == 0) {
+      const int bv = a.state[ST_BVALID];
+      if (bv > 0) {
+        a.stats[STAT_LOSS] += (double)ls / (double)bv;
+        a.stats[STAT_BATCHES] += 1.0;
+        a.stats[STAT_CORRECT] += (double)cs;
+        a.stats[STAT_SAMPLES] += (double)bv;
+      }
+      a.state[ST_CURSOR] += 1;
+    }
   }
 }
 
@@ -123,11 +174,14 @@ __global__ void __launch_bounds__(RT) sgd_apply_kernel(float* __restrict__ maste
 
 // ---- host launchers ---------------------------------------------------------------------
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
-  // ~one element per thread, at most one block per CU; +1 block for the bookkeeping
-  int nblk = (args.hi - args.lo + RT - 1) / RT;
-  if (nblk > 240) nblk = 240;
-  if (nblk < 1) nblk = 1;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3(nblk + (args.bookkeeping ? 1 : 0)), dim3(RT), 0, stream, args);
+  const bool mlp = args.hi > OFF_F1W;
+  const bool conv = args.lo < OFF_F1W;
+  int nblk = 0;
+  if (mlp) nblk += TILE_BLOCKS + 1;
+  if (conv) nblk += (CONV_ELEMS + RT - 1) / RT;
+  if (args.bookkeeping) nblk += 1;
+  if (nblk == 0) return;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(nblk), dim3(RT), 0, stream, args);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -58,7 +58,7 @@ def load_cifar10(root: str | os.PathLike, train: bool) -> Split:
 
 
 def synthetic(n: int, seed: int, train: bool = True) -> Split:
-    images, labels = native.io().synthetic(int(n), int(seed) * 2 + (0 if train else 1))
+    images, labels = native.io().synthetic(int(n), int(seed), split=0 if train else 1)
     return Split(torch.from_numpy(images), torch.from_numpy(labels), "synthetic-" + ("train" if train else "test"))
 
 

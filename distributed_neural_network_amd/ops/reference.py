@@ -78,7 +78,7 @@ def batch_grad(arena: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tenso
     a = arena.detach().float().cpu().clone().requires_grad_(True)
     loss = F.cross_entropy(forward(a, normalize_u8(images_u8.cpu())), labels.cpu().long())
     loss.backward()
-    return a.grad.detach(), float(loss)
+    return a.grad.detach(), float(loss.detach())
 
 
 def sgd_momentum_(params: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor, lr: float, momentum: float) -> None:

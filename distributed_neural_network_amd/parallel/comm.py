@@ -1,0 +1,226 @@
+"""Communicator: one process per GPU, collectives over RCCL (xGMI) or gloo (CPU).
+
+Capability parity: replaces the reference's pickled point-to-point mpi4py traffic
+(data_parallelism_train.py:118,135,210,227):
+
+  reference                                   here
+  [comm.send(state_dict, k) for k]  (:118)    broadcast_(arena) once at start-up
+  child send / parent recv + mean  (:210-240) allreduce_(arena, "avg")  (epoch-avg)
+  (future work in the report)                 bucketed per-step gradient all-reduce
+
+On MI355X the backend is torch.distributed "nccl", which IS RCCL: a flat fp32
+arena means one (or two bucketed) collectives per sync instead of 10 pickled
+tensors per child; the per-step gradient all-reduce is issued on RCCL's stream
+and overlapped with the conv-bucket reduction kernel (see GradAllReduce).
+
+Fault tolerance: the process group is created over our own TCPStore under a
+generation prefix, so survivors of a dropped rank can abort the old
+communicator and rendezvous a fresh one (generation + 1) with re-numbered ranks
+(ncclCommAbort + new ncclCommInitRank; torch's bundled RCCL 2.26 has no
+ncclCommShrink).  See fault.py for detection and recovery.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import os
+import time
+from typing import Callable, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .env import DistEnv, detect
+
+
+class CommError(RuntimeError):
+    """A collective failed (peer died, communicator aborted, timeout)."""
+
+
+class Communicator:
+    def __init__(self, env: DistEnv | None = None, device: torch.device | str = "cpu",
+                 backend: str | None = None, timeout_s: float = 300.0) -> None:
+        self.env = env or detect()
+        self.device = torch.device(device)
+        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        self.timeout = _dt.timedelta(seconds=timeout_s)
+        self.generation = 0
+        self.members: list[int] = list(range(self.env.world))  # original ranks of the live group
+        self.orig_rank = self.env.rank
+        self.store: dist.Store | None = None
+        self.aborted = False
+        if self.env.world > 1:
+            self._init_store()
+            self._init_group()
+
+    # -- identity ----------------------------------------------------------------------
+    @property
+    def rank(self) -> int:
+        return self.members.index(self.orig_rank) if self.env.world > 1 else 0
+
+    @property
+    def world(self) -> int:
+        return len(self.members)
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    # -- setup ---------------------------------------------------------------------------
+    def _init_store(self) -> None:
+        agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+        if agent:
+            # torchrun's agent already serves a TCPStore on MASTER_ADDR:MASTER_PORT.
+            self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
+                                       is_master=False, timeout=self.timeout)
+        else:
+            self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
+                                       is_master=self.env.rank == 0, timeout=self.timeout,
+                                       wait_for_workers=False)
+
+    def _init_group(self) -> None:
+        assert self.store is not None
+        prefix = dist.PrefixStore(f"dnn/g{self.generation}", self.store)
+        kwargs = {}
+        if self.backend == "nccl":
+            kwargs["device_id"] = self.device
+        dist.init_process_group(self.backend, store=prefix, rank=self.rank, world_size=self.world,
+                                timeout=self.timeout, **kwargs)
+        self.aborted = False
+
+    # -- collectives ---------------------------------------------------------------------
+    def _avg_op(self):
+        return dist.ReduceOp.AVG if self.backend == "nccl" else None
+
+    def allreduce_(self, t: torch.Tensor, op: str = "avg", async_op: bool = False):
+        """In-place all-reduce; ``op`` in {avg, sum, max, min}."""
+        if not self.distributed:
+            return None
+        try:
+            if op == "avg":
+                aop = self._avg_op()
+                if aop is not None:
+                    return dist.all_reduce(t, op=aop, async_op=async_op)
+                w = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=False)
+                t.div_(self.world)
+                return None if not async_op else _Done()
+            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+            return dist.all_reduce(t, op=rop, async_op=async_op)
+        except Exception as e:  # gloo raises on a dead peer; nccl after abort/timeout
+            raise CommError(str(e)) from e
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        if not self.distributed:
+            return
+        try:
+            dist.broadcast(t, src=src)
+        except Exception as e:
+            raise CommError(str(e)) from e
+
+    def barrier(self) -> None:
+        if not self.distributed:
+            return
+        try:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+        except Exception as e:
+            raise CommError(str(e)) from e
+
+    def reduce_scalar(self, x: float, op: str = "max") -> float:
+        if not self.distributed:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        self.allreduce_(t, op)
+        return float(t.item())
+
+    def gather_scalars(self, x: float) -> list[float]:
+        """All ranks' values of a scalar (rank order of the current group)."""
+        if not self.distributed:
+            return [float(x)]
+        dev = self.device if self.backend == "nccl" else "cpu"
+        t = torch.zeros(self.world, dtype=torch.float64, device=dev)
+        t[self.rank] = float(x)
+        self.allreduce_(t, "sum")
+        return [float(v) for v in t.cpu().tolist()]
+
+    # -- fault handling --------------------------------------------------------------------
+    def abort(self) -> None:
+        """Tear down the current communicator without waiting for peers."""
+        if self.aborted or not dist.is_initialized():
+            self.aborted = True
+            return
+        self.aborted = True
+        try:
+            pg = dist.distributed_c10d._get_default_group()
+            be = pg._get_backend(self.device) if self.backend == "nccl" else None
+            if be is not None and hasattr(be, "abort"):
+                be.abort()
+        except Exception:
+            pass
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+
+    def reform(self, dead: Sequence[int]) -> None:
+        """Re-create the group over the survivors (original rank ids not in ``dead``)."""
+        if self.orig_rank in dead:
+            raise CommError("a dropped rank cannot join the re-formed group")
+        self.abort()
+        self.members = [r for r in self.members if r not in set(dead)]
+        self.generation += 1
+        if self.world > 1:
+            self._init_group()
+
+    def close(self) -> None:
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+class _Done:
+    def wait(self) -> None:
+        return None
+
+
+class GradAllReduce:
+    """Per-step gradient averaging with bucket fusion and comm/compute overlap.
+
+    The engine hands over the flat gradient arena and the bucket ranges in the order
+    their gradients become ready.  Each bucket's all-reduce is issued asynchronously
+    (RCCL runs it on its own stream); ``before_last`` is the compute that produces
+    the last bucket, so it runs on the compute stream concurrently with the earlier
+    buckets' all-reduces.  All waits are stream-level (no host sync), so the whole
+    sequence can be captured into the step's hipGraph.
+    """
+
+    def __init__(self, comm: Communicator) -> None:
+        self.comm = comm
+
+    def allreduce_grads(self, grad: torch.Tensor, buckets: list[tuple[int, int]],
+                        before_last: Optional[Callable[[], None]] = None) -> None:
+        works = []
+        for i, (lo, hi) in enumerate(buckets):
+            if i == len(buckets) - 1 and before_last is not None:
+                before_last()
+            w = self.comm.allreduce_(grad[lo:hi], "avg", async_op=True)
+            if w is not None:
+                works.append(w)
+        for w in works:
+            w.wait()
+
+
+def wait_for_store_key(store: dist.Store, key: str, timeout_s: float) -> bool:
+    deadline = time.time() + timeout_s
+    while time.time() < deadline:
+        try:
+            if store.check([key]):
+                return True
+        except Exception:
+            return False
+        time.sleep(0.05)
+    return False

@@ -1,0 +1,123 @@
+"""Synchronisation policies of data-parallel training.
+
+* ``epoch-avg`` - the reference algorithm: every rank runs a
+  full local epoch of momentum SGD with a freshly created optimizer
+  (data_parallelism_train.py:187 - momentum restarts every epoch), then the models
+  are averaged (data_parallelism_train.py:238-244).  Here the average is ONE
+  all-reduce(avg) of the flat parameter arena instead of N-1 pickled sends + a
+  rank-0 mean.
+* ``parent``    - exact reference topology: rank 0 is a non-training parameter
+  server (data_parallelism_train.py:101-129); the average is over ranks 1..N-1
+  (rank 0 contributes zeros to a sum all-reduce, everyone divides by N-1).
+* ``step-allreduce`` - DDP-style per-step gradient averaging (the report's future
+  work, Project_Report.pdf p.4 §6.2): bucketed RCCL all-reduce overlapped with the
+  conv-bucket reduction, captured in the step hipGraph.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from .comm import Communicator, GradAllReduce
+
+SYNC_MODES = ("step-allreduce", "epoch-avg", "parent")
+
+
+class SyncPolicy:
+    name = "base"
+    reset_momentum_each_epoch = False
+
+    def __init__(self, comm: Communicator, reset_momentum_each_epoch: bool | None = None) -> None:
+        self.comm = comm
+        if reset_momentum_each_epoch is not None:
+            self.reset_momentum_each_epoch = reset_momentum_each_epoch
+        self.comm_time = 0.0
+
+    def trains(self) -> bool:
+        return True
+
+    def trainer_count(self) -> int:
+        return self.comm.world
+
+    def attach(self, engine) -> None:
+        self.engine = engine
+
+    def initial_broadcast(self, engine) -> None:
+        """Rank 0's initial weights are authoritative (reference: parent sends before epoch 0)."""
+        t0 = time.perf_counter()
+        self.comm.broadcast_(engine.master, src=0)
+        engine.params_changed()
+        engine.synchronize()
+        self.comm_time += time.perf_counter() - t0
+
+    def epoch_start(self, engine, epoch: int) -> None:
+        if self.reset_momentum_each_epoch:
+            engine.reset_momentum()
+
+    def epoch_end(self, engine, epoch: int) -> None:
+        pass
+
+
+class StepAllReduce(SyncPolicy):
+    name = "step-allreduce"
+
+    def attach(self, engine) -> None:
+        super().attach(engine)
+        engine.grad_sync = GradAllReduce(self.comm) if self.comm.distributed else None
+
+
+class EpochAverage(SyncPolicy):
+    name = "epoch-avg"
+    reset_momentum_each_epoch = True
+
+    def attach(self, engine) -> None:
+        super().attach(engine)
+        engine.grad_sync = None
+
+    def epoch_end(self, engine, epoch: int) -> None:
+        if not self.comm.distributed:
+            return
+        t0 = time.perf_counter()
+        self.comm.allreduce_(engine.master, "avg")
+        engine.params_changed()
+        engine.synchronize()
+        self.comm_time += time.perf_counter() - t0
+
+
+class ParentAverage(EpochAverage):
+    """Reference topology: rank 0 only averages/evaluates; ranks 1..N-1 train."""
+
+    name = "parent"
+
+    def __init__(self, comm: Communicator, reset_momentum_each_epoch: bool | None = None) -> None:
+        super().__init__(comm, reset_momentum_each_epoch)
+        if comm.world < 2:
+            raise ValueError("--sync parent needs >= 2 processes: rank 0 is the parameter server")
+
+    def trains(self) -> bool:
+        return self.comm.rank != 0
+
+    def trainer_count(self) -> int:
+        return self.comm.world - 1
+
+    def epoch_end(self, engine, epoch: int) -> None:
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            if self.comm.rank == 0:
+                engine.master.zero_()
+            self.comm.allreduce_(engine.master, "sum")
+            engine.master.div_(self.comm.world - 1)
+        engine.params_changed()
+        engine.synchronize()
+        self.comm_time += time.perf_counter() - t0
+
+
+def make_policy(mode: str, comm: Communicator, reset_momentum_each_epoch: bool | None = None) -> SyncPolicy:
+    if mode == "step-allreduce":
+        return StepAllReduce(comm, reset_momentum_each_epoch)
+    if mode == "epoch-avg":
+        return EpochAverage(comm, reset_momentum_each_epoch)
+    if mode == "parent":
+        return ParentAverage(comm, reset_momentum_each_epoch)
+    raise ValueError(f"unknown sync mode {mode!r}; expected one of {SYNC_MODES}")

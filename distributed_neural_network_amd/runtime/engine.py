@@ -210,7 +210,7 @@ class HipEngine(Engine):
         self.loss = torch.zeros(B, **f32)
         self.correct = torch.zeros(B, device=dev, dtype=torch.int32)
         self.order = torch.zeros(0, device=dev, dtype=torch.int32)
-        self.graph_chunk = max(1, int(graph_chunk))
+        self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
         self.stream = torch.cuda.Stream(dev)
@@ -301,6 +301,19 @@ class HipEngine(Engine):
             self._graphs[key] = g
         return g
 
+    def _chunk_sizes(self) -> list[int]:
+        sizes, k = [], 1
+        while k <= self.graph_chunk:
+            sizes.append(k)
+            k *= 2
+        return sizes[::-1]
+
+    def prepare_graphs(self) -> None:
+        """Capture every chunk graph up front (capture is not free: keep it out of timed loops)."""
+        if self.use_graphs:
+            for k in self._chunk_sizes():
+                self._graph(k)
+
     def run_steps(self, n: int) -> None:
         if n <= 0:
             return
@@ -309,15 +322,13 @@ class HipEngine(Engine):
                 for _ in range(n):
                     self._launch_step()
             return
-        full, rem = divmod(n, self.graph_chunk)
-        if full:
-            g = self._graph(self.graph_chunk)
-            for _ in range(full):
-                g.replay()
-        if rem:
-            g = self._graph(1)
-            for _ in range(rem):
-                g.replay()
+        # binary decomposition over power-of-two chunk graphs: <= log2(chunk)+n/chunk replays
+        for k in self._chunk_sizes():
+            reps, n = divmod(n, k)
+            if reps:
+                g = self._graph(k)
+                for _ in range(reps):
+                    g.replay()
 
     def epoch_stats(self, reset: bool = True) -> StepStats:
         v = self.stats.cpu().tolist()
