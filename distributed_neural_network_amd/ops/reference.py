@@ -73,11 +73,16 @@ def per_sample_outputs(arena: torch.Tensor, images_u8: torch.Tensor, labels: tor
             "slab": slabs, "loss": loss, "correct": correct, "logits": logits}
 
 
-def batch_grad(arena: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor) -> tuple[torch.Tensor, float]:
+def batch_grad(arena: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor,
+               return_correct: bool = False):
     """Flat-arena gradient of mean CrossEntropy over the batch (zeros in padding)."""
     a = arena.detach().float().cpu().clone().requires_grad_(True)
-    loss = F.cross_entropy(forward(a, normalize_u8(images_u8.cpu())), labels.cpu().long())
+    y = labels.cpu().long()
+    logits = forward(a, normalize_u8(images_u8.cpu()))
+    loss = F.cross_entropy(logits, y)
     loss.backward()
+    if return_correct:
+        return a.grad.detach(), float(loss.detach()), int((logits.detach().argmax(1) == y).sum())
     return a.grad.detach(), float(loss.detach())
 
 

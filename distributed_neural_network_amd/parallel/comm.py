@@ -67,9 +67,11 @@ class Communicator:
 
     # -- setup ---------------------------------------------------------------------------
     def _init_store(self) -> None:
-        agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+        agent = (os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+                 or os.environ.get("DNN_STORE_EXTERNAL", "") == "1")
         if agent:
-            # torchrun's agent already serves a TCPStore on MASTER_ADDR:MASTER_PORT.
+            # torchrun's agent (or parallel/launch.py) already serves a TCPStore on
+            # MASTER_ADDR:MASTER_PORT; every rank is a client, so any rank may die.
             self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
                                        is_master=False, timeout=self.timeout)
         else:

@@ -1,0 +1,145 @@
+"""Failure injection, detection and recovery.
+
+Capability parity:
+  * ``simulate_failure`` (data_parallelism_train.py:41-46, flags :266-269): with
+    probability p a rank prints ``Process {rank} failed! Sleeping for {d} seconds.``,
+    sleeps d seconds, prints ``Process {rank} woke up!`` - once per epoch, called by
+    the parent before the broadcast (:117) and by every child before training (:141).
+    A straggler, not a crash; reproduced verbatim (but seeded, so runs are repeatable).
+  * The reference has no detection and no recovery: a dead rank would
+    leave the parent blocked in ``comm.recv()`` forever.  Here:
+      - ``DropInjector``: ``--drop-rank R --drop-at-epoch E [--drop-at-step S]`` makes
+        rank R die hard (``os._exit``, no cleanup) at that point;
+      - ``Heartbeat``: every rank stamps ``hb/<rank>`` in the rendezvous TCPStore from
+        a background thread; a watchdog marks a rank dead when its stamp goes stale
+        and aborts the communicator so nobody stays blocked in a collective (gloo
+        collectives also fail fast with a CommError on a closed peer socket);
+      - ``agree_survivors``: the survivors agree on the new member list through the
+        store (first survivor to win a compare_set is the leader and publishes it);
+      - the trainer then re-forms the communicator over the survivors
+        (Communicator.reform: abort + new generation group), restores the last
+        consistent parameters (start-of-epoch snapshot), re-partitions the data over
+        the new world size and re-runs the epoch, reporting recovery latency.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .comm import Communicator
+
+DROP_EXIT_CODE = 17
+
+
+def simulate_failure(rank: int, probability: float, duration: float, rng: np.random.Generator) -> bool:
+    """Reference straggler injection; returns True if this rank slept."""
+    if probability > 0 and rng.random() < probability:
+        print(f"Process {rank} failed! Sleeping for {duration} seconds.", flush=True)
+        time.sleep(float(duration))
+        print(f"Process {rank} woke up!", flush=True)
+        return True
+    return False
+
+
+@dataclass
+class DropInjector:
+    rank: Optional[int] = None
+    at_epoch: int = 0
+    at_step: int = 0
+
+    def active(self) -> bool:
+        return self.rank is not None and self.rank >= 0
+
+    def step_limit(self, orig_rank: int, epoch: int) -> Optional[int]:
+        """Steps this rank may run in ``epoch`` before it must die (None: no limit)."""
+        if self.active() and orig_rank == self.rank and epoch == self.at_epoch:
+            return self.at_step
+        return None
+
+    def die(self, orig_rank: int, epoch: int, step: int) -> None:
+        print(f"[fault] injected drop: rank {orig_rank} exits at epoch {epoch} step {step}", flush=True)
+        os._exit(DROP_EXIT_CODE)
+
+
+class Heartbeat:
+    """Background heartbeat + watchdog over the rendezvous TCPStore."""
+
+    def __init__(self, comm: Communicator, period_s: float = 0.2, timeout_s: float = 3.0) -> None:
+        import torch.distributed as dist
+
+        self.comm = comm
+        self.period = period_s
+        self.timeout = timeout_s
+        self.dead: set[int] = set()
+        self._stop = threading.Event()
+        env = comm.env
+        # a private client connection for the thread
+        self.store = dist.TCPStore(env.master_addr, env.master_port, env.world, is_master=False,
+                                   timeout=comm.timeout)
+        self._beat()
+        self._thread = threading.Thread(target=self._run, name="dnn-heartbeat", daemon=True)
+        self._thread.start()
+
+    def _beat(self) -> None:
+        self.store.set(f"dnn/hb/{self.comm.orig_rank}", repr(time.time()))
+
+    def last_seen(self, rank: int) -> float:
+        try:
+            if not self.store.check([f"dnn/hb/{rank}"]):
+                return 0.0
+            return float(self.store.get(f"dnn/hb/{rank}").decode())
+        except Exception:
+            return 0.0
+
+    def stale(self, rank: int) -> bool:
+        return time.time() - self.last_seen(rank) > self.timeout
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.period):
+            try:
+                self._beat()
+                for r in list(self.comm.members):
+                    if r != self.comm.orig_rank and r not in self.dead and self.stale(r):
+                        self.dead.add(r)
+                        print(f"[fault] watchdog: rank {r} heartbeat stale > {self.timeout}s", flush=True)
+                        if self.comm.backend == "nccl":
+                            self.comm.abort()  # unblock collectives spinning on a dead peer
+            except Exception:
+                pass
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=2.0)
+
+
+def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0) -> list[int]:
+    """Survivors of generation g agree on the member list of generation g+1."""
+    assert comm.store is not None
+    st = comm.store
+    p = f"dnn/recover/{comm.generation}/"
+    st.set(f"{p}alive/{comm.orig_rank}", "1")
+    deadline = time.time() + wait_s
+    while True:
+        alive, undecided = [], []
+        for r in comm.members:
+            if st.check([f"{p}alive/{r}"]):
+                alive.append(r)
+            elif r in hb.dead or hb.stale(r):
+                pass
+            else:
+                undecided.append(r)
+        if not undecided or time.time() > deadline:
+            break
+        time.sleep(0.05)
+    # first survivor to win the compare_set publishes the member list
+    won = st.compare_set(f"{p}leader", "", str(comm.orig_rank)).decode() == str(comm.orig_rank)
+    if won:
+        st.set(f"{p}members", ",".join(str(r) for r in sorted(alive)))
+    st.wait([f"{p}members"])
+    members = [int(x) for x in st.get(f"{p}members").decode().split(",") if x]
+    return members

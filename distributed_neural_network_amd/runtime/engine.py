@@ -142,10 +142,7 @@ class CpuEngine(Engine):
                 continue
             x = self.train.images[idx]
             y = self.train.labels[idx]
-            g, loss = reference.batch_grad(self.master, x, y)
-            with torch.no_grad():
-                logits = reference.forward(self.master, reference.normalize_u8(x))
-                correct = int((logits.argmax(1) == y.long()).sum())
+            g, loss, correct = reference.batch_grad(self.master, x, y, return_correct=True)
             self.grad.copy_(g)
             if self.grad_sync is not None:
                 self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])

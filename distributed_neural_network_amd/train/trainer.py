@@ -1,0 +1,287 @@
+"""Orchestrator: epochs, sync policy, evaluation, fault recovery, logs and metrics.
+
+Capability parity with the reference orchestration:
+  * ``main()`` / parent-child roles / epoch loop  (data_parallelism_train.py:56-152,
+    model_replication_train.py:31-68, single_proc_train.py:16-105),
+  * ``run_child``  -> engine.run_steps over this rank's epoch order (:185-213),
+  * ``run_parent`` -> SyncPolicy.epoch_end (one all-reduce instead of N-1 receives
+    and a rank-0 mean, :219-254) + the same stdout lines,
+  * ``eval``       -> fused forward kernel over the test set, sharded over ranks,
+    with the reference metric definitions (:157-183),
+  * timers / log files / neptune series -> utils.timers / utils.logfiles /
+    utils.metrics,
+  * ``simulate_failure`` -> parallel.fault (plus real rank-drop recovery).
+
+Stdout lines are kept verbatim so log scrapers keep working.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..data import EpochSampler, get_splits
+from ..parallel import CommError, Communicator, detect, make_policy
+from ..parallel.fault import DropInjector, Heartbeat, agree_survivors, simulate_failure
+from ..runtime import eval_metrics, make_engine
+from ..utils import checkpoint, logfiles
+from ..utils.metrics import Run
+from ..utils.timers import PhaseTimers
+from .config import TrainConfig
+
+
+def resolve_device(spec: str, local_rank: int) -> torch.device:
+    if spec == "cpu":
+        return torch.device("cpu")
+    if spec == "auto":
+        if torch.cuda.is_available():
+            return torch.device("cuda", local_rank % torch.cuda.device_count())
+        return torch.device("cpu")
+    if spec == "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError("--device cuda requested but no ROCm GPU is visible")
+        return torch.device("cuda", local_rank % torch.cuda.device_count())
+    return torch.device(spec)
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig) -> None:
+        self.cfg = cfg
+        self.env = detect()
+        self.device = resolve_device(cfg.device, self.env.local_rank)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        if self.device.type == "cpu" and self.env.world > 1:
+            # N CPU ranks on one host: split the cores instead of oversubscribing them
+            # (the reference's anti-scaling mechanism, Project_Report.pdf p.3 §5.3)
+            torch.set_num_threads(max(1, (os.cpu_count() or 1) // self.env.world))
+        self.comm = Communicator(self.env, self.device)
+        self.rank0 = self.comm.orig_rank == 0
+        self.drop = DropInjector(cfg.drop_rank, cfg.drop_at_epoch, cfg.drop_at_step)
+        self.hb: Optional[Heartbeat] = Heartbeat(self.comm) if self.comm.distributed else None
+        self.rng = np.random.default_rng([cfg.seed, 0x57A66, self.comm.orig_rank])
+        self.run_log = Run(cfg.metrics if self.rank0 else None)
+        self.recoveries: list[dict] = []
+        self.history: list[dict] = []
+
+    # -- helpers --------------------------------------------------------------------------
+    def _sampler(self) -> EpochSampler:
+        c = self.cfg
+        n = len(self.train)
+        if c.mode in ("single", "replication"):
+            return EpochSampler.for_rank(n, self.comm.rank, self.comm.world, c.seed, mode="full")
+        return EpochSampler.for_rank(n, self.comm.rank, self.comm.world, c.seed, mode="shard",
+                                     parent=c.sync == "parent")
+
+    def _say(self, *a, **kw) -> None:
+        if self.rank0:
+            print(*a, **kw, flush=True)
+
+    def _evaluate(self) -> tuple[float, float]:
+        n = len(self.test)
+        if self.cfg.eval_sharded and self.comm.distributed:
+            lo, hi = self.comm.rank * n // self.comm.world, (self.comm.rank + 1) * n // self.comm.world
+        else:
+            lo, hi = 0, n
+        loss, corr = self.engine.evaluate_samples(self.test, lo, hi)
+        if self.cfg.eval_sharded and self.comm.distributed:
+            dev = self.device if self.comm.backend == "nccl" else torch.device("cpu")
+            full = torch.zeros(2, n, dtype=torch.float32, device=dev)
+            full[0, lo:hi] = loss.to(dev)
+            full[1, lo:hi] = corr.to(dev).float()
+            self.comm.allreduce_(full, "sum")
+            loss, corr = full[0], full[1]
+        return eval_metrics(loss, corr, self.cfg.batch_size)
+
+    def _train_epoch(self, epoch: int) -> None:
+        order = self.sampler.order(epoch)
+        self.engine.begin_epoch(order)
+        n = self.sampler.steps(self.cfg.batch_size)
+        lim = self.drop.step_limit(self.comm.orig_rank, epoch)
+        if lim is not None and lim <= n:
+            self.engine.run_steps(lim)
+            self.engine.synchronize()
+            self.drop.die(self.comm.orig_rank, epoch, lim)
+        self.engine.run_steps(n)
+        self.engine.synchronize()
+
+    def _recover(self, epoch: int, snap: tuple[torch.Tensor, torch.Tensor], err: Exception) -> None:
+        t0 = time.perf_counter()
+        old = list(self.comm.members)
+        assert self.hb is not None
+        members = agree_survivors(self.comm, self.hb)
+        if self.comm.orig_rank not in members:
+            raise RuntimeError("this rank was excluded from the re-formed group") from err
+        dead = [r for r in old if r not in members]
+        self.comm.reform(dead)
+        with torch.no_grad():
+            self.engine.master.copy_(snap[0])
+            self.engine.mom.copy_(snap[1])
+        self.engine.params_changed()
+        self.engine.epoch_stats(reset=True)
+        if hasattr(self.engine, "invalidate_graphs"):
+            self.engine.invalidate_graphs()  # captured collectives belong to the old communicator
+        self.policy.attach(self.engine)
+        self.sampler = self._sampler()
+        self.comm.barrier()
+        dt = time.perf_counter() - t0
+        rec = {"epoch": epoch, "dead": dead, "survivors": members, "generation": self.comm.generation,
+               "recovery_s": dt, "error": str(err).splitlines()[0][:200] if str(err) else type(err).__name__}
+        self.recoveries.append(rec)
+        self.rank0 = self.comm.rank == 0
+        if self.comm.rank == 0:
+            print(f"[fault] rank(s) {dead} dropped in epoch {epoch}; communicator re-formed "
+                  f"(generation {self.comm.generation}, {self.comm.world} ranks) in {dt:.3f} s; "
+                  f"data re-partitioned, epoch restarted from the last consistent parameters", flush=True)
+        self.run_log.record(event="recovery", **rec)
+
+    # -- main ------------------------------------------------------------------------------
+    def run(self) -> dict:
+        c = self.cfg
+        eng_kw = {}
+        if self.device.type == "cuda":
+            eng_kw = dict(graph_chunk=c.graph_chunk, overlap=c.overlap)
+        self.timers = PhaseTimers()
+        with self.timers.phase(PhaseTimers.DATA, sync=False):
+            self.train, self.test = get_splits(c.data, c.data_root, c.train_samples, c.test_samples, c.seed)
+            self.engine = make_engine(str(self.device) if self.device.type == "cuda" else "cpu", c.batch_size,
+                                      c.lr, c.momentum, seed=c.seed, **eng_kw)
+            self.engine.attach(self.train)
+            self.test = self.test.to(self.device)
+            self.engine.synchronize()
+        self.timers._sync = self.engine.synchronize
+        self.policy = make_policy(c.sync if self.comm.distributed else "step-allreduce", self.comm,
+                                  c.momentum_reset)
+        if c.mode == "single":
+            self.policy.reset_momentum_each_epoch = bool(c.momentum_reset)
+        self.policy.attach(self.engine)
+        self.sampler = self._sampler()
+
+        start_epoch = 0
+        if c.resume:
+            sd, side = checkpoint.load(c.resume)
+            self.engine.load_state_dict(sd)
+            if "momentum" in side:
+                self.engine.mom.copy_(side["momentum"].to(self.engine.mom.device))
+            start_epoch = int(side.get("epoch", -1)) + 1
+            self._say(f"(Resumed from {c.resume} at epoch {start_epoch})")
+        self.policy.initial_broadcast(self.engine)
+        self.comm_time_children = 0.0
+
+        if self.rank0:
+            self.run_log["parameters"] = {"learning_rate": c.lr, "momentum": c.momentum, "optimizer": "SGD",
+                                          "model_name": {"single": "nodistmodel"}.get(c.mode, "distmodel"),
+                                          "epochs": c.epochs, "batch_size": c.batch_size, "sync": c.sync,
+                                          "world_size": self.comm.world, "device": str(self.device)}
+        if c.mode == "single":
+            print(self.device, flush=True)
+            print(len(self.train), flush=True)
+            print(len(self.test), flush=True)
+        elif self.policy.trains():
+            print("(Loaded Train Dataset for worker {0} of length {1})".format(self.comm.orig_rank, len(self.sampler)),
+                  flush=True)
+
+        epoch = start_epoch
+        while epoch < c.epochs:
+            t_epoch = time.perf_counter()
+            if c.mode != "single":
+                self._say("Starting epoch ", epoch)
+            simulate_failure(self.comm.orig_rank, c.failure_probability, c.failure_duration, self.rng)
+            snap = (self.engine.master.detach().clone(), self.engine.mom.detach().clone())
+            try:
+                self.policy.epoch_start(self.engine, epoch)
+                if self.policy.trains():
+                    with self.timers.phase(PhaseTimers.TRAIN):
+                        self._train_epoch(epoch)
+                stats = self.engine.epoch_stats(reset=True)
+                t0 = time.perf_counter()
+                self.policy.epoch_end(self.engine, epoch)
+                tot = torch.tensor([stats.loss_sum, stats.batches, stats.correct, stats.samples],
+                                   dtype=torch.float64)
+                if self.comm.distributed:
+                    dev = self.device if self.comm.backend == "nccl" else torch.device("cpu")
+                    tt = tot.to(dev)
+                    self.comm.allreduce_(tt, "sum")
+                    tot = tt.cpu()
+                self.timers.add(PhaseTimers.COMM_PARENT if self.rank0 else PhaseTimers.COMM_CHILDREN,
+                                time.perf_counter() - t0)
+            except CommError as e:
+                if not self.comm.distributed or self.hb is None:
+                    raise
+                self._recover(epoch, snap, e)
+                continue
+            loss_sum, batches, correct, samples = [float(x) for x in tot.tolist()]
+            trainers = self.policy.trainer_count()
+            if c.mode == "single":
+                avg = loss_sum / max(batches, 1)
+                print(f"Epoch {epoch + 1}, Average Training Loss: {avg:.3f}", flush=True)
+            else:
+                for p in range(trainers):
+                    self._say("(Received a trained model from process {0} of {1} workers...)".format(p + 1, trainers))
+                self._say("* Averaging models...")
+                # reference quirk (§2.7 #1): it divides by 10 (state_dict keys) per worker
+                avg = loss_sum / (10.0 * trainers) if c.compat else loss_sum / max(batches, 1)
+                self._say(f"Global Average Training Loss: {avg}")
+                self._say("evaluating model")
+            with self.timers.phase(PhaseTimers.EVAL):
+                val_loss, val_acc = self._evaluate()
+            if c.mode == "single":
+                print("Validation Accuracy: %.2f %%" % val_acc, flush=True)
+                print("Validation Loss: %.3f" % val_loss, flush=True)
+            else:
+                self._say("Validation loss of updated master model: ", val_loss)
+            dt = time.perf_counter() - t_epoch
+            rec = {"epoch": epoch, "train_loss": avg, "train_acc": 100.0 * correct / max(samples, 1),
+                   "val_loss": val_loss, "val_acc": val_acc, "epoch_s": dt, "samples": samples,
+                   "img_per_s": samples / dt if dt > 0 else 0.0, "world": self.comm.world,
+                   "phases": self.timers.as_dict() if c.profile else None}
+            self.history.append(rec)
+            if self.rank0:
+                self.run_log["train/loss"].append(avg)
+                self.run_log["val/loss"].append(val_loss)
+                self.run_log["val/acc"].append(val_acc)
+                self.run_log.record(**rec)
+                if c.save:
+                    checkpoint.save(c.save, self.engine.state_dict(), self.engine.mom, epoch=epoch,
+                                    seed=c.seed, world=self.comm.world, sync=c.sync, mode=c.mode)
+            epoch += 1
+
+        self._finish()
+        return {"history": self.history, "recoveries": self.recoveries, "timers": self.timers.as_dict(),
+                "world": self.comm.world, "rank": self.comm.rank}
+
+    def _finish(self) -> None:
+        c = self.cfg
+        T = self.timers
+        if c.mode == "data-parallel":
+            if self.rank0:
+                print("Eval data loading time: {0}".format(T[PhaseTimers.DATA]), flush=True)
+                print("Time spent on evaluation: {0}".format(T[PhaseTimers.EVAL]), flush=True)
+                print("Time spent on parent communication and param sync: {0}".format(T[PhaseTimers.COMM_PARENT]),
+                      flush=True)
+                if c.write_logs:
+                    logfiles.write_log(c.log_dir, logfiles.log_name(c.batch_size, c.epochs, c.nb_proc, "parent"),
+                                       logfiles.parent_lines(T[PhaseTimers.DATA], T[PhaseTimers.EVAL],
+                                                             T[PhaseTimers.COMM_PARENT]))
+            # reference: rank 2 only (a 2-process job never wrote it); default: the
+            # lowest training rank other than 0 that exists
+            child = 2 if c.compat else min(2, self.comm.world - 1)
+            if self.comm.rank == child and (child != 0 or not c.compat) and self.policy.trains():
+                comm_c = T[PhaseTimers.COMM_CHILDREN] if child != 0 else T[PhaseTimers.COMM_PARENT]
+                print("Training data loading time: {0}".format(T[PhaseTimers.DATA]), flush=True)
+                print("Time spent on training: {0}".format(T[PhaseTimers.TRAIN]), flush=True)
+                print("Time spent on children communication: {0}".format(comm_c), flush=True)
+                if c.write_logs:
+                    logfiles.write_log(c.log_dir, logfiles.log_name(c.batch_size, c.epochs, c.nb_proc, "children"),
+                                       logfiles.children_lines(T[PhaseTimers.DATA], T[PhaseTimers.TRAIN], comm_c))
+        if self.hb is not None:
+            self.hb.stop()
+        self.run_log.stop()
+        self.comm.close()
+
+
+def run(cfg: TrainConfig) -> dict:
+    return Trainer(cfg).run()

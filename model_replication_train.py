@@ -1,0 +1,18 @@
+#!/usr/bin/env python3
+"""Reference-compatible entrypoint `model_replication_train.py` (mode: replication).
+
+Same flags and defaults as the reference script (typed), plus the framework options
+(--sync, --device, --data, --save/--resume, fault injection, ...); see
+`python model_replication_train.py --help` and distributed_neural_network_amd/train/config.py.
+Multi-process: `python -m distributed_neural_network_amd.parallel.launch -n N model_replication_train.py ...`,
+torchrun, or mpiexec (one process per GPU).
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_neural_network_amd.train import main  # noqa: E402
+
+if __name__ == "__main__":
+    main("replication")

@@ -1,0 +1,37 @@
+"""Worker launched (one process per rank) by tests/test_distributed_cpu.py."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
+from distributed_neural_network_amd.models.network import init_arena  # noqa: E402
+from distributed_neural_network_amd.parallel import Communicator, make_policy  # noqa: E402
+from distributed_neural_network_amd.runtime import CpuEngine  # noqa: E402
+
+
+def main(mode: str, out: str, n: int, batch: int, epochs: int) -> None:
+    torch.set_num_threads(1)
+    comm = Communicator(device="cpu")
+    data = synthetic(n, 3)
+    eng = CpuEngine(batch=batch, lr=0.05, momentum=0.9, arena=init_arena(seed=comm.rank + 100))  # differ on purpose
+    eng.attach(data)
+    policy = make_policy(mode, comm)
+    policy.attach(eng)
+    policy.initial_broadcast(eng)  # rank 0's init wins
+    samp = EpochSampler.for_rank(n, comm.rank, comm.world, seed=1, mode="shard", parent=mode == "parent",
+                                 shuffle=False)
+    for ep in range(epochs):
+        policy.epoch_start(eng, ep)
+        if policy.trains():
+            eng.begin_epoch(samp.order(ep))
+            eng.run_steps(samp.steps(batch))
+        policy.epoch_end(eng, ep)
+    torch.save({"master": eng.master, "rank": comm.rank}, os.path.join(out, f"rank{comm.rank}.pt"))
+    comm.close()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))

@@ -1,0 +1,156 @@
+"""Multi-process (gloo, CPU) correctness of the sync policies, the CLI and fault recovery.
+
+Every policy is checked against a single-process computation of the same math:
+  * step-allreduce, 2 ranks x batch b  == 1 process x batch 2b (gradient of the mean)
+  * epoch-avg                          == arithmetic mean of the locally trained models
+                                          (reference data_parallelism_train.py:238-240)
+  * parent                             == mean over workers 1..N-1 only
+"""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_neural_network_amd.data import EpochSampler, synthetic
+from distributed_neural_network_amd.models.network import LAYOUT, init_arena
+from distributed_neural_network_amd.runtime import CpuEngine
+from distributed_neural_network_amd.utils import checkpoint, logfiles
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _launch(n, args, cwd, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "distributed_neural_network_amd.parallel.launch", "-n", str(n), "--cpu"] + args
+    return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _run_worker(tmp_path, mode, world, n=192, batch=16, epochs=2):
+    r = _launch(world, [os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(tmp_path), str(n), str(batch),
+                        str(epochs)], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return [torch.load(tmp_path / f"rank{i}.pt", weights_only=True)["master"] for i in range(world)]
+
+
+def _local(arena, data, idx, batch, epochs_orders, lr=0.05, momentum=0.9, reset=False):
+    eng = CpuEngine(batch=batch, lr=lr, momentum=momentum, arena=arena)
+    eng.attach(data)
+    for order in epochs_orders:
+        if reset:
+            eng.reset_momentum()
+        eng.begin_epoch(order)
+        eng.run_steps((len(order) + batch - 1) // batch)
+    return eng
+
+
+def test_step_allreduce_equals_big_batch(tmp_path):
+    got = _run_worker(tmp_path, "step-allreduce", 2, n=192, batch=16, epochs=1)
+    assert torch.allclose(got[0], got[1], atol=0, rtol=0)  # replicas stay bitwise identical
+    data = synthetic(192, 3)
+    # single process, batch 32: step t takes shard0[16t:16t+16] + shard1[16t:16t+16]
+    order = np.concatenate([np.concatenate([np.arange(16 * t, 16 * t + 16), 96 + np.arange(16 * t, 16 * t + 16)])
+                            for t in range(6)]).astype(np.int32)
+    ref = _local(init_arena(seed=100), data, None, 32, [order])
+    assert torch.allclose(got[0], ref.master, atol=2e-6), float((got[0] - ref.master).abs().max())
+
+
+def test_epoch_average_equals_mean_of_local_models(tmp_path):
+    got = _run_worker(tmp_path, "epoch-avg", 2, n=192, batch=16, epochs=2)
+    assert torch.equal(got[0], got[1])
+    data = synthetic(192, 3)
+    a = init_arena(seed=100)
+    for ep in range(2):
+        ms = []
+        for r in range(2):
+            e = _local(a, data, None, 16, [np.arange(96 * r, 96 * r + 96, dtype=np.int32)], reset=True)
+            ms.append(e.master)
+        a = (ms[0] + ms[1]) / 2
+    assert torch.allclose(got[0], a, atol=1e-6)
+
+
+def test_parent_topology_averages_workers_only(tmp_path):
+    got = _run_worker(tmp_path, "parent", 3, n=192, batch=16, epochs=1)
+    assert torch.allclose(got[0], got[1]) and torch.allclose(got[1], got[2])
+    data = synthetic(192, 3)
+    a = init_arena(seed=100)
+    ms = [_local(a, data, None, 16, [np.arange(96 * r, 96 * r + 96, dtype=np.int32)], reset=True).master
+          for r in range(2)]
+    assert torch.allclose(got[0], (ms[0] + ms[1]) / 2, atol=1e-6)
+
+
+SMALL = ["--train-samples", "384", "--test-samples", "128", "--lr", "0.01", "--device", "cpu"]
+
+
+def test_cli_data_parallel_stdout_and_logs(tmp_path):
+    r = _launch(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2", "--batch-size", "32",
+                    "--nb-proc", "3", "--compat", "--metrics", "m.jsonl"] + SMALL, tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = r.stdout
+    assert out.count("Starting epoch  ") == 2
+    assert "(Received a trained model from process 3 of 3 workers...)" in out
+    assert "* Averaging models..." in out and "evaluating model" in out
+    assert re.search(r"Global Average Training Loss: [0-9.]+", out)
+    assert re.search(r"Validation loss of updated master model:  [0-9.]+", out)
+    assert "(Loaded Train Dataset for worker 2 of length 128)" in out
+    par = logfiles.read_log(str(tmp_path / "log" / "bs32_log_epochs2_proc3_parent.txt"))
+    chi = logfiles.read_log(str(tmp_path / "log" / "bs32_log_epochs2_proc3_children.txt"))
+    assert set(par) == {"Eval data loading time", "Time spent on evaluation",
+                        "Time spent on parent communication and param sync"}
+    assert set(chi) == {"Train data loading time", "Time spent on training", "Time spent on children communication"}
+    assert (tmp_path / "m.jsonl").exists()
+
+
+def test_cli_single_and_replication(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "single_proc_train.py"), "--epochs", "2"] + SMALL,
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "cpu" and lines[1] == "384" and lines[2] == "128"
+    assert re.match(r"Epoch 1, Average Training Loss: \d+\.\d{3}$", lines[3])
+    assert re.match(r"Validation Accuracy: \d+\.\d{2} %$", lines[4])
+    assert re.match(r"Validation Loss: \d+\.\d{3}$", lines[5])
+    r = _launch(2, [os.path.join(ROOT, "model_replication_train.py"), "--epochs", "1", "--batch-size", "64"] + SMALL,
+                tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "(Loaded Train Dataset for worker 1 of length 384)" in r.stdout  # full set on every worker
+
+
+def test_typed_cli_overrides_work():
+    from distributed_neural_network_amd.train import parse
+    c = parse("data-parallel", ["--lr", "0.05", "--momentum", "0.5", "--batch-size", "8", "--epochs", "3",
+                                "--failure-probability", "0.25", "--failure-duration", "0.1"])
+    assert (c.lr, c.momentum, c.batch_size, c.epochs) == (0.05, 0.5, 8, 3)
+    assert c.failure_probability == 0.25 and c.nb_proc == 4
+    d = parse("replication", [])
+    assert (d.batch_size, d.epochs, d.sync) == (16, 10, "epoch-avg")
+    s = parse("single", [])
+    assert (s.batch_size, s.epochs) == (4, 15)
+
+
+def test_straggler_prints(capsys):
+    from distributed_neural_network_amd.parallel.fault import simulate_failure
+    rng = np.random.default_rng(0)
+    assert simulate_failure(3, 1.0, 0.01, rng)
+    out = capsys.readouterr().out
+    assert "Process 3 failed! Sleeping for 0.01 seconds." in out and "Process 3 woke up!" in out
+    assert not simulate_failure(3, 0.0, 1.0, rng)
+
+
+@pytest.mark.parametrize("sync", ["step-allreduce", "epoch-avg"])
+def test_rank_drop_reforms_and_finishes(tmp_path, sync):
+    r = _launch(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "3", "--batch-size", "32",
+                    "--sync", sync, "--drop-rank", "1", "--drop-at-epoch", "1", "--drop-at-step", "2",
+                    "--save", "ck.pt", "--nb-proc", "3"] + SMALL, tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "rank 1 dropped (injected failure)" in r.stdout
+    m = re.search(r"\[fault\] rank\(s\) \[1\] dropped in epoch 1; communicator re-formed \(generation 1, 2 ranks\)",
+                  r.stdout)
+    assert m, r.stdout
+    assert r.stdout.count("Validation loss of updated master model:") == 3
+    sd, side = checkpoint.load(str(tmp_path / "ck.pt"))
+    assert side["epoch"] == 2 and side["world"] == 2
