@@ -11,6 +11,17 @@
 
 
 
+namespace dnn {
+int rccl_open(const std::string& path);
+std::string rccl_unique_id();
+uintptr_t rccl_init(const std::string& id_bytes, int nranks, int rank, int device);
+void rccl_allreduce(uintptr_t comm, uintptr_t buf, size_t count, int dtype, int op, uintptr_t stream);
+void rccl_broadcast(uintptr_t comm, uintptr_t buf, size_t count, int root, uintptr_t stream);
+int rccl_async_error(uintptr_t comm);
+void rccl_abort(uintptr_t comm);
+void rccl_destroy(uintptr_t comm);
+}  // namespace dnn
+
 namespace py = pybind11;
 using u = uintptr_t;
 
@@ -60,6 +71,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_grad_reduce(a, S(stream));
   });
   m.def("init", []() { dnn::init_kernels(); });
+  // native RCCL communicator (comm/rccl_comm.cpp)
+  m.def("rccl_open", &dnn::rccl_open, py::arg("path"));
+  m.def("rccl_unique_id", []() { return py::bytes(dnn::rccl_unique_id()); });
+  m.def("rccl_init", [](py::bytes id, int nranks, int rank, int device) {
+    py::gil_scoped_release nogil;  // blocks until every rank joined
+    return dnn::rccl_init(std::string(id), nranks, rank, device);
+  });
+  m.def("rccl_allreduce", &dnn::rccl_allreduce, py::arg("comm"), py::arg("buf"), py::arg("count"),
+        py::arg("dtype"), py::arg("op"), py::arg("stream"));
+  m.def("rccl_broadcast", &dnn::rccl_broadcast);
+  m.def("rccl_async_error", &dnn::rccl_async_error);
+  m.def("rccl_abort", [](uintptr_t c) { py::gil_scoped_release nogil; dnn::rccl_abort(c); });
+  m.def("rccl_destroy", [](uintptr_t c) { py::gil_scoped_release nogil; dnn::rccl_destroy(c); });
   m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
                         int pack_only, u stream) {
     dnn::launch_sgd_apply(P<float>(master), P<const float>(grad), P<float>(mom), P<bf16>(shadow), n, lr, momentum,

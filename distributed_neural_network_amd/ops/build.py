@@ -31,6 +31,7 @@ HIP_SOURCES = [
     CSRC / "kernels" / "reduce_sgd.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"
+HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp"]
 HIP_HEADERS = sorted((CSRC / "kernels").glob("*.h"))
 IO_SOURCES = [CSRC / "io" / "dataio.cpp"]
 
@@ -63,7 +64,7 @@ def _run(cmd: list[str]) -> None:
 
 def build_hip(force: bool = False, verbose_resources: bool = False) -> Path:
     target = hip_target()
-    deps = HIP_SOURCES + [HIP_BINDING] + HIP_HEADERS
+    deps = HIP_SOURCES + [HIP_BINDING] + HIP_HEADERS + HOST_SOURCES
     if not force and not _stale(target, deps):
         return target
     objdir = REPO / "build" / "hip"
@@ -75,11 +76,15 @@ def build_hip(force: bool = False, verbose_resources: bool = False) -> Path:
         extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resources else []
         _run(common + extra + ["-c", str(src), "-o", str(obj)])
         objs.append(str(obj))
+    for src in HOST_SOURCES:  # host-only C++ (RCCL via dlopen), compiled as HIP for the headers
+        obj = objdir / (src.stem + ".o")
+        _run(common + ["-x", "hip", "-c", str(src), "-o", str(obj)])
+        objs.append(str(obj))
     bobj = objdir / "bindings.o"
     _run(common + _pybind_includes() + ["-x", "hip", "-c", str(HIP_BINDING), "-o", str(bobj)])
     objs.append(str(bobj))
     tmp = target.with_suffix(".tmp.so")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-ldl"])
     os.replace(tmp, target)
     return target
 

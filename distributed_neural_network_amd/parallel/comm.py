@@ -48,14 +48,17 @@ class Communicator:
         self.orig_rank = self.env.rank
         self.store: dist.Store | None = None
         self.aborted = False
-        if self.env.world > 1:
+        # DNN_FORCE_COLLECTIVES=1: build a real process group and issue every collective
+        # even at world size 1 (exercises the RCCL + hipGraph-capture path on one GPU)
+        self.force = os.environ.get("DNN_FORCE_COLLECTIVES", "0") == "1"
+        if self.env.world > 1 or self.force:
             self._init_store()
             self._init_group()
 
     # -- identity ----------------------------------------------------------------------
     @property
     def rank(self) -> int:
-        return self.members.index(self.orig_rank) if self.env.world > 1 else 0
+        return self.members.index(self.orig_rank) if self.orig_rank in self.members else 0
 
     @property
     def world(self) -> int:
@@ -63,7 +66,7 @@ class Communicator:
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or (self.force and dist.is_initialized() and not self.aborted)
 
     # -- setup ---------------------------------------------------------------------------
     def _init_store(self) -> None:
@@ -150,6 +153,12 @@ class Communicator:
     # -- fault handling --------------------------------------------------------------------
     def abort(self) -> None:
         """Tear down the current communicator without waiting for peers."""
+        nat = getattr(self, "native", None)
+        if nat is not None:
+            try:
+                nat.abort()
+            except Exception:
+                pass
         if self.aborted or not dist.is_initialized():
             self.aborted = True
             return
@@ -173,7 +182,7 @@ class Communicator:
         self.abort()
         self.members = [r for r in self.members if r not in set(dead)]
         self.generation += 1
-        if self.world > 1:
+        if self.world > 1 or self.force:
             self._init_group()
 
     def close(self) -> None:

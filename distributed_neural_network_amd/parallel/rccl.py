@@ -1,0 +1,99 @@
+"""Native RCCL communicator for the per-step gradient all-reduce (GPU hot path).
+
+The torch ProcessGroup path costs ~16 us of framework overhead per collective on
+MI355X (work objects, per-collective stream fork/join) - measured: 33 us/step extra
+for two bucketed all-reduces even at world size 1.  The hot path therefore calls
+``ncclAllReduce`` from C++ (csrc/comm/rccl_comm.cpp) directly on the engine's stream;
+inside the step hipGraph it is one kernel node.  The communicator is bootstrapped
+through the job's TCPStore (rank 0 publishes the ncclUniqueId under the current
+generation prefix) and re-created after a rank drop (ncclCommAbort + new InitRank).
+
+Bucketing at this model size: the whole gradient is 248 KB (fp32) - a few
+microseconds of xGMI wire time, so the collective is latency-bound.  The default is
+ONE fused bucket per step (one collective latency).  ``overlap=True`` instead splits
+the MLP bucket (95% of the bytes) from the conv bucket and runs the MLP all-reduce on
+a side stream concurrently with the conv-bucket reduction kernel.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import torch
+
+from ..ops import native
+from .comm import Communicator
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def torch_rccl_path() -> str:
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+class RcclComm:
+    def __init__(self, comm: Communicator) -> None:
+        self.comm = comm
+        self.ext = native.hip()
+        self.version = self.ext.rccl_open(torch_rccl_path())
+        self.handle = 0
+        self._init()
+
+    def _init(self) -> None:
+        c = self.comm
+        assert c.store is not None
+        key = f"dnn/rccl/g{c.generation}/uid"
+        if c.rank == 0:
+            c.store.set(key, self.ext.rccl_unique_id())
+        uid = c.store.get(key)
+        self.handle = self.ext.rccl_init(uid, c.world, c.rank, c.device.index)
+        self.generation = c.generation
+
+    def allreduce_(self, t: torch.Tensor, op: str = "avg", stream: Optional[torch.cuda.Stream] = None) -> None:
+        assert t.is_contiguous() and t.device.type == "cuda"
+        s = (stream or torch.cuda.current_stream(t.device)).cuda_stream
+        self.ext.rccl_allreduce(self.handle, t.data_ptr(), t.numel(), _DT[t.dtype],
+                                {"sum": 0, "avg": 1, "max": 2}[op], s)
+
+    def healthy(self) -> bool:
+        return self.handle != 0 and self.ext.rccl_async_error(self.handle) == 0
+
+    def abort(self) -> None:
+        if self.handle:
+            self.ext.rccl_abort(self.handle)
+            self.handle = 0
+
+    def reinit(self) -> None:
+        """After Communicator.reform: new communicator over the survivors."""
+        self.abort()
+        self._init()
+
+
+class NativeGradAllReduce:
+    """GradSync over the native communicator (see module docstring)."""
+
+    def __init__(self, rc: RcclComm, device: torch.device, overlap: bool = False) -> None:
+        self.rc = rc
+        self.overlap = overlap
+        self.side = torch.cuda.Stream(device)
+        self.ev = [torch.cuda.Event() for _ in range(3)]
+
+    def allreduce_grads(self, grad: torch.Tensor, buckets: list[tuple[int, int]],
+                        before_last: Optional[Callable[[], None]] = None) -> None:
+        s = torch.cuda.current_stream(grad.device)
+        if not self.overlap or len(buckets) < 2 or before_last is None:
+            if before_last is not None:
+                before_last()
+            lo, hi = min(b[0] for b in buckets), max(b[1] for b in buckets)
+            self.rc.allreduce_(grad[lo:hi], "avg", stream=s)  # one fused bucket
+            return
+        (lo0, hi0), (lo1, hi1) = buckets[0], buckets[-1]
+        self.ev[0].record(s)
+        self.side.wait_event(self.ev[0])
+        self.rc.allreduce_(grad[lo0:hi0], "avg", stream=self.side)   # MLP bucket on the side stream
+        before_last()                                                  # conv-bucket reduce, concurrently
+        self.ev[1].record(s)
+        self.side.wait_event(self.ev[1])
+        self.rc.allreduce_(grad[lo1:hi1], "avg", stream=self.side)
+        self.ev[2].record(self.side)
+        s.wait_event(self.ev[2])

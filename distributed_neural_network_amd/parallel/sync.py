@@ -64,7 +64,20 @@ class StepAllReduce(SyncPolicy):
 
     def attach(self, engine) -> None:
         super().attach(engine)
-        engine.grad_sync = GradAllReduce(self.comm) if self.comm.distributed else None
+        if not self.comm.distributed:
+            engine.grad_sync = None
+        elif self.comm.backend == "nccl":
+            # GPU hot path: native RCCL communicator, all-reduce launched on the engine stream
+            from .rccl import NativeGradAllReduce, RcclComm
+
+            rc = getattr(self.comm, "native", None)
+            if rc is None:
+                rc = self.comm.native = RcclComm(self.comm)
+            elif rc.generation != self.comm.generation:
+                rc.reinit()
+            engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=getattr(engine, "overlap", False))
+        else:
+            engine.grad_sync = GradAllReduce(self.comm)
 
 
 class EpochAverage(SyncPolicy):

@@ -179,7 +179,7 @@ class HipEngine(Engine):
 
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
-                 use_graphs: bool = True, overlap: bool = True) -> None:
+                 use_graphs: bool = True, overlap: bool = False) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if not torch.cuda.is_available():
             raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
