@@ -38,7 +38,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
     d["fc1.weight"] = dnn::OFF_F1W; d["fc1.bias"] = dnn::OFF_F1B;
     d["fc2.weight"] = dnn::OFF_F2W; d["fc2.bias"] = dnn::OFF_F2B;
     d["fc3.weight"] = dnn::OFF_F3W; d["fc3.bias"] = dnn::OFF_F3B;
-    d["arena"] = dnn::ARENA; d["slab"] = dnn::SLAB;
+    d["arena"] = dnn::ARENA; d["slab"] = dnn::SLAB; d["shadow_total"] = dnn::SH_TOTAL;
+    d["sh_w1f"] = dnn::SH_W1F; d["sh_w2f"] = dnn::SH_W2F; d["sh_wf"] = dnn::SH_WF;
+    d["sh_w2t"] = dnn::SH_W2T; d["sh_w3t"] = dnn::SH_W3T;
     return d;
   });
   m.def("fused_train",

@@ -11,21 +11,29 @@
 // grad_reduce kernel sums them in a fixed order (bitwise deterministic, no atomics).
 //
 // MI355X design:
-//  * one workgroup = one sample = 8 waves (512 threads); every intermediate stays
-//    in LDS (160 KB budget laid out below), HBM sees the u8 image, the bf16 weights
-//    and the small per-sample output rows only.
-//  * conv fwd, conv wgrad and conv dgrad run on MFMA (v_mfma_f32_16x16x32_bf16 /
-//    16x16x16bf16_1k, f32 accumulate).  The im2col gather is removed by "window
-//    records": rec[c][y][x] = X[c][y][x..x+7] (16 B, bf16).  Ordering K as
-//    (c, ky, kx<8) makes every A/B fragment ONE aligned ds_read_b128, for the
-//    forward (8 kx per lane) AND for the weight gradient (8 consecutive pixels per
-//    lane).
-//  * ReLU + 2x2 maxpool are fused into the MFMA epilogue: each 16-row M-tile is 4
-//    pooling windows x 4 pixels, so a lane's 4 accumulator rows ARE one window.
-//    The argmax is kept as a 2-bit code (4 = no gradient, i.e. max <= 0), which
-//    replaces both max_pool2d_with_indices and threshold_backward.
-//  * conv2 dgrad is an MFMA col2im (dCols = dY2^T W2) followed by a deterministic
-//    gather-sum, not float atomics.
+//  * one workgroup = one sample = 8 waves (512 threads); every intermediate stays in
+//    LDS (159 KB map below); HBM/L2 see the u8 image, bf16 weights and the small
+//    per-sample output rows only.
+//  * EVERY matmul-shaped op runs on MFMA v_mfma_f32_16x16x32_bf16 (fp32 accumulate):
+//    conv fwd, conv wgrad, conv dgrad and all six MLP GEMVs (M = 1 row of a 16-row
+//    tile: latency, not FLOPs, is the budget at this size).
+//  * The im2col gather is replaced by "window records": rec[c][y][x] = X[c][y][x..x+7]
+//    (16 B, bf16).  Ordering K as (c, ky, kx<8) makes every conv A/B fragment ONE
+//    aligned ds_read_b128 - for the forward (8 kx per lane), the weight gradients
+//    (8 consecutive pixels per lane) and the data gradient (records of zero-padded
+//    dY2 against the flipped kernel).
+//  * ReLU + 2x2 maxpool are fused into the conv epilogues: each 16-row M-tile is 4
+//    pooling windows x 4 pixels, so a lane's 4 accumulator rows ARE one window.  The
+//    argmax is a 2-bit code (4 = no gradient: max <= 0), replacing both
+//    max_pool2d_with_indices and threshold_backward.
+//  * Weights arrive pre-packed: the optimizer kernels keep MFMA-fragment images of
+//    the conv kernels (incl. the flipped dgrad kernel) and transposed fc2/fc3 copies
+//    in the bf16 shadow (common.h SH_*), so every B fragment is one 16-B load.
+//  * fc1 (96 KB) streams into LDS by LDS-DMA (inline-asm global_load_lds) during the
+//    convolutions, the flipped conv2 kernel during the MLP; both cross LDS-only
+//    barriers (s_waitcnt lgkmcnt(0); s_barrier) that leave vmcnt alone.
+//  * Every MFMA loop issues all of a tile's operand loads before its MFMA chain
+//    (sched_barrier), so LDS latency is paid once per batch, not once per K-step.
 #include "launchers.h"
 
 namespace dnn {
@@ -33,36 +41,44 @@ namespace dnn {
 constexpr int NT = 512;
 
 // ---- LDS map (bytes) ----------------------------------------------------------------
-constexpr int L_REGA = 0;          // fc1 bf16 [120][400] | dCols/DY2/DY2T/DP1 | dY1
+constexpr int L_REGA = 0;          // fc1 bf16 [120][400] (A-D) | conv2-bwd scratch (E) | dY1 (F)
 constexpr int L_REGA_SZ = 96256;
-constexpr int L_REGB = L_REGA + L_REGA_SZ;  // R1 records [3][32][29] | R2 records [6][14][13]
+constexpr int L_REGB = L_REGA + L_REGA_SZ;  // R1 records [3][32][29] (A-B, F) | R2 + WF (C-E)
 constexpr int L_REGB_SZ = 44544;
+constexpr int B_WF = 17472;                 // REGB: flipped conv2 kernel fragments after R2 (20,480 B)
 constexpr int L_P1 = L_REGB + L_REGB_SZ;    // f32 [6][14][20] (cols 14..19 zero)
 constexpr int L_CODE1 = L_P1 + 6720;        // u8 [6][196]
-constexpr int L_A0 = L_CODE1 + 1184;        // f32 [400]
-constexpr int L_CODE2 = L_A0 + 1600;        // u8 [400]
+constexpr int L_A0 = L_CODE1 + 1184;        // f32 [400]  pooled conv2 output
+constexpr int L_A0B = L_A0 + 1600;          // bf16 [416] (MFMA operand, zero padded)
+constexpr int L_CODE2 = L_A0B + 832;        // u8 [400]
 constexpr int L_H1 = L_CODE2 + 400;         // f32 [128]
-constexpr int L_H2 = L_H1 + 512;            // f32 [96]
-constexpr int L_LOG = L_H2 + 384;           // f32 [16]
+constexpr int L_H1B = L_H1 + 512;           // bf16 [128]
+constexpr int L_H2 = L_H1B + 256;           // f32 [96]
+constexpr int L_H2B = L_H2 + 384;           // bf16 [96]
+constexpr int L_LOG = L_H2B + 192;          // f32 [16]
 constexpr int L_DZ3 = L_LOG + 64;           // f32 [16]
-constexpr int L_DZ2 = L_DZ3 + 64;           // f32 [96]
-constexpr int L_DZ1 = L_DZ2 + 384;          // f32 [128]
-constexpr int L_DA0 = L_DZ1 + 512;          // f32 [400]
-constexpr int L_W1S = L_DA0 + 1600;         // bf16 [6][75] (+pad)
-constexpr int L_W2S = L_W1S + 912;          // bf16 [16][150]
-constexpr int L_IMG = L_W2S + 4800;         // u8 [3][32][32] raw image (re-used by phase F)
-constexpr int L_MISC = L_IMG + 3072;        // scalars
-constexpr int LDS_TOTAL = L_MISC + 64;      // 163,072 B
+constexpr int L_DZ3B = L_DZ3 + 64;          // bf16 [32]
+constexpr int L_DZ2 = L_DZ3B + 64;          // f32 [96]
+constexpr int L_DZ2B = L_DZ2 + 384;         // bf16 [96]
+constexpr int L_DZ1 = L_DZ2B + 192;         // f32 [128]
+constexpr int L_DZ1B = L_DZ1 + 512;         // bf16 [128]
+constexpr int L_DA0 = L_DZ1B + 256;         // f32 [400]
+constexpr int L_IMG = L_DA0 + 1600;         // u8 [3][32][32] raw image (re-used by phase F)
+constexpr int L_MISC = L_IMG + 3072;
+constexpr int LDS_TOTAL = L_MISC + 64;      // 159,152 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
+static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
-// REGA sub-layout during the conv backward
-constexpr int DCOLS_LD = 164;               // f32 row stride of dCols [112][164]
-constexpr int A_DCOLS = 0;                  // 73,472
-constexpr int A_DY2 = 73472;                // bf16 [16][10][16]   5,120
-constexpr int A_DY2T = A_DY2 + 5120;        // bf16 [112][16]      3,584
-constexpr int A_DP1 = A_DY2T + 3584;        // f32 [6][196]        4,704
-constexpr int A_DY1 = 0;                    // bf16 [6][28][32]   10,752 (after dCols is dead)
-static_assert(A_DP1 + 4704 <= L_REGA_SZ, "REGA sub-layout");
+// REGA sub-layout during the conv backward (fc1 weights are dead after the MLP dgrad)
+constexpr int A_R3 = 0;                     // bf16x8 records [16][18][14] of zero-padded dY2  64,512
+constexpr int A_DY2 = 64512;                // bf16 [16][10][16]                                 5,120
+constexpr int A_DP1 = A_DY2 + 5120;         // f32 [6][196]                                      4,704
+constexpr int A_RS = A_DP1 + 4704;          // f32 [16][18] dY2 row sums (conv2 bias grad)       1,152
+constexpr int A_DY1 = 0;                    // bf16 [6] x 1808 B (28 rows x 64 B + 16 B pad)    10,848
+constexpr int DY1_CH = 1808;                //   channel stride: 452 dwords, breaks the 4-way bank conflict
+constexpr int A_RS1 = A_DY1 + 6 * DY1_CH;   // f32 [6][28] dY1 row sums (conv1 bias grad)          672
+static_assert(A_RS + 1152 <= L_REGA_SZ, "REGA sub-layout");
+static_assert(A_RS1 + 672 <= A_DP1, "phase F scratch must not overlap dP1");
 
 __device__ __forceinline__ float u8norm(uint32_t u) {
   // ToTensor (x/255) then Normalize(mean .5, std .5): same op order as torchvision.
@@ -71,7 +87,7 @@ __device__ __forceinline__ float u8norm(uint32_t u) {
 
 // Barrier for LDS hand-offs only: waits for this wave's LDS ops, not for vmcnt, so an
 // in-flight LDS-DMA (global_load_lds) keeps streaming across it.  __syncthreads()
-// would emit s_waitcnt vmcnt(0) and drain the DMA.
+// would emit s_waitcnt vmcnt(0) and drain the DMA (and every outstanding store).
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -95,31 +111,68 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
 
+// Make hipcc treat a register as defined here: it waits for the load that produced it
+// now (not at some later use where an asm DMA may be in flight behind it).
+template <typename T>
+__device__ __forceinline__ void consume(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
 __device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ short bf16_bits(float f) {
-  bf16 h = (bf16)f;
-  return __builtin_bit_cast(short, h);
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+  return z;
 }
 
-// Build the 29 window records of one input row (c, y) from the u8 image staged in LDS.
-__device__ __forceinline__ void build_r1_row(const uint8_t* img, bf16x8* R1, int row) {
-  const uint4* src = reinterpret_cast<const uint4*>(img + row * 32);
-  uint4 lo = src[0], hi = src[1];
-  uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  float v[40];
+// A operand of an M = 1 product: row 0 of the 16-row tile (lanes with fr == 0) holds
+// x[k0 .. k0+7]; every other row is zero.
+__device__ __forceinline__ bf16x8 row0(const bf16* x, int k0, int fr) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + k0);
+  return fr == 0 ? v : zero8();
+}
+
+// Transposed B fragment of a [K rows][N cols] row-major bf16 LDS matrix (row stride
+// `ld` elements): lane (fr, fg) gets B[k0 + 8fg + j][n0 + fr], j = 0..7, from two
+// ds_read_b64_tr_b16 (4 rows x 16 columns each).  Rows are clamped to kmax - 1 (the
+// clamped rows meet zero A entries).  EXEC must be all ones.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* m, int ld, int k0, int n0, int kmax, int lane) {
+  typedef __attribute__((address_space(3))) bf16x4* lp;
+  const int l16 = lane & 15, q = l16 >> 2, p = l16 & 3, fg = lane >> 4;
+  const int r0 = min(k0 + 8 * fg + q, kmax - 1), r1 = min(k0 + 8 * fg + 4 + q, kmax - 1);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp)(m + r0 * ld + n0 + 4 * p));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp)(m + r1 * ld + n0 + 4 * p));
+  bf16x8 v;
 #pragma unroll
-  for (int k = 0; k < 32; ++k) v[k] = u8norm((w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+  for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+  return v;
+}
+
+// Build window records x = 8q .. 8q+7 (x < 29) of input row (c, y) = `row` from the u8
+// image staged in LDS; 4 threads per row (q = 0..3).
+__device__ __forceinline__ void build_r1_part(const uint8_t* img, bf16x8* R1, int row, int q) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(img + row * 32);
+  uint32_t w[4];  // elements 8q .. 8q+15 (zero past the row end)
 #pragma unroll
-  for (int k = 32; k < 40; ++k) v[k] = 0.f;
+  for (int k = 0; k < 4; ++k) w[k] = (2 * q + k < 8) ? src[2 * q + k] : 0u;
+  float v[16];
 #pragma unroll
-  for (int x = 0; x < 29; ++x) {
-    bf16x8 r;
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t u = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    v[k] = (8 * q + k < 32) ? u8norm(u) : 0.f;
+  }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
-    R1[row * 29 + x] = r;
+  for (int x = 0; x < 8; ++x) {
+    if (8 * q + x < 29) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
+      R1[row * 29 + 8 * q + x] = r;
+    }
   }
 }
 
@@ -131,7 +184,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     int order_len, int batch, int base_index,
     int32_t* __restrict__ state,          // TRAIN: cursor/bvalid words
     const float* __restrict__ master,     // fp32 arena (biases)
-    const bf16* __restrict__ shadow,      // bf16 arena (weights)
+    const bf16* __restrict__ shadow,      // bf16 shadow: arena copy + kernel-ready weight images
     float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
     float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
@@ -144,6 +197,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const int fr = lane & 15;   // MFMA fragment row/col within the 16-tile
+  const int fg = lane >> 4;   // MFMA k-group (0..3)
   const int b = blockIdx.x;
 
   long gidx;
@@ -176,42 +231,54 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   bf16* fc1s = reinterpret_cast<bf16*>(smem + L_REGA);
   bf16x8* R1 = reinterpret_cast<bf16x8*>(smem + L_REGB);
   bf16x8* R2 = reinterpret_cast<bf16x8*>(smem + L_REGB);
+  bf16x8* WF = reinterpret_cast<bf16x8*>(smem + L_REGB + B_WF);
   float* P1 = reinterpret_cast<float*>(smem + L_P1);
   uint8_t* CODE1 = smem + L_CODE1;
   float* A0 = reinterpret_cast<float*>(smem + L_A0);
+  bf16* A0B = reinterpret_cast<bf16*>(smem + L_A0B);
   uint8_t* CODE2 = smem + L_CODE2;
   float* H1 = reinterpret_cast<float*>(smem + L_H1);
+  bf16* H1B = reinterpret_cast<bf16*>(smem + L_H1B);
   float* H2 = reinterpret_cast<float*>(smem + L_H2);
+  bf16* H2B = reinterpret_cast<bf16*>(smem + L_H2B);
   float* LOG = reinterpret_cast<float*>(smem + L_LOG);
   float* DZ3 = reinterpret_cast<float*>(smem + L_DZ3);
+  bf16* DZ3B = reinterpret_cast<bf16*>(smem + L_DZ3B);
   float* DZ2 = reinterpret_cast<float*>(smem + L_DZ2);
+  bf16* DZ2B = reinterpret_cast<bf16*>(smem + L_DZ2B);
   float* DZ1 = reinterpret_cast<float*>(smem + L_DZ1);
+  bf16* DZ1B = reinterpret_cast<bf16*>(smem + L_DZ1B);
   float* DA0 = reinterpret_cast<float*>(smem + L_DA0);
-  bf16* W1S = reinterpret_cast<bf16*>(smem + L_W1S);
-  bf16* W2S = reinterpret_cast<bf16*>(smem + L_W2S);
+  uint8_t* IMGS = smem + L_IMG;
 
   // ============ phase A: ingest + weight staging ======================================
-  // Loads are issued before any is consumed, in order of use: image + conv weights and
-  // biases (needed now), then fc1 (96 KB) by LDS-DMA straight into its LDS region; the
-  // DMA stays in flight through both convolutions (phases B-C synchronise with
-  // LDS-only barriers, which do not drain vmcnt) and is waited for before phase D.
-  uint8_t* IMGS = smem + L_IMG;
+  // Plain loads first (image, conv B fragments, conv biases), consumed before the fc1
+  // LDS-DMA is issued (hipcc would otherwise drain the DMA at their first use).
   const uint4 im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
-  const uint4 w1v = reinterpret_cast<const uint4*>(shadow + OFF_C1W)[min(tid, 56)];  // 450 bf16 + zero pad
-  const uint4 w2v = reinterpret_cast<const uint4*>(shadow + OFF_C2W)[max(tid - 212, 0)];
-  const float bias_c1 = master[OFF_C1B + min(lane & 15, 5)];
-  const float bias_c2 = master[OFF_C2B + (lane & 15)];
+  bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
+#pragma unroll
+  for (int sk = 0; sk < 4; ++sk) bw1[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W1F)[(4 * sk + fg) * 16 + fr];
+#pragma unroll
+  for (int sk = 0; sk < 8; ++sk) bw2[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W2F)[(4 * sk + fg) * 16 + fr];
+  float bias_c1 = master[OFF_C1B + min(fr, 5)];
+  float bias_c2 = master[OFF_C2B + fr];
   for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = 0.f;
+  if (tid < 16) A0B[400 + tid] = (bf16)0.f;                                   // MLP operand padding
+  else if (tid < 24) H1B[120 + tid - 16] = (bf16)0.f;
+  else if (tid < 36) H2B[84 + tid - 24] = (bf16)0.f;
+  else if (tid < 58) DZ3B[10 + tid - 36] = (bf16)0.f;
+  else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
+  else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
-  if (tid < 57) reinterpret_cast<uint4*>(smem + L_W1S)[tid] = w1v;
-  if (tid >= 212) reinterpret_cast<uint4*>(smem + L_W2S)[tid - 212] = w2v;
-  // (hipcc waits vmcnt(0) for a plain load consumed while an LDS-DMA is in flight, so the
-  //  loads above are consumed first and the DMA is issued after them)
-  float bc1 = bias_c1, bc2 = bias_c2;
-  asm volatile("" : "+v"(bc1), "+v"(bc2));  // consume (wait for) the bias loads before the DMA
+#pragma unroll
+  for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
+#pragma unroll
+  for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+  consume(bias_c1);
+  consume(bias_c2);
   {
-    // 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all in-arena).
-    // 12 per wave with the index clamped: a duplicate copies identical bytes.
+    // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all
+    // in-arena); 12 per wave with the index clamped (a duplicate copies identical bytes)
     const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
 #pragma unroll
@@ -221,42 +288,21 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   lds_barrier();
-  if (tid < 96) build_r1_row(IMGS, R1, tid);
+  if (tid < 384) build_r1_part(IMGS, R1, tid >> 2, tid & 3);
   lds_barrier();
   STAMP(1);
 
-  const int fr = lane & 15;   // MFMA fragment row/col within the 16-tile
-  const int fg = lane >> 4;   // MFMA k-group (0..3)
-
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
   {
-    bf16x8 bw[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int pr = 4 * s + fg;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        bw[s][j] = (fr < 6 && pr < 15 && j < 5) ? W1S[fr * 75 + pr * 5 + j] : (bf16)0.f;
-    }
-    const float bias = fr < 6 ? bc1 : 0.f;
+    const float bias = fr < 6 ? bias_c1 : 0.f;
     const int wi = fr >> 2, pi = fr & 3;  // A-operand row -> (window, pixel)
-    for (int t = wave; t < 49; t += 8) {
+    auto a_index = [&](int t, int sk) {  // R1 record of (tile t, K-step sk) for this lane
       const int q = 4 * t + wi;
       const int y = 2 * (q / 14) + (pi >> 1), x = 2 * (q % 14) + (pi & 1);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int pr = 4 * s + fg;
-        bf16x8 a;
-        if (pr < 15) {
-          const int c = pr / 5, ky = pr % 5;
-          a = R1[(c * 32 + y + ky) * 29 + x];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) a[j] = (bf16)0.f;
-        }
-        acc = mfma32(a, bw[s], acc);
-      }
+      const int pr = min(4 * sk + fg, 14);  // pair 15 is K padding: real data x zero weights
+      return (pr / 5 * 32 + y + pr % 5) * 29 + x;
+    };
+    auto epilogue = [&](int t, f32x4 acc) {
       if (fr < 6) {  // lane holds window fg of tile t for channel fr
         const int qo = 4 * t + fg;
         float best = acc[0] + bias;
@@ -269,42 +315,67 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         P1[(fr * 14 + qo / 14) * 20 + qo % 14] = fmaxf(best, 0.f);
         CODE1[fr * 196 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
       }
+    };
+    for (int t0 = wave; t0 < 49; t0 += 16) {  // two tiles per round: 8 loads in flight
+      const int t1 = t0 + 8 < 49 ? t0 + 8 : t0;
+      bf16x8 a0[4], a1[4];
+#pragma unroll
+      for (int sk = 0; sk < 4; ++sk) {
+        a0[sk] = R1[a_index(t0, sk)];
+        a1[sk] = R1[a_index(t1, sk)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sk = 0; sk < 4; ++sk) {
+        acc0 = mfma32(a0[sk], bw1[sk], acc0);
+        acc1 = mfma32(a1[sk], bw1[sk], acc1);
+      }
+      epilogue(t0, acc0);
+      if (t0 + 8 < 49) epilogue(t1, acc1);
     }
   }
   lds_barrier();
 
   STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============
-  // MLP operands each lane needs in phase D, loaded now so conv2 hides their latency.
-  const int mo = tid >> 2, mp = tid & 3;   // MLP lane roles: output (or input) index, quarter
-  bf16x8 w2f[4];                           // fc2 forward: row mo, chunks mp + 4k
+  // The MLP B fragments each lane needs in phase D are loaded now so conv2 hides their
+  // latency; lane roles in the MLP: wave w owns output columns 16w + fr.
+  const int ncol = 16 * wave + fr;
+  bf16x8 w2f[4], w2t[3], w3t, w3f[3];
+  {
+    const bf16* r2 = shadow + OFF_F2W + min(ncol, 83) * 120;             // fc2 row (forward)
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    w2f[k] = reinterpret_cast<const bf16x8*>(shadow + OFF_F2W + min(mo, 83) * 120)[min(mp + 4 * k, 14)];
-  bf16x4 w3f[6];                           // fc3 forward: row mo, chunks mp + 4k
+    for (int ks = 0; ks < 4; ++ks) w2f[ks] = *reinterpret_cast<const bf16x8*>(r2 + 32 * ks + 8 * fg);
+    const bf16* t2 = shadow + SH_W2T + min(ncol, 119) * 96;               // fc2^T row (dgrad)
 #pragma unroll
-  for (int k = 0; k < 6; ++k)
-    w3f[k] = reinterpret_cast<const bf16x4*>(shadow + OFF_F3W + min(mo, 9) * 84)[min(mp + 4 * k, 20)];
-  bf16 w3d[10];                            // fc3 dgrad: column tid
+    for (int ks = 0; ks < 3; ++ks) w2t[ks] = *reinterpret_cast<const bf16x8*>(t2 + 32 * ks + 8 * fg);
+    w3t = *reinterpret_cast<const bf16x8*>(shadow + SH_W3T + min(ncol, 83) * 16 + 8 * fg);  // fc3^T (dgrad)
+    const bf16* r3 = shadow + OFF_F3W + min(fr, 9) * 84;                  // fc3 row (forward; 8-B aligned)
 #pragma unroll
-  for (int o = 0; o < 10; ++o) w3d[o] = shadow[OFF_F3W + o * 84 + min(tid, 83)];
-  bf16 w2d[21];                            // fc2 dgrad: column mo, rows mp*21 + k
+    for (int ks = 0; ks < 3; ++ks) {
+      const bf16x4 lo = *reinterpret_cast<const bf16x4*>(r3 + 32 * ks + 8 * fg);
+      const bf16x4 hi = *reinterpret_cast<const bf16x4*>(r3 + 32 * ks + 8 * fg + 4);
 #pragma unroll
-  for (int k = 0; k < 21; ++k) w2d[k] = shadow[OFF_F2W + (mp * 21 + k) * 120 + min(mo, 119)];
-  const float bias_f1 = master[OFF_F1B + min(mo, 119)];
-  const float bias_f2 = master[OFF_F2B + min(mo, 83)];
-  const float bias_f3 = master[OFF_F3B + min(mo, 9)];
-  if (tid < 84) {  // window records of P1 rows (overwrite R1: dead until phase F)
-    const int row = tid;  // c*14 + y
-    float v[20];
+      for (int j = 0; j < 4; ++j) { w3f[ks][j] = lo[j]; w3f[ks][4 + j] = hi[j]; }
+    }
+  }
+  float bias_f1 = master[OFF_F1B + min(ncol, 119)];
+  float bias_f2 = master[OFF_F2B + min(ncol, 83)];
+  float bias_f3 = master[OFF_F3B + min(fr, 9)];
+  if (tid < 168) {  // window records of P1 rows (overwrite R1: dead until phase F); 2 threads per row
+    const int row = tid >> 1, h = tid & 1;  // row = c*14 + y; half h builds records 7h .. 7h+6 (< 13)
+    float v[14];
 #pragma unroll
-    for (int k = 0; k < 20; ++k) v[k] = P1[row * 20 + k];
+    for (int k = 0; k < 14; ++k) v[k] = P1[row * 20 + 7 * h + k];
 #pragma unroll
-    for (int x = 0; x < 13; ++x) {
-      bf16x8 r;
+    for (int x = 0; x < 7; ++x) {
+      if (7 * h + x < 13) {
+        bf16x8 r;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
-      R2[row * 13 + x] = r;
+        for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
+        R2[row * 13 + 7 * h + x] = r;
+      }
     }
   }
   lds_barrier();
@@ -314,273 +385,341 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     int q = 4 * t + wi;
     if (q > 24) q = 24;  // padding windows of the last tile: computed, discarded
     const int y = 2 * (q / 5) + (pi >> 1), x = 2 * (q % 5) + (pi & 1);
+    bf16x8 a[8];
+#pragma unroll
+    for (int sk = 0; sk < 8; ++sk) {
+      const int prc = min(4 * sk + fg, 29);  // pairs 30,31: zero weights in the B image
+      a[sk] = R2[(prc / 5 * 14 + y + prc % 5) * 13 + x];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int pr = 4 * s + fg;
-      bf16x8 a, bw;
-      if (pr < 30) {
-        const int c = pr / 5, ky = pr % 5;
-        a = R2[(c * 14 + y + ky) * 13 + x];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bw[j] = j < 5 ? W2S[fr * 150 + pr * 5 + j] : (bf16)0.f;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { a[j] = (bf16)0.f; bw[j] = (bf16)0.f; }
-      }
-      acc = mfma32(a, bw, acc);
-    }
+    for (int sk = 0; sk < 8; ++sk) acc = mfma32(a[sk], bw2[sk], acc);
     const int qo = 4 * t + fg;
     if (qo < 25) {
-      const float bias = bc2;
-      float best = acc[0] + bias;
+      float best = acc[0] + bias_c2;
       int arg = 0;
 #pragma unroll
       for (int i = 1; i < 4; ++i) {
-        const float v = acc[i] + bias;
+        const float v = acc[i] + bias_c2;
         if (v > best) { best = v; arg = i; }
       }
-      A0[fr * 25 + qo] = fmaxf(best, 0.f);  // torch.flatten order [16][5][5]
+      const float r = fmaxf(best, 0.f);
+      A0[fr * 25 + qo] = r;  // torch.flatten order [16][5][5]
+      A0B[fr * 25 + qo] = (bf16)r;
       CODE2[fr * 25 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // fc1 LDS-DMA (and MLP prefetch) landed
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // fc1 LDS-DMA and the MLP fragments landed
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) consume(w2f[ks]);
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) { consume(w2t[ks]); consume(w3f[ks]); }
+  consume(w3t);
+  consume(bias_f1);
+  consume(bias_f2);
+  consume(bias_f3);
+  lds_barrier();
 
   STAMP(3);
   // ============ phase D: MLP forward, cross-entropy, MLP data-backward ==================
-  {  // fc1: 120 x 400, 4 lanes per output
-    const int o = tid >> 2, p = tid & 3;
-    float acc = 0.f;
-    if (o < 120) {
-      const bf16x8* wrow = reinterpret_cast<const bf16x8*>(fc1s + o * 400);
-      for (int c8 = p; c8 < 50; c8 += 4) {
-        const bf16x8 w = wrow[c8];
-        const float4 xa = reinterpret_cast<const float4*>(A0)[2 * c8];
-        const float4 xb = reinterpret_cast<const float4*>(A0)[2 * c8 + 1];
-        acc += (float)w[0] * xa.x + (float)w[1] * xa.y + (float)w[2] * xa.z + (float)w[3] * xa.w +
-               (float)w[4] * xb.x + (float)w[5] * xb.y + (float)w[6] * xb.z + (float)w[7] * xb.w;
-      }
+  if (TRAIN) {
+    // flipped conv2 kernel (20,480 B) for phase E: LDS-DMA into REGB behind R2 (W2 images
+    // and R1 are dead), in flight during the whole MLP
+    const uint4* src = reinterpret_cast<const uint4*>(shadow + SH_WF);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGB + B_WF));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = min(wave + 8 * k, 19);
+      dma16(src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (o < 120 && p == 0) H1[o] = fmaxf(acc + bias_f1, 0.f);
   }
-  __syncthreads();
-  {  // fc2: 84 x 120 (prefetched fragments)
-    float acc = 0.f;
-    if (mo < 84) {
+  {  // fc1: h1 = relu(W1 a0 + b1), 120 x 400; wave w -> output tile w
+    const bf16* wrow = fc1s + min(ncol, 119) * 400;
+    bf16x8 av[13], bv[13];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c8 = mp + 4 * k;
-        if (c8 < 15) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc += (float)w2f[k][j] * H1[c8 * 8 + j];
-        }
-      }
+    for (int ks = 0; ks < 13; ++ks) {
+      bv[ks] = *reinterpret_cast<const bf16x8*>(wrow + 32 * ks + 8 * fg);
+      av[ks] = row0(A0B, 32 * ks + 8 * fg, fr);
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (mo < 84 && mp == 0) H2[mo] = fmaxf(acc + bias_f2, 0.f);
-  }
-  __syncthreads();
-  {  // fc3: 10 x 84 (prefetched fragments)
-    float acc = 0.f;
-    if (mo < 10) {
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int c4 = mp + 4 * k;
-        if (c4 < 21) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc += (float)w3f[k][j] * H2[c4 * 4 + j];
-        }
-      }
+    for (int ks = 0; ks < 13; ++ks) acc = mfma32(av[ks], bv[ks], acc);
+    if (fg == 0 && ncol < 120) {
+      const float h = fmaxf(acc[0] + bias_f1, 0.f);
+      H1[ncol] = h;
+      H1B[ncol] = (bf16)h;
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (mo < 10 && mp == 0) LOG[mo] = acc + bias_f3;
   }
-  __syncthreads();
-  if (tid == 0) {  // CrossEntropy (mean over the valid batch) + accuracy
-    float mx = LOG[0];
-    int pred = 0;
+  lds_barrier();
+  if (wave < 6) {  // fc2: 84 x 120
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int o = 1; o < 10; ++o) if (LOG[o] > mx) { mx = LOG[o]; pred = o; }
-    float e[10], sum = 0.f;
+    for (int ks = 0; ks < 4; ++ks) acc = mfma32(row0(H1B, 32 * ks + 8 * fg, fr), w2f[ks], acc);
+    if (fg == 0 && ncol < 84) {
+      const float h = fmaxf(acc[0] + bias_f2, 0.f);
+      H2[ncol] = h;
+      H2B[ncol] = (bf16)h;
+    }
+  }
+  lds_barrier();
+  if (wave == 0) {  // fc3 (10 x 84) + CrossEntropy (mean over the valid batch) + accuracy
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int o = 0; o < 10; ++o) { e[o] = expf(LOG[o] - mx); sum += e[o]; }
+    for (int ks = 0; ks < 3; ++ks) acc = mfma32(row0(H2B, 32 * ks + 8 * fg, fr), w3f[ks], acc);
+    // row 0 of the tile lives in lanes 0..15 (fg == 0): lane o holds logit o
+    const bool act = lane < 10;
+    const float lg = act ? acc[0] + bias_f3 : -INFINITY;
+    float mx = lg;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 16));
+    const float e = act ? expf(lg - mx) : 0.f;
+    float sum = e;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
+    int pred = (act && lg == mx) ? lane : 64;  // first max wins (torch.argmax)
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) pred = min(pred, __shfl_xor(pred, off, 16));
     const float lse = mx + logf(sum);
-    loss_out[b] = lse - LOG[label];
-    correct_out[b] = pred == label ? 1 : 0;
-    if (TRAIN) {
-      const float inv = 1.0f / (float)bvalid;
-      const float rs = 1.0f / sum;
-#pragma unroll
-      for (int o = 0; o < 16; ++o) DZ3[o] = o < 10 ? (e[o] * rs - (o == label ? 1.f : 0.f)) * inv : 0.f;
+    const float ll = __shfl(lg, label & 15, 16);
+    if (lane == 0) {
+      loss_out[b] = lse - ll;
+      correct_out[b] = pred == label ? 1 : 0;
+    }
+    if (TRAIN && lane < 32) {
+      const float dz = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
+      DZ3B[lane] = (bf16)dz;
+      if (lane < 16) DZ3[lane] = dz;
     }
   }
   if (!TRAIN) return;
-  __syncthreads();
+  lds_barrier();
   STAMP(4);
-  if (tid < 84) {  // fc3 dgrad + ReLU mask (prefetched column)
-    float acc = 0.f;
-#pragma unroll
-    for (int o = 0; o < 10; ++o) acc += DZ3[o] * (float)w3d[o];
-    DZ2[tid] = H2[tid] > 0.f ? acc : 0.f;
-  }
-  __syncthreads();
-  {  // fc2 dgrad + ReLU mask: 4 lanes per input, 21 prefetched rows each
-    float acc = 0.f;
-    if (mo < 120) {
-#pragma unroll
-      for (int k = 0; k < 21; ++k) acc += DZ2[mp * 21 + k] * (float)w2d[k];
+  if (wave < 6) {  // fc3 dgrad: dh2 = W3^T dz3 (84 x 10), ReLU mask
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma32(row0(DZ3B, 8 * fg, fr), w3t, acc);
+    if (fg == 0 && ncol < 84) {
+      const float d = H2[ncol] > 0.f ? acc[0] : 0.f;
+      DZ2[ncol] = d;
+      DZ2B[ncol] = (bf16)d;
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (mo < 120 && mp == 0) DZ1[mo] = H1[mo] > 0.f ? acc : 0.f;
   }
-  __syncthreads();
-  if (tid < 400) {  // fc1 dgrad (mask applied through CODE2 below)
-    float acc = 0.f;
-#pragma unroll 8
-    for (int o = 0; o < 120; ++o) acc += DZ1[o] * (float)fc1s[o * 400 + tid];
-    DA0[tid] = acc;
+  lds_barrier();
+  {  // fc2 dgrad: dh1 = W2^T dz2 (120 x 84), ReLU mask
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) acc = mfma32(row0(DZ2B, 32 * ks + 8 * fg, fr), w2t[ks], acc);
+    if (fg == 0 && ncol < 120) {
+      const float d = H1[ncol] > 0.f ? acc[0] : 0.f;
+      DZ1[ncol] = d;
+      DZ1B[ncol] = (bf16)d;
+    }
+  }
+  lds_barrier();
+  // fc1 dgrad: dA0 = W1^T dz1 (400 x 120), B fragments by transposed LDS reads of fc1
+  for (int nt = wave; nt < 25; nt += 8) {
+    bf16x8 av[4], bv[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bv[ks] = tr_frag(fc1s, 400, 32 * ks, 16 * nt, 120, lane);
+      av[ks] = row0(DZ1B, 32 * ks + 8 * fg, fr);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) acc = mfma32(av[ks], bv[ks], acc);
+    if (fg == 0) DA0[16 * nt + fr] = acc[0];  // (the pool2/ReLU mask is applied via CODE2)
   }
   // per-sample rows for the batch-reduced fc weight gradients
   for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
   if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
   if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
   if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
-  __syncthreads();
+  lds_barrier();
 
   STAMP(5);
   // ============ phase E: conv2 backward =================================================
+  // dY2 = unpool(dA0) masked by ReLU is materialised by rows, branch-free, twice:
+  //  * DY2 [16][10][16]: A operand of the conv2 weight gradient (8 pixels per lane),
+  //  * R3  [16][18][14] window records of dY2 zero-padded by 4 in y and x: A operand of
+  //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
+  //    flipped kernel WF - no col2im scratch, no gather pass.
   float* slab = slab_out + (size_t)b * SLAB;
-  bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);     // [16][10][16]
-  bf16* DY2T = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2T);   // [112][16]
-  float* DCOLS = reinterpret_cast<float*>(smem + L_REGA + A_DCOLS);
+  bf16x8* R3 = reinterpret_cast<bf16x8*>(smem + L_REGA + A_R3);
+  bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
-  // unpool + ReLU mask -> dY2 (two layouts); wave w owns channels w and w+8 and
-  // reduces their bias gradient with shuffles (fixed order: deterministic)
-  for (int o = wave; o < 16; o += 8) {
-    float bsum = 0.f;
-    for (int r = lane; r < 160; r += 64) {
-      const int y = r >> 4, x = r & 15;
-      float v = 0.f;
-      if (x < 10) {
-        const int q = (y >> 1) * 5 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
-        if (CODE2[o * 25 + q] == i) v = DA0[o * 25 + q];
-        DY2T[(y * 10 + x) * 16 + o] = (bf16)v;
-      }
-      DY2[o * 160 + r] = (bf16)v;
-      bsum += v;
+  float* RS = reinterpret_cast<float*>(smem + L_REGA + A_RS);
+  for (int t = tid; t < 288; t += NT) {
+    const int o = t / 18, yy = t - 18 * (t / 18), y = yy - 4;
+    const bool yv = y >= 0 && y < 10;
+    const int yc = yv ? y : 0, yb = (yc & 1) << 1;
+    int cd[5];
+    float da[5];
+#pragma unroll
+    for (int px = 0; px < 5; ++px) {
+      const int q = o * 25 + (yc >> 1) * 5 + px;
+      cd[px] = CODE2[q];
+      da[px] = DA0[q];
+    }
+    float v[22];  // v[cc] = dY2[o][y][cc - 4]
+    float rs = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 22; ++cc) {
+      const int x = cc - 4;
+      float tv = 0.f;
+      if (x >= 0 && x < 10) tv = (yv && cd[x >> 1] == (yb | (x & 1))) ? da[x >> 1] : 0.f;
+      v[cc] = tv;
+      rs += tv;
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_xor(bsum, off);
-    if (lane == 0) slab[SLAB_C2B + o] = bsum;
+    for (int xr = 0; xr < 14; ++xr) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[xr + j];
+      R3[(o * 18 + yy) * 14 + xr] = r;
+    }
+    if (yv) {
+      bf16x8 r0, r1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        r0[j] = (bf16)v[4 + j];
+        r1[j] = (bf16)(j < 2 ? v[12 + j] : 0.f);
+      }
+      bf16x8* drow = reinterpret_cast<bf16x8*>(DY2 + (o * 10 + y) * 16);
+      drow[0] = r0;
+      drow[1] = r1;
+    }
+    RS[o * 18 + yy] = rs;
   }
-  for (int e = tid; e < 12 * 16; e += NT) DY2T[100 * 16 + e] = (bf16)0.f;
-  __syncthreads();
-  // conv2 wgrad: dW2[o][(c,ky,kx)] = sum_pix dY2[o][pix] * P1[c][y+ky][x+kx]
-  for (int nt = wave; nt < 10; nt += 8) {
-    const int n = nt * 16 + fr;
-    const int c = n / 25, ky = (n % 25) / 5, kx = n % 5;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (LDS-DMA, issued in phase D) landed
+  lds_barrier();
+  STAMP(8);
+  if (wave == 7) {  // conv2 bias gradient: 4 lanes per channel over its 18 row sums
+    const int o = lane >> 2, part = lane & 3;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t += (part + 4 * k < 18) ? RS[o * 18 + min(part + 4 * k, 17)] : 0.f;
+    t += __shfl_xor(t, 1);
+    t += __shfl_xor(t, 2);
+    if (part == 0) slab[SLAB_C2B + o] = t;
+  }
+  // conv2 data gradient: 13 pixel tiles x 20 K-steps (waves 0-7 take tiles w, w+8)
+  for (int mt = wave; mt < 13; mt += 8) {
+    const int m = min(mt * 16 + fr, 195);
+    const int y = m / 14, x = m - 14 * (m / 14);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const int y = 2 * s + (fg >> 1), x0 = 8 * (fg & 1);
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(DY2 + (fr * 10 + y) * 16 + x0);
-      bf16x8 bb;
+    for (int h = 0; h < 2; ++h) {  // 10 K-steps per batch: 20 operand loads in flight
+      bf16x8 av[10], bv[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const int p = 4 * (10 * h + k) + fg, o = p / 5, kyp = p - 5 * (p / 5);
+        av[k] = R3[(o * 18 + y + kyp) * 14 + x];
+        bv[k] = WF[p * 16 + fr];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) acc = mfma32(av[k], bv[k], acc);
+    }
+    if (fr < 6) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pix = mt * 16 + 4 * fg + i;
+        if (pix < 196) DP1[fr * 196 + pix] = acc[i];
+      }
+    }
+  }
+  // conv2 weight gradient: dW2[o][(c,ky,kx)] = sum_pix dY2[o][pix] * P1[c][y+ky][x+kx]
+  // (waves 5-7, which hold one data-gradient tile each)
+  if (wave >= 5) {
+    const int nt0 = wave == 5 ? 0 : (wave == 6 ? 4 : 7), nt1 = wave == 5 ? 4 : (wave == 6 ? 7 : 10);
+    for (int nt = nt0; nt < nt1; ++nt) {
+      const int n = nt * 16 + fr, nc = min(n, 149);
+      const int c = nc / 25, ky = (nc % 25) / 5, kx = nc % 5;
+      bf16x8 av[5], bv[5];
+#pragma unroll
+      for (int sk = 0; sk < 5; ++sk) {
+        const int y = 2 * sk + (fg >> 1), x0 = 8 * (fg & 1);
+        av[sk] = *reinterpret_cast<const bf16x8*>(DY2 + (fr * 10 + y) * 16 + x0);
+        bv[sk] = R2[(c * 14 + y + ky) * 13 + x0 + kx];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sk = 0; sk < 5; ++sk) acc = mfma32(av[sk], bv[sk], acc);
       if (n < 150) {
-        bb = R2[(c * 14 + y + ky) * 13 + x0 + kx];
-      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bb[j] = (bf16)0.f;
-      }
-      acc = mfma32(a, bb, acc);
-    }
-    if (n < 150) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) slab[SLAB_C2W + (4 * fg + i) * 150 + n] = acc[i];
-    }
-  }
-  // conv2 dgrad, col2im form: dCols[pix][(c,ky,kx)] = sum_o dY2[pix][o] * W2[o][(c,ky,kx)]
-  for (int p = wave; p < 70; p += 8) {
-    const int mt = p / 10, nt = p % 10;
-    const s16x4 a = *reinterpret_cast<const s16x4*>(DY2T + (mt * 16 + fr) * 16 + 4 * fg);
-    const int n = nt * 16 + fr;
-    s16x4 bb;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bb[j] = n < 150 ? __builtin_bit_cast(short, W2S[(4 * fg + j) * 150 + n]) : (short)0;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bb, acc, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) DCOLS[(mt * 16 + 4 * fg + i) * DCOLS_LD + n] = acc[i];
-  }
-  __syncthreads();
-  for (int e = tid; e < 6 * 196; e += NT) {  // deterministic col2im gather
-    const int c = e / 196, r = e % 196, y = r / 14, x = r % 14;
-    float s = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 5; ++ky) {
-      const int y2 = y - ky;
-      if (y2 < 0 || y2 >= 10) continue;
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx) {
-        const int x2 = x - kx;
-        if (x2 < 0 || x2 >= 10) continue;
-        s += DCOLS[(y2 * 10 + x2) * DCOLS_LD + c * 25 + ky * 5 + kx];
+        for (int i = 0; i < 4; ++i) slab[SLAB_C2W + (4 * fg + i) * 150 + n] = acc[i];
       }
     }
-    DP1[e] = s;
   }
-  __syncthreads();
+  lds_barrier();
 
   STAMP(6);
   // ============ phase F: conv1 weight gradient ==========================================
-  bf16* DY1 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY1);  // [6][28][32]
-  if (wave < 6) {  // wave c: unpool + ReLU mask -> dY1[c], and the conv1 bias gradient
-    const int c = wave;
-    float bsum = 0.f;
-#pragma unroll 2
-    for (int r = lane; r < 896; r += 64) {
-      const int y = r >> 5, x = r & 31;
-      float v = 0.f;
-      if (x < 28) {
-        const int q = (y >> 1) * 14 + (x >> 1), i = ((y & 1) << 1) | (x & 1);
-        if (CODE1[c * 196 + q] == i) v = DP1[c * 196 + q];
-      }
-      DY1[c * 896 + r] = (bf16)v;
-      bsum += v;
+  unsigned char* DY1 = smem + L_REGA + A_DY1;  // bf16 [6] x [28][32] (channel stride DY1_CH bytes)
+  float* RS1 = reinterpret_cast<float*>(smem + L_REGA + A_RS1);
+  if (tid < 168) {  // one dY1 row per thread: unpool dP1 by CODE1, ReLU-masked
+    const int c = tid / 28, y = tid - 28 * (tid / 28), yb = (y & 1) << 1;
+    int cd[14];
+    float dv[14];
+#pragma unroll
+    for (int px = 0; px < 14; ++px) {
+      const int q = c * 196 + (y >> 1) * 14 + px;
+      cd[px] = CODE1[q];
+      dv[px] = DP1[q];
     }
+    float rs = 0.f;
+    bf16x8* drow = reinterpret_cast<bf16x8*>(DY1 + c * DY1_CH + y * 64);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_xor(bsum, off);
-    if (lane == 0) slab[SLAB_C1B + c] = bsum;
-  } else if (tid - 384 < 96) {
-    build_r1_row(IMGS, R1, tid - 384);  // R2 is dead: rebuild R1
+    for (int g8 = 0; g8 < 4; ++g8) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int x = 8 * g8 + j;
+        float tv = 0.f;
+        if (x < 28) tv = cd[x >> 1] == (yb | (x & 1)) ? dv[x >> 1] : 0.f;
+        rs += tv;
+        r[j] = (bf16)tv;
+      }
+      drow[g8] = r;
+    }
+    RS1[c * 28 + y] = rs;
+  } else {
+    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, R1, t >> 2, t & 3);  // R2 dead
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(10);
+  if (wave == 7) {  // conv1 bias gradient: 8 lanes per channel over its 28 row sums
+    const int c = min(lane >> 3, 5), part = lane & 7;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t += (part + 8 * k < 28) ? RS1[c * 28 + min(part + 8 * k, 27)] : 0.f;
+    t += __shfl_xor(t, 1);
+    t += __shfl_xor(t, 2);
+    t += __shfl_xor(t, 4);
+    if (part == 0 && lane < 48) slab[SLAB_C1B + c] = t;
+  }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
-    const int nt = wave;
-    const int n = nt * 16 + fr;
-    const int c = n / 25, ky = (n % 25) / 5, kx = n % 5;
+    const int n = wave * 16 + fr, nc = min(n, 74);
+    const int c = nc / 25, ky = (nc % 25) / 5, kx = nc % 5;
+    // rows o >= 6 of A read past dY1 into other (finite) LDS data: they only feed
+    // accumulator rows that are discarded, so the loads stay branch-free
+    const unsigned char* arow = DY1 + fr * DY1_CH + fg * 16;
+    const bf16x8* brow = R1 + (c * 32 + ky) * 29 + 8 * fg + kx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < 28; ++s) {  // one K-step = one 32-pixel output row
-      bf16x8 a, bb;
-      if (fr < 6) {
-        a = *reinterpret_cast<const bf16x8*>(DY1 + (fr * 28 + s) * 32 + 8 * fg);
-      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = (bf16)0.f;
-      }
-      if (n < 75) {
-        bb = R1[(c * 32 + s + ky) * 29 + 8 * fg + kx];
-      } else {
+    for (int g = 0; g < 4; ++g) {  // one K-step = one 32-pixel output row; 7 per batch
+      bf16x8 av[7], bv[7];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bb[j] = (bf16)0.f;
+      for (int k = 0; k < 7; ++k) {
+        av[k] = *reinterpret_cast<const bf16x8*>(arow + (7 * g + k) * 64);
+        bv[k] = brow[(7 * g + k) * 29];
       }
-      acc = mfma32(a, bb, acc);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) acc = mfma32(av[k], bv[k], acc);
     }
     if (n < 75) {
 #pragma unroll

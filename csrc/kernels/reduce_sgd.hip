@@ -27,7 +27,7 @@ __device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs a) {
     const float p = a.master[e] - a.lr * m;
     a.mom[e] = m;
     a.master[e] = p;
-    a.shadow[e] = (bf16)p;
+    write_shadow(a.shadow, e, p);
   } else {
     a.grad[e] = g;
   }
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(RT) sgd_apply_kernel(float* __restrict__ maste
       mom[e] = m;
       master[e] = p;
     }
-    shadow[e] = (bf16)p;
+    write_shadow(shadow, e, p);
   }
 }
 

@@ -100,9 +100,10 @@ def per_sample_outputs_bf16(shadow: torch.Tensor, master: torch.Tensor, images_u
                             labels: torch.Tensor, bvalid: int | None = None) -> Dict[str, torch.Tensor]:
     """The fused kernel's math with bf16 rounding at exactly the kernel's rounding points.
 
-    Weights come from the bf16 shadow, biases from the fp32 master; the image, the
-    pooled conv1 output (conv2 input), dY2 and dY1 are rounded to bf16 because they
-    are MFMA operands; everything else (accumulators, MLP, loss, bias grads) is fp32.
+    Weights come from the bf16 shadow, biases from the fp32 master; every MFMA
+    operand is rounded to bf16 (the image, the pooled conv1 output, the MLP inputs
+    a0/h1/h2 and deltas dz3/dz2/dz1, dY2 and dY1); accumulators, losses and bias
+    gradients are fp32.
     A correct kernel matches this to accumulation-order noise.
     """
     w = LAYOUT.views(shadow.detach().float().cpu())
@@ -118,15 +119,16 @@ def per_sample_outputs_bf16(shadow: torch.Tensor, master: torch.Tensor, images_u
     c2 = F.conv2d(p1b, W2, bm["conv2.bias"])
     p2, i2 = F.max_pool2d_with_indices(F.relu(c2), 2, 2)
     a0 = p2.flatten(1)
-    h1 = F.relu(F.linear(a0, w["fc1.weight"], bm["fc1.bias"]))
-    h2 = F.relu(F.linear(h1, w["fc2.weight"], bm["fc2.bias"]))
-    logits = F.linear(h2, w["fc3.weight"], bm["fc3.bias"])
+    # MLP: activations / deltas are bf16 MFMA operands, accumulation fp32
+    h1 = F.relu(F.linear(_bf(a0), w["fc1.weight"], bm["fc1.bias"]))
+    h2 = F.relu(F.linear(_bf(h1), w["fc2.weight"], bm["fc2.bias"]))
+    logits = F.linear(_bf(h2), w["fc3.weight"], bm["fc3.bias"])
     loss = F.cross_entropy(logits, y, reduction="none")
     correct = (logits.argmax(1) == y).int()
     z3 = (torch.softmax(logits, 1) - F.one_hot(y, 10).float()) / bvalid
-    z2 = (z3 @ w["fc3.weight"]) * (h2 > 0).float()
-    z1 = (z2 @ w["fc2.weight"]) * (h1 > 0).float()
-    da0 = z1 @ w["fc1.weight"]
+    z2 = (_bf(z3) @ w["fc3.weight"]) * (h2 > 0).float()
+    z1 = (_bf(z2) @ w["fc2.weight"]) * (h1 > 0).float()
+    da0 = _bf(z1) @ w["fc1.weight"]
     dp2 = da0.view(B, 16, 5, 5) * (p2 > 0).float()
     dy2 = F.max_unpool2d(dp2, i2, 2, 2, output_size=c2.shape[-2:])
     db2 = dy2.sum((2, 3))

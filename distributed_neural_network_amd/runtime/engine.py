@@ -194,7 +194,8 @@ class HipEngine(Engine):
         self.master = self._init_arena.to(**f32).contiguous()
         self.grad = torch.zeros(LAYOUT.total, **f32)
         self.mom = torch.zeros(LAYOUT.total, **f32)
-        self.shadow = torch.zeros(LAYOUT.total, device=dev, dtype=torch.bfloat16)
+        # bf16 [plain arena copy | kernel-ready weight images] (csrc/kernels/common.h SH_*)
+        self.shadow = torch.zeros(self.ext.layout()["shadow_total"], device=dev, dtype=torch.bfloat16)
         self.state = torch.zeros(4, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(4, device=dev, dtype=torch.float64)
         self.a0 = torch.zeros(B, 400, **f32)

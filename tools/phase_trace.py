@@ -16,7 +16,9 @@ from distributed_neural_network_amd.data import synthetic  # noqa: E402
 from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
 
 PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' MLP bwd",
-          "E conv2 bwd", "F conv1 wgrad"]
+          "E conv2 bwd", "F conv1 wgrad",
+          "  C1 prefetch+R2 build", "  E1 dY2 build", "  E2 wgrad2+col2im", "  E3 dP1 gather",
+          "  F1 dY1 + R1 rebuild"]
 
 
 def main(reps: int = 50, batch: int = 64):
@@ -40,11 +42,12 @@ def main(reps: int = 50, batch: int = 64):
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
         s = stamps.cpu().numpy()
-        rows.append(np.diff(s[:8]) * 0.01)  # 100 MHz ticks -> us
+        rows.append(np.concatenate([np.diff(s[:8]), [s[11] - s[2], s[8] - s[5], s[9] - s[8], s[6] - s[9],
+                                                      s[10] - s[6]]]) * 0.01)  # 100 MHz ticks -> us
     med = np.median(np.array(rows[5:]), axis=0)
     for name, v in zip(PHASES, med):
         print(f"{name:20s} {v:8.2f} us")
-    print(f"{'sum (block 0)':20s} {med.sum():8.2f} us")
+    print(f"{'sum (block 0)':20s} {med[:7].sum():8.2f} us")
     print(f"{'kernel wall (event)':20s} {np.median(walls[5:]):8.2f} us")
 
 
