@@ -64,12 +64,13 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("grad_reduce", [](u a0, u h1, u h2, u z1, u z2, u z3, u slab, u loss, u correct, int batch, u master,
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
-                          int fuse_sgd, int lo, int hi, int bookkeeping, u stream) {
+                          int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
+                          u stream) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
-                      P<bf16>(shadow), P<int32_t>(state), P<double>(stats), lr, momentum, grad_scale, fuse_sgd,
-                      lo, hi, bookkeeping};
+                      P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order), order_len,
+                      P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping};
     dnn::launch_grad_reduce(a, S(stream));
   });
   m.def("init", []() { dnn::init_kernels(); });

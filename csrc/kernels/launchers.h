@@ -19,6 +19,7 @@ struct ReduceArgs {
   int batch;
   float* master; float* grad; float* mom; bf16* shadow;
   int32_t* state; double* stats;
+  const int32_t* order; int order_len; int32_t* batch_ids;  // epoch order -> next step's sample ids
   float lr, momentum, grad_scale;
   int fuse_sgd;   // 1: apply SGD in place (local step); 0: write grads only
   int lo, hi;     // arena element range [lo, hi) handled by this launch (gradient bucket)

@@ -64,8 +64,9 @@ constexpr int L_DZ1 = L_DZ2B + 192;         // f32 [128]
 constexpr int L_DZ1B = L_DZ1 + 512;         // bf16 [128]
 constexpr int L_DA0 = L_DZ1B + 256;         // f32 [400]
 constexpr int L_IMG = L_DA0 + 1600;         // u8 [3][32][32] raw image (re-used by phase F)
-constexpr int L_MISC = L_IMG + 3072;
-constexpr int LDS_TOTAL = L_MISC + 64;      // 159,152 B
+constexpr int L_LUT = L_IMG + 3072;         // bf16 [256] normalised value of each u8 code
+constexpr int L_MISC = L_LUT + 512;
+constexpr int LDS_TOTAL = L_MISC + 64;      // 159,664 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
@@ -153,24 +154,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* m, int ld, int k0, int n0,
 }
 
 // Build window records x = 8q .. 8q+7 (x < 29) of input row (c, y) = `row` from the u8
-// image staged in LDS; 4 threads per row (q = 0..3).
-__device__ __forceinline__ void build_r1_part(const uint8_t* img, bf16x8* R1, int row, int q) {
+// image staged in LDS, normalising through the per-block bf16 LUT; 4 threads per row.
+__device__ __forceinline__ void build_r1_part(const uint8_t* img, const bf16* lut, bf16x8* R1, int row, int q) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(img + row * 32);
   uint32_t w[4];  // elements 8q .. 8q+15 (zero past the row end)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) w[k] = (2 * q + k < 8) ? src[2 * q + k] : 0u;
-  float v[16];
+  for (int k = 0; k < 4; ++k) w[k] = src[min(2 * q + k, 7)];
+  bf16 v[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const uint32_t u = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    v[k] = (8 * q + k < 32) ? u8norm(u) : 0.f;
+    const bf16 t = lut[u];
+    v[k] = (8 * q + k < 32) ? t : (bf16)0.f;
   }
 #pragma unroll
   for (int x = 0; x < 8; ++x) {
     if (8 * q + x < 29) {
       bf16x8 r;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
+      for (int j = 0; j < 8; ++j) r[j] = v[x + j];
       R1[row * 29 + 8 * q + x] = r;
     }
   }
@@ -201,18 +203,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int fg = lane >> 4;   // MFMA k-group (0..3)
   const int b = blockIdx.x;
 
-  long gidx;
-  int bvalid = 1;
+  // TRAIN: the sample ids and valid count of this step were published by the previous
+  // step's reduce kernel (begin_epoch for the first step): one dependent load level less
+  // than cursor -> order -> sample.
+  int bvalid = 1, sample = 0;
+  bool valid;
   if (TRAIN) {
-    const int cursor = state[ST_CURSOR];
-    gidx = (long)cursor * batch + b;
-    long rem = (long)order_len - (long)cursor * batch;
-    bvalid = rem < batch ? (rem > 0 ? (int)rem : 0) : batch;
-    if (b == 0 && tid == 0) state[ST_BVALID] = bvalid;
+    bvalid = state[ST_BVALID];
+    sample = order[b];  // `order` = the published batch ids [batch]
+    valid = b < bvalid;
   } else {
-    gidx = (long)base_index + b;
+    const long gidx = (long)base_index + b;
+    valid = gidx < order_len;
+    sample = (int)gidx;
   }
-  const bool valid = gidx < order_len;
   if (!valid) {
     if (TRAIN) {
       for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
@@ -224,7 +228,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     return;
   }
-  const int sample = order ? order[gidx] : (int)gidx;
   const int label = labels[sample];
   const uint8_t* img = images + (size_t)sample * IMG;
 
@@ -250,6 +253,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   bf16* DZ1B = reinterpret_cast<bf16*>(smem + L_DZ1B);
   float* DA0 = reinterpret_cast<float*>(smem + L_DA0);
   uint8_t* IMGS = smem + L_IMG;
+  bf16* LUT = reinterpret_cast<bf16*>(smem + L_LUT);
 
   // ============ phase A: ingest + weight staging ======================================
   // Plain loads first (image, conv B fragments, conv biases), consumed before the fc1
@@ -270,6 +274,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
   else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  if (tid < 256) LUT[tid] = (bf16)u8norm((uint32_t)tid);  // exact ToTensor+Normalize, once per block
 #pragma unroll
   for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
 #pragma unroll
@@ -288,7 +293,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   lds_barrier();
-  if (tid < 384) build_r1_part(IMGS, R1, tid >> 2, tid & 3);
+  if (tid < 384) build_r1_part(IMGS, LUT, R1, tid >> 2, tid & 3);
   lds_barrier();
   STAMP(1);
 
@@ -687,7 +692,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     RS1[c * 28 + y] = rs;
   } else {
-    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, R1, t >> 2, t & 3);  // R2 dead
+    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, LUT, R1, t >> 2, t & 3);  // R2 dead
   }
   lds_barrier();
   STAMP(10);

@@ -20,11 +20,13 @@ constexpr int RT = 256;
 
 
 
-__device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs a) {
+// SGD epilogue with the master/momentum values already in registers (prefetched
+// together with the gradient operands, so the update costs no extra memory latency).
+__device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs a) {
   g *= a.grad_scale;
   if (a.fuse_sgd) {
-    const float m = a.momentum * a.mom[e] + g;
-    const float p = a.master[e] - a.lr * m;
+    const float m = a.momentum * m_old + g;
+    const float p = p_old - a.lr * m;
     a.mom[e] = m;
     a.master[e] = p;
     write_shadow(a.shadow, e, p);
@@ -35,37 +37,45 @@ __device__ __forceinline__ void sgd_update(int e, float g, const ReduceArgs a) {
 
 // fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
 // output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).
-struct FcLayer { int O, I, IT, tiles, arena_off, zld, xld, which; };
-__constant__ FcLayer kFc[3] = {
-    {120, 400, 25, 8 * 25, OFF_F1W, Z1_LD, A0_LD, 0},
-    {84, 120, 8, 6 * 8, OFF_F2W, Z2_LD, H1_LD, 1},
-    {10, 84, 6, 1 * 6, OFF_F3W, Z3_LD, H2_LD, 2},
-};
-constexpr int FC_TILES = 200 + 48 + 6;        // 254 wave-tiles
+template <int LAYER> struct Fc;
+template <> struct Fc<0> { static constexpr int O = 120, I = 400, IT = 25, OFF = OFF_F1W, ZLD = Z1_LD, XLD = A0_LD; };
+template <> struct Fc<1> { static constexpr int O = 84, I = 120, IT = 8, OFF = OFF_F2W, ZLD = Z2_LD, XLD = H1_LD; };
+template <> struct Fc<2> { static constexpr int O = 10, I = 84, IT = 6, OFF = OFF_F3W, ZLD = Z3_LD, XLD = H2_LD; };
+constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
+constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
 constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
 
+template <int LAYER>
 __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
-  int l = 0;
-  while (l < 2 && t >= kFc[l].tiles) { t -= kFc[l].tiles; ++l; }
-  const FcLayer L = kFc[l];
-  const float* z = L.which == 0 ? a.z1 : (L.which == 1 ? a.z2 : a.z3);
-  const float* x = L.which == 0 ? a.a0 : (L.which == 1 ? a.h1 : a.h2);
+  using L = Fc<LAYER>;
+  const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
+  const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, kq = lane >> 4;
-  const int o0 = (t / L.IT) * 16, i0 = (t % L.IT) * 16;
+  const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
   const int om = o0 + col, in = i0 + col;
-  const bool ov = om < L.O, iv = in < L.I;
+  const bool ov = om < L::O, iv = in < L::I;
+  // this lane's 4 output elements: rows o0 + 4kq + j, column in
+  int e[4];
+  float pv[4], mv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = min(o0 + 4 * kq + j, L::O - 1);
+    e[j] = L::OFF + o * L::I + (iv ? in : 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { pv[j] = a.master[e[j]]; mv[j] = a.mom[e[j]]; }  // (unused if !fuse_sgd)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int omc = ov ? om : 0, inc = iv ? in : 0;
   for (int b0 = 0; b0 < a.batch; b0 += 64) {
-    float av[16], bv[16];
     // every operand load is unconditional (clamped address) and issued before the first
     // MFMA; out-of-range operands are zeroed by a select afterwards
-    const int omc = ov ? om : 0, inc = iv ? in : 0;
+    float av[16], bv[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int b = min(b0 + 4 * s + kq, a.batch - 1);
-      av[s] = z[(size_t)b * L.zld + omc];
-      bv[s] = x[(size_t)b * L.xld + inc];
+      av[s] = z[(size_t)b * L::ZLD + omc];
+      bv[s] = x[(size_t)b * L::XLD + inc];
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -79,11 +89,12 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + 4 * kq + j;
-    if (o < L.O && iv) sgd_update(L.arena_off + o * L.I + in, acc[j], a);
+    if (o < L::O && iv) sgd_finish(e[j], acc[j], pv[j], mv[j], a);
   }
 }
 
-// element tasks: fc biases (sum_b z[b][o]) and conv slab columns (sum_b slab[b][j])
+// element tasks: fc biases (sum_b z[b][o]) and conv slab columns (sum_b slab[b][j]);
+// all 64 rows of a chunk are loaded before the (fixed-order) sum
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int CONV_ELEMS = SLAB;
 __device__ __forceinline__ void elem_task(int e, bool mlp_part, const ReduceArgs a) {
@@ -102,18 +113,19 @@ __device__ __forceinline__ void elem_task(int e, bool mlp_part, const ReduceArgs
     else if (e < SLAB_C2B) dst = OFF_C2W + (e - SLAB_C2W);
     else dst = OFF_C2B + (e - SLAB_C2B);
   }
+  const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
   float g = 0.f;
-  for (int b0 = 0; b0 < a.batch; b0 += 16) {
-    float v[16];
+  for (int b0 = 0; b0 < a.batch; b0 += 64) {
+    float v[64];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = src[(size_t)min(b0 + k, a.batch - 1) * ld + col];
+    for (int k = 0; k < 64; ++k) v[k] = src[(size_t)min(b0 + k, a.batch - 1) * ld + col];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) g += (b0 + k < a.batch) ? v[k] : 0.f;
+    for (int k = 0; k < 64; ++k) g += (b0 + k < a.batch) ? v[k] : 0.f;
   }
-  sgd_update(dst, g, a);
+  sgd_finish(dst, g, pv, mv, a);
 }
 
-__global__ void __launch_bounds__(RT) grad_reduce_kernel(ReduceArgs a) {
+__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(ReduceArgs a) {
   // block roles: [MLP tile blocks][MLP bias block][conv element blocks][bookkeeping]
   const bool mlp = a.hi > OFF_F1W;
   const bool conv = a.lo < OFF_F1W;
@@ -121,7 +133,9 @@ __global__ void __launch_bounds__(RT) grad_reduce_kernel(ReduceArgs a) {
   if (mlp) {
     if (blk < TILE_BLOCKS) {
       const int t = blk * 4 + (threadIdx.x >> 6);
-      if (t < FC_TILES) fc_tile(t, a);
+      if (t < FC_T0) fc_tile<0>(t, a);
+      else if (t < FC_T0 + FC_T1) fc_tile<1>(t - FC_T0, a);
+      else if (t < FC_TILES) fc_tile<2>(t - FC_T0 - FC_T1, a);
       return;
     }
     blk -= TILE_BLOCKS;
@@ -134,22 +148,33 @@ __global__ void __launch_bounds__(RT) grad_reduce_kernel(ReduceArgs a) {
     blk -= CB;
   }
   if (a.bookkeeping && blk == 0 && threadIdx.x < 64) {
-    // epoch statistics + cursor advance (one wave, fixed order)
+    // (1) epoch statistics of the step that just ran (one wave, fixed order)
     const int lane = threadIdx.x;
     float ls = 0.f;
     int cs = 0;
     for (int b = lane; b < a.batch; b += 64) { ls += a.loss[b]; cs += a.correct[b]; }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
+    const int bv = a.state[ST_BVALID];
+    const int next = a.state[ST_CURSOR] + 1;
+    if (lane == 0 && bv > 0) {
+      a.stats[STAT_LOSS] += (double)ls / (double)bv;
+      a.stats[STAT_BATCHES] += 1.0;
+      a.stats[STAT_CORRECT] += (double)cs;
+      a.stats[STAT_SAMPLES] += (double)bv;
+    }
+    // (2) publish the NEXT step: cursor, valid count and its sample ids, so the next
+    //     fused kernel reads its sample id directly (no cursor -> order dependency)
+    const long base = (long)next * a.batch;
+    for (int b = lane; b < a.batch; b += 64) {
+      const long g = base + b;
+      a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
+    }
+    const long rem = (long)a.order_len - base;
+    const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
     if (lane == 0) {
-      const int bv = a.state[ST_BVALID];
-      if (bv > 0) {
-        a.stats[STAT_LOSS] += (double)ls / (double)bv;
-        a.stats[STAT_BATCHES] += 1.0;
-        a.stats[STAT_CORRECT] += (double)cs;
-        a.stats[STAT_SAMPLES] += (double)bv;
-      }
-      a.state[ST_CURSOR] += 1;
+      a.state[ST_CURSOR] = next;
+      a.state[ST_BVALID] = nbv;
     }
   }
 }

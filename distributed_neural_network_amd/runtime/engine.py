@@ -208,6 +208,7 @@ class HipEngine(Engine):
         self.loss = torch.zeros(B, **f32)
         self.correct = torch.zeros(B, device=dev, dtype=torch.int32)
         self.order = torch.zeros(0, device=dev, dtype=torch.int32)
+        self.batch_ids = torch.zeros(B, device=dev, dtype=torch.int32)  # sample ids of the next step
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
@@ -251,7 +252,13 @@ class HipEngine(Engine):
         self.order_len = n
         if n:
             self.order[:n].copy_(torch.from_numpy(order), non_blocking=False)
+        # step 0 of the epoch: cursor, valid count and sample ids (later steps are
+        # published on device by the reduce kernel's bookkeeping block)
+        first = min(self.batch, n)
         self.state[0] = 0
+        self.state[1] = first
+        if first:
+            self.batch_ids[:first].copy_(self.order[:first])
 
     # -- one step (launch sequence; also what graphs capture) ---------------------------
     def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int) -> None:
@@ -259,12 +266,13 @@ class HipEngine(Engine):
                              self._p(self.z2), self._p(self.z3), self._p(self.slab), self._p(self.loss),
                              self._p(self.correct), self.batch, self._p(self.master), self._p(self.grad),
                              self._p(self.mom), self._p(self.shadow), self._p(self.state), self._p(self.stats),
-                             self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, s)
+                             self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, self._p(self.order),
+                             self.order_len, self._p(self.batch_ids), s)
 
     def _launch_step(self) -> None:
         assert self.train is not None
         s = self._stream()
-        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.order),
+        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
                              self.order_len, self.batch, self._p(self.state), self._p(self.master),
                              self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
                              self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),

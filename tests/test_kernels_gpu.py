@@ -31,7 +31,7 @@ def test_fused_rows_match_oracle(B, n):
     s = eng._stream()
     ext = eng.ext
     with torch.cuda.device(eng.device):
-        ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.order), eng.order_len,
+        ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids), eng.order_len,
                         eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
                         eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
                         eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), s)

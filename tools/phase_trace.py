@@ -31,9 +31,9 @@ def main(reps: int = 50, batch: int = 64):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     walls = []
     for r in range(reps):
-        eng.state[0] = r % 60
+        eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
         ev0.record()
-        eng.ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.order), eng.order_len,
+        eng.ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids), eng.order_len,
                             eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
                             eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
                             eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), eng._stream(),
