@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
+    ap.add_argument("--in-launch-reduce", action="store_true",
+                    help="experimental: batch reduction + SGD in reducer workgroups inside the fused launch "
+                         "(counter hand-off) instead of a second kernel")
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -88,7 +91,7 @@ def main():
     train, test = synthetic(50_000, args.seed, True), synthetic(10_000, args.seed, False)
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
     engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                       overlap=args.overlap)
+                       overlap=args.overlap, in_launch_reduce=args.in_launch_reduce)
     engine.attach(train)
     test_dev = test.to(device)
     policy = make_policy(args.sync, comm)
@@ -109,6 +112,8 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
+    if engine.sync_error():
+        raise RuntimeError("in-launch reducer hand-off timed out (sync error flag set)")
     dt = comm.reduce_scalar(dt, "max")
     ms_per_step = 1000.0 * dt / args.steps
     value = comm.world * B * args.steps / dt
@@ -156,7 +161,8 @@ def main():
                "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)",
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
-                          "optimizer": "SGD lr=0.001 momentum=0.9, every step"},
+                          "optimizer": "SGD lr=0.001 momentum=0.9, every step",
+                          "reduce": "in-launch" if args.in_launch_reduce else "separate-kernel"},
                **epoch}
         print(json.dumps(out), flush=True)
     comm.close()

@@ -50,12 +50,33 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
-                                  P<long long>(stamps), S(stream));
+                                  P<long long>(stamps), nullptr, nullptr, S(stream));
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0);
+  // fused training step WITH the in-launch reducer workgroups (batch reduction + SGD)
+  m.def("fused_train_reduce",
+        [](u images, u labels, u batch_ids, int batch, u state, u master, u shadow, u a0, u h1, u h2, u z1, u z2,
+           u z3, u slab, u loss, u correct, u grad, u mom, u stats, u order, int order_len, float lr,
+           float momentum, int fuse_sgd, u sync, u stream, u stamps) {
+          dnn::ReduceArgs r{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
+                            P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
+                            P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
+                            P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order),
+                            order_len, P<int32_t>(batch_ids), lr, momentum, 1.0f, fuse_sgd, 0, dnn::ARENA, 1};
+          dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(batch_ids),
+                                  order_len, batch, P<int32_t>(state), P<const float>(master),
+                                  P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
+                                  P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
+                                  P<long long>(stamps), &r, P<unsigned>(sync), S(stream));
+        },
+        py::arg("images"), py::arg("labels"), py::arg("batch_ids"), py::arg("batch"), py::arg("state"),
+        py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"),
+        py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("grad"),
+        py::arg("mom"), py::arg("stats"), py::arg("order"), py::arg("order_len"), py::arg("lr"),
+        py::arg("momentum"), py::arg("fuse_sgd"), py::arg("sync"), py::arg("stream"), py::arg("stamps") = 0);
   m.def("fused_eval", [](u images, u labels, u order, int n, int base, int count, u master, u shadow, u loss,
                          u correct, u stream) {
     dnn::launch_fused_eval(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), n, base,

@@ -4,14 +4,6 @@
 
 namespace dnn {
 
-void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
-                        int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
-                        float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
-                        int32_t* correct, long long* stamps, hipStream_t stream);
-void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
-                       int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
-                       hipStream_t stream);
-
 struct ReduceArgs {
   const float* a0; const float* h1; const float* h2;
   const float* z1; const float* z2; const float* z3;
@@ -25,6 +17,17 @@ struct ReduceArgs {
   int lo, hi;     // arena element range [lo, hi) handled by this launch (gradient bucket)
   int bookkeeping;  // 1: this launch also advances the cursor / epoch statistics
 };
+
+void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
+                        int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
+                        float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
+                        int32_t* correct, long long* stamps, const ReduceArgs* ra, unsigned* sync,
+                        hipStream_t stream);
+void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
+                       int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
+                       hipStream_t stream);
+
+
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);

@@ -1,0 +1,193 @@
+// Device code of the batch gradient reduction + momentum SGD, shared by the standalone
+// grad_reduce kernel (reduce_sgd.hip) and the reducer workgroups that run inside the
+// fused training launch (lenet_fused.hip).  See reduce_sgd.hip for the parity notes.
+#pragma once
+#include "launchers.h"
+
+namespace dnn {
+
+// Operand source of the reduction.  COH = the bytes were handed over INSIDE the launch by
+// other workgroups (in-launch reducers): every load is a buffer load with sc1 (aux 16),
+// which bypasses this CU's L1, so no agent acquire is needed; the producers store them
+// write-through (sc1) and drain before signalling (MI355X_MICROARCH.md, visibility, valid
+// forms row 1).  The descriptor is built from wave-uniform values only.
+template <bool COH, typename T = float>
+struct Src {
+  const T* p;
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Src(const T* p_, int n) : p(p_) {
+    if constexpr (COH) r = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(p_), 0, n * (int)sizeof(T), 0x00020000);
+  }
+  __device__ __forceinline__ T operator[](int i) const {
+    if constexpr (COH) {
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, i * (int)sizeof(T), 0, 16));
+    } else {
+      return p[i];
+    }
+  }
+};
+
+// SGD epilogue with the master/momentum values already in registers (prefetched
+// together with the gradient operands, so the update costs no extra memory latency).
+__device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs a) {
+  g *= a.grad_scale;
+  if (a.fuse_sgd) {
+    const float m = a.momentum * m_old + g;
+    const float p = p_old - a.lr * m;
+    a.mom[e] = m;
+    a.master[e] = p;
+    write_shadow(a.shadow, e, p);
+  } else {
+    a.grad[e] = g;
+  }
+}
+
+// fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
+// output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).
+template <int LAYER> struct Fc;
+template <> struct Fc<0> { static constexpr int O = 120, I = 400, IT = 25, OFF = OFF_F1W, ZLD = Z1_LD, XLD = A0_LD; };
+template <> struct Fc<1> { static constexpr int O = 84, I = 120, IT = 8, OFF = OFF_F2W, ZLD = Z2_LD, XLD = H1_LD; };
+template <> struct Fc<2> { static constexpr int O = 10, I = 84, IT = 6, OFF = OFF_F3W, ZLD = Z3_LD, XLD = H2_LD; };
+constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
+constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
+constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
+
+template <int LAYER, bool COH>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
+  using L = Fc<LAYER>;
+  const Src<COH> z(LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3), a.batch * L::ZLD);
+  const Src<COH> x(LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2), a.batch * L::XLD);
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15, kq = lane >> 4;
+  const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
+  const int om = o0 + col, in = i0 + col;
+  const bool ov = om < L::O, iv = in < L::I;
+  // this lane's 4 output elements: rows o0 + 4kq + j, column in
+  int e[4];
+  float pv[4], mv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = min(o0 + 4 * kq + j, L::O - 1);
+    e[j] = L::OFF + o * L::I + (iv ? in : 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { pv[j] = a.master[e[j]]; mv[j] = a.mom[e[j]]; }  // (unused if !fuse_sgd)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int omc = ov ? om : 0, inc = iv ? in : 0;
+  for (int b0 = 0; b0 < a.batch; b0 += 64) {
+    // every operand load is unconditional (clamped address) and issued before the first
+    // MFMA; out-of-range operands are zeroed by a select afterwards
+    float av[16], bv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int b = min(b0 + 4 * s + kq, a.batch - 1);
+      av[s] = z[b * L::ZLD + omc];
+      bv[s] = x[b * L::XLD + inc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool bvld = b0 + 4 * s + kq < a.batch;
+      av[s] = (bvld && ov) ? av[s] : 0.f;
+      bv[s] = (bvld && iv) ? bv[s] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = o0 + 4 * kq + j;
+    if (o < L::O && iv) sgd_finish(e[j], acc[j], pv[j], mv[j], a);
+  }
+}
+
+// element tasks: fc biases (sum_b z[b][o]) and conv slab columns (sum_b slab[b][j]);
+// all 64 rows of a chunk are loaded before the (fixed-order) sum
+template <bool COH>
+__device__ __forceinline__ float column_sum(const Src<COH>& src, int ld, int col, int batch) {
+  float g = 0.f;
+  for (int b0 = 0; b0 < batch; b0 += 64) {
+    float v[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = src[min(b0 + k, batch - 1) * ld + col];
+    __builtin_amdgcn_sched_barrier(0);  // all 64 loads in flight before the first wait
+#pragma unroll
+    for (int k = 0; k < 64; ++k) g += (b0 + k < batch) ? v[k] : 0.f;
+  }
+  return g;
+}
+
+// fc-bias slots.  COH: wave-aligned so each wave reads ONE source (buffer descriptor in
+// SGPRs): [0,128) fc1 (120 used), [128,256) fc2 (84 used), [256,320) fc3 (10 used).
+// Plain loads: compact [0,214).
+constexpr int FCB_SLOTS = 320, FCB_ELEMS = 120 + 84 + 10;
+template <bool COH>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
+  const float* zp;
+  int ld, col, n, off;
+  if constexpr (COH) {
+    const int grp = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform source (descriptor in SGPRs)
+    if (grp < 2) { zp = a.z1; ld = Z1_LD; col = t; n = 120; off = OFF_F1B; }
+    else if (grp < 4) { zp = a.z2; ld = Z2_LD; col = t - 128; n = 84; off = OFF_F2B; }
+    else { zp = a.z3; ld = Z3_LD; col = t - 256; n = 10; off = OFF_F3B; }
+  } else {  // plain loads: compact slots [0, 214)
+    if (t < 120) { zp = a.z1; ld = Z1_LD; col = t; n = 120; off = OFF_F1B; }
+    else if (t < 204) { zp = a.z2; ld = Z2_LD; col = t - 120; n = 84; off = OFF_F2B; }
+    else { zp = a.z3; ld = Z3_LD; col = t - 204; n = 10; off = OFF_F3B; }
+  }
+  const Src<COH> src(zp, a.batch * ld);
+  if (t >= (COH ? FCB_SLOTS : FCB_ELEMS) || col >= n) return;
+  const int dst = off + col;
+  const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
+  sgd_finish(dst, column_sum(src, ld, col, a.batch), pv, mv, a);
+}
+
+constexpr int CONV_ELEMS = SLAB;
+template <bool COH>
+__device__ __forceinline__ void conv_task(int e, const ReduceArgs a) {
+  const Src<COH> src(a.slab, a.batch * SLAB);
+  if (e >= CONV_ELEMS) return;
+  int dst;
+  if (e < SLAB_C1B) dst = OFF_C1W + e;
+  else if (e < SLAB_C2W) dst = OFF_C1B + (e - SLAB_C1B);
+  else if (e < SLAB_C2B) dst = OFF_C2W + (e - SLAB_C2W);
+  else dst = OFF_C2B + (e - SLAB_C2B);
+  const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
+  sgd_finish(dst, column_sum(src, SLAB, e, a.batch), pv, mv, a);
+}
+
+// Epoch statistics of the step that just ran + publication of the next step's cursor,
+// valid count and sample ids.  One wave (lanes 0..63), fixed summation order.
+template <bool COH>
+__device__ __forceinline__ void bookkeeping(const ReduceArgs a, int lane) {
+    const Src<COH> loss(a.loss, a.batch);
+    const Src<COH, int32_t> correct(a.correct, a.batch);
+    float ls = 0.f;
+    int cs = 0;
+    for (int b = lane; b < a.batch; b += 64) { ls += loss[b]; cs += correct[b]; }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
+    const int bv = a.state[ST_BVALID];
+    const int next = a.state[ST_CURSOR] + 1;
+    if (lane == 0 && bv > 0) {
+      a.stats[STAT_LOSS] += (double)ls / (double)bv;
+      a.stats[STAT_BATCHES] += 1.0;
+      a.stats[STAT_CORRECT] += (double)cs;
+      a.stats[STAT_SAMPLES] += (double)bv;
+    }
+    // (2) publish the NEXT step: cursor, valid count and its sample ids, so the next
+    //     fused kernel reads its sample id directly (no cursor -> order dependency)
+    const long base = (long)next * a.batch;
+    for (int b = lane; b < a.batch; b += 64) {
+      const long g = base + b;
+      a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
+    }
+    const long rem = (long)a.order_len - base;
+    const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
+    if (lane == 0) {
+      a.state[ST_CURSOR] = next;
+      a.state[ST_BVALID] = nbv;
+    }
+}
+
+}  // namespace dnn

@@ -48,6 +48,7 @@ class Communicator:
         self.orig_rank = self.env.rank
         self.store: dist.Store | None = None
         self.aborted = False
+        self.watch: Optional[Callable[[], Sequence[int]]] = None  # liveness watch (fault.Heartbeat)
         # DNN_FORCE_COLLECTIVES=1: build a real process group and issue every collective
         # even at world size 1 (exercises the RCCL + hipGraph-capture path on one GPU)
         self.force = os.environ.get("DNN_FORCE_COLLECTIVES", "0") == "1"
@@ -96,6 +97,25 @@ class Communicator:
     def _avg_op(self):
         return dist.ReduceOp.AVG if self.backend == "nccl" else None
 
+    def _wait(self, w) -> None:
+        """Wait for a host-blocking (gloo) collective, interruptibly.
+
+        A gloo ring peer of a dead rank can sit in recv on a LIVE rank that has already
+        left the collective, until that rank tears its group down.  With a liveness
+        watch installed (fault.Heartbeat), the wait polls and raises as soon as a
+        member is declared dead instead of blocking to the group timeout."""
+        watch = self.watch
+        if watch is None or self.backend == "nccl":
+            w.wait()
+            return
+        members = set(self.members)
+        while not w.is_completed():
+            lost = set(watch()) & members
+            if lost:
+                raise CommError(f"peer rank(s) {sorted(lost)} lost during a collective")
+            time.sleep(0.0005)
+        w.wait()  # re-raises the collective's own error, if any
+
     def allreduce_(self, t: torch.Tensor, op: str = "avg", async_op: bool = False):
         """In-place all-reduce; ``op`` in {avg, sum, max, min}."""
         if not self.distributed:
@@ -105,11 +125,16 @@ class Communicator:
                 aop = self._avg_op()
                 if aop is not None:
                     return dist.all_reduce(t, op=aop, async_op=async_op)
-                w = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=False)
+                self._wait(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
                 t.div_(self.world)
                 return None if not async_op else _Done()
             rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-            return dist.all_reduce(t, op=rop, async_op=async_op)
+            if async_op or self.backend == "nccl":
+                return dist.all_reduce(t, op=rop, async_op=async_op)
+            self._wait(dist.all_reduce(t, op=rop, async_op=True))
+            return None
+        except CommError:
+            raise
         except Exception as e:  # gloo raises on a dead peer; nccl after abort/timeout
             raise CommError(str(e)) from e
 
@@ -117,7 +142,12 @@ class Communicator:
         if not self.distributed:
             return
         try:
-            dist.broadcast(t, src=src)
+            if self.backend == "nccl":
+                dist.broadcast(t, src=src)
+            else:
+                self._wait(dist.broadcast(t, src=src, async_op=True))
+        except CommError:
+            raise
         except Exception as e:
             raise CommError(str(e)) from e
 
@@ -128,7 +158,9 @@ class Communicator:
             if self.backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
-                dist.barrier()
+                self._wait(dist.barrier(async_op=True))
+        except CommError:
+            raise
         except Exception as e:
             raise CommError(str(e)) from e
 

@@ -82,6 +82,7 @@ class Heartbeat:
         self.store = dist.TCPStore(env.master_addr, env.master_port, env.world, is_master=False,
                                    timeout=comm.timeout)
         self._beat()
+        comm.watch = lambda: tuple(self.dead)  # makes host-blocking collectives interruptible
         self._thread = threading.Thread(target=self._run, name="dnn-heartbeat", daemon=True)
         self._thread.start()
 
@@ -113,6 +114,7 @@ class Heartbeat:
                 pass
 
     def stop(self) -> None:
+        self.comm.watch = None
         self._stop.set()
         self._thread.join(timeout=2.0)
 

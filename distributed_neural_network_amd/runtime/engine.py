@@ -179,7 +179,7 @@ class HipEngine(Engine):
 
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
-                 use_graphs: bool = True, overlap: bool = False) -> None:
+                 use_graphs: bool = True, overlap: bool = False, in_launch_reduce: bool = False) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if not torch.cuda.is_available():
             raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -209,6 +209,10 @@ class HipEngine(Engine):
         self.correct = torch.zeros(B, device=dev, dtype=torch.int32)
         self.order = torch.zeros(0, device=dev, dtype=torch.int32)
         self.batch_ids = torch.zeros(B, device=dev, dtype=torch.int32)  # sample ids of the next step
+        # in-launch reducer hand-off counters [rows, slabs, done, error] (lenet_fused.hip);
+        # zero between launches (the last reducer resets them)
+        self.sync = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.in_launch_reduce = in_launch_reduce
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
@@ -269,9 +273,31 @@ class HipEngine(Engine):
                              self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, self._p(self.order),
                              self.order_len, self._p(self.batch_ids), s)
 
+    def _launch_fused_reduce(self, fuse_sgd: int, s: int) -> None:
+        """Fused step with the batch reduction (+ SGD when fuse_sgd) in the same launch."""
+        self.ext.fused_train_reduce(
+            self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids), self.batch,
+            self._p(self.state), self._p(self.master), self._p(self.shadow), self._p(self.a0), self._p(self.h1),
+            self._p(self.h2), self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
+            self._p(self.loss), self._p(self.correct), self._p(self.grad), self._p(self.mom), self._p(self.stats),
+            self._p(self.order), self.order_len, self.lr, self.momentum, fuse_sgd, self._p(self.sync), s)
+
+    def sync_error(self) -> bool:
+        """True if an in-launch reducer gave up waiting (hand-off protocol broken)."""
+        return bool(self.sync[3].item())
+
     def _launch_step(self) -> None:
         assert self.train is not None
         s = self._stream()
+        if self.in_launch_reduce and not self.overlap:
+            if self.grad_sync is None:
+                self._launch_fused_reduce(1, s)
+                return
+            self._launch_fused_reduce(0, s)
+            self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])
+            self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
+                               LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
+            return
         self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
                              self.order_len, self.batch, self._p(self.state), self._p(self.master),
                              self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
@@ -294,7 +320,7 @@ class HipEngine(Engine):
                            LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, self.grad_sync is not None, self.overlap, self.order_len)
+        key = (nsteps, self.grad_sync is not None, self.overlap, self.in_launch_reduce, self.order_len)
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.

@@ -112,6 +112,10 @@ class Trainer:
         t0 = time.perf_counter()
         old = list(self.comm.members)
         assert self.hb is not None
+        # tear our side of the broken group down FIRST: closing its sockets/communicator
+        # fails the collectives peers may still be blocked in on us (a gloo ring peer would
+        # otherwise sit in recv until our reform, past the agreement deadline)
+        self.comm.abort()
         members = agree_survivors(self.comm, self.hb)
         if self.comm.orig_rank not in members:
             raise RuntimeError("this rank was excluded from the re-formed group") from err

@@ -21,27 +21,42 @@ PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' 
           "  F1 dY1 + R1 rebuild"]
 
 
-def main(reps: int = 50, batch: int = 64):
+def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False)
     eng.attach(tr)
     eng.begin_epoch(np.arange(4096, dtype=np.int32))
-    stamps = torch.zeros(16, dtype=torch.int64, device=eng.device)
+    stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
+    blocks = []
+    red = []
     rows = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     walls = []
     for r in range(reps):
         eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
         ev0.record()
-        eng.ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids), eng.order_len,
-                            eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
-                            eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
-                            eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), eng._stream(),
-                            stamps=stamps.data_ptr())
+        if in_launch:
+            e = eng
+            e.ext.fused_train_reduce(
+                e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.batch, e._p(e.state),
+                e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2), e._p(e.z1), e._p(e.z2),
+                e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct), e._p(e.grad), e._p(e.mom),
+                e._p(e.stats), e._p(e.order), e.order_len, e.lr, e.momentum, 1, e._p(e.sync), e._stream(),
+                stamps=stamps.data_ptr())
+        else:
+            e = eng
+            e.ext.fused_train(e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.order_len, e.batch,
+                              e._p(e.state), e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2),
+                              e._p(e.z1), e._p(e.z2), e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct),
+                              e._stream(), stamps=stamps.data_ptr())
         ev1.record()
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
         s = stamps.cpu().numpy()
+        nb = batch + (39 if in_launch else 0)
+        blocks.append(s[16:16 + 4 * nb].reshape(nb, 4).copy())
+        if in_launch:
+            red.append((s[12:16] - s[0]) * 0.01)
         rows.append(np.concatenate([np.diff(s[:8]), [s[11] - s[2], s[8] - s[5], s[9] - s[8], s[6] - s[9],
                                                       s[10] - s[6]]]) * 0.01)  # 100 MHz ticks -> us
     med = np.median(np.array(rows[5:]), axis=0)
@@ -49,7 +64,31 @@ def main(reps: int = 50, batch: int = 64):
         print(f"{name:20s} {v:8.2f} us")
     print(f"{'sum (block 0)':20s} {med[:7].sum():8.2f} us")
     print(f"{'kernel wall (event)':20s} {np.median(walls[5:]):8.2f} us")
+    # per-block timeline (us from the earliest block start), medians over repeats
+    bl = np.array(blocks[5:])  # [reps, nb, 4]
+    t0 = bl[:, :, 0].min(axis=1, keepdims=True)
+    rel = (bl[:, :, :3] - t0[:, :, None]) * 0.01
+    med_b = np.median(rel, axis=0)
+    smp = med_b[:batch]
+    print("sample blocks  start min/med/max %.2f/%.2f/%.2f  rows %.2f/%.2f/%.2f  end %.2f/%.2f/%.2f us" % (
+        smp[:, 0].min(), np.median(smp[:, 0]), smp[:, 0].max(), smp[:, 1].min(), np.median(smp[:, 1]),
+        smp[:, 1].max(), smp[:, 2].min(), np.median(smp[:, 2]), smp[:, 2].max()))
+    xcc = bl[-1, :, 3]
+    for x in sorted(set(xcc[:batch].tolist())):
+        m = xcc[:batch] == x
+        print(f"  xcc {x}: {m.sum():2d} blocks, end med {np.median(smp[m, 2]):.2f} max {smp[m, 2].max():.2f} us")
+    slow = np.argsort(-smp[:, 2])[:6]
+    print("  slowest blocks:", ", ".join(f"b{i}(xcc{xcc[i]}) start {smp[i, 0]:.2f} rows {smp[i, 1]:.2f} "
+                                         f"end {smp[i, 2]:.2f}" for i in slow))
+    if in_launch:
+        red_b = med_b[batch:]
+        print("reducer blocks start min/max %.2f/%.2f  end min/med/max %.2f/%.2f/%.2f us" % (
+            red_b[:, 0].min(), red_b[:, 0].max(), red_b[:, 2].min(), np.median(red_b[:, 2]), red_b[:, 2].max()))
+        r = np.median(np.array(red[5:]), axis=0)
+        print(f"reducers (from block 0 start): fc released {r[0]:.2f} done {r[1]:.2f} | "
+              f"conv released {r[2]:.2f} done {r[3]:.2f} us")
+        assert not eng.sync_error()
 
 
 if __name__ == "__main__":
-    main()
+    main(in_launch="--in-launch" in sys.argv)
