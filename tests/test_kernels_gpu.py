@@ -21,9 +21,9 @@ def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-@pytest.mark.parametrize("B,n", [(4, 4), (16, 13), (64, 64)])
+@pytest.mark.parametrize("B,n", [(1, 1), (3, 2), (4, 4), (16, 13), (64, 64), (257, 257), (257, 200)])
 def test_fused_rows_match_oracle(B, n):
-    split = synthetic(97, seed=3)
+    split = synthetic(300, seed=3)
     eng = HipEngine(batch=B, seed=1, use_graphs=False)
     eng.attach(split)
     order = np.arange(5, 5 + n, dtype=np.int32)
@@ -56,12 +56,58 @@ def test_fused_rows_match_oracle(B, n):
         assert v < 1e-3, f"{k}: rel err vs bf16 emulation {v:.3e}"
     # (2) end-to-end precision vs the pure fp32 oracle
     #     (bf16 operands: ReLU-mask / argmax flips make small batches noisy)
+    #     a single flipped mask is not averaged away below a few samples: looser there
+    loose = 3.0 if bvalid < 4 else 1.0
     for k, tol in [("a0", 1e-2), ("h1", 1e-2), ("h2", 1e-2), ("loss", 1e-2), ("z3", 1e-2), ("z2", 0.15),
                    ("z1", 0.15), ("dW2", 0.15), ("dW1", 0.2)]:
-        assert errs[k] < tol, f"{k}: rel err {errs[k]:.3e}"
+        assert errs[k] < tol * loose, f"{k}: rel err {errs[k]:.3e}"
     if B > n:  # tail rows must be zero
         assert float(eng.a0[bvalid:].abs().sum()) == 0.0
         assert float(eng.slab[bvalid:].abs().sum()) == 0.0
+
+
+def _launch_fused(eng):
+    eng.ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids), eng.order_len,
+                        eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
+                        eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
+                        eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), eng._stream())
+
+
+@pytest.mark.parametrize("B,n", [(1, 1), (3, 3), (16, 11), (64, 64), (257, 257), (300, 290)])
+def test_batch_reduction_is_exact(B, n):
+    """grad_reduce (fuse_sgd=0) vs an fp64 reduction of the kernel's own per-sample rows:
+    isolates the batch reduction (fc MFMA f32 tiles, column sums, 64-row chunks, tails)."""
+    split = synthetic(320, seed=4)
+    eng = HipEngine(batch=B, seed=3, use_graphs=False)
+    eng.attach(split)
+    eng.begin_epoch(np.arange(n, dtype=np.int32))
+    with torch.cuda.device(eng.device):
+        _launch_fused(eng)
+        eng.ext.grad_reduce(eng._p(eng.a0), eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2),
+                            eng._p(eng.z3), eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), eng.batch,
+                            eng._p(eng.master), eng._p(eng.grad), eng._p(eng.mom), eng._p(eng.shadow),
+                            eng._p(eng.state), eng._p(eng.stats), eng.lr, eng.momentum, 1.0, 0, 0, LAYOUT.total, 0,
+                            eng._p(eng.order), eng.order_len, eng._p(eng.batch_ids), eng._stream())
+    torch.cuda.synchronize()
+    bv = min(B, n)
+    r = {k: getattr(eng, k)[:bv].double().cpu() for k in ["a0", "h1", "h2", "z1", "z2", "z3", "slab"]}
+    exp = torch.zeros(LAYOUT.total, dtype=torch.float64)
+    v = LAYOUT.views(exp)
+    v["fc1.weight"].copy_(r["z1"].T @ r["a0"])
+    v["fc1.bias"].copy_(r["z1"].sum(0))
+    v["fc2.weight"].copy_(r["z2"].T @ r["h1"])
+    v["fc2.bias"].copy_(r["z2"].sum(0))
+    v["fc3.weight"].copy_(r["z3"][:, :10].T @ r["h2"])
+    v["fc3.bias"].copy_(r["z3"][:, :10].sum(0))
+    sl = r["slab"].sum(0)
+    v["conv1.weight"].copy_(sl[0:450].view(6, 3, 5, 5))
+    v["conv1.bias"].copy_(sl[450:456])
+    v["conv2.weight"].copy_(sl[456:2856].view(16, 6, 5, 5))
+    v["conv2.bias"].copy_(sl[2856:2872])
+    got = LAYOUT.views(eng.grad.double().cpu())
+    for k, t in v.items():
+        err = float((got[k] - t).abs().max() / (t.abs().max() + 1e-30))
+        assert err < 1e-4, f"{k}: max rel err {err:.3e}"
 
 
 def test_train_steps_track_cpu_oracle():
