@@ -75,8 +75,8 @@ constexpr int A_R3 = 0;                     // bf16x8 records [16][18][14] of ze
 constexpr int A_DY2 = 64512;                // bf16 [16][10][16]                                 5,120
 constexpr int A_DP1 = A_DY2 + 5120;         // f32 [6][196]                                      4,704
 constexpr int A_RS = A_DP1 + 4704;          // f32 [16][18] dY2 row sums (conv2 bias grad)       1,152
-constexpr int A_DY1 = 0;                    // bf16 [6] x 1808 B (28 rows x 64 B + 16 B pad)    10,848
-constexpr int DY1_CH = 1808;                //   channel stride: 452 dwords, breaks the 4-way bank conflict
+constexpr int A_DY1 = 0;                    // bf16 [6] x 1824 B (28 rows x 64 B + 32 B pad)    10,944
+constexpr int DY1_CH = 1824;                //   channel stride 456 dwords (= 8 mod 64): conv1-wgrad A reads conflict-free
 constexpr int A_RS1 = A_DY1 + 6 * DY1_CH;   // f32 [6][28] dY1 row sums (conv1 bias grad)          672
 static_assert(A_RS + 1152 <= L_REGA_SZ, "REGA sub-layout");
 static_assert(A_RS1 + 672 <= A_DP1, "phase F scratch must not overlap dP1");
@@ -178,6 +178,12 @@ __device__ __forceinline__ void build_r1_part(const uint8_t* img, const bf16* lu
   }
 }
 
+// R1 builder thread -> (row, quarter): the 8 lanes of a ds_write_b128 group take 8
+// different rows (row stride 29 records = 116 dwords -> 8 distinct 4-dword bank slots),
+// conflict-free; the natural (row = t / 4) map put 4 lanes on one slot (tools/lds_banks.py).
+__device__ __forceinline__ int r1_row(int t) { return (t & 7) + 8 * (t >> 5); }
+__device__ __forceinline__ int r1_q(int t) { return (t >> 3) & 3; }
+
 // ---- in-launch reducer workgroups ------------------------------------------------------
 // The batch reduction of the weight gradients (+ SGD) runs in RED_BLOCKS extra
 // workgroups of the same launch, on CUs the sample workgroups leave idle.  The fc
@@ -195,19 +201,24 @@ constexpr int RED_FC_BLOCKS = (FC_TILES + 7) / 8;   // 32 (8 wave-tiles per bloc
 constexpr int RED_CONV_BLOCKS = (CONV_ELEMS + NT - 1) / NT;  // 6
 constexpr int RED_BLOCKS = RED_FC_BLOCKS + 1 + RED_CONV_BLOCKS;  // + fc-bias/bookkeeping block
 
-// write-through stores (sc1): the line leaves the XCD's L2 for memory at once
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// Write-through stores (sc1): the line leaves the XCD's L2 for memory at once.
+// Scalar values go through buffer-store builtins (cache policy 16 = sc1) so hipcc sees
+// the instruction and inserts the MFMA/VALU -> VMEM wait states itself (an inline-asm
+// store of an MFMA result would read the accumulator before it is written).  The
+// descriptor is built from the wave-uniform base; `i` is the element index.
+template <typename T>
+__device__ __forceinline__ void st_out(T* base, int i, T v, bool wt) {
+  if (wt) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, i * 4, 0, 16);
+  } else {
+    base[i] = v;
+  }
 }
-__device__ __forceinline__ void st_wt(int32_t* p, int32_t v) {
-  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
+// 16-B row store from LDS-loaded registers (no pipeline hazard: the compiler's waitcnt
+// covers the ds_read; `s_nop 1` keeps hipcc from reusing the data VGPRs too early)
 __device__ __forceinline__ void st_wt4(float* p, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-template <typename T>
-__device__ __forceinline__ void st_out(T* p, T v, bool wt) {
-  if (wt) st_wt(p, v); else *p = v;
 }
 
 __device__ __forceinline__ void signal_count(unsigned* cnt) {  // all threads of the producer block
@@ -325,18 +336,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (!valid) {
     if (TRAIN) {
       constexpr bool wt = INL;
-      for (int i = tid; i < A0_LD; i += NT) st_out(a0_out + (size_t)b * A0_LD + i, 0.f, wt);
+      for (int i = tid; i < A0_LD; i += NT) st_out(a0_out + (size_t)b * A0_LD, i, 0.f, wt);
       for (int i = tid; i < H1_LD; i += NT) {
-        st_out(h1_out + (size_t)b * H1_LD + i, 0.f, wt);
-        st_out(z1_out + (size_t)b * Z1_LD + i, 0.f, wt);
+        st_out(h1_out + (size_t)b * H1_LD, i, 0.f, wt);
+        st_out(z1_out + (size_t)b * Z1_LD, i, 0.f, wt);
       }
       for (int i = tid; i < H2_LD; i += NT) {
-        st_out(h2_out + (size_t)b * H2_LD + i, 0.f, wt);
-        st_out(z2_out + (size_t)b * Z2_LD + i, 0.f, wt);
+        st_out(h2_out + (size_t)b * H2_LD, i, 0.f, wt);
+        st_out(z2_out + (size_t)b * Z2_LD, i, 0.f, wt);
       }
-      for (int i = tid; i < Z3_LD; i += NT) st_out(z3_out + (size_t)b * Z3_LD + i, 0.f, wt);
-      for (int i = tid; i < SLAB; i += NT) st_out(slab_out + (size_t)b * SLAB + i, 0.f, wt);
-      if (tid == 0) { st_out(loss_out + b, 0.f, wt); st_out(correct_out + b, 0, wt); }
+      for (int i = tid; i < Z3_LD; i += NT) st_out(z3_out + (size_t)b * Z3_LD, i, 0.f, wt);
+      for (int i = tid; i < SLAB; i += NT) st_out(slab_out + (size_t)b * SLAB, i, 0.f, wt);
+      if (tid == 0) { st_out(loss_out, b, 0.f, wt); st_out(correct_out, b, 0, wt); }
       if constexpr (INL) {
         signal_count(&sync[0]);
         if (threadIdx.x == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -409,7 +420,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   lds_barrier();
-  if (tid < 384) build_r1_part(IMGS, LUT, R1, tid >> 2, tid & 3);
+  if (tid < 384) build_r1_part(IMGS, LUT, R1, r1_row(tid), r1_q(tid));
   lds_barrier();
   STAMP(1);
 
@@ -605,8 +616,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
-      st_out(loss_out + b, lse - ll, INL);
-      st_out(correct_out + b, pred == label ? 1 : 0, INL);
+      st_out(loss_out, b, lse - ll, INL);
+      st_out(correct_out, b, pred == label ? 1 : 0, INL);
     }
     if (TRAIN && lane < 32) {
       const float dz = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
@@ -742,7 +753,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int k = 0; k < 5; ++k) t += (part + 4 * k < 18) ? RS[o * 18 + min(part + 4 * k, 17)] : 0.f;
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
-    if (part == 0) st_out(slab + SLAB_C2B + o, t, wt);
+    if (part == 0) st_out(slab, SLAB_C2B + o, t, wt);
   }
   // conv2 data gradient: 13 pixel tiles x 20 K-steps (waves 0-7 take tiles w, w+8)
   for (int mt = wave; mt < 13; mt += 8) {
@@ -790,7 +801,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       for (int sk = 0; sk < 5; ++sk) acc = mfma32(av[sk], bv[sk], acc);
       if (n < 150) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st_out(slab + SLAB_C2W + (4 * fg + i) * 150 + n, acc[i], wt);
+        for (int i = 0; i < 4; ++i) st_out(slab, SLAB_C2W + (4 * fg + i) * 150 + n, acc[i], wt);
       }
     }
   }
@@ -827,7 +838,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     RS1[c * 28 + y] = rs;
   } else {
-    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, LUT, R1, t >> 2, t & 3);  // R2 dead
+    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, LUT, R1, r1_row(t), r1_q(t));  // R2 dead
   }
   lds_barrier();
   STAMP(10);
@@ -839,7 +850,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
     t += __shfl_xor(t, 4);
-    if (part == 0 && lane < 48) st_out(slab + SLAB_C1B + c, t, wt);
+    if (part == 0 && lane < 48) st_out(slab, SLAB_C1B + c, t, wt);
   }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
     const int n = wave * 16 + fr, nc = min(n, 74);
@@ -865,7 +876,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = 4 * fg + i;
-        if (o < 6) st_out(slab + SLAB_C1W + o * 75 + n, acc[i], wt);
+        if (o < 6) st_out(slab, SLAB_C1W + o * 75 + n, acc[i], wt);
       }
     }
   }

@@ -1,0 +1,26 @@
+"""Summarise rocprofv3 --pmc CSV runs (one directory per counter pass) for one kernel."""
+import collections
+import csv
+import glob
+import sys
+
+root, pattern = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "lenet_fused_kernelILb1"
+agg = collections.defaultdict(list)
+for f in glob.glob(f"{root}/*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        if pattern in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
+for k in sorted(med):
+    print(f"{k:28s} median {med[k]:12.4g}  (n={len(agg[k])})")
+g = med.get
+if g("SQ_WAVE_CYCLES"):
+    wc = g("SQ_WAVE_CYCLES")
+    print(f"\nwave-cycle split: waiting (s_waitcnt/barrier) {g('SQ_WAIT_ANY', 0) / wc:.0%}, "
+          f"issue-stalled {g('SQ_WAIT_INST_ANY', 0) / wc:.0%}, issuing {g('SQ_ACTIVE_INST_ANY', 0) / wc:.0%}")
+if g("SQ_LDS_IDX_ACTIVE"):
+    print(f"LDS bank-conflict cycles / LDS active cycles: {g('SQ_LDS_BANK_CONFLICT', 0) / g('SQ_LDS_IDX_ACTIVE'):.0%}")
+if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum"):
+    print(f"L2 hit rate: {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.0%}")
+if g("SQ_VALU_MFMA_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
+    print(f"MFMA busy cycles (sum over SIMDs) / GPU active cycles: {g('SQ_VALU_MFMA_BUSY_CYCLES') / g('GRBM_GUI_ACTIVE'):.2f}")
