@@ -55,7 +55,7 @@ constexpr int IMG = 3 * 32 * 32;
 // loads MFMA fragments with one 16-B load each instead of re-arranging weights per sample.
 constexpr int SH_W1F = ARENA;               // conv1 fwd B frags  [16 pairs (c,ky)][16 n][8 kx]
 constexpr int SH_W2F = SH_W1F + 16 * 16 * 8;  // conv2 fwd B frags  [32 pairs (c,ky)][16 n][8 kx]
-constexpr int SH_WF = SH_W2F + 32 * 16 * 8;   // conv2 dgrad B frags (flipped) [80 (o,ky')][16 c][8 kx']
+constexpr int SH_WF = SH_W2F + 32 * 16 * 8;   // conv2 dgrad B frags (flipped) [80 (ky',o)][16 c][8 kx']
 constexpr int SH_W2T = SH_WF + 80 * 16 * 8;   // fc2 transposed [120 i][96 o]
 constexpr int SH_W3T = SH_W2T + 120 * 96;     // fc3 transposed [84 i][16 o]
 constexpr int SH_TOTAL = SH_W3T + 84 * 16 + 64;  // + slack so padded fragment reads stay in bounds
@@ -69,7 +69,7 @@ __device__ __forceinline__ void write_shadow(bf16* __restrict__ sh, int e, float
   } else if (e >= OFF_C2W && e < OFF_C2W + 2400) {
     const int r = e - OFF_C2W, n = r / 150, rem = r - 150 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
     sh[SH_W2F + ((c * 5 + ky) * 16 + n) * 8 + kx] = v;
-    sh[SH_WF + ((n * 5 + (4 - ky)) * 16 + c) * 8 + (4 - kx)] = v;
+    sh[SH_WF + (((4 - ky) * 16 + n) * 16 + c) * 8 + (4 - kx)] = v;  // K pairs kyp-major: p = 16 kyp + o
   } else if (e >= OFF_F2W && e < OFF_F2W + 10080) {
     const int r = e - OFF_F2W, o = r / 120, i = r - 120 * o;
     sh[SH_W2T + i * 96 + o] = v;

@@ -46,8 +46,8 @@ constexpr int L_REGA_SZ = 96256;
 constexpr int L_REGB = L_REGA + L_REGA_SZ;  // R1 records [3][32][29] (A-B, F) | R2 + WF (C-E)
 constexpr int L_REGB_SZ = 44544;
 constexpr int B_WF = 17472;                 // REGB: flipped conv2 kernel fragments after R2 (20,480 B)
-constexpr int L_P1 = L_REGB + L_REGB_SZ;    // f32 [6][14][20] (cols 14..19 zero)
-constexpr int L_CODE1 = L_P1 + 6720;        // u8 [6][196]
+constexpr int L_P1 = L_REGB + L_REGB_SZ;    // bf16 [6][14][20] (cols 14..19 zero; R2 holds bf16 anyway)
+constexpr int L_CODE1 = L_P1 + 3360;        // u8 [6][196]
 constexpr int L_A0 = L_CODE1 + 1184;        // f32 [400]  pooled conv2 output
 constexpr int L_A0B = L_A0 + 1600;          // bf16 [416] (MFMA operand, zero padded)
 constexpr int L_CODE2 = L_A0B + 832;        // u8 [400]
@@ -64,15 +64,14 @@ constexpr int L_DZ1 = L_DZ2B + 192;         // f32 [128]
 constexpr int L_DZ1B = L_DZ1 + 512;         // bf16 [128]
 constexpr int L_DA0 = L_DZ1B + 256;         // f32 [400]
 constexpr int L_IMG = L_DA0 + 1600;         // u8 [3][32][32] raw image (re-used by phase F)
-constexpr int L_LUT = L_IMG + 3072;         // bf16 [256] normalised value of each u8 code
-constexpr int L_MISC = L_LUT + 512;
-constexpr int LDS_TOTAL = L_MISC + 64;      // 159,664 B
+constexpr int L_MISC = L_IMG + 3072;
+constexpr int LDS_TOTAL = L_MISC + 64;      // 156,304 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
 // REGA sub-layout during the conv backward (fc1 weights are dead after the MLP dgrad)
-constexpr int A_R3 = 0;                     // bf16x8 records [16][18][14] of zero-padded dY2  64,512
-constexpr int A_DY2 = 64512;                // bf16 [16][10][16]                                 5,120
+constexpr int A_R3 = 0;                     // bf16x8 records [16][18][16 (14 used)] of padded dY2 73,728
+constexpr int A_DY2 = 73728;                // bf16 [16][10][16]                                 5,120
 constexpr int A_DP1 = A_DY2 + 5120;         // f32 [6][196]                                      4,704
 constexpr int A_RS = A_DP1 + 4704;          // f32 [16][18] dY2 row sums (conv2 bias grad)       1,152
 constexpr int A_DY1 = 0;                    // bf16 [6] x 1824 B (28 rows x 64 B + 32 B pad)    10,944
@@ -81,9 +80,11 @@ constexpr int A_RS1 = A_DY1 + 6 * DY1_CH;   // f32 [6][28] dY1 row sums (conv1 b
 static_assert(A_RS + 1152 <= L_REGA_SZ, "REGA sub-layout");
 static_assert(A_RS1 + 672 <= A_DP1, "phase F scratch must not overlap dP1");
 
-__device__ __forceinline__ float u8norm(uint32_t u) {
-  // ToTensor (x/255) then Normalize(mean .5, std .5): same op order as torchvision.
-  return ((float)u / 255.0f - 0.5f) / 0.5f;
+// bf16 of the normalised value by ONE fma: fmaf(u, 2/255, -1) rounds to the same bf16 as
+// the exact ToTensor+Normalize value for every u in 0..255 (checked exhaustively in
+// tests/test_oracle_cpu.py), so no lookup table is needed.
+__device__ __forceinline__ bf16 u8norm_bf16(uint32_t u) {
+  return (bf16)__builtin_fmaf((float)u, (float)(2.0 / 255.0), -1.0f);
 }
 
 // Barrier for LDS hand-offs only: waits for this wave's LDS ops, not for vmcnt, so an
@@ -154,8 +155,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* m, int ld, int k0, int n0,
 }
 
 // Build window records x = 8q .. 8q+7 (x < 29) of input row (c, y) = `row` from the u8
-// image staged in LDS, normalising through the per-block bf16 LUT; 4 threads per row.
-__device__ __forceinline__ void build_r1_part(const uint8_t* img, const bf16* lut, bf16x8* R1, int row, int q) {
+// image staged in LDS (normalised by u8norm_bf16, no table lookups); 4 threads per row.
+__device__ __forceinline__ void build_r1_part(const uint8_t* img, bf16x8* R1, int row, int q) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(img + row * 32);
   uint32_t w[4];  // elements 8q .. 8q+15 (zero past the row end)
 #pragma unroll
@@ -164,7 +165,7 @@ __device__ __forceinline__ void build_r1_part(const uint8_t* img, const bf16* lu
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const uint32_t u = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    const bf16 t = lut[u];
+    const bf16 t = u8norm_bf16(u);
     v[k] = (8 * q + k < 32) ? t : (bf16)0.f;
   }
 #pragma unroll
@@ -183,6 +184,12 @@ __device__ __forceinline__ void build_r1_part(const uint8_t* img, const bf16* lu
 // conflict-free; the natural (row = t / 4) map put 4 lanes on one slot (tools/lds_banks.py).
 __device__ __forceinline__ int r1_row(int t) { return (t & 7) + 8 * (t >> 5); }
 __device__ __forceinline__ int r1_q(int t) { return (t >> 3) & 3; }
+
+// R3 record (o, yy, x), x < 14: 16-record rows, x XOR-swizzled by yy & 7.  The conv2
+// dgrad K order is kyp-major (p = 16 kyp + o, o = 4 (kk % 4) + fg), so the four K-groups of
+// a K-step read the SAME yy of four channels: one XOR for all of them, 16 distinct 4-dword
+// bank slots per read group; the builder's write groups (8 consecutive yy) hit 8 slots.
+__device__ __forceinline__ int r3_index(int o, int yy, int x) { return (o * 18 + yy) * 16 + (x ^ (yy & 7)); }
 
 // ---- in-launch reducer workgroups ------------------------------------------------------
 // The batch reduction of the weight gradients (+ SGD) runs in RED_BLOCKS extra
@@ -362,7 +369,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   bf16x8* R1 = reinterpret_cast<bf16x8*>(smem + L_REGB);
   bf16x8* R2 = reinterpret_cast<bf16x8*>(smem + L_REGB);
   bf16x8* WF = reinterpret_cast<bf16x8*>(smem + L_REGB + B_WF);
-  float* P1 = reinterpret_cast<float*>(smem + L_P1);
+  bf16* P1 = reinterpret_cast<bf16*>(smem + L_P1);
   uint8_t* CODE1 = smem + L_CODE1;
   float* A0 = reinterpret_cast<float*>(smem + L_A0);
   bf16* A0B = reinterpret_cast<bf16*>(smem + L_A0B);
@@ -380,7 +387,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   bf16* DZ1B = reinterpret_cast<bf16*>(smem + L_DZ1B);
   float* DA0 = reinterpret_cast<float*>(smem + L_DA0);
   uint8_t* IMGS = smem + L_IMG;
-  bf16* LUT = reinterpret_cast<bf16*>(smem + L_LUT);
 
   // ============ phase A: ingest + weight staging ======================================
   // Plain loads first (image, conv B fragments, conv biases), consumed before the fc1
@@ -393,7 +399,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   for (int sk = 0; sk < 8; ++sk) bw2[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W2F)[(4 * sk + fg) * 16 + fr];
   float bias_c1 = master[OFF_C1B + min(fr, 5)];
   float bias_c2 = master[OFF_C2B + fr];
-  for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = 0.f;
+  for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = (bf16)0.f;
   if (tid < 16) A0B[400 + tid] = (bf16)0.f;                                   // MLP operand padding
   else if (tid < 24) H1B[120 + tid - 16] = (bf16)0.f;
   else if (tid < 36) H2B[84 + tid - 24] = (bf16)0.f;
@@ -401,7 +407,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
   else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
-  if (tid < 256) LUT[tid] = (bf16)u8norm((uint32_t)tid);  // exact ToTensor+Normalize, once per block
 #pragma unroll
   for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
 #pragma unroll
@@ -420,7 +425,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   lds_barrier();
-  if (tid < 384) build_r1_part(IMGS, LUT, R1, r1_row(tid), r1_q(tid));
+  if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
   lds_barrier();
   STAMP(1);
 
@@ -444,7 +449,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
           const float v = acc[i] + bias;
           if (v > best) { best = v; arg = i; }
         }
-        P1[(fr * 14 + qo / 14) * 20 + qo % 14] = fmaxf(best, 0.f);
+        P1[(fr * 14 + qo / 14) * 20 + qo % 14] = (bf16)fmaxf(best, 0.f);
         CODE1[fr * 196 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
       }
     };
@@ -497,7 +502,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   float bias_f3 = master[OFF_F3B + min(fr, 9)];
   if (tid < 168) {  // window records of P1 rows (overwrite R1: dead until phase F); 2 threads per row
     const int row = tid >> 1, h = tid & 1;  // row = c*14 + y; half h builds records 7h .. 7h+6 (< 13)
-    float v[14];
+    bf16 v[14];
 #pragma unroll
     for (int k = 0; k < 14; ++k) v[k] = P1[row * 20 + 7 * h + k];
 #pragma unroll
@@ -505,7 +510,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       if (7 * h + x < 13) {
         bf16x8 r;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = (bf16)v[x + j];
+        for (int j = 0; j < 8; ++j) r[j] = v[x + j];
         R2[row * 13 + 7 * h + x] = r;
       }
     }
@@ -728,7 +733,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       bf16x8 r;
 #pragma unroll
       for (int j = 0; j < 8; ++j) r[j] = (bf16)v[xr + j];
-      R3[(o * 18 + yy) * 14 + xr] = r;
+      R3[r3_index(o, yy, xr)] = r;
     }
     if (yv) {
       bf16x8 r0, r1;
@@ -746,7 +751,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (LDS-DMA, issued in phase D) landed
   lds_barrier();
   STAMP(8);
-  if (wave == 7) {  // conv2 bias gradient: 4 lanes per channel over its 18 row sums
+  if (wave == 3) {  // conv2 bias gradient: 4 lanes per channel over its 18 row sums
     const int o = lane >> 2, part = lane & 3;
     float t = 0.f;
 #pragma unroll
@@ -755,56 +760,105 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     t += __shfl_xor(t, 2);
     if (part == 0) st_out(slab, SLAB_C2B + o, t, wt);
   }
-  // conv2 data gradient: 13 pixel tiles x 20 K-steps (waves 0-7 take tiles w, w+8)
-  for (int mt = wave; mt < 13; mt += 8) {
-    const int m = min(mt * 16 + fr, 195);
-    const int y = m / 14, x = m - 14 * (m / 14);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // conv2 data gradient: 14 tiles (one output row each, lanes x >= 14 duplicate x = 13)
+  // x 20 K-steps in two halves.  Waves 0-5 run rows w and w + 8 TOGETHER (one WF
+  // fragment load feeds both rows' MFMAs), waves 6-7 row w.  K-step kk: kyp = kk / 4
+  // (compile-time), o = 4 (kk % 4) + fg, so every A load is a per-(lane, kyp) base
+  // address + an immediate offset: no per-load address arithmetic.
+  {
+    const bool two = wave < 6;
+    const int y0 = wave, y1 = two ? wave + 8 : wave, x = min(fr, 13);
+    const unsigned char* r3b = reinterpret_cast<const unsigned char*>(R3);
+    const unsigned char* base0[5];
+    const unsigned char* base1[5];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // 10 K-steps per batch: 20 operand loads in flight
-      bf16x8 av[10], bv[10];
+    for (int kyp = 0; kyp < 5; ++kyp) {
+      base0[kyp] = r3b + 16 * r3_index(fg, y0 + kyp, x);
+      base1[kyp] = r3b + 16 * r3_index(fg, y1 + kyp, x);
+    }
+    const bf16x8* wfl = WF + fg * 16 + fr;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 a0[10], a1[10], bv[10];
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
-        const int p = 4 * (10 * h + k) + fg, o = p / 5, kyp = p - 5 * (p / 5);
-        av[k] = R3[(o * 18 + y + kyp) * 14 + x];
-        bv[k] = WF[p * 16 + fr];
+        const int kk = 10 * h + k, kyp = kk / 4, orow = 4 * (kk % 4) * 18 * 16 * 16;  // o offset, bytes
+        bv[k] = wfl[kk * 64];
+        a0[k] = *reinterpret_cast<const bf16x8*>(base0[kyp] + orow);
+        if (two) a1[k] = *reinterpret_cast<const bf16x8*>(base1[kyp] + orow);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (two) {
 #pragma unroll
-      for (int k = 0; k < 10; ++k) acc = mfma32(av[k], bv[k], acc);
+        for (int k = 0; k < 10; ++k) {
+          acc0 = mfma32(a0[k], bv[k], acc0);
+          acc1 = mfma32(a1[k], bv[k], acc1);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) acc0 = mfma32(a0[k], bv[k], acc0);
+      }
     }
     if (fr < 6) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int pix = mt * 16 + 4 * fg + i;
-        if (pix < 196) DP1[fr * 196 + pix] = acc[i];
+        const int xo = 4 * fg + i;
+        if (xo < 14) {
+          DP1[fr * 196 + y0 * 14 + xo] = acc0[i];
+          if (two) DP1[fr * 196 + y1 * 14 + xo] = acc1[i];
+        }
       }
     }
   }
   // conv2 weight gradient: dW2[o][(c,ky,kx)] = sum_pix dY2[o][pix] * P1[c][y+ky][x+kx]
-  // (waves 5-7, which hold one data-gradient tile each)
-  if (wave >= 5) {
-    const int nt0 = wave == 5 ? 0 : (wave == 6 ? 4 : 7), nt1 = wave == 5 ? 4 : (wave == 6 ? 7 : 10);
-    for (int nt = nt0; nt < nt1; ++nt) {
-      const int n = nt * 16 + fr, nc = min(n, 149);
-      const int c = nc / 25, ky = (nc % 25) / 5, kx = nc % 5;
-      bf16x8 av[5], bv[5];
+  // 10 column tiles, two per wave in one round, on waves 0, 2, 5, 6, 7: waves w and w + 4
+  // share a SIMD, so this evens the per-SIMD load (paired rows on 0-5, single rows on 6-7,
+  // conv2 bias gradient on 3).  The A operand (dY2 rows) depends only on the lane.
+  if (wave == 0 || wave == 2 || wave >= 5) {
+    const int slot = wave == 0 ? 0 : (wave == 2 ? 1 : wave - 3);
+    const int nt_begin = 2 * slot, nt_end = nt_begin + 2;
+    bf16x8 av[5];
+#pragma unroll
+    for (int sk = 0; sk < 5; ++sk) {
+      const int y = 2 * sk + (fg >> 1), x0 = 8 * (fg & 1);
+      av[sk] = *reinterpret_cast<const bf16x8*>(DY2 + (fr * 10 + y) * 16 + x0);
+    }
+    for (int nt = nt_begin; nt < nt_end; nt += 2) {
+      const bool two = nt + 1 < nt_end;
+      int n[2], boff[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        n[u] = (nt + (two ? u : 0)) * 16 + fr;
+        const int nc = min(n[u], 149);
+        const int c = nc / 25, ky = (nc % 25) / 5, kx = nc % 5;
+        boff[u] = (c * 14 + ky) * 13 + kx;
+      }
+      bf16x8 bv[2][5];
 #pragma unroll
       for (int sk = 0; sk < 5; ++sk) {
         const int y = 2 * sk + (fg >> 1), x0 = 8 * (fg & 1);
-        av[sk] = *reinterpret_cast<const bf16x8*>(DY2 + (fr * 10 + y) * 16 + x0);
-        bv[sk] = R2[(c * 14 + y + ky) * 13 + x0 + kx];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bv[u][sk] = R2[boff[u] + y * 13 + x0];
       }
       __builtin_amdgcn_sched_barrier(0);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int sk = 0; sk < 5; ++sk) acc = mfma32(av[sk], bv[sk], acc);
-      if (n < 150) {
+      for (int sk = 0; sk < 5; ++sk) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st_out(slab, SLAB_C2W + (4 * fg + i) * 150 + n, acc[i], wt);
+        for (int u = 0; u < 2; ++u) acc[u] = mfma32(av[sk], bv[u][sk], acc[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if ((u == 0 || two) && n[u] < 150) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st_out(slab, SLAB_C2W + (4 * fg + i) * 150 + n[u], acc[u][i], wt);
+        }
       }
     }
   }
+  // diagnostic: per-wave end of the phase-E work (block 0, lane 0 of each wave)
+  if (stamps != nullptr && blockIdx.x == 0 && lane == 0) stamps[3000 + wave] = (long long)__builtin_amdgcn_s_memrealtime();
   lds_barrier();
 
   STAMP(6);
@@ -838,7 +892,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     RS1[c * 28 + y] = rs;
   } else {
-    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, LUT, R1, r1_row(t), r1_q(t));  // R2 dead
+    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, R1, r1_row(t), r1_q(t));  // R2 dead
   }
   lds_barrier();
   STAMP(10);

@@ -61,3 +61,15 @@ def test_eval_metric_definitions():
     vl, acc = eval_metrics(loss, corr, batch_size=2)
     # batches: [1,2] [3,4] [10] -> means 1.5, 3.5, 10 -> mean 5.0 (np.mean of batch means)
     assert abs(vl - 5.0) < 1e-12 and abs(acc - 60.0) < 1e-12
+
+
+def test_fma_normalisation_matches_totensor_normalize_in_bf16():
+    """The fused kernel normalises u8 pixels with ONE fma, fmaf(u, 2/255, -1), instead of
+    ToTensor+Normalize ((u/255 - 0.5)/0.5, data_parallelism_train.py:24-27).  The fp32
+    values differ in the last bits, but the bf16 MFMA operand must be identical for all
+    256 codes (fma = exact product + single rounding, emulated in float64)."""
+    import numpy as np
+    u = np.arange(256, dtype=np.float32)
+    exact = (u / np.float32(255) - np.float32(0.5)) / np.float32(0.5)
+    fma = (u.astype(np.float64) * np.float64(np.float32(2.0 / 255.0)) - 1.0).astype(np.float32)
+    assert torch.equal(torch.from_numpy(exact).bfloat16(), torch.from_numpy(fma).bfloat16())

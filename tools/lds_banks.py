@@ -46,6 +46,10 @@ def fr(l): return l & 15
 def fg(l): return l >> 4
 
 
+def r1b(row, x):
+    return row * 32 + (x ^ ((row & 1) * 9 ^ ((row >> 1) & 1) * 4 ^ ((row >> 2) & 1) * 2))
+
+
 def phaseB():
     for t in range(49):
         for sk in range(4):
@@ -91,16 +95,18 @@ def fc1_tr():
                 yield a
 
 
+def r3(o, yy, x):
+    return (o * 18 + yy) * 16 + (x ^ (yy & 7))
+
+
 def dgrad2():
-    for mt in range(13):
+    for mt in range(14):
         for kk in range(20):
-            a, b = [], []
+            a = []
             for l in lanes:
-                m = min(mt * 16 + fr(l), 195)
-                y, x = m // 14, m % 14
-                p = 4 * kk + fg(l)
-                o, kyp = p // 5, p % 5
-                a.append(((o * 18 + y + kyp) * 14 + x) * 16)
+                y, x = mt, min(fr(l), 13)
+                o, kyp = 4 * (kk % 4) + fg(l), kk // 4
+                a.append(r3(o, y + kyp, x) * 16)
             yield a
 
 
@@ -141,16 +147,19 @@ def wgrad1(which):
     return gen
 
 
-def r1_write():
-    # build_r1_part: thread t -> row t>>2, q t&3; writes record row*29 + 8q + x for x in 0..7
-    for w in range(6):
-        for x in range(8):
-            a = []
-            for l in lanes:
-                t = 64 * w + l
-                row, q = (t & 7) + 8 * (t >> 5), (t >> 3) & 3
-                a.append(REGB + (row * 29 + 8 * q + x) * 16 if 8 * q + x < 29 else None)
-            yield a
+def r1_write(fwd):
+    # build_r1_part: thread t -> (row, q); writes records x = 8q .. 8q+7
+    def gen():
+        for w in range(6):
+            for x in range(8):
+                a = []
+                for l in lanes:
+                    t = 64 * w + l
+                    row, q = (t & 7) + 8 * (t >> 5), (t >> 3) & 3
+                    r = r1b(row, 8 * q + x) if fwd else row * 29 + 8 * q + x
+                    a.append(REGB + r * 16 if 8 * q + x < 29 else None)
+                yield a
+    return gen
 
 
 def r3_write():
@@ -163,7 +172,7 @@ def r3_write():
                     a.append(None)
                     continue
                 o, yy = t // 18, t % 18
-                a.append(((o * 18 + yy) * 14 + xr) * 16)
+                a.append(r3(o, yy, xr) * 16)
             yield a
 
 
@@ -177,5 +186,5 @@ if __name__ == "__main__":
     report("E  conv2 wgrad A/B (DY2, R2)", wgrad2)
     report("F  conv1 wgrad A (DY1 rows)", wgrad1("A"))
     report("F  conv1 wgrad B (R1 records)", wgrad1("B"))
-    report("A  R1 record build (write)", r1_write, "w128")
+    report("A/F R1 record build (write)", r1_write(False), "w128")
     report("E  R3 record build (write)", r3_write, "w128")

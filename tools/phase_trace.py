@@ -17,8 +17,7 @@ from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
 
 PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' MLP bwd",
           "E conv2 bwd", "F conv1 wgrad",
-          "  C1 prefetch+R2 build", "  E1 dY2 build", "  E2 wgrad2+col2im", "  E3 dP1 gather",
-          "  F1 dY1 + R1 rebuild"]
+          "  E1 dY2 records build", "  E2 dgrad + wgrad2", "  F1 dY1 + R1 rebuild", "  F2 conv1 wgrad"]
 
 
 def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
@@ -28,6 +27,7 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
     eng.begin_epoch(np.arange(4096, dtype=np.int32))
     stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
     blocks = []
+    waves_e = []
     red = []
     rows = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,16 +53,19 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
         s = stamps.cpu().numpy()
+        waves_e.append((s[3000:3008] - s[8]) * 0.01)
         nb = batch + (39 if in_launch else 0)
         blocks.append(s[16:16 + 4 * nb].reshape(nb, 4).copy())
         if in_launch:
             red.append((s[12:16] - s[0]) * 0.01)
-        rows.append(np.concatenate([np.diff(s[:8]), [s[11] - s[2], s[8] - s[5], s[9] - s[8], s[6] - s[9],
-                                                      s[10] - s[6]]]) * 0.01)  # 100 MHz ticks -> us
+        rows.append(np.concatenate([np.diff(s[:8]), [s[8] - s[5], s[6] - s[8], s[10] - s[6],
+                                                      s[7] - s[10]]]) * 0.01)  # 100 MHz ticks -> us
     med = np.median(np.array(rows[5:]), axis=0)
     for name, v in zip(PHASES, med):
         print(f"{name:20s} {v:8.2f} us")
     print(f"{'sum (block 0)':20s} {med[:7].sum():8.2f} us")
+    we = np.median(np.array(waves_e[5:]), axis=0)
+    print("  E2 per-wave finish (us after E1):", " ".join(f"w{i}:{v:.2f}" for i, v in enumerate(we)))
     print(f"{'kernel wall (event)':20s} {np.median(walls[5:]):8.2f} us")
     # per-block timeline (us from the earliest block start), medians over repeats
     bl = np.array(blocks[5:])  # [reps, nb, 4]
