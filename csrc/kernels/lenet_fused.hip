@@ -389,8 +389,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   uint8_t* IMGS = smem + L_IMG;
 
   // ============ phase A: ingest + weight staging ======================================
-  // Plain loads first (image, conv B fragments, conv biases), consumed before the fc1
-  // LDS-DMA is issued (hipcc would otherwise drain the DMA at their first use).
+  // Plain loads first: the image (issued first, so storing it to LDS waits for it alone),
+  // then the conv B fragments and biases, whose latency hides behind the R1 record build;
+  // they are consumed before the fc1 LDS-DMA is issued (hipcc would otherwise drain the
+  // DMA at their first use, or under-count vmcnt for them).
   const uint4 im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
 #pragma unroll
@@ -407,12 +409,16 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
   else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  lds_barrier();
+  STAMP(9);
+  if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
 #pragma unroll
   for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
 #pragma unroll
   for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
   consume(bias_c1);
   consume(bias_c2);
+  STAMP(11);
   {
     // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all
     // in-arena); 12 per wave with the index clamped (a duplicate copies identical bytes)
@@ -424,8 +430,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       dma16(f1src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
     }
   }
-  lds_barrier();
-  if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
   lds_barrier();
   STAMP(1);
 

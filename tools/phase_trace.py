@@ -17,7 +17,8 @@ from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
 
 PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' MLP bwd",
           "E conv2 bwd", "F conv1 wgrad",
-          "  E1 dY2 records build", "  E2 dgrad + wgrad2", "  F1 dY1 + R1 rebuild", "  F2 conv1 wgrad"]
+          "  E1 dY2 records build", "  E2 dgrad + wgrad2", "  F1 dY1 + R1 rebuild", "  F2 conv1 wgrad",
+          "  A1 image landed", "  A2 R1 build + weights landed", "  A3 fc1 DMA issue + barrier"]
 
 
 def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
@@ -59,7 +60,8 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
         if in_launch:
             red.append((s[12:16] - s[0]) * 0.01)
         rows.append(np.concatenate([np.diff(s[:8]), [s[8] - s[5], s[6] - s[8], s[10] - s[6],
-                                                      s[7] - s[10]]]) * 0.01)  # 100 MHz ticks -> us
+                                                      s[7] - s[10], s[9] - s[0], s[11] - s[9],
+                                                      s[1] - s[11]]]) * 0.01)  # 100 MHz ticks -> us
     med = np.median(np.array(rows[5:]), axis=0)
     for name, v in zip(PHASES, med):
         print(f"{name:20s} {v:8.2f} us")
