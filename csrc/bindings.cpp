@@ -95,6 +95,66 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_grad_reduce(a, S(stream));
   });
   m.def("init", []() { dnn::init_kernels(); });
+  // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
+  m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
+    dnn::launch_ingest(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(ids), batch, per_img,
+                       P<float>(out), P<int32_t>(lab_out), S(stream));
+  });
+  m.def("im2col", [](u x, int B, int C, int H, int W, int K, int pad, u cols, u stream) {
+    dnn::launch_im2col(P<const float>(x), B, C, H, W, K, pad, P<float>(cols), S(stream));
+  });
+  m.def("col2im", [](u dcols, int B, int C, int H, int W, int K, int pad, u dx, u stream) {
+    dnn::launch_col2im(P<const float>(dcols), B, C, H, W, K, pad, P<float>(dx), S(stream));
+  });
+  m.def("relu_pool_fwd", [](u x, int BC, int H, int W, u y, u code, u stream) {
+    dnn::launch_relu_pool_fwd(P<const float>(x), BC, H, W, P<float>(y), P<uint8_t>(code), S(stream));
+  });
+  m.def("relu_pool_bwd", [](u dy, u code, int BC, int H, int W, u dx, u stream) {
+    dnn::launch_relu_pool_bwd(P<const float>(dy), P<const uint8_t>(code), BC, H, W, P<float>(dx), S(stream));
+  });
+  m.def("relu_fwd", [](u x, long n, u y, u stream) { dnn::launch_relu_fwd(P<const float>(x), n, P<float>(y), S(stream)); });
+  m.def("relu_bwd", [](u dy, u y, long n, u dx, u stream) {
+    dnn::launch_relu_bwd(P<const float>(dy), P<const float>(y), n, P<float>(dx), S(stream));
+  });
+  m.def("bias_add", [](u y, u bias, int B, int C, int L, u stream) {
+    dnn::launch_bias_add(P<float>(y), P<const float>(bias), B, C, L, S(stream));
+  });
+  m.def("bn_fwd_train", [](u x, int B, int C, int L, u state, u gamma, u beta, float eps, float mom, u rmean,
+                           u rvar, u y, u smean, u sinvstd, u stream) {
+    dnn::launch_bn_fwd_train(P<const float>(x), B, C, L, P<const int32_t>(state), P<const float>(gamma),
+                             P<const float>(beta), eps, mom, P<float>(rmean), P<float>(rvar), P<float>(y),
+                             P<float>(smean), P<float>(sinvstd), S(stream));
+  });
+  m.def("bn_fwd_eval", [](u x, int B, int C, int L, u gamma, u beta, float eps, u rmean, u rvar, u y, u stream) {
+    dnn::launch_bn_fwd_eval(P<const float>(x), B, C, L, P<const float>(gamma), P<const float>(beta), eps,
+                            P<const float>(rmean), P<const float>(rvar), P<float>(y), S(stream));
+  });
+  m.def("bn_bwd", [](u dy, u x, int B, int C, int L, u state, u gamma, u smean, u sinvstd, u dx, u dgamma,
+                     u dbeta, u stream) {
+    dnn::launch_bn_bwd(P<const float>(dy), P<const float>(x), B, C, L, P<const int32_t>(state), P<const float>(gamma),
+                       P<const float>(smean), P<const float>(sinvstd), P<float>(dx), P<float>(dgamma),
+                       P<float>(dbeta), S(stream));
+  });
+  m.def("xent", [](u logits, u labels, int B, int NC, u state, u loss, u correct, u dlogits, u stream) {
+    dnn::launch_xent(P<const float>(logits), P<const int32_t>(labels), B, NC, P<const int32_t>(state), P<float>(loss),
+                     P<int32_t>(correct), P<float>(dlogits), S(stream));
+  });
+  m.def("layer_bookkeeping", [](u loss, u correct, int batch, u state, u stats, u order, int order_len,
+                                u batch_ids, u stream) {
+    dnn::ReduceArgs a{};
+    a.loss = P<const float>(loss);
+    a.correct = P<const int32_t>(correct);
+    a.batch = batch;
+    a.state = P<int32_t>(state);
+    a.stats = P<double>(stats);
+    a.order = P<const int32_t>(order);
+    a.order_len = order_len;
+    a.batch_ids = P<int32_t>(batch_ids);
+    dnn::launch_layer_bookkeeping(a, S(stream));
+  });
+  m.def("sgd_flat", [](u p, u g, u mom, long n, float lr, float momentum, float grad_scale, u stream) {
+    dnn::launch_sgd_flat(P<float>(p), P<const float>(g), P<float>(mom), n, lr, momentum, grad_scale, S(stream));
+  });
   // native RCCL communicator (comm/rccl_comm.cpp)
   m.def("rccl_open", &dnn::rccl_open, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dnn::rccl_unique_id()); });

@@ -34,4 +34,27 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
 void launch_sgd_apply(float* master, const float* grad, float* mom, bf16* shadow, int n, float lr, float momentum,
                       float grad_scale, int pack_only, hipStream_t stream);
 
+// ---- generic layer kernels (layers.hip) --------------------------------------------------
+void launch_ingest(const uint8_t* images, const int32_t* labels, const int32_t* ids, int batch, int per_img,
+                   float* out, int32_t* lab_out, hipStream_t s);
+void launch_im2col(const float* x, int B, int C, int H, int W, int K, int pad, float* cols, hipStream_t s);
+void launch_col2im(const float* dcols, int B, int C, int H, int W, int K, int pad, float* dx, hipStream_t s);
+void launch_relu_pool_fwd(const float* x, int BC, int H, int W, float* y, uint8_t* code, hipStream_t s);
+void launch_relu_pool_bwd(const float* dy, const uint8_t* code, int BC, int H, int W, float* dx, hipStream_t s);
+void launch_relu_fwd(const float* x, long n, float* y, hipStream_t s);
+void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStream_t s);
+void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream_t s);
+void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                         const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
+                         float* sinvstd, hipStream_t s);
+void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
+                        const float* rmean, const float* rvar, float* y, hipStream_t s);
+void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, hipStream_t s);
+void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
+                 int32_t* correct, float* dlogits, hipStream_t s);
+void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s);
+void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     hipStream_t s);
+
 }  // namespace dnn

@@ -1,0 +1,384 @@
+// Generic CNN layer kernels (gfx950) for the modular engine (runtime/layer_engine.py).
+//
+// The fused LeNet kernel (lenet_fused.hip) is the fast path for the reference model.
+// These kernels make the framework usable for other CNN stacks built from the layer set
+// the north star names - Conv2d, ReLU, MaxPool, BatchNorm, Linear, CrossEntropy, SGD -
+// in fp32 (exact parity with the reference's fp32 CPU arithmetic) or with bf16 GEMM
+// operands.  Capability parity: the ATen ops of SURVEY.md §2.5 K0-K23.
+//
+// Split of work (MI355X-first):
+//  * the GEMM-shaped parts of Conv2d / Linear go to the library GEMMs (hipBLASLt via
+//    torch.matmul): conv = im2col (here) -> batched GEMM -> col2im (here, a deterministic
+//    gather instead of an atomic scatter);
+//  * everything else is a hand-written kernel: ingest (u8 gather + ToTensor/Normalize),
+//    fused ReLU + 2x2 max-pool with a 2-bit argmax code (the same encoding as the fused
+//    kernel: 4 = no gradient), BatchNorm2d train/eval forward + backward with the tail
+//    batch masked out of the statistics, fused softmax cross-entropy forward + backward +
+//    accuracy, step bookkeeping (shared with the fused path), flat momentum SGD.
+//  * every reduction is a fixed-order tree (no float atomics): bitwise reproducible.
+#include "reduce_common.h"
+
+namespace dnn {
+
+namespace {
+
+constexpr int LT = 256;  // threads per block of the element-wise kernels
+
+__device__ __forceinline__ int valid_count(const int32_t* state, int batch) {
+  return state ? min(state[ST_BVALID], batch) : batch;
+}
+
+// ---- ingest: gather the batch's u8 images by sample id, ToTensor + Normalize ----------
+__global__ void __launch_bounds__(LT) ingest_kernel(const uint8_t* __restrict__ images,
+                                                    const int32_t* __restrict__ labels,
+                                                    const int32_t* __restrict__ ids, int batch, int per_img,
+                                                    float* __restrict__ out, int32_t* __restrict__ lab_out) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  const long total = (long)batch * per_img;
+  if (i >= total) return;
+  const int b = (int)(i / per_img), e = (int)(i - (long)b * per_img);
+  const int sid = ids[b];
+  const uint32_t u = images[(size_t)sid * per_img + e];
+  // torchvision op order (data_parallelism_train.py:24-27), IEEE-rounded division
+  out[i] = __fdiv_rn(__fdiv_rn((float)u, 255.0f) - 0.5f, 0.5f);
+  if (e == 0) lab_out[b] = labels[sid];
+}
+
+// ---- im2col / col2im (stride 1, square kernel, zero padding) -----------------------
+// cols[b][(c*K + ky)*K + kx][oy*OW + ox] = x[b][c][oy+ky-pad][ox+kx-pad]
+__global__ void __launch_bounds__(LT) im2col_kernel(const float* __restrict__ x, int B, int C, int H, int W,
+                                                    int K, int pad, int OH, int OW, float* __restrict__ cols) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  const int L = OH * OW, CKK = C * K * K;
+  const long total = (long)B * CKK * L;
+  if (i >= total) return;
+  const int l = (int)(i % L);
+  const long r = i / L;
+  const int ck = (int)(r % CKK), b = (int)(r / CKK);
+  const int c = ck / (K * K), kk = ck - c * K * K, ky = kk / K, kx = kk - ky * K;
+  const int oy = l / OW, ox = l - oy * OW;
+  const int y = oy + ky - pad, xx = ox + kx - pad;
+  cols[i] = (y >= 0 && y < H && xx >= 0 && xx < W) ? x[(((size_t)b * C + c) * H + y) * W + xx] : 0.f;
+}
+
+// dx[b][c][y][x] = sum over (ky, kx) of dcols[b][(c,ky,kx)][(y-ky+pad, x-kx+pad)]: a gather
+// in a fixed (ky, kx) order - deterministic, no atomics.
+__global__ void __launch_bounds__(LT) col2im_kernel(const float* __restrict__ dcols, int B, int C, int H, int W,
+                                                    int K, int pad, int OH, int OW, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  const long total = (long)B * C * H * W;
+  if (i >= total) return;
+  const int xx = (int)(i % W);
+  long r = i / W;
+  const int y = (int)(r % H);
+  r /= H;
+  const int c = (int)(r % C), b = (int)(r / C);
+  const int L = OH * OW, CKK = C * K * K;
+  float s = 0.f;
+  for (int ky = 0; ky < K; ++ky) {
+    const int oy = y - ky + pad;
+    if (oy < 0 || oy >= OH) continue;
+    for (int kx = 0; kx < K; ++kx) {
+      const int ox = xx - kx + pad;
+      if (ox < 0 || ox >= OW) continue;
+      s += dcols[((size_t)b * CKK + (c * K + ky) * K + kx) * L + oy * OW + ox];
+    }
+  }
+  dx[i] = s;
+}
+
+// ---- fused ReLU + 2x2 max-pool (stride 2, floor) with a 2-bit argmax code -------------
+// max_pool2d(relu(x)) == relu(max_pool2d(x)); code = first argmax (torch order) or 4 when
+// the max is <= 0 (no gradient reaches the input: ReLU and pool backward in one test).
+__global__ void __launch_bounds__(LT) relu_pool_fwd_kernel(const float* __restrict__ x, int BC, int H, int W,
+                                                           float* __restrict__ y, uint8_t* __restrict__ code) {
+  const int OH = H / 2, OW = W / 2;
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= (long)BC * OH * OW) return;
+  const int ox = (int)(i % OW);
+  const long r = i / OW;
+  const int oy = (int)(r % OH), bc = (int)(r / OH);
+  const float* p = x + ((size_t)bc * H + 2 * oy) * W + 2 * ox;
+  float best = p[0];
+  int arg = 0;
+  const float v1 = p[1], v2 = p[W], v3 = p[W + 1];
+  if (v1 > best) { best = v1; arg = 1; }
+  if (v2 > best) { best = v2; arg = 2; }
+  if (v3 > best) { best = v3; arg = 3; }
+  y[i] = fmaxf(best, 0.f);
+  code[i] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+}
+
+__global__ void __launch_bounds__(LT) relu_pool_bwd_kernel(const float* __restrict__ dy,
+                                                           const uint8_t* __restrict__ code, int BC, int H, int W,
+                                                           float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= (long)BC * H * W) return;
+  const int OH = H / 2, OW = W / 2;
+  const int xx = (int)(i % W);
+  const long r = i / W;
+  const int y = (int)(r % H), bc = (int)(r / H);
+  const int oy = y >> 1, ox = xx >> 1;
+  float v = 0.f;
+  if (oy < OH && ox < OW) {
+    const long o = ((long)bc * OH + oy) * OW + ox;
+    if (code[o] == (uint8_t)(((y & 1) << 1) | (xx & 1))) v = dy[o];
+  }
+  dx[i] = v;
+}
+
+// ---- ReLU (for the fc stack) ------------------------------------------------------------
+__global__ void __launch_bounds__(LT) relu_fwd_kernel(const float* __restrict__ x, long n, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i < n) y[i] = fmaxf(x[i], 0.f);
+}
+__global__ void __launch_bounds__(LT) relu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                      long n, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i < n) dx[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+// ---- per-channel bias add (conv output [B][C][L]) ----------------------------------------
+__global__ void __launch_bounds__(LT) bias_add_kernel(float* __restrict__ y, const float* __restrict__ bias,
+                                                      int B, int C, int L) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= (long)B * C * L) return;
+  y[i] += bias[(i / L) % C];
+}
+
+// ---- block reduction (fixed order) ----------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], float* red) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[wave * N + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float s = 0.f;
+    for (int w = 0; w < LT / 64; ++w) s += red[w * N + k];
+    v[k] = s;
+  }
+}
+
+// ---- BatchNorm2d -------------------------------------------------------------------------
+// One block per channel.  Training: batch statistics over the VALID samples only (the
+// padded tail batch of a captured step must not pollute them), biased variance for the
+// normalisation, unbiased for the running estimate (torch semantics, momentum m).
+__global__ void __launch_bounds__(LT) bn_fwd_train_kernel(const float* __restrict__ x, int B, int C, int L,
+                                                          const int32_t* __restrict__ state,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float m,
+                                                          float* __restrict__ running_mean,
+                                                          float* __restrict__ running_var, float* __restrict__ y,
+                                                          float* __restrict__ save_mean,
+                                                          float* __restrict__ save_invstd) {
+  __shared__ float red[(LT / 64) * 2];
+  const int c = blockIdx.x;
+  const int bv = valid_count(state, B);
+  const long n = (long)bv * L;
+  float s[1] = {0.f};
+  for (long t = threadIdx.x; t < n; t += LT) {
+    const long b = t / L, l = t - b * L;
+    s[0] += x[((size_t)b * C + c) * L + l];
+  }
+  block_sum<1>(s, red);
+  const float mean = n > 0 ? s[0] / (float)n : 0.f;
+  float q[1] = {0.f};
+  for (long t = threadIdx.x; t < n; t += LT) {
+    const long b = t / L, l = t - b * L;
+    const float d = x[((size_t)b * C + c) * L + l] - mean;
+    q[0] += d * d;
+  }
+  block_sum<1>(q, red);
+  const float var = n > 0 ? q[0] / (float)n : 0.f;
+  const float invstd = rsqrtf(var + eps);
+  const float g = gamma[c], bb = beta[c];
+  for (long t = threadIdx.x; t < (long)B * L; t += LT) {
+    const long b = t / L, l = t - b * L;
+    const size_t o = ((size_t)b * C + c) * L + l;
+    y[o] = b < bv ? (x[o] - mean) * invstd * g + bb : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (n > 0) {
+      const float unb = n > 1 ? var * (float)n / (float)(n - 1) : var;
+      running_mean[c] = (1.f - m) * running_mean[c] + m * mean;
+      running_var[c] = (1.f - m) * running_var[c] + m * unb;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(LT) bn_fwd_eval_kernel(const float* __restrict__ x, int B, int C, int L,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps,
+                                                         const float* __restrict__ running_mean,
+                                                         const float* __restrict__ running_var,
+                                                         float* __restrict__ y) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= (long)B * C * L) return;
+  const int c = (int)((i / L) % C);
+  y[i] = (x[i] - running_mean[c]) * rsqrtf(running_var[c] + eps) * gamma[c] + beta[c];
+}
+
+__global__ void __launch_bounds__(LT) bn_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                    int B, int C, int L, const int32_t* __restrict__ state,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ save_mean,
+                                                    const float* __restrict__ save_invstd,
+                                                    float* __restrict__ dx, float* __restrict__ dgamma,
+                                                    float* __restrict__ dbeta) {
+  __shared__ float red[(LT / 64) * 2];
+  const int c = blockIdx.x;
+  const int bv = valid_count(state, B);
+  const long n = (long)bv * L;
+  const float mean = save_mean[c], invstd = save_invstd[c];
+  float s[2] = {0.f, 0.f};  // sum dy, sum dy * xhat
+  for (long t = threadIdx.x; t < n; t += LT) {
+    const long b = t / L, l = t - b * L;
+    const size_t o = ((size_t)b * C + c) * L + l;
+    const float d = dy[o];
+    s[0] += d;
+    s[1] += d * (x[o] - mean) * invstd;
+  }
+  block_sum<2>(s, red);
+  const float g = gamma[c];
+  const float mdy = n > 0 ? s[0] / (float)n : 0.f, mdyx = n > 0 ? s[1] / (float)n : 0.f;
+  for (long t = threadIdx.x; t < (long)B * L; t += LT) {
+    const long b = t / L, l = t - b * L;
+    const size_t o = ((size_t)b * C + c) * L + l;
+    dx[o] = b < bv ? g * invstd * (dy[o] - mdy - (x[o] - mean) * invstd * mdyx) : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    dgamma[c] = s[1];
+    dbeta[c] = s[0];
+  }
+}
+
+// ---- fused softmax cross-entropy forward + backward + accuracy -----------------------------
+// One thread per sample.  loss[b] / correct[b] per sample (0 for the padded tail),
+// dlogits = (softmax - onehot) / bvalid  (CrossEntropyLoss mean reduction).
+__global__ void __launch_bounds__(LT) xent_kernel(const float* __restrict__ logits, const int32_t* __restrict__ labels,
+                                                  int B, int NC, const int32_t* __restrict__ state,
+                                                  float* __restrict__ loss, int32_t* __restrict__ correct,
+                                                  float* __restrict__ dlogits) {
+  const int b = blockIdx.x * LT + threadIdx.x;
+  if (b >= B) return;
+  const int bv = valid_count(state, B);
+  const float* z = logits + (size_t)b * NC;
+  float* dz = dlogits ? dlogits + (size_t)b * NC : nullptr;
+  if (b >= bv) {
+    loss[b] = 0.f;
+    correct[b] = 0;
+    if (dz) for (int k = 0; k < NC; ++k) dz[k] = 0.f;
+    return;
+  }
+  float mx = z[0];
+  int arg = 0;
+  for (int k = 1; k < NC; ++k) {
+    if (z[k] > mx) { mx = z[k]; arg = k; }  // first max wins (torch.argmax)
+  }
+  float sum = 0.f;
+  for (int k = 0; k < NC; ++k) sum += expf(z[k] - mx);
+  const int y = labels[b];
+  loss[b] = mx + logf(sum) - z[y];
+  correct[b] = arg == y ? 1 : 0;
+  if (dz) {
+    const float inv = 1.f / (float)bv;
+    for (int k = 0; k < NC; ++k) dz[k] = (expf(z[k] - mx) / sum - (k == y ? 1.f : 0.f)) * inv;
+  }
+}
+
+// ---- step bookkeeping (epoch loss/accuracy, next batch ids) - shared with the fused path --
+__global__ void __launch_bounds__(64) layer_bookkeeping_kernel(ReduceArgs a) { bookkeeping<false>(a, threadIdx.x); }
+
+// ---- flat momentum SGD over an arena (no bf16 shadow: generic models) -------------------------
+__global__ void __launch_bounds__(LT) sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, long n, float lr, float momentum,
+                                                      float grad_scale) {
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i] * grad_scale;
+  const float mi = momentum * m[i] + gi;  // torch.optim.SGD: dampening 0, no nesterov
+  m[i] = mi;
+  p[i] -= lr * mi;
+}
+
+inline unsigned blocks(long n) { return (unsigned)((n + LT - 1) / LT); }
+
+}  // namespace
+
+void launch_ingest(const uint8_t* images, const int32_t* labels, const int32_t* ids, int batch, int per_img,
+                   float* out, int32_t* lab_out, hipStream_t s) {
+  const long n = (long)batch * per_img;
+  if (n) hipLaunchKernelGGL(ingest_kernel, dim3(blocks(n)), dim3(LT), 0, s, images, labels, ids, batch, per_img, out,
+                            lab_out);
+}
+void launch_im2col(const float* x, int B, int C, int H, int W, int K, int pad, float* cols, hipStream_t s) {
+  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  const long n = (long)B * C * K * K * OH * OW;
+  if (n) hipLaunchKernelGGL(im2col_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, B, C, H, W, K, pad, OH, OW, cols);
+}
+void launch_col2im(const float* dcols, int B, int C, int H, int W, int K, int pad, float* dx, hipStream_t s) {
+  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  const long n = (long)B * C * H * W;
+  if (n) hipLaunchKernelGGL(col2im_kernel, dim3(blocks(n)), dim3(LT), 0, s, dcols, B, C, H, W, K, pad, OH, OW, dx);
+}
+void launch_relu_pool_fwd(const float* x, int BC, int H, int W, float* y, uint8_t* code, hipStream_t s) {
+  const long n = (long)BC * (H / 2) * (W / 2);
+  if (n) hipLaunchKernelGGL(relu_pool_fwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, BC, H, W, y, code);
+}
+void launch_relu_pool_bwd(const float* dy, const uint8_t* code, int BC, int H, int W, float* dx, hipStream_t s) {
+  const long n = (long)BC * H * W;
+  if (n) hipLaunchKernelGGL(relu_pool_bwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, dy, code, BC, H, W, dx);
+}
+void launch_relu_fwd(const float* x, long n, float* y, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(relu_fwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, n, y);
+}
+void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(relu_bwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, dy, y, n, dx);
+}
+void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream_t s) {
+  const long n = (long)B * C * L;
+  if (n) hipLaunchKernelGGL(bias_add_kernel, dim3(blocks(n)), dim3(LT), 0, s, y, bias, B, C, L);
+}
+void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                         const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
+                         float* sinvstd, hipStream_t s) {
+  if (C) hipLaunchKernelGGL(bn_fwd_train_kernel, dim3(C), dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m,
+                            rmean, rvar, y, smean, sinvstd);
+}
+void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
+                        const float* rmean, const float* rvar, float* y, hipStream_t s) {
+  const long n = (long)B * C * L;
+  if (n) hipLaunchKernelGGL(bn_fwd_eval_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, B, C, L, gamma, beta, eps, rmean,
+                            rvar, y);
+}
+void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, hipStream_t s) {
+  if (C) hipLaunchKernelGGL(bn_bwd_kernel, dim3(C), dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
+                            dgamma, dbeta);
+}
+void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
+                 int32_t* correct, float* dlogits, hipStream_t s) {
+  if (B) hipLaunchKernelGGL(xent_kernel, dim3(blocks(B)), dim3(LT), 0, s, logits, labels, B, NC, state, loss, correct,
+                            dlogits);
+}
+void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(layer_bookkeeping_kernel, dim3(1), dim3(64), 0, s, a);
+}
+void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     hipStream_t s) {
+  if (n) hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks(n)), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale);
+}
+
+}  // namespace dnn

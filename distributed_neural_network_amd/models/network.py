@@ -65,11 +65,11 @@ class ArenaLayout:
     num_params: int     # real parameter count (62,006)
 
     @staticmethod
-    def build() -> "ArenaLayout":
+    def build(param_shapes: "List[Tuple[str, Tuple[int, ...]]] | None" = None) -> "ArenaLayout":
         offsets, shapes = {}, {}
         cur = 0
         n = 0
-        for key, shape in PARAM_SHAPES:
+        for key, shape in (PARAM_SHAPES if param_shapes is None else param_shapes):
             offsets[key] = cur
             shapes[key] = shape
             k = _numel(shape)
@@ -90,7 +90,7 @@ class ArenaLayout:
 
     def views(self, arena: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
         out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
-        for key, shape in PARAM_SHAPES:
+        for key, shape in self.shapes.items():
             o = self.offsets[key]
             out[key] = arena[o:o + _numel(shape)].view(shape)
         return out
@@ -98,7 +98,7 @@ class ArenaLayout:
     def pad_mask(self) -> torch.Tensor:
         """Boolean mask over the arena: True where a real parameter lives."""
         m = torch.zeros(self.total, dtype=torch.bool)
-        for key, shape in PARAM_SHAPES:
+        for key, shape in self.shapes.items():
             o = self.offsets[key]
             m[o:o + _numel(shape)] = True
         return m

@@ -29,6 +29,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 HIP_SOURCES = [
     CSRC / "kernels" / "lenet_fused.hip",
     CSRC / "kernels" / "reduce_sgd.hip",
+    CSRC / "kernels" / "layers.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"
 HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp"]

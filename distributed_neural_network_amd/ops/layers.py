@@ -1,0 +1,271 @@
+"""Autograd layer ops of the modular engine, backed by csrc/kernels/layers.hip on MI355X.
+
+Every op has two implementations with the SAME semantics:
+
+* on a ROCm device: the hand-written gfx950 kernels (``_dnn_hip``) for everything that is
+  not a plain GEMM, and the library GEMMs (hipBLASLt via ``torch.matmul``) for the
+  matrix products of Conv2d (im2col -> batched GEMM -> col2im) and Linear;
+* on the CPU: plain PyTorch ops - the test double / CPU-only path (never used on a GPU:
+  a missing extension there raises instead of silently falling back).
+
+Masking: a captured training step always runs the full batch shape; ``state`` (device
+int32, word ST_BVALID) holds how many samples of it are real.  BatchNorm statistics and
+the cross-entropy mean exclude the padded tail, exactly like the reference's smaller
+last batch (drop_last=False, data_parallelism_train.py:74-79).
+
+Capability parity: the ATen ops of SURVEY.md §2.5 (K1-K20) - conv (fwd, dgrad, wgrad),
+ReLU, max-pool (with first-max tie-break), BatchNorm2d (north star), linear,
+CrossEntropyLoss (mean), SGD-momentum.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+ST_BVALID = 1
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _ext():
+    return native.hip()
+
+
+def _s(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def _bvalid_cpu(state: torch.Tensor | None, batch: int) -> int:
+    return batch if state is None else min(int(state[ST_BVALID]), batch)
+
+
+def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Library GEMM with optional bf16 operands (fp32 accumulate / result)."""
+    if dtype == torch.float32:
+        return torch.matmul(a, b)
+    return torch.matmul(a.to(dtype), b.to(dtype)).float()
+
+
+# ---- Conv2d (stride 1, square kernel, zero padding) -------------------------------------------
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype):
+        B, C, H, W = x.shape
+        Cout, _, K, _ = w.shape
+        OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+        x = x.contiguous()
+        if _is_gpu(x):
+            cols = torch.empty(B, C * K * K, OH * OW, device=x.device, dtype=torch.float32)
+            _ext().im2col(_p(x), B, C, H, W, K, pad, _p(cols), _s(x))
+        else:
+            cols = F.unfold(x, K, padding=pad)
+        y = _gemm(w.reshape(Cout, -1), cols, gemm_dtype)  # [B, Cout, L]: NCHW directly
+        if _is_gpu(x):
+            _ext().bias_add(_p(y), _p(b), B, Cout, OH * OW, _s(x))
+        else:
+            y = y + b.view(1, Cout, 1)
+        ctx.save_for_backward(cols, w)
+        ctx.shape = (B, C, H, W, K, pad, OH, OW)
+        ctx.gemm_dtype = gemm_dtype
+        return y.view(B, Cout, OH, OW)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, w = ctx.saved_tensors
+        B, C, H, W, K, pad, OH, OW = ctx.shape
+        Cout = w.shape[0]
+        dy2 = dy.contiguous().view(B, Cout, OH * OW)
+        dw = _gemm(dy2, cols.transpose(1, 2), ctx.gemm_dtype).sum(0).view_as(w)
+        db = dy2.sum((0, 2))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
+            if _is_gpu(dy):
+                dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
+                _ext().col2im(_p(dcols), B, C, H, W, K, pad, _p(dx), _s(dy))
+            else:
+                dx = F.fold(dcols, (H, W), K, padding=pad)
+        return dx, dw, db, None, None
+
+
+# ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------
+class ReluPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        OH, OW = H // 2, W // 2
+        x = x.contiguous()
+        if _is_gpu(x):
+            y = torch.empty(B, C, OH, OW, device=x.device, dtype=torch.float32)
+            code = torch.empty(B, C, OH, OW, device=x.device, dtype=torch.uint8)
+            _ext().relu_pool_fwd(_p(x), B * C, H, W, _p(y), _p(code), _s(x))
+        else:
+            win = x[:, :, :2 * OH, :2 * OW].reshape(B, C, OH, 2, OW, 2).permute(0, 1, 2, 4, 3, 5)
+            win = win.reshape(B, C, OH, OW, 4)
+            best, arg = win.max(-1)  # first maximal index (torch tie rule)
+            y = best.clamp_min(0.0)
+            code = torch.where(best > 0, arg, torch.full_like(arg, 4)).to(torch.uint8)
+        ctx.save_for_backward(code)
+        ctx.shape = (B, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (code,) = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        dy = dy.contiguous()
+        if _is_gpu(dy):
+            dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
+            _ext().relu_pool_bwd(_p(dy), _p(code), B * C, H, W, _p(dx), _s(dy))
+            return dx
+        OH, OW = H // 2, W // 2
+        pos = torch.arange(4).view(1, 1, 1, 1, 4)
+        g = torch.where(code.long().unsqueeze(-1) == pos, dy.unsqueeze(-1), torch.zeros(()))
+        g = g.view(B, C, OH, OW, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, 2 * OH, 2 * OW)
+        dx = torch.zeros(B, C, H, W)
+        dx[:, :, :2 * OH, :2 * OW] = g
+        return dx
+
+
+# ---- ReLU -----------------------------------------------------------------------------------
+class ReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        if _is_gpu(x):
+            y = torch.empty_like(x)
+            _ext().relu_fwd(_p(x), x.numel(), _p(y), _s(x))
+        else:
+            y = x.clamp_min(0.0)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        if _is_gpu(dy):
+            dx = torch.empty_like(dy)
+            _ext().relu_bwd(_p(dy), _p(y), dy.numel(), _p(dx), _s(dy))
+            return dx
+        return torch.where(y > 0, dy, torch.zeros(()))
+
+
+# ---- Linear ---------------------------------------------------------------------------------
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, gemm_dtype: torch.dtype):
+        ctx.save_for_backward(x, w)
+        ctx.gemm_dtype = gemm_dtype
+        return _gemm(x, w.t(), gemm_dtype) + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = _gemm(dy, w, ctx.gemm_dtype) if ctx.needs_input_grad[0] else None
+        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None
+
+
+# ---- BatchNorm2d (train: masked batch statistics; eval: running statistics) -----------------
+class BatchNorm2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, state, training: bool, eps: float, momentum: float):
+        B, C, H, W = x.shape
+        L = H * W
+        x = x.contiguous()
+        if not training:
+            if _is_gpu(x):
+                y = torch.empty_like(x)
+                _ext().bn_fwd_eval(_p(x), B, C, L, _p(gamma), _p(beta), eps, _p(running_mean), _p(running_var),
+                                   _p(y), _s(x))
+            else:
+                y = (x - running_mean.view(1, C, 1, 1)) * torch.rsqrt(running_var.view(1, C, 1, 1) + eps) \
+                    * gamma.view(1, C, 1, 1) + beta.view(1, C, 1, 1)
+            ctx.training = False
+            return y
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        if _is_gpu(x):
+            y = torch.empty_like(x)
+            _ext().bn_fwd_train(_p(x), B, C, L, _p(state) if state is not None else 0, _p(gamma), _p(beta), eps,
+                                momentum, _p(running_mean), _p(running_var), _p(y), _p(mean), _p(invstd), _s(x))
+        else:
+            bv = _bvalid_cpu(state, B)
+            xv = x[:bv]
+            n = bv * L
+            mu = xv.mean((0, 2, 3)) if bv else torch.zeros(C)
+            var = ((xv - mu.view(1, C, 1, 1)) ** 2).mean((0, 2, 3)) if bv else torch.zeros(C)
+            mean.copy_(mu)
+            invstd.copy_(torch.rsqrt(var + eps))
+            y = torch.zeros_like(x)
+            y[:bv] = (xv - mu.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1) * gamma.view(1, C, 1, 1) \
+                + beta.view(1, C, 1, 1)
+            if n > 0:
+                unb = var * n / (n - 1) if n > 1 else var
+                running_mean.mul_(1 - momentum).add_(momentum * mu)
+                running_var.mul_(1 - momentum).add_(momentum * unb)
+        ctx.training = True
+        ctx.save_for_backward(x, gamma, mean, invstd, state if state is not None else torch.zeros(0))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        assert ctx.training, "BatchNorm2d backward in eval mode is not supported"
+        x, gamma, mean, invstd, state = ctx.saved_tensors
+        state = state if state.numel() else None
+        B, C, H, W = x.shape
+        L = H * W
+        dy = dy.contiguous()
+        if _is_gpu(dy):
+            dx = torch.empty_like(x)
+            dgamma = torch.empty(C, device=x.device, dtype=torch.float32)
+            dbeta = torch.empty(C, device=x.device, dtype=torch.float32)
+            _ext().bn_bwd(_p(dy), _p(x), B, C, L, _p(state) if state is not None else 0, _p(gamma), _p(mean),
+                          _p(invstd), _p(dx), _p(dgamma), _p(dbeta), _s(dy))
+            return dx, dgamma, dbeta, None, None, None, None, None, None
+        bv = _bvalid_cpu(state, B)
+        n = bv * L
+        xhat = (x[:bv] - mean.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
+        d = dy[:bv]
+        dbeta = d.sum((0, 2, 3))
+        dgamma = (d * xhat).sum((0, 2, 3))
+        dx = torch.zeros_like(x)
+        if n:
+            dx[:bv] = gamma.view(1, C, 1, 1) * invstd.view(1, C, 1, 1) * (
+                d - dbeta.view(1, C, 1, 1) / n - xhat * dgamma.view(1, C, 1, 1) / n)
+        return dx, dgamma, dbeta, None, None, None, None, None, None
+
+
+# ---- softmax cross-entropy (mean over the valid batch) + accuracy ----------------------------
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, state: torch.Tensor | None, want_grad: bool = True):
+    """Returns (per-sample loss [B], per-sample correct [B] int32, dlogits [B, NC] or None)."""
+    B, NC = logits.shape
+    logits = logits.contiguous()
+    if _is_gpu(logits):
+        loss = torch.empty(B, device=logits.device, dtype=torch.float32)
+        corr = torch.empty(B, device=logits.device, dtype=torch.int32)
+        dl = torch.empty_like(logits) if want_grad else None
+        _ext().xent(_p(logits), _p(labels), B, NC, _p(state) if state is not None else 0, _p(loss), _p(corr),
+                    _p(dl) if dl is not None else 0, _s(logits))
+        return loss, corr, dl
+    bv = _bvalid_cpu(state, B)
+    lab = labels.long()
+    loss = torch.zeros(B)
+    corr = torch.zeros(B, dtype=torch.int32)
+    z = logits.detach()
+    loss[:bv] = F.cross_entropy(z[:bv], lab[:bv], reduction="none")
+    corr[:bv] = (z[:bv].argmax(1) == lab[:bv]).int()
+    dl = None
+    if want_grad:
+        dl = torch.zeros_like(z)
+        if bv:
+            dl[:bv] = (torch.softmax(z[:bv], 1) - F.one_hot(lab[:bv], NC).float()) / bv
+    return loss, corr, dl

@@ -47,6 +47,9 @@ class SyncPolicy:
         """Rank 0's initial weights are authoritative (reference: parent sends before epoch 0)."""
         t0 = time.perf_counter()
         self.comm.broadcast_(engine.master, src=0)
+        buf = getattr(engine, "buffers", None)
+        if buf is not None:
+            self.comm.broadcast_(buf, src=0)
         engine.params_changed()
         engine.synchronize()
         self.comm_time += time.perf_counter() - t0
@@ -56,7 +59,41 @@ class SyncPolicy:
             engine.reset_momentum()
 
     def epoch_end(self, engine, epoch: int) -> None:
-        pass
+        self.sync_buffers(engine)
+
+    def sync_buffers(self, engine, trainers_only: bool = False) -> None:
+        """Average non-trained state (BatchNorm running statistics of layer-engine models)
+        over the training ranks, so every replica evaluates / checkpoints the same model."""
+        buf = getattr(engine, "buffers", None)
+        if buf is None or not self.comm.distributed:
+            return
+        with torch.no_grad():
+            if trainers_only:
+                if not self.trains():
+                    buf.zero_()
+                self.comm.allreduce_(buf, "sum")
+                buf.div_(self.trainer_count())
+            else:
+                self.comm.allreduce_(buf, "avg")
+
+
+def replica_checksums(engine) -> tuple[float, float]:
+    """(sum, position-weighted sum) of the fp32 parameter arena in fp64: equal on two
+    ranks iff (with overwhelming probability) their arenas are bit-identical."""
+    m = engine.master.detach().double()
+    w = torch.arange(1, m.numel() + 1, device=m.device, dtype=torch.float64).remainder_(9973).add_(1)
+    return float(m.sum()), float((m * w).sum())
+
+
+def assert_replicas_identical(comm: Communicator, engine) -> None:
+    """Cross-rank parameter checksum after a synchronisation point: catches
+    replica divergence and comm/compute stream races."""
+    if not comm.distributed:
+        return
+    a, b = replica_checksums(engine)
+    sa, sb = comm.gather_scalars(a), comm.gather_scalars(b)
+    if len(set(sa)) != 1 or len(set(sb)) != 1:
+        raise RuntimeError(f"replicas diverged: parameter checksums per rank {sa} / {sb}")
 
 
 class StepAllReduce(SyncPolicy):
@@ -93,6 +130,7 @@ class EpochAverage(SyncPolicy):
             return
         t0 = time.perf_counter()
         self.comm.allreduce_(engine.master, "avg")
+        self.sync_buffers(engine)
         engine.params_changed()
         engine.synchronize()
         self.comm_time += time.perf_counter() - t0
@@ -121,6 +159,7 @@ class ParentAverage(EpochAverage):
                 engine.master.zero_()
             self.comm.allreduce_(engine.master, "sum")
             engine.master.div_(self.comm.world - 1)
+        self.sync_buffers(engine, trainers_only=True)
         engine.params_changed()
         engine.synchronize()
         self.comm_time += time.perf_counter() - t0

@@ -1,3 +1,5 @@
-from .engine import CpuEngine, Engine, HipEngine, StepStats, eval_metrics, make_engine
+from .engine import ENGINES, CpuEngine, Engine, HipEngine, StepStats, eval_metrics, make_engine
+from .layer_engine import LayerEngine
 
-__all__ = ["CpuEngine", "Engine", "HipEngine", "StepStats", "eval_metrics", "make_engine"]
+__all__ = ["ENGINES", "CpuEngine", "Engine", "HipEngine", "LayerEngine", "StepStats", "eval_metrics",
+           "make_engine"]

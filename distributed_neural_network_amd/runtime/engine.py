@@ -384,8 +384,34 @@ class HipEngine(Engine):
         return loss, corr
 
 
+ENGINES = ("auto", "fused", "layers")
+
+
 def make_engine(device: str, batch: int, lr: float, momentum: float, arena: torch.Tensor | None = None,
-                seed: int | None = None, **kw) -> Engine:
-    if device == "cpu":
-        return CpuEngine(batch, lr, momentum, arena, seed)
-    return HipEngine(batch, lr, momentum, arena, seed, device=device, **kw)
+                seed: int | None = None, model: str = "lenet", engine: str = "auto", dtype: str = "bf16",
+                **kw) -> Engine:
+    """Pick the engine for (model, device, dtype).
+
+    * ``fused``  - the reference LeNet as ONE hand-scheduled gfx950 kernel per step, bf16
+      MFMA operands / fp32 accumulation (the performance path; GPU only).
+    * ``layers`` - any zoo model on the generic layer kernels (runtime/layer_engine.py),
+      fp32 or bf16 GEMM operands, BatchNorm support; CPU or GPU.
+    * ``auto``   - fused for lenet/bf16 on a GPU, the CPU oracle engine for lenet on the
+      CPU, layers otherwise.
+    """
+    if engine not in ENGINES:
+        raise ValueError(f"unknown engine {engine!r}; expected one of {ENGINES}")
+    if engine == "auto":
+        if model == "lenet" and device == "cpu":
+            return CpuEngine(batch, lr, momentum, arena, seed)
+        engine = "fused" if (model == "lenet" and dtype == "bf16") else "layers"
+    if engine == "fused":
+        if model != "lenet":
+            raise ValueError(f"the fused engine implements the reference lenet only, not {model!r}")
+        if device == "cpu":
+            return CpuEngine(batch, lr, momentum, arena, seed)
+        return HipEngine(batch, lr, momentum, arena, seed, device=device, **kw)
+    from .layer_engine import LayerEngine
+    lkw = {k: v for k, v in kw.items() if k in ("use_graphs", "graph_chunk")}
+    return LayerEngine(batch, lr, momentum, model=model, arena=arena, seed=seed, device=device,
+                       gemm_dtype=dtype, **lkw)

@@ -1,0 +1,286 @@
+"""Modular engine: any zoo model (models/zoo.py) on the generic layer kernels.
+
+Same interface as ``HipEngine`` (attach / begin_epoch / run_steps / epoch_stats /
+evaluate_samples / master / grad / mom / grad_sync), so the trainer, every sync policy,
+fault recovery and checkpointing work unchanged.  Where the fused engine is one
+hand-scheduled kernel for the reference LeNet in bf16, this engine runs a layer stack
+(csrc/kernels/layers.hip + library GEMMs) in fp32 - bit-for-bit the reference's
+arithmetic class - or with bf16 GEMM operands, and supports BatchNorm.
+
+MI355X design points kept from the fused engine:
+  * flat fp32 parameter / gradient / momentum arenas; autograd accumulates straight into
+    views of the gradient arena (``param.grad`` IS the arena slice), so a per-step
+    all-reduce is one collective on one buffer and SGD is one kernel;
+  * BatchNorm running statistics live in a second flat arena (averaged across ranks at
+    the epoch sync);
+  * the step cursor, tail-batch size, next batch ids and epoch loss/accuracy live on the
+    device (the fused engine's bookkeeping kernel), so a whole step - ingest, forward,
+    loss, backward, all-reduce, SGD - is captured in a hipGraph and replays with no host
+    work; the tail batch runs at full shape with the padding masked out of BatchNorm
+    statistics and the loss mean.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..data.datasets import Split
+from ..models import zoo
+from ..ops import layers as L
+from ..ops import native
+from .engine import Engine, StepStats
+
+
+class LayerEngine(Engine):
+    def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, model: str = "lenet",
+                 arena: torch.Tensor | None = None, seed: int | None = None, device: str | torch.device = "cpu",
+                 gemm_dtype: str = "fp32", use_graphs: bool = True, graph_chunk: int = 8,
+                 buffers: torch.Tensor | None = None) -> None:
+        self.model = model
+        self.spec = zoo.spec(model)
+        p0, b0 = zoo.init_arenas(model, seed)
+        super().__init__(batch, lr, momentum, arena if arena is not None else p0, seed)
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.gpu = self.device.type == "cuda"
+        if self.gpu:
+            self.ext = native.hip()  # fails loudly if the extension is missing on a GPU host
+        self.gemm_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[gemm_dtype]
+        self.play, self.blay = zoo.layouts(model)
+        dev = self.device
+        self.master = self._init_arena.to(dev, torch.float32).clone()
+        self.grad = torch.zeros_like(self.master)
+        self.mom = torch.zeros_like(self.master)
+        self.buffers = (buffers if buffers is not None else b0).to(dev, torch.float32).clone()
+        self.num_batches_tracked = 0
+        self.P = self.play.views(self.master)
+        self.G = self.play.views(self.grad)
+        self.Bf = self.blay.views(self.buffers)
+        for k, v in self.P.items():
+            v.requires_grad_(True)
+            v.grad = self.G[k]
+        B = self.batch
+        self.state = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.stats = torch.zeros(4, device=dev, dtype=torch.float64)
+        self.batch_ids = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.order = torch.zeros(0, device=dev, dtype=torch.int32)
+        self.x = torch.zeros(B, 3, 32, 32, device=dev)
+        self.labels = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.use_graphs = use_graphs and self.gpu
+        self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)
+        self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._warm = False
+
+    # -- parameters / checkpoints ------------------------------------------------------------
+    def state_dict(self):
+        return zoo.state_dict_from_arenas(self.model, self.master, self.buffers, self.num_batches_tracked)
+
+    def load_state_dict(self, sd) -> None:
+        p, b = zoo.arenas_from_state_dict(self.model, sd)
+        with torch.no_grad():
+            self.master.copy_(p.to(self.device))
+            self.buffers.copy_(b.to(self.device))
+        k = next((key for key in sd if key.endswith("num_batches_tracked")), None)
+        if k is not None:
+            self.num_batches_tracked = int(sd[k])
+
+    def checkpoint_keys(self):
+        return zoo.checkpoint_keys(self.model)
+
+    def synchronize(self) -> None:
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+
+    def invalidate_graphs(self) -> None:
+        self._graphs.clear()
+
+    # -- data -------------------------------------------------------------------------------------
+    def attach(self, train: Split) -> None:
+        self.train = train.to(self.device)
+        self.invalidate_graphs()
+
+    def begin_epoch(self, order: np.ndarray) -> None:
+        order = np.ascontiguousarray(order, dtype=np.int32)
+        n = int(order.shape[0])
+        if self.order.numel() < n:
+            self.order = torch.zeros(n, device=self.device, dtype=torch.int32)
+            self.invalidate_graphs()
+        if n != self.order_len:
+            self.invalidate_graphs()
+        self.order_len = n
+        if n:
+            self.order[:n].copy_(torch.from_numpy(order))
+        first = min(self.batch, n)
+        self.state[0] = 0
+        self.state[1] = first
+        self.batch_ids.zero_()
+        if first:
+            self.batch_ids[:first].copy_(self.order[:first])
+
+    # -- model ------------------------------------------------------------------------------------
+    def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None) -> torch.Tensor:
+        P, Bf, dt = self.P, self.Bf, self.gemm_dtype
+        for layer in self.spec:
+            if isinstance(layer, zoo.Conv):
+                x = L.Conv2dFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"], layer.pad, dt)
+            elif isinstance(layer, zoo.BN):
+                x = L.BatchNorm2dFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"],
+                                          Bf[f"{layer.name}.running_mean"], Bf[f"{layer.name}.running_var"],
+                                          state, training, layer.eps, layer.momentum)
+            elif isinstance(layer, zoo.ReluPool):
+                x = L.ReluPoolFn.apply(x)
+            elif isinstance(layer, zoo.Relu):
+                x = L.ReluFn.apply(x)
+            elif isinstance(layer, zoo.Flatten):
+                x = x.reshape(x.shape[0], -1)
+            elif isinstance(layer, zoo.FC):
+                x = L.LinearFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"], dt)
+        return x
+
+    def _ingest(self) -> None:
+        tr = self.train
+        if self.gpu:
+            self.ext.ingest(tr.images.data_ptr(), tr.labels.data_ptr(), self.batch_ids.data_ptr(), self.batch,
+                            3 * 32 * 32, self.x.data_ptr(), self.labels.data_ptr(),
+                            torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            ids = self.batch_ids.long()
+            self.x.copy_((tr.images[ids].float() / 255.0 - 0.5) / 0.5)
+            self.labels.copy_(tr.labels[ids])
+
+    def _bookkeeping(self, loss: torch.Tensor, corr: torch.Tensor) -> None:
+        if self.gpu:
+            self.ext.layer_bookkeeping(loss.data_ptr(), corr.data_ptr(), self.batch, self.state.data_ptr(),
+                                       self.stats.data_ptr(), self.order.data_ptr(), self.order_len,
+                                       self.batch_ids.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+            return
+        bv = int(self.state[1])
+        if bv > 0:
+            self.stats[0] += float(loss[:bv].double().sum()) / bv
+            self.stats[1] += 1
+            self.stats[2] += int(corr[:bv].sum())
+            self.stats[3] += bv
+        nxt = int(self.state[0]) + 1
+        base = nxt * self.batch
+        for b in range(self.batch):
+            g = base + b
+            self.batch_ids[b] = self.order[g] if g < self.order_len else 0
+        self.state[0] = nxt
+        self.state[1] = max(0, min(self.batch, self.order_len - base))
+
+    def _launch_step(self) -> None:
+        assert self.train is not None
+        self._ingest()
+        logits = self.forward(self.x, True, self.state)
+        loss, corr, dl = L.cross_entropy(logits, self.labels, self.state)
+        self.grad.zero_()
+        logits.backward(dl)
+        if self.grad_sync is not None:
+            self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
+        if self.gpu:
+            self.ext.sgd_flat(self.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.play.total,
+                              self.lr, self.momentum, 1.0, torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            with torch.no_grad():
+                self.mom.mul_(self.momentum).add_(self.grad)
+                self.master.sub_(self.lr * self.mom)
+        self._bookkeeping(loss, corr)
+
+    def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
+        key = (nsteps, self.grad_sync is not None, self.order_len)
+        g = self._graphs.get(key)
+        if g is None:
+            if not self._warm:
+                self._warmup()
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(nsteps):
+                    self._launch_step()
+            torch.cuda.synchronize(self.device)
+            self._graphs[key] = g
+        return g
+
+    def _warmup(self) -> None:
+        """Run two eager steps on a side stream (library/allocator lazy init happens outside
+        any capture), then restore every piece of state they touched."""
+        saved = [t.clone() for t in (self.master, self.mom, self.buffers, self.state, self.stats, self.batch_ids)]
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._launch_step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for t, v in zip((self.master, self.mom, self.buffers, self.state, self.stats, self.batch_ids), saved):
+            t.copy_(v)
+        self._warm = True
+
+    def prepare_graphs(self) -> None:
+        if self.use_graphs:
+            k = 1
+            while k <= self.graph_chunk:
+                self._graph(k)
+                k *= 2
+
+    def run_steps(self, n: int) -> None:
+        if n <= 0:
+            return
+        if not self.use_graphs:
+            ctx = torch.cuda.device(self.device) if self.gpu else _Null()
+            with ctx:
+                for _ in range(n):
+                    self._launch_step()
+            self.num_batches_tracked += n
+            return
+        k = self.graph_chunk
+        total = n
+        while k >= 1:
+            reps, n = divmod(n, k)
+            if reps:
+                g = self._graph(k)
+                for _ in range(reps):
+                    g.replay()
+            k //= 2
+        self.num_batches_tracked += total
+
+    def epoch_stats(self, reset: bool = True) -> StepStats:
+        v = self.stats.cpu().tolist()
+        if reset:
+            self.stats.zero_()
+        return StepStats(v[0], int(round(v[1])), int(round(v[2])), int(round(v[3])))
+
+    # -- evaluation -------------------------------------------------------------------------------
+    def evaluate_samples(self, split: Split, lo: int = 0, hi: int | None = None, chunk: int = 1000):
+        split = split.to(self.device)
+        hi = len(split) if hi is None else hi
+        losses, corrs = [], []
+        with torch.no_grad():
+            for s in range(lo, hi, chunk):
+                e = min(hi, s + chunk)
+                if self.gpu:  # same ingest kernel as training (IEEE division, like ToTensor)
+                    ids = torch.arange(s, e, device=self.device, dtype=torch.int32)
+                    x = torch.empty(e - s, 3, 32, 32, device=self.device)
+                    lab = torch.empty(e - s, device=self.device, dtype=torch.int32)
+                    self.ext.ingest(split.images.data_ptr(), split.labels.data_ptr(), ids.data_ptr(), e - s,
+                                    3 * 32 * 32, x.data_ptr(), lab.data_ptr(),
+                                    torch.cuda.current_stream(self.device).cuda_stream)
+                else:
+                    x = (split.images[s:e].float() / 255.0 - 0.5) / 0.5
+                    lab = split.labels[s:e].to(torch.int32).contiguous()
+                logits = self.forward(x, False, None)
+                loss, corr, _ = L.cross_entropy(logits, lab, None, want_grad=False)
+                losses.append(loss)
+                corrs.append(corr)
+        if not losses:
+            return (torch.zeros(0, device=self.device), torch.zeros(0, device=self.device, dtype=torch.int32))
+        return torch.cat(losses), torch.cat(corrs)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

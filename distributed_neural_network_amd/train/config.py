@@ -12,7 +12,8 @@ Every reference flag keeps its name and default, but is TYPED (the reference's u
 argparse crashes on ``--lr 0.01`` / ``--batch-size 8`` from the CLI; quirk §2.7 #7).
 New flags: --sync, --device, --data, --data-root, --seed, --save, --resume,
 --drop-rank/--drop-at-epoch/--drop-at-step, --overlap, --compat, --profile,
---metrics, --log-dir, --graph-chunk, --train-samples/--test-samples, --eval-sharded.
+--metrics, --log-dir, --graph-chunk, --train-samples/--test-samples, --eval-sharded,
+--model, --engine, --dtype, --check-sync.
 """
 from __future__ import annotations
 
@@ -20,7 +21,9 @@ import argparse
 from dataclasses import dataclass, field
 from typing import Optional
 
+from ..models.zoo import MODELS
 from ..parallel.sync import SYNC_MODES
+from ..runtime.engine import ENGINES
 
 DEFAULTS = {
     "single": dict(batch_size=4, epochs=15, sync="step-allreduce"),
@@ -60,6 +63,10 @@ class TrainConfig:
     graph_chunk: int = 32
     eval_sharded: bool = True
     momentum_reset: Optional[bool] = None  # default: per policy (epoch-avg resets, like the reference)
+    model: str = "lenet"
+    engine: str = "auto"
+    dtype: str = "bf16"
+    check_sync: bool = False
     extra: dict = field(default_factory=dict)
 
 
@@ -95,6 +102,18 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
     g.add_argument("--log-dir", default="log")
     g.add_argument("--graph-chunk", type=int, default=32, help="optimizer steps per captured hipGraph")
     g.add_argument("--no-eval-sharding", dest="eval_sharded", action="store_false")
+    g.add_argument("--model", default="lenet", choices=sorted(MODELS),
+                   help="lenet = the reference Network (models/model.py); lenet-bn / cifar-vgg: zoo models "
+                        "with BatchNorm (layer engine)")
+    g.add_argument("--engine", default="auto", choices=ENGINES,
+                   help="fused: one gfx950 kernel per step (lenet, bf16); layers: generic layer kernels "
+                        "(any model, fp32 or bf16); auto picks")
+    g.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="MFMA/GEMM operand precision (fp32 accumulation always); fp32 = the reference's "
+                        "arithmetic, via the layer engine")
+    g.add_argument("--check-sync", action="store_true",
+                   help="after every synchronisation assert that all ranks hold bit-identical parameters "
+                        "(cross-rank checksum)")
 
 
 def parser(mode: str) -> argparse.ArgumentParser:

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from ..data import EpochSampler, get_splits
-from ..parallel import CommError, Communicator, detect, make_policy
+from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
 from ..parallel.fault import DropInjector, Heartbeat, agree_survivors, simulate_failure
 from ..runtime import eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
@@ -152,7 +152,8 @@ class Trainer:
         with self.timers.phase(PhaseTimers.DATA, sync=False):
             self.train, self.test = get_splits(c.data, c.data_root, c.train_samples, c.test_samples, c.seed)
             self.engine = make_engine(str(self.device) if self.device.type == "cuda" else "cpu", c.batch_size,
-                                      c.lr, c.momentum, seed=c.seed, **eng_kw)
+                                      c.lr, c.momentum, seed=c.seed, model=c.model, engine=c.engine,
+                                      dtype=c.dtype, **eng_kw)
             self.engine.attach(self.train)
             self.test = self.test.to(self.device)
             self.engine.synchronize()
@@ -166,7 +167,7 @@ class Trainer:
 
         start_epoch = 0
         if c.resume:
-            sd, side = checkpoint.load(c.resume)
+            sd, side = checkpoint.load(c.resume, getattr(self.engine, "checkpoint_keys", lambda: None)())
             self.engine.load_state_dict(sd)
             if "momentum" in side:
                 self.engine.mom.copy_(side["momentum"].to(self.engine.mom.device))
@@ -203,6 +204,8 @@ class Trainer:
                 stats = self.engine.epoch_stats(reset=True)
                 t0 = time.perf_counter()
                 self.policy.epoch_end(self.engine, epoch)
+                if c.check_sync:
+                    assert_replicas_identical(self.comm, self.engine)
                 tot = torch.tensor([stats.loss_sum, stats.batches, stats.correct, stats.samples],
                                    dtype=torch.float64)
                 if self.comm.distributed:

@@ -32,22 +32,28 @@ def _atomic_save(obj: Any, path: str) -> None:
 
 def save(path: str, state_dict: "OrderedDict[str, torch.Tensor]", momentum: torch.Tensor | None = None,
          **meta: Any) -> None:
-    sd = OrderedDict((k, state_dict[k].detach().float().cpu().contiguous()) for k, _ in PARAM_SHAPES)
+    """Write ``state_dict`` (all of its keys, in order: the reference 10 for the reference
+    model; parameters + BatchNorm buffers for zoo models) + the resume sidecar."""
+    sd = OrderedDict((k, v.detach().cpu().contiguous() if not v.is_floating_point()
+                      else v.detach().float().cpu().contiguous()) for k, v in state_dict.items())
     _atomic_save(sd, path)
-    side = {"format": "dnn-amd-resume-v1", "arena_total": LAYOUT.total, **meta}
+    side = {"format": "dnn-amd-resume-v1", "arena_total": int(momentum.numel()) if momentum is not None
+            else LAYOUT.total, **meta}
     if momentum is not None:
         side["momentum"] = momentum.detach().float().cpu().clone()
     _atomic_save(side, path + ".resume.pt")
 
 
-def load(path: str) -> tuple["OrderedDict[str, torch.Tensor]", dict]:
-    """Load a checkpoint (weights_only: nothing from the file is executed)."""
+def load(path: str, expected: "list[tuple[str, tuple[int, ...]]] | None" = None
+         ) -> tuple["OrderedDict[str, torch.Tensor]", dict]:
+    """Load a checkpoint (weights_only: nothing from the file is executed) and check it
+    against ``expected`` (key, shape) pairs - the reference Network's by default."""
     sd = torch.load(path, map_location="cpu", weights_only=True)
-    for k, shape in PARAM_SHAPES:
+    for k, shape in (PARAM_SHAPES if expected is None else expected):
         if k not in sd:
             raise KeyError(f"{path}: missing {k}")
-        if tuple(sd[k].shape) != shape:
-            raise ValueError(f"{path}: {k} has shape {tuple(sd[k].shape)}, expected {shape}")
+        if tuple(sd[k].shape) != tuple(shape):
+            raise ValueError(f"{path}: {k} has shape {tuple(sd[k].shape)}, expected {tuple(shape)}")
     side = {}
     sp = path + ".resume.pt"
     if os.path.exists(sp):

@@ -1,0 +1,161 @@
+"""Generic layer kernels (csrc/kernels/layers.hip) vs the fp32 PyTorch implementations of
+the same ops (ops/layers.py CPU path, itself pinned to torch.nn in test_layers_cpu.py),
+and the layer engine on the GPU vs the CPU."""
+import numpy as np
+import pytest
+import torch
+
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.ops import layers as L
+from distributed_neural_network_amd.runtime import CpuEngine, LayerEngine
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, tol=1e-5):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
+    assert err <= tol, f"rel err {err:.2e}"
+
+
+def _both(fn, *tensors):
+    """Run fn on CPU copies and on GPU copies (leaf, requires_grad where floating)."""
+    outs = []
+    for dev in ("cpu", DEV):
+        args = [t.detach().to(dev).requires_grad_(t.is_floating_point() and t.requires_grad) if torch.is_tensor(t)
+                else t for t in tensors]
+        outs.append((fn(*args), args))
+    return outs
+
+
+@pytest.mark.parametrize("B,C,H,K,pad,Cout", [(3, 3, 32, 5, 0, 6), (4, 6, 14, 5, 0, 16), (2, 8, 9, 3, 1, 5)])
+def test_conv2d_fwd_bwd(B, C, H, K, pad, Cout):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, C, H, H, generator=g).requires_grad_()
+    w = torch.randn(Cout, C, K, K, generator=g).requires_grad_()
+    b = torch.randn(Cout, generator=g).requires_grad_()
+    (yc, ac), (yg, ag) = _both(lambda x, w, b: L.Conv2dFn.apply(x, w, b, pad, torch.float32), x, w, b)
+    _close(yg, yc)
+    dy = torch.randn(yc.shape, generator=g)
+    yc.backward(dy)
+    yg.backward(dy.to(DEV))
+    for tc, tg in zip(ac, ag):
+        _close(tg.grad, tc.grad)
+
+
+@pytest.mark.parametrize("shape", [(2, 6, 28, 28), (3, 4, 7, 9)])
+def test_relu_pool_fwd_bwd(shape):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(shape, generator=g)
+    x[0, 0, :2, :2] = 0.5  # ties: first max wins (torch order)
+    x = x.requires_grad_()
+    (yc, ac), (yg, ag) = _both(L.ReluPoolFn.apply, x)
+    _close(yg, yc, 0)
+    dy = torch.randn(yc.shape, generator=g)
+    yc.backward(dy)
+    yg.backward(dy.to(DEV))
+    _close(ag[0].grad, ac[0].grad, 0)
+
+
+def test_relu_fwd_bwd():
+    x = torch.randn(5, 37).requires_grad_()
+    (yc, ac), (yg, ag) = _both(L.ReluFn.apply, x)
+    _close(yg, yc, 0)
+    dy = torch.randn(5, 37)
+    yc.backward(dy)
+    yg.backward(dy.to(DEV))
+    _close(ag[0].grad, ac[0].grad, 0)
+
+
+@pytest.mark.parametrize("bvalid", [6, 4])
+def test_batchnorm_train_masked_and_eval(bvalid):
+    g = torch.Generator().manual_seed(2)
+    B, C = 6, 5
+    x = torch.randn(B, C, 7, 7, generator=g).requires_grad_()
+    gamma = (torch.rand(C, generator=g) + 0.5).requires_grad_()
+    beta = torch.randn(C, generator=g).requires_grad_()
+    rm0, rv0 = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    outs = []
+    for dev in ("cpu", DEV):
+        xs, gs, bs = (t.detach().to(dev).requires_grad_() for t in (x, gamma, beta))
+        rm, rv = rm0.clone().to(dev), rv0.clone().to(dev)
+        st = torch.tensor([0, bvalid, 0, 0], dtype=torch.int32, device=dev)
+        y = L.BatchNorm2dFn.apply(xs, gs, bs, rm, rv, st, True, 1e-5, 0.1)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(dev)
+        y.backward(dy)
+        ye = L.BatchNorm2dFn.apply(xs.detach(), gs.detach(), bs.detach(), rm, rv, None, False, 1e-5, 0.1)
+        outs.append((y, xs.grad, gs.grad, bs.grad, rm, rv, ye))
+    for c, gg in zip(*outs):
+        _close(gg, c, 2e-5)
+    assert float(outs[1][0][bvalid:].abs().sum()) == 0.0  # padded tail masked out
+
+
+def test_cross_entropy_masked():
+    g = torch.Generator().manual_seed(4)
+    z = torch.randn(9, 10, generator=g)
+    y = torch.randint(0, 10, (9,), generator=g, dtype=torch.int32)
+    st = torch.tensor([0, 7, 0, 0], dtype=torch.int32)
+    c = L.cross_entropy(z, y, st)
+    gg = L.cross_entropy(z.to(DEV), y.to(DEV), st.to(DEV))
+    for a, b in zip(gg, c):
+        _close(a.float(), b.float(), 1e-5)
+
+
+def test_ingest_and_sgd_flat():
+    data = synthetic(50, 5).to(DEV)
+    eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)
+    eng.attach(data)
+    eng.begin_epoch(np.arange(50, dtype=np.int32)[::-1].copy())
+    eng._ingest()
+    ids = eng.batch_ids.long().cpu()
+    # CPU torch = IEEE division, as torchvision's ToTensor on the reference's CPU workers
+    # (torch's CUDA scalar division multiplies by the reciprocal instead)
+    ref = (data.images.cpu()[ids].float() / 255.0 - 0.5) / 0.5
+    assert torch.equal(eng.x.cpu(), ref) and torch.equal(eng.labels.cpu(), data.labels.cpu()[ids].int())
+    p, gr, m = torch.randn(1000, device=DEV), torch.randn(1000, device=DEV), torch.randn(1000, device=DEV)
+    p0, m0 = p.clone(), m.clone()
+    eng.ext.sgd_flat(p.data_ptr(), gr.data_ptr(), m.data_ptr(), 1000, 0.01, 0.9, 1.0,
+                     torch.cuda.current_stream().cuda_stream)
+    m_ref = 0.9 * m0 + gr
+    _close(m, m_ref, 1e-6)
+    _close(p, p0 - 0.01 * m_ref, 1e-6)
+
+
+def _run(eng, data, steps):
+    eng.attach(data)
+    eng.begin_epoch(np.arange(len(data), dtype=np.int32))
+    eng.run_steps(steps)
+    return eng
+
+
+def test_layer_engine_gpu_fp32_matches_cpu_oracle():
+    data = synthetic(200, 1)
+    a = init_arena(seed=3)
+    ref = _run(CpuEngine(batch=16, arena=a), data, 13)
+    gpu = _run(LayerEngine(batch=16, arena=a, model="lenet", device=DEV, graph_chunk=4), data, 13)
+    _close(gpu.master - a.to(DEV), ref.master - a, 1e-4)
+    s1, s2 = ref.epoch_stats(), gpu.epoch_stats()
+    assert s1.samples == s2.samples == 200 and abs(s1.loss_sum - s2.loss_sum) < 1e-4
+
+
+def test_layer_engine_bn_gpu_graphs_match_eager_and_cpu():
+    data = synthetic(72, 2)
+    e_cpu = _run(LayerEngine(batch=16, model="lenet-bn", seed=5), data, 5)
+    e_eag = _run(LayerEngine(batch=16, model="lenet-bn", seed=5, device=DEV, use_graphs=False), data, 5)
+    e_gr = _run(LayerEngine(batch=16, model="lenet-bn", seed=5, device=DEV, graph_chunk=2), data, 5)
+    assert torch.equal(e_eag.master, e_gr.master) and torch.equal(e_eag.buffers, e_gr.buffers)
+    _close(e_gr.master - e_cpu.master.to(DEV) + e_cpu.master.to(DEV), e_cpu.master, 1e-5)
+    _close(e_gr.buffers, e_cpu.buffers, 1e-5)
+    l1, c1 = e_cpu.evaluate_samples(data, 0, 72)
+    l2, c2 = e_gr.evaluate_samples(data, 0, 72)
+    _close(l2, l1, 1e-4)
+
+
+def test_layer_engine_bf16_gemms_track_fp32():
+    data = synthetic(256, 6)
+    e32 = _run(LayerEngine(batch=32, model="cifar-vgg", seed=7, device=DEV), data, 8)
+    e16 = _run(LayerEngine(batch=32, model="cifar-vgg", seed=7, device=DEV, gemm_dtype="bf16"), data, 8)
+    s32, s16 = e32.epoch_stats(), e16.epoch_stats()
+    assert abs(s32.mean_loss - s16.mean_loss) < 0.05 * abs(s32.mean_loss)
