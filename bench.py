@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
-from distributed_neural_network_amd.runtime import HipEngine, eval_metrics  # noqa: E402
+from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 
 BASELINE_IMG_S = 1261.0  # BASELINE.md headline: bs64, "4 procs", training-phase whole-node img/s
 METRIC = "images/sec (whole node) + epoch time, CIFAR-10 CNN bs=64 at 1/2/4/8 MI355X"
@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--in-launch-reduce", action="store_true",
                     help="experimental: batch reduction + SGD in reducer workgroups inside the fused launch "
                          "(counter hand-off) instead of a second kernel")
+    ap.add_argument("--model", default="lenet", help="lenet (headline) | lenet-bn | cifar-vgg (layer engine)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "layers"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -90,8 +93,12 @@ def main():
 
     train, test = synthetic(50_000, args.seed, True), synthetic(10_000, args.seed, False)
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
-    engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                       overlap=args.overlap, in_launch_reduce=args.in_launch_reduce)
+    if args.model == "lenet" and args.engine in ("auto", "fused") and args.dtype == "bf16":
+        engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
+                           overlap=args.overlap, in_launch_reduce=args.in_launch_reduce)
+    else:  # modular layer engine (other models / fp32)
+        engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
+                             dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16))
     engine.attach(train)
     test_dev = test.to(device)
     policy = make_policy(args.sync, comm)
@@ -112,7 +119,7 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
-    if engine.sync_error():
+    if getattr(engine, "sync_error", lambda: False)():
         raise RuntimeError("in-launch reducer hand-off timed out (sync error flag set)")
     dt = comm.reduce_scalar(dt, "max")
     ms_per_step = 1000.0 * dt / args.steps
@@ -156,9 +163,11 @@ def main():
         out = {"metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": comm.world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 6),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
-               "dtype": "bf16", "data": "synthetic (CIFAR-10-shaped 3x32x32 uint8, 50k train / 10k test), "
+               "dtype": args.dtype, "data": "synthetic (CIFAR-10-shaped 3x32x32 uint8, 50k train / 10k test), "
                                         "random-init weights",
-               "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)",
+               "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)"
+                          if args.model == "lenet" else args.model,
+                          "engine": type(engine).__name__,
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
