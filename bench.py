@@ -61,7 +61,18 @@ class EpochCursor:
             k -= n
 
 
+def _reserve_stdout() -> int:
+    """Route fd 1 to stderr for the whole run and return a private handle on the real
+    stdout: RCCL (and other native libraries) print banners with printf, and the driver
+    expects exactly ONE line - the JSON result - on stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return real
+
+
 def main():
+    out_fd = _reserve_stdout()
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5000)
@@ -173,7 +184,7 @@ def main():
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
                           "reduce": "in-launch" if args.in_launch_reduce else "separate-kernel"},
                **epoch}
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     comm.close()
 
 
