@@ -86,14 +86,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("grad_reduce", [](u a0, u h1, u h2, u z1, u z2, u z3, u slab, u loss, u correct, int batch, u master,
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
-                          u stream) {
+                          u stream, u stamps) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
                       P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order), order_len,
-                      P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping};
+                      P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping,
+                      P<long long>(stamps)};
     dnn::launch_grad_reduce(a, S(stream));
-  });
+  }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
+     py::arg("loss"), py::arg("correct"), py::arg("batch"), py::arg("master"), py::arg("grad"), py::arg("mom"),
+     py::arg("shadow"), py::arg("state"), py::arg("stats"), py::arg("lr"), py::arg("momentum"),
+     py::arg("grad_scale"), py::arg("fuse_sgd"), py::arg("lo"), py::arg("hi"), py::arg("bookkeeping"),
+     py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {

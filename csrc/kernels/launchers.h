@@ -16,6 +16,7 @@ struct ReduceArgs {
   int fuse_sgd;   // 1: apply SGD in place (local step); 0: write grads only
   int lo, hi;     // arena element range [lo, hi) handled by this launch (gradient bucket)
   int bookkeeping;  // 1: this launch also advances the cursor / epoch statistics
+  long long* stamps = nullptr;  // diagnostic: per-block [start, end] s_memrealtime (grad_reduce)
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

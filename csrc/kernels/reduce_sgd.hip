@@ -21,7 +21,7 @@ static_assert(RT >= FCB_ELEMS, "one fc-bias slot per thread");
 
 
 
-__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(ReduceArgs a) {
+__device__ __forceinline__ void grad_reduce_body(const ReduceArgs& a) {
   // block roles: [MLP tile blocks][MLP bias block][conv element blocks][bookkeeping]
   const bool mlp = a.hi > OFF_F1W;
   const bool conv = a.lo < OFF_F1W;
@@ -47,6 +47,22 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     blk -= CB;
   }
   if (a.bookkeeping && blk == 0 && threadIdx.x < 64) bookkeeping<false>(a, threadIdx.x);
+}
+
+// diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
+// end of the block's work (after its stores drained)
+__device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
+  if (a.stamps != nullptr && threadIdx.x == 0) {
+    if (k) __builtin_amdgcn_s_waitcnt(0);
+    a.stamps[2 * blockIdx.x + k] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
+__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(ReduceArgs a) {
+  reduce_stamp(a, 0);
+  grad_reduce_body(a);
+  if (a.stamps != nullptr) __syncthreads();
+  reduce_stamp(a, 1);
 }
 
 // grads -> momentum SGD on the flat arena (+ bf16 shadow refresh).  Used after the

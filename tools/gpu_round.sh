@@ -1,4 +1,3 @@
 set -e
 mkdir -p gpurun_out
-export DNN_FORCE_COLLECTIVES=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
-timeout -k 10 300 python bench.py --steps 3000 --warmup 300 --no-epoch > gpurun_out/bf.json 2> gpurun_out/bf.err
+timeout -k 10 120 python tools/reduce_trace.py > gpurun_out/rt.txt 2>&1
