@@ -241,11 +241,13 @@ class GradAllReduce:
     sequence can be captured into the step's hipGraph.
     """
 
-    def __init__(self, comm: Communicator) -> None:
+    def __init__(self, comm: Communicator, bucket_kb: int = 0) -> None:
         self.comm = comm
+        self.bucket_elems = max(0, int(bucket_kb)) * 256  # fp32 elements per bucket (0: no split)
 
     def allreduce_grads(self, grad: torch.Tensor, buckets: list[tuple[int, int]],
                         before_last: Optional[Callable[[], None]] = None) -> None:
+        buckets = split_buckets(buckets, self.bucket_elems)
         works = []
         for i, (lo, hi) in enumerate(buckets):
             if i == len(buckets) - 1 and before_last is not None:
@@ -255,6 +257,19 @@ class GradAllReduce:
                 works.append(w)
         for w in works:
             w.wait()
+
+
+def split_buckets(buckets: list[tuple[int, int]], max_elems: int) -> list[tuple[int, int]]:
+    """``--bucket-kb``: cut each [lo, hi) range into pieces of at most ``max_elems``
+    (0 = keep the ranges).  At this model size one fused bucket is latency-optimal; for
+    layer-engine models with MB-scale gradients, smaller buckets pipeline the ring."""
+    if max_elems <= 0:
+        return list(buckets)
+    out = []
+    for lo, hi in buckets:
+        for a in range(lo, hi, max_elems):
+            out.append((a, min(hi, a + max_elems)))
+    return out
 
 
 def wait_for_store_key(store: dist.Store, key: str, timeout_s: float) -> bool:

@@ -22,7 +22,7 @@ from typing import Callable, Optional
 import torch
 
 from ..ops import native
-from .comm import Communicator
+from .comm import Communicator, split_buckets
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
@@ -72,9 +72,10 @@ class RcclComm:
 class NativeGradAllReduce:
     """GradSync over the native communicator (see module docstring)."""
 
-    def __init__(self, rc: RcclComm, device: torch.device, overlap: bool = False) -> None:
+    def __init__(self, rc: RcclComm, device: torch.device, overlap: bool = False, bucket_kb: int = 0) -> None:
         self.rc = rc
         self.overlap = overlap
+        self.bucket_elems = max(0, int(bucket_kb)) * 256
         self.side = torch.cuda.Stream(device)
         self.ev = [torch.cuda.Event() for _ in range(3)]
 
@@ -85,7 +86,8 @@ class NativeGradAllReduce:
             if before_last is not None:
                 before_last()
             lo, hi = min(b[0] for b in buckets), max(b[1] for b in buckets)
-            self.rc.allreduce_(grad[lo:hi], "avg", stream=s)  # one fused bucket
+            for a, b in split_buckets([(lo, hi)], self.bucket_elems):  # default: one fused bucket
+                self.rc.allreduce_(grad[a:b], "avg", stream=s)
             return
         (lo0, hi0), (lo1, hi1) = buckets[0], buckets[-1]
         self.ev[0].record(s)

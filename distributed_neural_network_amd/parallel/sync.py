@@ -28,6 +28,8 @@ class SyncPolicy:
     name = "base"
     reset_momentum_each_epoch = False
 
+    bucket_kb = 0  # step-allreduce: gradient bucket size limit (0 = one fused bucket)
+
     def __init__(self, comm: Communicator, reset_momentum_each_epoch: bool | None = None) -> None:
         self.comm = comm
         if reset_momentum_each_epoch is not None:
@@ -112,9 +114,10 @@ class StepAllReduce(SyncPolicy):
                 rc = self.comm.native = RcclComm(self.comm)
             elif rc.generation != self.comm.generation:
                 rc.reinit()
-            engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=getattr(engine, "overlap", False))
+            engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=getattr(engine, "overlap", False),
+                                                   bucket_kb=self.bucket_kb)
         else:
-            engine.grad_sync = GradAllReduce(self.comm)
+            engine.grad_sync = GradAllReduce(self.comm, bucket_kb=self.bucket_kb)
 
 
 class EpochAverage(SyncPolicy):

@@ -67,6 +67,7 @@ class TrainConfig:
     engine: str = "auto"
     dtype: str = "bf16"
     check_sync: bool = False
+    bucket_kb: int = 0
     extra: dict = field(default_factory=dict)
 
 
@@ -111,6 +112,9 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
     g.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                    help="MFMA/GEMM operand precision (fp32 accumulation always); fp32 = the reference's "
                         "arithmetic, via the layer engine")
+    g.add_argument("--bucket-kb", type=int, default=0,
+                   help="step-allreduce: split the flat gradient into all-reduce buckets of at most this many "
+                        "KB (0 = one fused bucket, latency-optimal for the 248 KB reference gradient)")
     g.add_argument("--check-sync", action="store_true",
                    help="after every synchronisation assert that all ranks hold bit-identical parameters "
                         "(cross-rank checksum)")

@@ -162,6 +162,7 @@ class Trainer:
                                   c.momentum_reset)
         if c.mode == "single":
             self.policy.reset_momentum_each_epoch = bool(c.momentum_reset)
+        self.policy.bucket_kb = c.bucket_kb
         self.policy.attach(self.engine)
         self.sampler = self._sampler()
 

@@ -106,3 +106,18 @@ def test_trainer_data_parallel_on_gpu(tmp_path):
     from distributed_neural_network_amd.models.network import Network
     net = Network()
     net.load_state_dict(torch.load(tmp_path / "ck.pt", weights_only=True))
+
+
+@pytest.mark.parametrize("model,dtype", [("lenet", "fp32"), ("lenet-bn", "fp32"), ("cifar-vgg", "bf16")])
+def test_trainer_layer_engine_on_gpu(tmp_path, model, dtype):
+    """Entry point -> trainer -> LayerEngine on the GPU (zoo models, fp32 / bf16 GEMMs),
+    checkpoint loadable by the torch module of the same spec."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2",
+                        "--batch-size", "32", "--train-samples", "1024", "--test-samples", "256", "--lr", "0.01",
+                        "--model", model, "--dtype", dtype, "--save", "ck.pt", "--device", "cuda"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Validation loss of updated master model:") == 2
+    from distributed_neural_network_amd.models import zoo
+    zoo.SpecNet(model).load_state_dict(torch.load(tmp_path / "ck.pt", weights_only=True))

@@ -1,3 +1,3 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 120 python tools/reduce_trace.py > gpurun_out/rt.txt 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -q -rA > gpurun_out/t.log 2>&1
