@@ -124,21 +124,25 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("bias_add", [](u y, u bias, int B, int C, int L, u stream) {
     dnn::launch_bias_add(P<float>(y), P<const float>(bias), B, C, L, S(stream));
   });
+  m.def("chan_parts", [](int B, int L) { return dnn::chan_parts(B, L); });
   m.def("bn_fwd_train", [](u x, int B, int C, int L, u state, u gamma, u beta, float eps, float mom, u rmean,
-                           u rvar, u y, u smean, u sinvstd, u stream) {
+                           u rvar, u y, u smean, u sinvstd, u part, u stream) {
     dnn::launch_bn_fwd_train(P<const float>(x), B, C, L, P<const int32_t>(state), P<const float>(gamma),
                              P<const float>(beta), eps, mom, P<float>(rmean), P<float>(rvar), P<float>(y),
-                             P<float>(smean), P<float>(sinvstd), S(stream));
+                             P<float>(smean), P<float>(sinvstd), P<double>(part), S(stream));
   });
   m.def("bn_fwd_eval", [](u x, int B, int C, int L, u gamma, u beta, float eps, u rmean, u rvar, u y, u stream) {
     dnn::launch_bn_fwd_eval(P<const float>(x), B, C, L, P<const float>(gamma), P<const float>(beta), eps,
                             P<const float>(rmean), P<const float>(rvar), P<float>(y), S(stream));
   });
   m.def("bn_bwd", [](u dy, u x, int B, int C, int L, u state, u gamma, u smean, u sinvstd, u dx, u dgamma,
-                     u dbeta, u stream) {
+                     u dbeta, u part, u stream) {
     dnn::launch_bn_bwd(P<const float>(dy), P<const float>(x), B, C, L, P<const int32_t>(state), P<const float>(gamma),
                        P<const float>(smean), P<const float>(sinvstd), P<float>(dx), P<float>(dgamma),
-                       P<float>(dbeta), S(stream));
+                       P<float>(dbeta), P<double>(part), S(stream));
+  });
+  m.def("chan_sum", [](u a, int B, int C, int L, u out, u part, u stream) {
+    dnn::launch_chan_sum(P<const float>(a), B, C, L, P<float>(out), P<double>(part), S(stream));
   });
   m.def("xent", [](u logits, u labels, int B, int NC, u state, u loss, u correct, u dlogits, u stream) {
     dnn::launch_xent(P<const float>(logits), P<const int32_t>(labels), B, NC, P<const int32_t>(state), P<float>(loss),

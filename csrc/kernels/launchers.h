@@ -45,13 +45,16 @@ void launch_relu_pool_bwd(const float* dy, const uint8_t* code, int BC, int H, i
 void launch_relu_fwd(const float* x, long n, float* y, hipStream_t s);
 void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStream_t s);
 void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream_t s);
+int chan_parts(int B, int L);  // partitions per channel of the two-stage channel reductions
 void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
-                         float* sinvstd, hipStream_t s);
+                         float* sinvstd, double* part, hipStream_t s);
 void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
                         const float* rmean, const float* rvar, float* y, hipStream_t s);
 void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
-                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, hipStream_t s);
+                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
+                   hipStream_t s);
+void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s);
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
                  int32_t* correct, float* dlogits, hipStream_t s);
 void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s);

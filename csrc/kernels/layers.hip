@@ -146,75 +146,123 @@ __global__ void __launch_bounds__(LT) bias_add_kernel(float* __restrict__ y, con
   y[i] += bias[(i / L) % C];
 }
 
-// ---- block reduction (fixed order) ----------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void block_sum(float (&v)[N], float* red) {
+// ---- per-channel reductions over (batch, pixels): deterministic two-stage ---------------
+// Stage 1: grid (P, C) blocks, block (p, c) reduces a fixed slice of channel c's B*L plane
+// into fp64 partials; stage 2 merges the P partials of a channel in a fixed order.  The
+// slicing depends only on (B, L), never on the valid count, so graph replays and tail
+// batches reduce in the same order (bitwise reproducible).  fp64 partial sums make the
+// one-pass E[x^2] - E[x]^2 variance safe.
+__host__ __device__ inline int chan_parts_of(int B, int L) {
+  const long n = (long)B * L;
+  const int p = (int)((n + 4095) / 4096);
+  return p < 1 ? 1 : (p > 64 ? 64 : p);
+}
+
+__device__ __forceinline__ void block_sum2_d(double& s0, double& s1, double* red) {
 #pragma unroll
-  for (int k = 0; k < N; ++k) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off);
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_down(s0, off);
+    s1 += __shfl_down(s1, off);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
   if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) red[wave * N + k] = v[k];
+    red[2 * wave] = s0;
+    red[2 * wave + 1] = s1;
   }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    float s = 0.f;
-    for (int w = 0; w < LT / 64; ++w) s += red[w * N + k];
-    v[k] = s;
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int w = 0; w < LT / 64; ++w) {
+      a += red[2 * w];
+      b += red[2 * w + 1];
+    }
+    s0 = a;
+    s1 = b;
+  }
+}
+
+// MODE 0: (sum x, sum x^2)   MODE 1: (sum dy, sum dy * xhat)   MODE 2: (sum a, 0)
+template <int MODE>
+__global__ void __launch_bounds__(LT) chan_partial_kernel(const float* __restrict__ a, const float* __restrict__ x,
+                                                          int B, int C, int L, const int32_t* __restrict__ state,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          double* __restrict__ part) {
+  __shared__ double red[2 * (LT / 64)];
+  const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
+  const int bv = valid_count(state, B);
+  const long n = (long)bv * L, chunk = ((long)B * L + P - 1) / P;
+  const long lo = (long)p * chunk, hi = min(n, lo + chunk);
+  const float mu = MODE == 1 ? mean[c] : 0.f, is = MODE == 1 ? invstd[c] : 0.f;
+  double s0 = 0.0, s1 = 0.0;
+  for (long t = lo + threadIdx.x; t < hi; t += LT) {
+    const long b = t / L, l = t - b * L;
+    const size_t o = ((size_t)b * C + c) * L + l;
+    const float v = a[o];
+    s0 += (double)v;
+    if (MODE == 0) s1 += (double)v * (double)v;
+    if (MODE == 1) s1 += (double)v * (double)((x[o] - mu) * is);
+  }
+  block_sum2_d(s0, s1, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)c * P + p) * 2] = s0;
+    part[((size_t)c * P + p) * 2 + 1] = s1;
+  }
+}
+
+__device__ __forceinline__ void merge_parts(const double* part, int c, int P, double& s0, double& s1) {
+  s0 = 0.0;
+  s1 = 0.0;
+  for (int q = 0; q < P; ++q) {
+    s0 += part[((size_t)c * P + q) * 2];
+    s1 += part[((size_t)c * P + q) * 2 + 1];
   }
 }
 
 // ---- BatchNorm2d -------------------------------------------------------------------------
-// One block per channel.  Training: batch statistics over the VALID samples only (the
-// padded tail batch of a captured step must not pollute them), biased variance for the
-// normalisation, unbiased for the running estimate (torch semantics, momentum m).
-__global__ void __launch_bounds__(LT) bn_fwd_train_kernel(const float* __restrict__ x, int B, int C, int L,
-                                                          const int32_t* __restrict__ state,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps, float m,
-                                                          float* __restrict__ running_mean,
-                                                          float* __restrict__ running_var, float* __restrict__ y,
-                                                          float* __restrict__ save_mean,
-                                                          float* __restrict__ save_invstd) {
-  __shared__ float red[(LT / 64) * 2];
-  const int c = blockIdx.x;
+// Training: batch statistics over the VALID samples only (the padded tail batch of a
+// captured step must not pollute them), biased variance for the normalisation, unbiased
+// for the running estimate (torch semantics, momentum m).  Grid (P, C) like the partials:
+// each block merges its channel's partials, then normalises its slice.
+__global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restrict__ x, int B, int C, int L,
+                                                            const int32_t* __restrict__ state,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps, float m,
+                                                            float* __restrict__ running_mean,
+                                                            float* __restrict__ running_var, float* __restrict__ y,
+                                                            float* __restrict__ save_mean,
+                                                            float* __restrict__ save_invstd,
+                                                            const double* __restrict__ part) {
+  __shared__ float st[2];
+  const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
-  const long n = (long)bv * L;
-  float s[1] = {0.f};
-  for (long t = threadIdx.x; t < n; t += LT) {
-    const long b = t / L, l = t - b * L;
-    s[0] += x[((size_t)b * C + c) * L + l];
+  if (threadIdx.x == 0) {
+    double s0, s1;
+    merge_parts(part, c, P, s0, s1);
+    const double n = (double)bv * L;
+    const double mean = n > 0 ? s0 / n : 0.0;
+    const double var = n > 0 ? fmax(s1 / n - mean * mean, 0.0) : 0.0;
+    const float invstd = rsqrtf((float)var + eps);
+    st[0] = (float)mean;
+    st[1] = invstd;
+    if (p == 0) {
+      save_mean[c] = (float)mean;
+      save_invstd[c] = invstd;
+      if (n > 0) {
+        const double unb = n > 1 ? var * n / (n - 1) : var;
+        running_mean[c] = (1.f - m) * running_mean[c] + m * (float)mean;
+        running_var[c] = (1.f - m) * running_var[c] + m * (float)unb;
+      }
+    }
   }
-  block_sum<1>(s, red);
-  const float mean = n > 0 ? s[0] / (float)n : 0.f;
-  float q[1] = {0.f};
-  for (long t = threadIdx.x; t < n; t += LT) {
-    const long b = t / L, l = t - b * L;
-    const float d = x[((size_t)b * C + c) * L + l] - mean;
-    q[0] += d * d;
-  }
-  block_sum<1>(q, red);
-  const float var = n > 0 ? q[0] / (float)n : 0.f;
-  const float invstd = rsqrtf(var + eps);
-  const float g = gamma[c], bb = beta[c];
-  for (long t = threadIdx.x; t < (long)B * L; t += LT) {
+  __syncthreads();
+  const float mean = st[0], invstd = st[1], g = gamma[c], bb = beta[c];
+  const long total = (long)B * L, chunk = (total + P - 1) / P;
+  const long lo = (long)p * chunk, hi = min(total, lo + chunk);
+  for (long t = lo + threadIdx.x; t < hi; t += LT) {
     const long b = t / L, l = t - b * L;
     const size_t o = ((size_t)b * C + c) * L + l;
     y[o] = b < bv ? (x[o] - mean) * invstd * g + bb : 0.f;
-  }
-  if (threadIdx.x == 0) {
-    save_mean[c] = mean;
-    save_invstd[c] = invstd;
-    if (n > 0) {
-      const float unb = n > 1 ? var * (float)n / (float)(n - 1) : var;
-      running_mean[c] = (1.f - m) * running_mean[c] + m * mean;
-      running_var[c] = (1.f - m) * running_var[c] + m * unb;
-    }
   }
 }
 
@@ -230,38 +278,48 @@ __global__ void __launch_bounds__(LT) bn_fwd_eval_kernel(const float* __restrict
   y[i] = (x[i] - running_mean[c]) * rsqrtf(running_var[c] + eps) * gamma[c] + beta[c];
 }
 
-__global__ void __launch_bounds__(LT) bn_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
-                                                    int B, int C, int L, const int32_t* __restrict__ state,
-                                                    const float* __restrict__ gamma,
-                                                    const float* __restrict__ save_mean,
-                                                    const float* __restrict__ save_invstd,
-                                                    float* __restrict__ dx, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta) {
-  __shared__ float red[(LT / 64) * 2];
-  const int c = blockIdx.x;
+__global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                          int B, int C, int L, const int32_t* __restrict__ state,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ save_mean,
+                                                          const float* __restrict__ save_invstd,
+                                                          float* __restrict__ dx, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta,
+                                                          const double* __restrict__ part) {
+  __shared__ float st[2];
+  const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
-  const long n = (long)bv * L;
-  const float mean = save_mean[c], invstd = save_invstd[c];
-  float s[2] = {0.f, 0.f};  // sum dy, sum dy * xhat
-  for (long t = threadIdx.x; t < n; t += LT) {
-    const long b = t / L, l = t - b * L;
-    const size_t o = ((size_t)b * C + c) * L + l;
-    const float d = dy[o];
-    s[0] += d;
-    s[1] += d * (x[o] - mean) * invstd;
+  if (threadIdx.x == 0) {
+    double s0, s1;
+    merge_parts(part, c, P, s0, s1);
+    const double n = (double)bv * L;
+    st[0] = n > 0 ? (float)(s0 / n) : 0.f;
+    st[1] = n > 0 ? (float)(s1 / n) : 0.f;
+    if (p == 0) {
+      dgamma[c] = (float)s1;
+      dbeta[c] = (float)s0;
+    }
   }
-  block_sum<2>(s, red);
-  const float g = gamma[c];
-  const float mdy = n > 0 ? s[0] / (float)n : 0.f, mdyx = n > 0 ? s[1] / (float)n : 0.f;
-  for (long t = threadIdx.x; t < (long)B * L; t += LT) {
+  __syncthreads();
+  const float mdy = st[0], mdyx = st[1];
+  const float mean = save_mean[c], invstd = save_invstd[c], g = gamma[c];
+  const long total = (long)B * L, chunk = (total + P - 1) / P;
+  const long lo = (long)p * chunk, hi = min(total, lo + chunk);
+  for (long t = lo + threadIdx.x; t < hi; t += LT) {
     const long b = t / L, l = t - b * L;
     const size_t o = ((size_t)b * C + c) * L + l;
     dx[o] = b < bv ? g * invstd * (dy[o] - mdy - (x[o] - mean) * invstd * mdyx) : 0.f;
   }
-  if (threadIdx.x == 0) {
-    dgamma[c] = s[1];
-    dbeta[c] = s[0];
-  }
+}
+
+// per-channel sum of a [B][C][L] tensor (conv bias gradient): stage 2
+__global__ void __launch_bounds__(64) chan_sum_finalize_kernel(const double* __restrict__ part, int C, int P,
+                                                               float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  double s0, s1;
+  merge_parts(part, c, P, s0, s1);
+  out[c] = (float)s0;
 }
 
 // ---- fused softmax cross-entropy forward + backward + accuracy -----------------------------
@@ -351,11 +409,17 @@ void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream
   const long n = (long)B * C * L;
   if (n) hipLaunchKernelGGL(bias_add_kernel, dim3(blocks(n)), dim3(LT), 0, s, y, bias, B, C, L);
 }
+int chan_parts(int B, int L) { return chan_parts_of(B, L); }
+
 void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
-                         float* sinvstd, hipStream_t s) {
-  if (C) hipLaunchKernelGGL(bn_fwd_train_kernel, dim3(C), dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m,
-                            rmean, rvar, y, smean, sinvstd);
+                         float* sinvstd, double* part, hipStream_t s) {
+  if (!C) return;
+  const dim3 grid(chan_parts_of(B, L), C);
+  hipLaunchKernelGGL(chan_partial_kernel<0>, grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr, nullptr,
+                     part);
+  hipLaunchKernelGGL(bn_apply_train_kernel, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
+                     rvar, y, smean, sinvstd, part);
 }
 void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
                         const float* rmean, const float* rvar, float* y, hipStream_t s) {
@@ -364,9 +428,20 @@ void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma,
                             rvar, y);
 }
 void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
-                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, hipStream_t s) {
-  if (C) hipLaunchKernelGGL(bn_bwd_kernel, dim3(C), dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
-                            dgamma, dbeta);
+                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
+                   hipStream_t s) {
+  if (!C) return;
+  const dim3 grid(chan_parts_of(B, L), C);
+  hipLaunchKernelGGL(chan_partial_kernel<1>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd, part);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
+                     dgamma, dbeta, part);
+}
+void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s) {
+  if (!C) return;
+  const int P = chan_parts_of(B, L);
+  hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(P, C), dim3(LT), 0, s, a, nullptr, B, C, L, nullptr, nullptr,
+                     nullptr, part);
+  hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, part, C, P, out);
 }
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
                  int32_t* correct, float* dlogits, hipStream_t s) {

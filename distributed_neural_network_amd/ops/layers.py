@@ -47,6 +47,11 @@ def _bvalid_cpu(state: torch.Tensor | None, batch: int) -> int:
     return batch if state is None else min(int(state[ST_BVALID]), batch)
 
 
+def _partials(t: torch.Tensor, B: int, C: int, L: int) -> torch.Tensor:
+    """fp64 workspace of the two-stage per-channel reductions (layers.hip)."""
+    return torch.empty(C * _ext().chan_parts(B, L) * 2, device=t.device, dtype=torch.float64)
+
+
 def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Library GEMM with optional bf16 operands (fp32 accumulate / result)."""
     if dtype == torch.float32:
@@ -56,8 +61,12 @@ def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 # ---- Conv2d (stride 1, square kernel, zero padding) -------------------------------------------
 class Conv2dFn(torch.autograd.Function):
+    """``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
+    them (views of the engine's flat gradient arena) and autograd gets None for the
+    parameters - no per-parameter accumulation kernels, no arena zeroing."""
+
     @staticmethod
-    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype):
+    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -75,6 +84,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(cols, w)
         ctx.shape = (B, C, H, W, K, pad, OH, OW)
         ctx.gemm_dtype = gemm_dtype
+        ctx.gw, ctx.gb = gw, gb
         return y.view(B, Cout, OH, OW)
 
     @staticmethod
@@ -83,8 +93,13 @@ class Conv2dFn(torch.autograd.Function):
         B, C, H, W, K, pad, OH, OW = ctx.shape
         Cout = w.shape[0]
         dy2 = dy.contiguous().view(B, Cout, OH * OW)
-        dw = _gemm(dy2, cols.transpose(1, 2), ctx.gemm_dtype).sum(0).view_as(w)
-        db = dy2.sum((0, 2))
+        dw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
+        torch.sum(_gemm(dy2, cols.transpose(1, 2), ctx.gemm_dtype), 0, out=dw.view(Cout, -1))
+        db = ctx.gb if ctx.gb is not None else torch.empty(Cout, device=dy.device, dtype=torch.float32)
+        if _is_gpu(dy2):
+            _ext().chan_sum(_p(dy2), B, Cout, OH * OW, _p(db), _p(_partials(dy2, B, Cout, OH * OW)), _s(dy2))
+        else:
+            db.copy_(dy2.sum((0, 2)))
         dx = None
         if ctx.needs_input_grad[0]:
             dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
@@ -93,7 +108,9 @@ class Conv2dFn(torch.autograd.Function):
                 _ext().col2im(_p(dcols), B, C, H, W, K, pad, _p(dx), _s(dy))
             else:
                 dx = F.fold(dcols, (H, W), K, padding=pad)
-        return dx, dw, db, None, None
+        if ctx.gw is not None:
+            return dx, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 # ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------
@@ -161,23 +178,37 @@ class ReluFn(torch.autograd.Function):
 
 # ---- Linear ---------------------------------------------------------------------------------
 class LinearFn(torch.autograd.Function):
+    """y = x W^T + b; fp32 GEMMs carry the bias in the GEMM epilogue (addmm).  ``gw`` /
+    ``gb``: gradient arena views written in place (see Conv2dFn)."""
+
     @staticmethod
-    def forward(ctx, x, w, b, gemm_dtype: torch.dtype):
+    def forward(ctx, x, w, b, gemm_dtype: torch.dtype, gw=None, gb=None):
         ctx.save_for_backward(x, w)
         ctx.gemm_dtype = gemm_dtype
+        ctx.gw, ctx.gb = gw, gb
+        if gemm_dtype == torch.float32:
+            return torch.addmm(b, x, w.t())
         return _gemm(x, w.t(), gemm_dtype) + b
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dx = _gemm(dy, w, ctx.gemm_dtype) if ctx.needs_input_grad[0] else None
-        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None
+        if ctx.gw is not None:
+            if ctx.gemm_dtype == torch.float32:
+                torch.mm(dy.t(), x, out=ctx.gw)
+            else:
+                ctx.gw.copy_(_gemm(dy.t(), x, ctx.gemm_dtype))
+            torch.sum(dy, 0, out=ctx.gb)
+            return dx, None, None, None, None, None
+        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None, None, None
 
 
 # ---- BatchNorm2d (train: masked batch statistics; eval: running statistics) -----------------
 class BatchNorm2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, state, training: bool, eps: float, momentum: float):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, state, training: bool, eps: float, momentum: float,
+                ggamma=None, gbeta=None):
         B, C, H, W = x.shape
         L = H * W
         x = x.contiguous()
@@ -195,8 +226,10 @@ class BatchNorm2dFn(torch.autograd.Function):
         invstd = torch.empty(C, device=x.device, dtype=torch.float32)
         if _is_gpu(x):
             y = torch.empty_like(x)
+            part = _partials(x, B, C, L)
             _ext().bn_fwd_train(_p(x), B, C, L, _p(state) if state is not None else 0, _p(gamma), _p(beta), eps,
-                                momentum, _p(running_mean), _p(running_var), _p(y), _p(mean), _p(invstd), _s(x))
+                                momentum, _p(running_mean), _p(running_var), _p(y), _p(mean), _p(invstd), _p(part),
+                                _s(x))
         else:
             bv = _bvalid_cpu(state, B)
             xv = x[:bv]
@@ -213,6 +246,7 @@ class BatchNorm2dFn(torch.autograd.Function):
                 running_mean.mul_(1 - momentum).add_(momentum * mu)
                 running_var.mul_(1 - momentum).add_(momentum * unb)
         ctx.training = True
+        ctx.gg, ctx.gb = ggamma, gbeta
         ctx.save_for_backward(x, gamma, mean, invstd, state if state is not None else torch.zeros(0))
         return y
 
@@ -224,13 +258,17 @@ class BatchNorm2dFn(torch.autograd.Function):
         B, C, H, W = x.shape
         L = H * W
         dy = dy.contiguous()
+        inplace = ctx.gg is not None
+        none9 = (None,) * 8
         if _is_gpu(dy):
             dx = torch.empty_like(x)
-            dgamma = torch.empty(C, device=x.device, dtype=torch.float32)
-            dbeta = torch.empty(C, device=x.device, dtype=torch.float32)
+            dgamma = ctx.gg if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
+            dbeta = ctx.gb if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
             _ext().bn_bwd(_p(dy), _p(x), B, C, L, _p(state) if state is not None else 0, _p(gamma), _p(mean),
-                          _p(invstd), _p(dx), _p(dgamma), _p(dbeta), _s(dy))
-            return dx, dgamma, dbeta, None, None, None, None, None, None
+                          _p(invstd), _p(dx), _p(dgamma), _p(dbeta), _p(_partials(dy, B, C, L)), _s(dy))
+            if inplace:
+                return (dx, None, None) + none9
+            return (dx, dgamma, dbeta) + none9
         bv = _bvalid_cpu(state, B)
         n = bv * L
         xhat = (x[:bv] - mean.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
@@ -241,7 +279,11 @@ class BatchNorm2dFn(torch.autograd.Function):
         if n:
             dx[:bv] = gamma.view(1, C, 1, 1) * invstd.view(1, C, 1, 1) * (
                 d - dbeta.view(1, C, 1, 1) / n - xhat * dgamma.view(1, C, 1, 1) / n)
-        return dx, dgamma, dbeta, None, None, None, None, None, None
+        if inplace:
+            ctx.gg.copy_(dgamma)
+            ctx.gb.copy_(dbeta)
+            return (dx, None, None) + none9
+        return (dx, dgamma, dbeta) + none9
 
 
 # ---- softmax cross-entropy (mean over the valid batch) + accuracy ----------------------------

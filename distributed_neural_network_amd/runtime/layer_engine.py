@@ -8,9 +8,10 @@ hand-scheduled kernel for the reference LeNet in bf16, this engine runs a layer 
 arithmetic class - or with bf16 GEMM operands, and supports BatchNorm.
 
 MI355X design points kept from the fused engine:
-  * flat fp32 parameter / gradient / momentum arenas; autograd accumulates straight into
-    views of the gradient arena (``param.grad`` IS the arena slice), so a per-step
-    all-reduce is one collective on one buffer and SGD is one kernel;
+  * flat fp32 parameter / gradient / momentum arenas; every layer op writes its parameter
+    gradients straight into views of the gradient arena (no per-parameter accumulation
+    kernels), so a per-step all-reduce is one collective on one buffer and SGD is one
+    kernel;
   * BatchNorm running statistics live in a second flat arena (averaged across ranks at
     the epoch sync);
   * the step cursor, tail-batch size, next batch ids and epoch loss/accuracy live on the
@@ -57,9 +58,8 @@ class LayerEngine(Engine):
         self.P = self.play.views(self.master)
         self.G = self.play.views(self.grad)
         self.Bf = self.blay.views(self.buffers)
-        for k, v in self.P.items():
-            v.requires_grad_(True)
-            v.grad = self.G[k]
+        for v in self.P.values():
+            v.requires_grad_(True)  # builds the autograd graph; gradients land in G directly
         B = self.batch
         self.state = torch.zeros(4, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(4, device=dev, dtype=torch.float64)
@@ -120,14 +120,18 @@ class LayerEngine(Engine):
 
     # -- model ------------------------------------------------------------------------------------
     def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None) -> torch.Tensor:
-        P, Bf, dt = self.P, self.Bf, self.gemm_dtype
+        """Layer stack.  Training: every op writes its parameter gradients straight into the
+        flat gradient arena (views ``G``), so backward leaves ``grad`` complete with no
+        accumulation or zeroing kernels."""
+        P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
         for layer in self.spec:
+            n = getattr(layer, "name", "")
+            gw, gb = (G[f"{n}.weight"], G[f"{n}.bias"]) if (training and n) else (None, None)
             if isinstance(layer, zoo.Conv):
-                x = L.Conv2dFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"], layer.pad, dt)
+                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb)
             elif isinstance(layer, zoo.BN):
-                x = L.BatchNorm2dFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"],
-                                          Bf[f"{layer.name}.running_mean"], Bf[f"{layer.name}.running_var"],
-                                          state, training, layer.eps, layer.momentum)
+                x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
+                                          Bf[f"{n}.running_var"], state, training, layer.eps, layer.momentum, gw, gb)
             elif isinstance(layer, zoo.ReluPool):
                 x = L.ReluPoolFn.apply(x)
             elif isinstance(layer, zoo.Relu):
@@ -135,7 +139,7 @@ class LayerEngine(Engine):
             elif isinstance(layer, zoo.Flatten):
                 x = x.reshape(x.shape[0], -1)
             elif isinstance(layer, zoo.FC):
-                x = L.LinearFn.apply(x, P[f"{layer.name}.weight"], P[f"{layer.name}.bias"], dt)
+                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], dt, gw, gb)
         return x
 
     def _ingest(self) -> None:
@@ -174,8 +178,7 @@ class LayerEngine(Engine):
         self._ingest()
         logits = self.forward(self.x, True, self.state)
         loss, corr, dl = L.cross_entropy(logits, self.labels, self.state)
-        self.grad.zero_()
-        logits.backward(dl)
+        logits.backward(dl)  # writes every parameter gradient into self.grad (no zeroing needed)
         if self.grad_sync is not None:
             self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
         if self.gpu:
