@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "layers"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
@@ -97,8 +99,9 @@ def main():
     if env.world != args.gpus:
         if env.world == 1 and args.gpus > 1:
             sys.exit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks (found WORLD_SIZE=1)")
-    torch.cuda.set_device(env.local_rank)
-    device = torch.device("cuda", env.local_rank)
+    dev_index = env.local_rank % torch.cuda.device_count()  # 1 GPU per rank (wraps only in tests)
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     comm = Communicator(env, device)
     B = args.batch_size
 
@@ -106,10 +109,11 @@ def main():
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
     if args.model == "lenet" and args.engine in ("auto", "fused") and args.dtype == "bf16":
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                           overlap=args.overlap, in_launch_reduce=args.in_launch_reduce)
+                           overlap=args.overlap, in_launch_reduce=args.in_launch_reduce,
+                           use_graphs=not args.no_graphs)
     else:  # modular layer engine (other models / fp32)
         engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
-                             dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16))
+                             dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16), use_graphs=not args.no_graphs)
     engine.attach(train)
     test_dev = test.to(device)
     policy = make_policy(args.sync, comm)

@@ -41,7 +41,9 @@ class Communicator:
                  backend: str | None = None, timeout_s: float = 300.0) -> None:
         self.env = env or detect()
         self.device = torch.device(device)
-        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        # DNN_BACKEND=gloo forces host collectives (multi-rank tests on a single GPU, where
+        # RCCL refuses two ranks on one device)
+        self.backend = backend or os.environ.get("DNN_BACKEND") or ("nccl" if self.device.type == "cuda" else "gloo")
         self.timeout = _dt.timedelta(seconds=timeout_s)
         self.generation = 0
         self.members: list[int] = list(range(self.env.world))  # original ranks of the live group

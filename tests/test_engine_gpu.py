@@ -121,3 +121,20 @@ def test_trainer_layer_engine_on_gpu(tmp_path, model, dtype):
     assert r.stdout.count("Validation loss of updated master model:") == 2
     from distributed_neural_network_amd.models import zoo
     zoo.SpecNet(model).load_state_dict(torch.load(tmp_path / "ck.pt", weights_only=True))
+
+
+def test_bench_two_ranks_one_gpu_gloo(tmp_path):
+    """Multi-rank bench.py plumbing (torchrun, barriers, max over ranks, eval sharding,
+    rank-0-only JSON) with 2 ranks sharing the one GPU of the test box over gloo."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29677", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "20", "--warmup", "4", "--no-graphs"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    import json
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 128
+    assert out["value"] > 0 and out["steps"] == 20 and 0 <= out["val_acc"] <= 100
