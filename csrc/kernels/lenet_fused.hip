@@ -204,9 +204,12 @@ __device__ __forceinline__ int r3_index(int o, int yy, int x) { return (o * 18 +
 // on the sample blocks' critical path) and no acquire.  Sample blocks never wait and
 // have the lowest block ids, so no residency / dispatch-order assumption is needed.
 // sync[0] rows-ready count, [1] slabs-ready count, [2] reducers-done count, [3] error.
-constexpr int RED_FC_BLOCKS = (FC_TILES + 7) / 8;   // 32 (8 wave-tiles per block)
-constexpr int RED_CONV_BLOCKS = (CONV_ELEMS + NT - 1) / NT;  // 6
-constexpr int RED_BLOCKS = RED_FC_BLOCKS + 1 + RED_CONV_BLOCKS;  // + fc-bias/bookkeeping block
+constexpr int RED_FC_BLOCKS = (FC_TILES + 7) / 8;          // 32 (8 wave-tiles per block)
+constexpr int RED_FCB_BLOCKS = (FCB_SLOTS + NT - 1) / NT;    // 2 (fc biases; the 2nd block's
+                                                             //    wave 7 runs the bookkeeping)
+constexpr int RED_CONV_BLOCKS = (CONV_SLOTS + NT - 1) / NT;  // 23
+constexpr int RED_BLOCKS = RED_FC_BLOCKS + RED_FCB_BLOCKS + RED_CONV_BLOCKS;
+static_assert(RED_FCB_BLOCKS * NT - FCB_SLOTS >= 64, "a free wave for the bookkeeping");
 
 // Write-through stores (sc1): the line leaves the XCD's L2 for memory at once.
 // Scalar values go through buffer-store builtins (cache policy 16 = sc1) so hipcc sees
@@ -253,9 +256,9 @@ __device__ __forceinline__ void reducer_block(int r, const ReduceArgs ra, unsign
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // diagnostic stamps: [12] fc reducer 0 released, [13] its tile done, [14] conv reducer 0
   // released, [15] its columns done
-  const int si = r == 0 ? 12 : (r == RED_FC_BLOCKS + 1 ? 14 : -1);
+  const int si = r == 0 ? 12 : (r == RED_FC_BLOCKS + RED_FCB_BLOCKS ? 14 : -1);
   const bool stamp = stamps != nullptr && si >= 0 && tid == 0;
-  if (r <= RED_FC_BLOCKS) {
+  if (r < RED_FC_BLOCKS + RED_FCB_BLOCKS) {
     wait_count(&sync[0], (unsigned)ra.batch, &sync[3]);
     if (stamp) stamps[si] = (long long)__builtin_amdgcn_s_memrealtime();
     if (r < RED_FC_BLOCKS) {
@@ -264,13 +267,14 @@ __device__ __forceinline__ void reducer_block(int r, const ReduceArgs ra, unsign
       else if (t < FC_T0 + FC_T1) fc_tile<1, true>(t - FC_T0, ra);
       else if (t < FC_TILES) fc_tile<2, true>(t - FC_T0 - FC_T1, ra);
     } else {
-      if (tid < FCB_SLOTS) fcb_task<true>(tid, ra);
-      else if (wave == 7 && ra.bookkeeping) bookkeeping<true>(ra, lane);
+      const int slot = (r - RED_FC_BLOCKS) * NT + tid;
+      if (slot < FCB_SLOTS) fcb_task<true>(slot, ra);
+      else if (r == RED_FC_BLOCKS + RED_FCB_BLOCKS - 1 && wave == 7 && ra.bookkeeping) bookkeeping<true>(ra, lane);
     }
   } else {
     wait_count(&sync[1], (unsigned)ra.batch, &sync[3]);
     if (stamp) stamps[si] = (long long)__builtin_amdgcn_s_memrealtime();
-    conv_task<true>((r - RED_FC_BLOCKS - 1) * NT + tid, ra);
+    conv_task<true>((r - RED_FC_BLOCKS - RED_FCB_BLOCKS) * NT + tid, ra);
   }
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);

@@ -101,59 +101,68 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
   }
 }
 
-// element tasks: fc biases (sum_b z[b][o]) and conv slab columns (sum_b slab[b][j]);
-// all 64 rows of a chunk are loaded before the (fixed-order) sum
+// Column sums (fc biases: sum_b z[b][o]; conv slab columns: sum_b slab[b][j]) with SPLIT = 4
+// consecutive lanes per column: lane part q sums rows {64 c + 16 q + k}, then the 4
+// partials combine as (p0 + p1) + (p2 + p3) through lane shuffles - a fixed order (bitwise
+// reproducible, identical in the standalone and the in-launch reducers), 16-load chains
+// instead of 64, 4x the threads in flight.
+constexpr int SPLIT = 4;
 template <bool COH>
-__device__ __forceinline__ float column_sum(const Src<COH>& src, int ld, int col, int batch) {
+__device__ __forceinline__ float column_sum_split(const Src<COH>& src, int ld, int col, int batch, int q) {
   float g = 0.f;
   for (int b0 = 0; b0 < batch; b0 += 64) {
-    float v[64];
+    float v[16];
 #pragma unroll
-    for (int k = 0; k < 64; ++k) v[k] = src[min(b0 + k, batch - 1) * ld + col];
-    __builtin_amdgcn_sched_barrier(0);  // all 64 loads in flight before the first wait
+    for (int k = 0; k < 16; ++k) v[k] = src[min(b0 + 16 * q + k, batch - 1) * ld + col];
+    __builtin_amdgcn_sched_barrier(0);  // all 16 loads in flight before the first wait
 #pragma unroll
-    for (int k = 0; k < 64; ++k) g += (b0 + k < batch) ? v[k] : 0.f;
+    for (int k = 0; k < 16; ++k) g += (b0 + 16 * q + k < batch) ? v[k] : 0.f;
   }
+  g += __shfl_xor(g, 1);  // (p0 + p1), (p2 + p3) ...
+  g += __shfl_xor(g, 2);  // ... then their sum, identical in all 4 lanes
   return g;
 }
 
-// fc-bias slots.  COH: wave-aligned so each wave reads ONE source (buffer descriptor in
-// SGPRs): [0,128) fc1 (120 used), [128,256) fc2 (84 used), [256,320) fc3 (10 used).
-// Plain loads: compact [0,214).
-constexpr int FCB_SLOTS = 320, FCB_ELEMS = 120 + 84 + 10;
+// fc-bias slots: columns padded per source to multiples of 16 (one wave = 16 columns), so
+// each wave reads ONE source and its buffer descriptor stays in SGPRs (COH): fc1 [0,128)
+// (120 used), fc2 [128,224) (84 used), fc3 [224,240) (10 used); slot = column * 4 + q.
+constexpr int FCB_ELEMS = 120 + 84 + 10;
+constexpr int FCB_COLS = 128 + 96 + 16;
+constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
 template <bool COH>
 __device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
+  const int tc = min(t, FCB_SLOTS - 1);
+  const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
+  const int colp = tc / SPLIT, q = t % SPLIT;
   const float* zp;
   int ld, col, n, off;
-  if constexpr (COH) {
-    const int grp = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform source (descriptor in SGPRs)
-    if (grp < 2) { zp = a.z1; ld = Z1_LD; col = t; n = 120; off = OFF_F1B; }
-    else if (grp < 4) { zp = a.z2; ld = Z2_LD; col = t - 128; n = 84; off = OFF_F2B; }
-    else { zp = a.z3; ld = Z3_LD; col = t - 256; n = 10; off = OFF_F3B; }
-  } else {  // plain loads: compact slots [0, 214)
-    if (t < 120) { zp = a.z1; ld = Z1_LD; col = t; n = 120; off = OFF_F1B; }
-    else if (t < 204) { zp = a.z2; ld = Z2_LD; col = t - 120; n = 84; off = OFF_F2B; }
-    else { zp = a.z3; ld = Z3_LD; col = t - 204; n = 10; off = OFF_F3B; }
-  }
+  if (grp < 8) { zp = a.z1; ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; }
+  else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; }
+  else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; }
   const Src<COH> src(zp, a.batch * ld);
-  if (t >= (COH ? FCB_SLOTS : FCB_ELEMS) || col >= n) return;
-  const int dst = off + col;
+  const int cc = min(col, n - 1);  // padding lanes recompute a real column (no divergence)
+  const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  sgd_finish(dst, column_sum(src, ld, col, a.batch), pv, mv, a);
+  const float g = column_sum_split(src, ld, cc, a.batch, q);  // every lane shuffles: no early exit
+  if (t < FCB_SLOTS && col < n && q == 0) sgd_finish(dst, g, pv, mv, a);
 }
 
 constexpr int CONV_ELEMS = SLAB;
+constexpr int CONV_SLOTS = CONV_ELEMS * SPLIT;  // 11,488
+__device__ __forceinline__ int conv_dst(int e) {
+  if (e < SLAB_C1B) return OFF_C1W + e;
+  if (e < SLAB_C2W) return OFF_C1B + (e - SLAB_C1B);
+  if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
+  return OFF_C2B + (e - SLAB_C2B);
+}
 template <bool COH>
-__device__ __forceinline__ void conv_task(int e, const ReduceArgs a) {
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs a) {
   const Src<COH> src(a.slab, a.batch * SLAB);
-  if (e >= CONV_ELEMS) return;
-  int dst;
-  if (e < SLAB_C1B) dst = OFF_C1W + e;
-  else if (e < SLAB_C2W) dst = OFF_C1B + (e - SLAB_C1B);
-  else if (e < SLAB_C2B) dst = OFF_C2W + (e - SLAB_C2W);
-  else dst = OFF_C2B + (e - SLAB_C2B);
+  const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
+  const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  sgd_finish(dst, column_sum(src, SLAB, e, a.batch), pv, mv, a);
+  const float g = column_sum_split(src, SLAB, e, a.batch, q);
+  if (t < CONV_SLOTS && q == 0) sgd_finish(dst, g, pv, mv, a);
 }
 
 // Epoch statistics of the step that just ran + publication of the next step's cursor,

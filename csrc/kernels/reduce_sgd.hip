@@ -17,7 +17,7 @@
 namespace dnn {
 
 constexpr int RT = 256;
-static_assert(RT >= FCB_ELEMS, "one fc-bias slot per thread");
+static_assert(RT % SPLIT == 0, "split column lanes stay inside a wave");
 
 
 
@@ -35,14 +35,15 @@ __device__ __forceinline__ void grad_reduce_body(const ReduceArgs& a) {
       return;
     }
     blk -= TILE_BLOCKS;
-    if (blk < 1) {
-      fcb_task<false>(threadIdx.x, a);  // RT >= FCB_ELEMS
+    constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
+    if (blk < FB) {
+      fcb_task<false>(blk * RT + threadIdx.x, a);
       return;
     }
-    blk -= 1;
+    blk -= FB;
   }
   if (conv) {
-    constexpr int CB = (CONV_ELEMS + RT - 1) / RT;
+    constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
     if (blk < CB) { conv_task<false>(blk * RT + threadIdx.x, a); return; }
     blk -= CB;
   }
@@ -88,8 +89,8 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
   const bool mlp = args.hi > OFF_F1W;
   const bool conv = args.lo < OFF_F1W;
   int nblk = 0;
-  if (mlp) nblk += TILE_BLOCKS + 1;
-  if (conv) nblk += (CONV_ELEMS + RT - 1) / RT;
+  if (mlp) nblk += TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
+  if (conv) nblk += (CONV_SLOTS + RT - 1) / RT;
   if (args.bookkeeping) nblk += 1;
   if (nblk == 0) return;
   hipLaunchKernelGGL(grad_reduce_kernel, dim3(nblk), dim3(RT), 0, stream, args);

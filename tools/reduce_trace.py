@@ -40,8 +40,8 @@ def main(reps: int = 40, batch: int = 64):
     a = a[:, :nb]
     t0 = a[:, :, 0].min(axis=1, keepdims=True)
     rel = np.median((a - t0[:, :, None]) * 0.01, axis=0)
-    roles = [("fc1 tiles", 0, 50), ("fc2 tiles", 50, 62), ("fc3 tiles", 62, 64), ("fc bias", 64, 65),
-             ("conv cols", 65, 77), ("bookkeeping", 77, 78)]
+    roles = [("fc1 tiles", 0, 50), ("fc2 tiles", 50, 62), ("fc3 tiles", 62, 64), ("fc bias", 64, 68),
+             ("conv cols", 68, 113), ("bookkeeping", 113, 114)]  # RT = 256: 960 / 11,488 split slots
     for name, lo, hi in roles:
         if hi <= nb:
             r = rel[lo:hi]
