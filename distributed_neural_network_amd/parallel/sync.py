@@ -118,6 +118,11 @@ class StepAllReduce(SyncPolicy):
                                                    bucket_kb=self.bucket_kb)
         else:
             engine.grad_sync = GradAllReduce(self.comm, bucket_kb=self.bucket_kb)
+            if getattr(engine, "use_graphs", False):
+                # host-side (gloo) collectives cannot live inside a captured hipGraph
+                engine.use_graphs = False
+                if hasattr(engine, "invalidate_graphs"):
+                    engine.invalidate_graphs()
 
 
 class EpochAverage(SyncPolicy):

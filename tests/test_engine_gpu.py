@@ -138,3 +138,19 @@ def test_bench_two_ranks_one_gpu_gloo(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 128
     assert out["value"] > 0 and out["steps"] == 20 and 0 <= out["val_acc"] <= 100
+
+
+@pytest.mark.parametrize("sync", ["step-allreduce", "epoch-avg"])
+def test_rank_drop_recovery_on_gpu_engine(tmp_path, sync):
+    """Fault recovery with the fused GPU engine: 3 ranks share the box's GPU over gloo,
+    rank 1 dies mid-epoch; survivors re-form, restore, re-partition and finish."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "distributed_neural_network_amd.parallel.launch", "-n", "3",
+                        os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "3", "--batch-size", "32",
+                        "--sync", sync, "--drop-rank", "1", "--drop-at-epoch", "1", "--drop-at-step", "2",
+                        "--train-samples", "768", "--test-samples", "256", "--device", "cuda", "--save", "ck.pt",
+                        "--nb-proc", "3", "--check-sync"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "communicator re-formed (generation 1, 2 ranks)" in r.stdout
+    assert r.stdout.count("Validation loss of updated master model:") == 3
