@@ -71,19 +71,26 @@ def build_hip(force: bool = False, verbose_resources: bool = False) -> Path:
     objdir = REPO / "build" / "hip"
     objdir.mkdir(parents=True, exist_ok=True)
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{CSRC}"]
-    objs = []
+    jobs, objs = [], []
     for src in HIP_SOURCES:
         obj = objdir / (src.stem + ".o")
         extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resources else []
-        _run(common + extra + ["-c", str(src), "-o", str(obj)])
+        jobs.append(common + extra + ["-c", str(src), "-o", str(obj)])
         objs.append(str(obj))
     for src in HOST_SOURCES:  # host-only C++ (RCCL via dlopen), compiled as HIP for the headers
         obj = objdir / (src.stem + ".o")
-        _run(common + ["-x", "hip", "-c", str(src), "-o", str(obj)])
+        jobs.append(common + ["-x", "hip", "-c", str(src), "-o", str(obj)])
         objs.append(str(obj))
     bobj = objdir / "bindings.o"
-    _run(common + _pybind_includes() + ["-x", "hip", "-c", str(HIP_BINDING), "-o", str(bobj)])
+    jobs.append(common + _pybind_includes() + ["-x", "hip", "-c", str(HIP_BINDING), "-o", str(bobj)])
     objs.append(str(bobj))
+    # translation units compile in parallel (bounded by MAX_JOBS / the CPU count)
+    from concurrent.futures import ThreadPoolExecutor
+
+    width = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+    with ThreadPoolExecutor(width) as ex:
+        for f in [ex.submit(_run, j) for j in jobs]:
+            f.result()
     tmp = target.with_suffix(".tmp.so")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-ldl"])
     os.replace(tmp, target)
