@@ -6,13 +6,13 @@ per GPU (weak scaling), synthetic CIFAR-shaped data (50,000 train / 10,000 test,
 3x32x32 uint8 -> normalised in-kernel), random-init weights, bf16 MFMA operands
 with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--sync epoch-avg|step-allreduce]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sync step-allreduce|epoch-avg]
 
-Synchronisation defaults to the reference algorithm (data_parallelism_train.py:185-254):
-local SGD over the rank's shard with a fresh momentum buffer per epoch, parameters
-averaged by an RCCL all-reduce at every epoch end (epoch boundaries fall inside the timed
-window: 50,000 / N samples per rank and epoch).  --sync step-allreduce averages the
-gradient on every step instead.
+Synchronisation defaults to a per-step gradient all-reduce (native RCCL, one fused 248 KB
+bucket inside the step hipGraph).  --sync epoch-avg runs the reference algorithm
+(data_parallelism_train.py:185-254): local SGD over the rank's shard with a fresh momentum
+buffer per epoch and an RCCL parameter all-reduce at every epoch end (epoch boundaries fall
+inside the timed window: 50,000 / N samples per rank and epoch).
 
 For N > 1 run under torchrun (one rank per GPU, RCCL over xGMI).  W untimed warmup
 steps, then EXACTLY K timed optimizer steps bracketed by barrier + device sync;
@@ -84,11 +84,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5000)
     ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--batch-size", type=int, default=64, help="per-GPU batch")
-    ap.add_argument("--sync", default="epoch-avg", choices=["epoch-avg", "step-allreduce"],
-                    help="epoch-avg (default) = the reference data_parallelism_train.py algorithm: every rank "
-                         "runs local momentum-SGD steps on its shard, parameters are all-reduced (avg) at every "
-                         "epoch end; step-allreduce = DDP-style per-step gradient all-reduce (stricter sync, "
-                         "the reference's listed future work)")
+    ap.add_argument("--sync", default="step-allreduce", choices=["step-allreduce", "epoch-avg"],
+                    help="step-allreduce (default, the performance path) = DDP-style per-step gradient "
+                         "all-reduce over RCCL; epoch-avg = the reference data_parallelism_train.py algorithm: "
+                         "local momentum-SGD steps on each shard, parameters all-reduced (avg) at every epoch end")
     ap.add_argument("--graph-chunk", type=int, default=64)
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
