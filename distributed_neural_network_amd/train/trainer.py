@@ -247,6 +247,11 @@ class Trainer:
                    "img_per_s": samples / dt if dt > 0 else 0.0, "world": self.comm.world,
                    "phases": self.timers.as_dict() if c.profile else None}
             self.history.append(rec)
+            if self.recoveries and self.recoveries[-1]["epoch"] == epoch and self.rank0:
+                # recovery latency is printed by _recover; this is the
+                # throughput of the first epoch on the re-formed group
+                print(f"[fault] post-recovery epoch {epoch}: {rec['img_per_s']:.1f} img/s on "
+                      f"{self.comm.world} ranks", flush=True)
             if self.rank0:
                 self.run_log["train/loss"].append(avg)
                 self.run_log["val/loss"].append(val_loss)

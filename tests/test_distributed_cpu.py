@@ -152,5 +152,6 @@ def test_rank_drop_reforms_and_finishes(tmp_path, sync):
                   r.stdout)
     assert m, r.stdout
     assert r.stdout.count("Validation loss of updated master model:") == 3
+    assert "[fault] post-recovery epoch 1:" in r.stdout
     sd, side = checkpoint.load(str(tmp_path / "ck.pt"))
     assert side["epoch"] == 2 and side["world"] == 2
