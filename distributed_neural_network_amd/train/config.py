@@ -93,6 +93,10 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
     g.add_argument("--drop-rank", type=int, default=None, help="fault injection: this rank dies hard")
     g.add_argument("--drop-at-epoch", type=int, default=0)
     g.add_argument("--drop-at-step", type=int, default=0)
+    g.add_argument("--no-overlap", dest="overlap", action="store_false", default=False,
+                   help="one fused gradient bucket on the compute stream (the default)")
+    g.add_argument("--emulate-parent", dest="sync", action="store_const", const="parent",
+                   help="alias of --sync parent: rank 0 is the reference's non-training parameter server")
     g.add_argument("--overlap", dest="overlap", action="store_true",
                    help="step-allreduce: 2 gradient buckets, the MLP all-reduce overlapped with the conv-bucket "
                         "reduction on a side stream (default: one fused bucket, latency-optimal at 248 KB)")

@@ -112,3 +112,13 @@ def test_cifar_binary_reader_roundtrip(tmp_path):
     assert np.array_equal(tr.images[7:14].numpy(), imgs[2][0])
     assert np.array_equal(tr.labels[:7].numpy(), imgs[1][1])
     assert np.array_equal(te.images.numpy(), xt)
+
+
+def test_cli_aliases_from_survey_flag_list():
+    from distributed_neural_network_amd.train.config import parse
+    assert parse("data-parallel", []).overlap is False
+    assert parse("data-parallel", ["--overlap"]).overlap is True
+    assert parse("data-parallel", ["--overlap", "--no-overlap"]).overlap is False
+    assert parse("data-parallel", ["--emulate-parent"]).sync == "parent"
+    c = parse("data-parallel", ["--dtype", "fp32", "--model", "lenet-bn", "--bucket-kb", "64", "--check-sync"])
+    assert (c.dtype, c.model, c.bucket_kb, c.check_sync) == ("fp32", "lenet-bn", 64, True)
