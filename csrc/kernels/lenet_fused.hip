@@ -73,7 +73,7 @@ static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 constexpr int A_R3 = 0;                     // bf16x8 records [16][18][16 (14 used)] of padded dY2 73,728
 constexpr int A_DY2 = 73728;                // bf16 [16][10][16]                                 5,120
 constexpr int A_DP1 = A_DY2 + 5120;         // f32 [6][196]                                      4,704
-constexpr int A_RS = A_DP1 + 4704;          // f32 [16][18] dY2 row sums (conv2 bias grad)       1,152
+constexpr int A_RS = A_DP1 + 4704;          // f32 [16][10] dY2 row sums (conv2 bias grad)         640
 constexpr int A_DY1 = 0;                    // bf16 [6] x 1824 B (28 rows x 64 B + 32 B pad)    10,944
 constexpr int DY1_CH = 1824;                //   channel stride 456 dwords (= 8 mod 64): conv1-wgrad A reads conflict-free
 constexpr int A_RS1 = A_DY1 + 6 * DY1_CH;   // f32 [6][28] dY1 row sums (conv1 bias grad)          672
@@ -190,6 +190,41 @@ __device__ __forceinline__ int r1_q(int t) { return (t >> 3) & 3; }
 // a K-step read the SAME yy of four channels: one XOR for all of them, 16 distinct 4-dword
 // bank slots per read group; the builder's write groups (8 consecutive yy) hit 8 slots.
 __device__ __forceinline__ int r3_index(int o, int yy, int x) { return (o * 18 + yy) * 16 + (x ^ (yy & 7)); }
+
+// conv2 data gradient of output row Y0 (and Y0 + 8 when TWO) against the flipped kernel:
+// K-step kk = (kyp, o-group) reads R3 row Y + kyp, and only rows 4..13 hold dY2, so the
+// K-steps of the y-padding rows are dropped at compile time (row Y0 <= 7 needs
+// kyp >= 4 - Y0, row Y0 + 8 needs kyp <= 5 - Y0).  Loads are batched per half.
+template <int Y0, bool TWO>
+__device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x8* wfl, int fg, int x,
+                                           f32x4& acc0, f32x4& acc1) {
+  constexpr int Y1 = TWO ? Y0 + 8 : Y0;
+  const unsigned char* base0[5];
+  const unsigned char* base1[5];
+#pragma unroll
+  for (int kyp = 0; kyp < 5; ++kyp) {
+    base0[kyp] = r3b + 16 * r3_index(fg, Y0 + kyp, x);
+    base1[kyp] = r3b + 16 * r3_index(fg, Y1 + kyp, x);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bf16x8 a0[10], a1[10], bv[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int kk = 10 * h + k, kyp = kk / 4, orow = 4 * (kk % 4) * 18 * 16 * 16;  // o offset, bytes
+      bv[k] = wfl[kk * 64];
+      if (Y0 + kyp >= 4) a0[k] = *reinterpret_cast<const bf16x8*>(base0[kyp] + orow);
+      if (TWO && Y1 + kyp <= 13) a1[k] = *reinterpret_cast<const bf16x8*>(base1[kyp] + orow);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int kyp = (10 * h + k) / 4;
+      if (Y0 + kyp >= 4) acc0 = mfma32(a0[k], bv[k], acc0);
+      if (TWO && Y1 + kyp <= 13) acc1 = mfma32(a1[k], bv[k], acc1);
+    }
+  }
+}
 
 // ---- in-launch reducer workgroups ------------------------------------------------------
 // The batch reduction of the weight gradients (+ SGD) runs in RED_BLOCKS extra
@@ -710,7 +745,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // ============ phase E: conv2 backward =================================================
   // dY2 = unpool(dA0) masked by ReLU is materialised by rows, branch-free, twice:
   //  * DY2 [16][10][16]: A operand of the conv2 weight gradient (8 pixels per lane),
-  //  * R3  [16][18][14] window records of dY2 zero-padded by 4 in y and x: A operand of
+  //  * R3  [16][18][14] window records of dY2 zero-padded by 4 in x (y rows 4..13; the y
+  //    padding rows are skipped by the consumer, never stored): A operand of
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
   //    flipped kernel WF - no col2im scratch, no gather pass.
   float* slab = slab_out + (size_t)b * SLAB;
@@ -719,56 +755,69 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
   float* RS = reinterpret_cast<float*>(smem + L_REGA + A_RS);
-  for (int t = tid; t < 288; t += NT) {
-    const int o = t / 18, yy = t - 18 * (t / 18), y = yy - 4;
-    const bool yv = y >= 0 && y < 10;
-    const int yc = yv ? y : 0, yb = (yc & 1) << 1;
-    int cd[5];
-    float da[5];
+  // 160 dY2 rows (o, y) x 2 record halves; the half is wave-uniform: threads 0-191 (waves
+  // 0-2) build records 0-6 and the first DY2 record, threads 192-383 (waves 3-5) records
+  // 7-13, the second DY2 record and the row sum.  The zero-padding rows of R3 (yy 0-3 and
+  // 14-17) are never written: the data gradient skips the K-steps that would read them.
+  {
+    const int half = tid >= 192 ? 1 : 0;
+    const int r = tid - 192 * half;
+    if (tid < 384 && r < 160) {
+      const int o = r / 10, y = r - 10 * o, yy = y + 4, yb = (y & 1) << 1;
+      int cd[5];
+      float da[5];
 #pragma unroll
-    for (int px = 0; px < 5; ++px) {
-      const int q = o * 25 + (yc >> 1) * 5 + px;
-      cd[px] = CODE2[q];
-      da[px] = DA0[q];
-    }
-    float v[22];  // v[cc] = dY2[o][y][cc - 4]
-    float rs = 0.f;
+      for (int px = 0; px < 5; ++px) {
+        const int q = o * 25 + (y >> 1) * 5 + px;
+        cd[px] = CODE2[q];
+        da[px] = DA0[q];
+      }
+      float v[22];  // v[cc] = dY2[o][y][cc - 4]
 #pragma unroll
-    for (int cc = 0; cc < 22; ++cc) {
-      const int x = cc - 4;
-      float tv = 0.f;
-      if (x >= 0 && x < 10) tv = (yv && cd[x >> 1] == (yb | (x & 1))) ? da[x >> 1] : 0.f;
-      v[cc] = tv;
-      rs += tv;
-    }
-#pragma unroll
-    for (int xr = 0; xr < 14; ++xr) {
-      bf16x8 r;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[xr + j];
-      R3[r3_index(o, yy, xr)] = r;
-    }
-    if (yv) {
-      bf16x8 r0, r1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        r0[j] = (bf16)v[4 + j];
-        r1[j] = (bf16)(j < 2 ? v[12 + j] : 0.f);
+      for (int cc = 0; cc < 22; ++cc) {
+        const int x = cc - 4;
+        v[cc] = (x >= 0 && x < 10 && cd[x >> 1] == (yb | (x & 1))) ? da[x >> 1] : 0.f;
       }
       bf16x8* drow = reinterpret_cast<bf16x8*>(DY2 + (o * 10 + y) * 16);
-      drow[0] = r0;
-      drow[1] = r1;
+      if (half == 0) {
+#pragma unroll
+        for (int xr = 0; xr < 7; ++xr) {
+          bf16x8 rr;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rr[j] = (bf16)v[xr + j];
+          R3[r3_index(o, yy, xr)] = rr;
+        }
+        bf16x8 r0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r0[j] = (bf16)v[4 + j];
+        drow[0] = r0;
+      } else {
+#pragma unroll
+        for (int xr = 7; xr < 14; ++xr) {
+          bf16x8 rr;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rr[j] = (bf16)v[xr + j];
+          R3[r3_index(o, yy, xr)] = rr;
+        }
+        bf16x8 r1;
+        float rs = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r1[j] = (bf16)(j < 2 ? v[12 + j] : 0.f);
+#pragma unroll
+        for (int x = 0; x < 10; ++x) rs += v[4 + x];
+        drow[1] = r1;
+        RS[o * 10 + y] = rs;
+      }
     }
-    RS[o * 18 + yy] = rs;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (LDS-DMA, issued in phase D) landed
   lds_barrier();
   STAMP(8);
-  if (wave == 3) {  // conv2 bias gradient: 4 lanes per channel over its 18 row sums
+  if (wave == 3) {  // conv2 bias gradient: 4 lanes per channel over its 10 row sums
     const int o = lane >> 2, part = lane & 3;
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) t += (part + 4 * k < 18) ? RS[o * 18 + min(part + 4 * k, 17)] : 0.f;
+    for (int k = 0; k < 3; ++k) t += (part + 4 * k < 10) ? RS[o * 10 + min(part + 4 * k, 9)] : 0.f;
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
     if (part == 0) st_out(slab, SLAB_C2B + o, t, wt);
@@ -777,41 +826,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // x 20 K-steps in two halves.  Waves 0-5 run rows w and w + 8 TOGETHER (one WF
   // fragment load feeds both rows' MFMAs), waves 6-7 row w.  K-step kk: kyp = kk / 4
   // (compile-time), o = 4 (kk % 4) + fg, so every A load is a per-(lane, kyp) base
-  // address + an immediate offset: no per-load address arithmetic.
+  // address + an immediate offset: no per-load address arithmetic.  The wave-uniform switch
+  // picks a straight-line instance without the y-padding K-steps (max 28 MFMAs per wave).
   {
-    const bool two = wave < 6;
-    const int y0 = wave, y1 = two ? wave + 8 : wave, x = min(fr, 13);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool two = wv < 6;
+    const int y0 = wv, y1 = two ? wv + 8 : wv, x = min(fr, 13);
     const unsigned char* r3b = reinterpret_cast<const unsigned char*>(R3);
-    const unsigned char* base0[5];
-    const unsigned char* base1[5];
-#pragma unroll
-    for (int kyp = 0; kyp < 5; ++kyp) {
-      base0[kyp] = r3b + 16 * r3_index(fg, y0 + kyp, x);
-      base1[kyp] = r3b + 16 * r3_index(fg, y1 + kyp, x);
-    }
     const bf16x8* wfl = WF + fg * 16 + fr;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 a0[10], a1[10], bv[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int kk = 10 * h + k, kyp = kk / 4, orow = 4 * (kk % 4) * 18 * 16 * 16;  // o offset, bytes
-        bv[k] = wfl[kk * 64];
-        a0[k] = *reinterpret_cast<const bf16x8*>(base0[kyp] + orow);
-        if (two) a1[k] = *reinterpret_cast<const bf16x8*>(base1[kyp] + orow);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (two) {
-#pragma unroll
-        for (int k = 0; k < 10; ++k) {
-          acc0 = mfma32(a0[k], bv[k], acc0);
-          acc1 = mfma32(a1[k], bv[k], acc1);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 10; ++k) acc0 = mfma32(a0[k], bv[k], acc0);
-      }
+    switch (wv) {
+      case 0: dgrad_rows<0, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 1: dgrad_rows<1, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 2: dgrad_rows<2, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 3: dgrad_rows<3, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 4: dgrad_rows<4, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 5: dgrad_rows<5, true>(r3b, wfl, fg, x, acc0, acc1); break;
+      case 6: dgrad_rows<6, false>(r3b, wfl, fg, x, acc0, acc1); break;
+      default: dgrad_rows<7, false>(r3b, wfl, fg, x, acc0, acc1); break;
     }
     if (fr < 6) {
 #pragma unroll
