@@ -8,8 +8,10 @@ with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--sync step-allreduce|epoch-avg]
 
-Synchronisation defaults to a per-step gradient all-reduce (native RCCL, one fused 248 KB
-bucket inside the step hipGraph).  --sync epoch-avg runs the reference algorithm
+Synchronisation defaults to a per-step gradient all-reduce inside the step hipGraph: on
+one node the one-shot xGMI all-reduce kernel fused with the SGD update (every rank reads
+all peers' 248 KB gradients over the xGMI mesh in one hop; parallel/xgmi.py), or native
+RCCL (DNN_ALLREDUCE=rccl, multi-node, or if the xGMI self-test fails).  --sync epoch-avg runs the reference algorithm
 (data_parallelism_train.py:185-254): local SGD over the rank's shard with a fresh momentum
 buffer per epoch and an RCCL parameter all-reduce at every epoch end (epoch boundaries fall
 inside the timed window: 50,000 / N samples per rank and epoch).
@@ -65,6 +67,15 @@ class EpochCursor:
             self.engine.run_steps(n)
             self.left -= n
             k -= n
+
+
+def _allreduce_kind(engine) -> str | None:
+    """Which per-step gradient all-reduce ran: xgmi (one-shot IPC kernel fused with SGD),
+    rccl (native ncclAllReduce), torch-pg (host process group), or None (one rank)."""
+    gs = getattr(engine, "grad_sync", None)
+    if gs is None:
+        return None
+    return {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
 
 
 def _reserve_stdout() -> int:
@@ -200,7 +211,8 @@ def main():
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
-                          "reduce": "in-launch" if args.in_launch_reduce else "separate-kernel"},
+                          "reduce": "in-launch" if args.in_launch_reduce else "separate-kernel",
+                          "allreduce": _allreduce_kind(engine)},
                **epoch}
         os.write(out_fd, (json.dumps(out) + "\n").encode())
     comm.close()

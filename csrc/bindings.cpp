@@ -3,8 +3,11 @@
 // extension does not depend on libtorch's C++ ABI and launches onto whatever stream
 // python (or a hipGraph capture) is using.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <stdexcept>
+#include <tuple>
+#include <vector>
 #include <string>
 
 #include "kernels/launchers.h"
@@ -20,6 +23,20 @@ void rccl_broadcast(uintptr_t comm, uintptr_t buf, size_t count, int root, uintp
 int rccl_async_error(uintptr_t comm);
 void rccl_abort(uintptr_t comm);
 void rccl_destroy(uintptr_t comm);
+// one-shot xGMI all-reduce (comm/xgmi_allreduce.hip)
+std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
+uintptr_t xgmi_open(const std::string& handle);
+void xgmi_close(uintptr_t p);
+void xgmi_free(uintptr_t p);
+std::pair<uintptr_t, uintptr_t> xgmi_abort_word();
+void xgmi_set_abort(uintptr_t host_word, unsigned v);
+void xgmi_free_abort_word(uintptr_t host_word);
+int xgmi_max_blocks(long long capacity);
+long long xgmi_region_bytes(long long capacity);
+void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
+                           const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
+                           float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
+                           double timeout_s, int fences, hipStream_t stream);
 }  // namespace dnn
 
 namespace py = pybind11;
@@ -177,6 +194,26 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("rccl_async_error", &dnn::rccl_async_error);
   m.def("rccl_abort", [](uintptr_t c) { py::gil_scoped_release nogil; dnn::rccl_abort(c); });
   m.def("rccl_destroy", [](uintptr_t c) { py::gil_scoped_release nogil; dnn::rccl_destroy(c); });
+  // one-shot xGMI all-reduce (+ fused SGD) over IPC-mapped peer regions
+  m.def("xgmi_alloc", [](long long capacity) {
+    auto [p, h, kind] = dnn::xgmi_alloc(capacity);
+    return py::make_tuple(p, py::bytes(h), kind);
+  });
+  m.def("xgmi_open", [](py::bytes h) { return dnn::xgmi_open(std::string(h)); });
+  m.def("xgmi_close", &dnn::xgmi_close);
+  m.def("xgmi_free", &dnn::xgmi_free);
+  m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
+  m.def("xgmi_set_abort", &dnn::xgmi_set_abort);
+  m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);
+  m.def("xgmi_max_blocks", &dnn::xgmi_max_blocks);
+  m.def("xgmi_region_bytes", &dnn::xgmi_region_bytes);
+  m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
+                             u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
+                             double timeout_s, int fences, u stream) {
+    dnn::launch_xgmi_allreduce(regions, rank, capacity, n, P<const float>(grad), P<float>(out), P<float>(master),
+                               P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
+                               P<const unsigned>(abort_w), timeout_s, fences, S(stream));
+  });
   m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
                         int pack_only, u stream) {
     dnn::launch_sgd_apply(P<float>(master), P<const float>(grad), P<float>(mom), P<bf16>(shadow), n, lr, momentum,

@@ -187,6 +187,12 @@ class Communicator:
     # -- fault handling --------------------------------------------------------------------
     def abort(self) -> None:
         """Tear down the current communicator without waiting for peers."""
+        xg = getattr(self, "xgmi", None)
+        if xg is not None:
+            try:
+                xg.abort()  # releases xGMI flag waits spinning on a dead peer
+            except Exception:
+                pass
         nat = getattr(self, "native", None)
         if nat is not None:
             try:

@@ -110,6 +110,8 @@ class Heartbeat:
                         print(f"[fault] watchdog: rank {r} heartbeat stale > {self.timeout}s", flush=True)
                         if self.comm.backend == "nccl":
                             self.comm.abort()  # unblock collectives spinning on a dead peer
+                        elif getattr(self.comm, "xgmi", None) is not None:
+                            self.comm.xgmi.abort()  # xGMI flag waits (host collectives fail by themselves)
             except Exception:
                 pass
 

@@ -10,8 +10,10 @@
   server (data_parallelism_train.py:101-129); the average is over ranks 1..N-1
   (rank 0 contributes zeros to a sum all-reduce, everyone divides by N-1).
 * ``step-allreduce`` - DDP-style per-step gradient averaging (the report's future
-  work, Project_Report.pdf p.4 §6.2): bucketed RCCL all-reduce overlapped with the
-  conv-bucket reduction, captured in the step hipGraph.
+  work, Project_Report.pdf p.4 §6.2), captured in the step hipGraph: on one node a
+  one-shot xGMI all-reduce fused with the SGD update (parallel/xgmi.py); otherwise
+  (or with --overlap / --bucket-kb) bucketed RCCL all-reduces, the MLP bucket
+  overlapped with the conv-bucket reduction.
 """
 from __future__ import annotations
 
@@ -105,6 +107,11 @@ class StepAllReduce(SyncPolicy):
         super().attach(engine)
         if not self.comm.distributed:
             engine.grad_sync = None
+        elif (xg := self._xgmi_group(engine)) is not None:
+            # GPU hot path on one node: one-shot xGMI all-reduce fused with the optimizer
+            from .xgmi import XgmiGradSync
+
+            engine.grad_sync = XgmiGradSync(xg)
         elif self.comm.backend == "nccl":
             # GPU hot path: native RCCL communicator, all-reduce launched on the engine stream
             from .rccl import NativeGradAllReduce, RcclComm
@@ -123,6 +130,38 @@ class StepAllReduce(SyncPolicy):
                 engine.use_graphs = False
                 if hasattr(engine, "invalidate_graphs"):
                     engine.invalidate_graphs()
+
+
+    XGMI_MAX_ELEMS = 4 << 20  # one-shot reads N x the gradient: beyond ~16 MB the RCCL ring wins
+
+    def _xgmi_group(self, engine):
+        """The one-shot xGMI group for this generation (built collectively, self-tested;
+        None -> RCCL).  ``--overlap`` / ``--bucket-kb`` ask for the bucketed RCCL path."""
+        from . import xgmi
+
+        if getattr(engine, "overlap", False) or self.bucket_kb or not xgmi.wanted(self.comm):
+            return None
+        n = engine.grad.numel()
+        if n > self.XGMI_MAX_ELEMS:
+            return None
+        grp = getattr(self.comm, "xgmi", None)
+        stale = None
+        if grp is not None and (grp.generation != self.comm.generation or grp.capacity < n):
+            stale, grp = grp, None
+        if grp is None and not getattr(self.comm, "xgmi_refused", False):
+            grp = self.comm.xgmi = xgmi.build_group(self.comm, n)
+            self.comm.xgmi_refused = grp is None
+        if stale is not None:
+            stale.close()  # after the new regions exist: no address of the old ones is reused
+        if hasattr(engine, "invalidate_graphs"):
+            engine.invalidate_graphs()
+        return grp
+
+    def epoch_end(self, engine, epoch: int) -> None:
+        check = getattr(engine.grad_sync, "check", None)
+        if check is not None:
+            check()  # a timed-out / aborted xGMI wait surfaces here as a CommError
+        super().epoch_end(engine, epoch)
 
 
 class EpochAverage(SyncPolicy):

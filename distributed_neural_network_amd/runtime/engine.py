@@ -14,8 +14,9 @@ model_replication_train.py:96-114, single_proc_train.py:61-74) and ``eval``
 (data_parallelism_train.py:157-183).
 
 HipEngine design (MI355X): a step is 2 kernels (fused per-sample fwd/bwd, batch
-reduce + SGD) or, with a per-step gradient all-reduce, 2 + 1 kernels around
-bucketed RCCL all-reduces.  Steps are captured into hipGraphs (through
+reduce + SGD) or, with a per-step gradient all-reduce, 3 kernels (fused, batch reduce,
+one-shot xGMI all-reduce + SGD; parallel/xgmi.py) - or 2 + 1 kernels around bucketed
+RCCL all-reduces when the xGMI path is unavailable.  Steps are captured into hipGraphs (through
 torch.cuda.CUDAGraph) in chunks of ``graph_chunk`` steps; the step cursor, the
 tail-batch size and the epoch loss/accuracy accumulators live on the device, so a
 chunk replays with zero host work per step and no host<->device sync until the
@@ -294,6 +295,10 @@ class HipEngine(Engine):
                 self._launch_fused_reduce(1, s)
                 return
             self._launch_fused_reduce(0, s)
+            if getattr(self.grad_sync, "fuses_sgd", False):
+                self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
+                                             self.momentum, LAYOUT.total)
+                return
             self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])
             self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
                                LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
@@ -305,6 +310,13 @@ class HipEngine(Engine):
                              self._p(self.loss), self._p(self.correct), s)
         if self.grad_sync is None:
             self._reduce(1, 0, LAYOUT.total, 1, s)
+            return
+        if getattr(self.grad_sync, "fuses_sgd", False):
+            # one-shot xGMI all-reduce: batch reduction -> [publish, 1 hop, rank-order sum,
+            # momentum SGD, bf16 weight images] in ONE launch (parallel/xgmi.py)
+            self._reduce(0, 0, LAYOUT.total, 1, s)
+            self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum,
+                                         LAYOUT.total)
             return
         mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
         if self.overlap:

@@ -179,6 +179,11 @@ class LayerEngine(Engine):
         logits = self.forward(self.x, True, self.state)
         loss, corr, dl = L.cross_entropy(logits, self.labels, self.state)
         logits.backward(dl)  # writes every parameter gradient into self.grad (no zeroing needed)
+        if self.grad_sync is not None and getattr(self.grad_sync, "fuses_sgd", False):
+            # one-shot xGMI all-reduce with the momentum-SGD update in the same launch
+            self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, None, self.lr, self.momentum,
+                                         self.play.total)
+            return
         if self.grad_sync is not None:
             self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
         if self.gpu:

@@ -90,7 +90,8 @@ assert all(torch.allclose(res[0], r, atol=1e-6) for r in res[1:])
 comm.close()
 print("OK")
 '''
-    r = _run_py(code, {"DNN_FORCE_COLLECTIVES": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29611"})
+    r = _run_py(code, {"DNN_FORCE_COLLECTIVES": "1", "DNN_ALLREDUCE": "rccl", "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": "29611"})
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 

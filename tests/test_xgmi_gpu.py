@@ -1,0 +1,129 @@
+"""GPU tests of the one-shot xGMI gradient all-reduce (csrc/comm/xgmi_allreduce.hip).
+
+The box has one GPU, so the multi-rank cases run 2 processes on the same device (IPC
+regions of another process on the same GPU go through the same hipIpc path as peers on
+other GPUs); host collectives use gloo there (RCCL refuses two ranks on one device).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _py(code, env_extra, timeout=300):
+    env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
+    return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_xgmi_one_rank_matches_local_sgd():
+    """World size 1 with forced collectives: batch reduce -> xGMI kernel (publish, flag,
+    gather, SGD + bf16 images) must reproduce the fused local-SGD step bitwise."""
+    code = r'''
+import numpy as np, torch
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.parallel import Communicator, make_policy
+from distributed_neural_network_amd.parallel.xgmi import XgmiGradSync
+from distributed_neural_network_amd.runtime import HipEngine
+torch.cuda.set_device(0)
+comm = Communicator(device=torch.device("cuda", 0))
+data = synthetic(1000, 5)
+a = init_arena(seed=9)
+res = []
+for sync_on, graphs, inl in [(False, True, False), (True, True, False), (True, False, False), (True, True, True)]:
+    eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, in_launch_reduce=inl)
+    pol = make_policy("step-allreduce", comm)
+    pol.attach(eng)
+    if not sync_on:
+        eng.grad_sync = None
+    else:
+        assert isinstance(eng.grad_sync, XgmiGradSync), type(eng.grad_sync)
+    eng.attach(data); eng.begin_epoch(np.arange(1000, dtype=np.int32)); eng.run_steps(16)
+    torch.cuda.synchronize()
+    if sync_on:
+        pol.epoch_end(eng, 0)  # raises if a wait timed out
+    res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), eng.epoch_stats()))
+for m, mo, sh, st in res[1:]:
+    assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo) and torch.equal(res[0][2], sh)
+    assert st.samples == 1000 and st.loss_sum == res[0][3].loss_sum
+print("kind", comm.xgmi.kind)
+comm.close()
+print("OK")
+'''
+    r = _py(code, {"DNN_FORCE_COLLECTIVES": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29631"})
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+_TWO_RANK = r'''
+import os, sys, numpy as np, torch
+from distributed_neural_network_amd.data import EpochSampler, synthetic
+from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.parallel import Communicator, make_policy, replica_checksums
+torch.cuda.set_device(0)
+comm = Communicator(device=torch.device("cuda", 0))
+from distributed_neural_network_amd.runtime import HipEngine
+data = synthetic(2048, 3)
+eng = HipEngine(batch=64, arena=init_arena(seed=11), graph_chunk=8, use_graphs=os.environ["GRAPHS"] == "1")
+eng.attach(data)
+pol = make_policy("step-allreduce", comm)
+pol.attach(eng)
+pol.initial_broadcast(eng)
+samp = EpochSampler.for_rank(len(data), comm.rank, comm.world, seed=1, mode="shard")
+for ep in range(2):
+    pol.epoch_start(eng, ep)
+    eng.begin_epoch(samp.order(ep))
+    eng.run_steps(samp.steps(64))
+    eng.synchronize()
+    pol.epoch_end(eng, ep)
+kind = type(eng.grad_sync).__name__
+torch.save({"master": eng.master.cpu(), "kind": kind}, os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
+comm.close()
+'''
+
+
+def _two_ranks(tmp_path, allreduce, graphs, port):
+    out = tmp_path / allreduce
+    out.mkdir()
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
+               OUT=str(out), GRAPHS=graphs)
+    script = tmp_path / "w.py"
+    script.write_text(_TWO_RANK)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    import torch
+    return [torch.load(out / f"r{i}.pt", weights_only=True) for i in range(2)], r
+
+
+def test_xgmi_two_ranks_match_host_allreduce(tmp_path):
+    """2 ranks on the box's GPU: the IPC one-shot all-reduce + fused SGD keeps the replicas
+    bit-identical and matches the gloo all-reduce + sgd_apply path."""
+    import torch
+
+    xg, r = _two_ranks(tmp_path, "xgmi", "1", 29641)
+    assert xg[0]["kind"] == "XgmiGradSync", r.stderr[-2000:]
+    assert torch.equal(xg[0]["master"], xg[1]["master"])
+    host, _ = _two_ranks(tmp_path, "rccl", "0", 29643)  # DNN_BACKEND=gloo: host all-reduce, eager
+    assert host[0]["kind"] == "GradAllReduce"
+    assert torch.equal(host[0]["master"], host[1]["master"])
+    # same math up to fma contraction: sgd_apply rounds grad * grad_scale separately
+    assert torch.allclose(xg[0]["master"], host[0]["master"], rtol=0, atol=1e-6), \
+        float((xg[0]["master"] - host[0]["master"]).abs().max())
+
+
+def test_bench_two_ranks_xgmi(tmp_path):
+    """bench.py with 2 ranks sharing the GPU: graph-captured xGMI step all-reduce."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29657", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "200", "--warmup", "20"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] == "xgmi", out
