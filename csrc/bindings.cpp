@@ -36,7 +36,10 @@ long long xgmi_region_bytes(long long capacity);
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, int fences, hipStream_t stream);
+                           double timeout_s, int fences, int prepub, hipStream_t stream);
+long long xgmi_slot_bytes(long long capacity);
+void xgmi_clear_slots(uintptr_t region, long long capacity);
+long long xgmi_flag_bytes(long long capacity);
 }  // namespace dnn
 
 namespace py = pybind11;
@@ -103,19 +106,25 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("grad_reduce", [](u a0, u h1, u h2, u z1, u z2, u z3, u slab, u loss, u correct, int batch, u master,
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
-                          u stream, u stamps) {
+                          u stream, u stamps, u xg_region, long long xg_slot_bytes, long long xg_flag_bytes,
+                          u xg_ctr) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
                       P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order), order_len,
                       P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping,
                       P<long long>(stamps)};
+    a.xg_region = P<unsigned char>(xg_region);
+    a.xg_slot_bytes = xg_slot_bytes;
+    a.xg_flag_bytes = xg_flag_bytes;
+    a.xg_ctr = P<const unsigned>(xg_ctr);
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
      py::arg("loss"), py::arg("correct"), py::arg("batch"), py::arg("master"), py::arg("grad"), py::arg("mom"),
      py::arg("shadow"), py::arg("state"), py::arg("stats"), py::arg("lr"), py::arg("momentum"),
      py::arg("grad_scale"), py::arg("fuse_sgd"), py::arg("lo"), py::arg("hi"), py::arg("bookkeeping"),
-     py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0);
+     py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
+     py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
@@ -207,12 +216,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);
   m.def("xgmi_max_blocks", &dnn::xgmi_max_blocks);
   m.def("xgmi_region_bytes", &dnn::xgmi_region_bytes);
+  m.def("xgmi_slot_bytes", &dnn::xgmi_slot_bytes);
+  m.def("xgmi_clear_slots", &dnn::xgmi_clear_slots);
+  m.def("xgmi_flag_bytes", &dnn::xgmi_flag_bytes);
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
-                             double timeout_s, int fences, u stream) {
+                             double timeout_s, int fences, int prepub, u stream) {
     dnn::launch_xgmi_allreduce(regions, rank, capacity, n, P<const float>(grad), P<float>(out), P<float>(master),
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
-                               P<const unsigned>(abort_w), timeout_s, fences, S(stream));
+                               P<const unsigned>(abort_w), timeout_s, fences, prepub, S(stream));
   });
   m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
                         int pack_only, u stream) {

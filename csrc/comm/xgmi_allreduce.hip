@@ -60,6 +60,8 @@ struct XgmiArgs {
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int fences;               // bit 0: system release before the flag push, bit 1: system acquire after the wait
+  int prepub;               // 1: the previous kernel (grad_reduce) already stored this step's gradients in
+                            //    the own slot (system-coherent): no publish copy, flags go out at once
 };
 
 __device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
@@ -90,19 +92,21 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
     const int e = min(lo + k * XG_THREADS + tid, a.n - 1);
-    mine[k] = g[e];
+    mine[k] = a.prepub ? ld_sys(my_slot + e) : g[e];
     if (a.mode != 0) {
       p_old[k] = a.master[e];
       m_old[k] = a.mom[e];
     }
   }
+  if (!a.prepub) {
 #pragma unroll
-  for (int k = 0; k < XG_PER_THREAD; ++k) {
-    const int e = lo + k * XG_THREADS + tid;
-    if (e < a.n) st_sys(my_slot + e, mine[k]);
+    for (int k = 0; k < XG_PER_THREAD; ++k) {
+      const int e = lo + k * XG_THREADS + tid;
+      if (e < a.n) st_sys(my_slot + e, mine[k]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   if (tid < 64) {
     if (a.fences & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
     if (tid < a.nranks && tid != a.rank) {  // (own data stays in registers: no own flag)
@@ -214,6 +218,14 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity) {
   return {reinterpret_cast<uintptr_t>(p), std::string(h.reserved, HIP_IPC_HANDLE_SIZE), kind};
 }
 
+// zero both data slots (keeps the flags): elements a pre-published step never writes (arena
+// padding) must read as 0 after the self-test filled the slots
+void xgmi_clear_slots(uintptr_t region, long long capacity) {
+  xcheck(hipMemset(reinterpret_cast<unsigned char*>(region) + xgmi_flag_bytes(capacity), 0,
+                   2 * xgmi_slot_bytes(capacity)), "hipMemset(xgmi slots)");
+  xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
 uintptr_t xgmi_open(const std::string& handle) {
   if (handle.size() != HIP_IPC_HANDLE_SIZE) throw std::runtime_error("bad IPC handle size");
   hipIpcMemHandle_t h;
@@ -252,7 +264,7 @@ void xgmi_free_abort_word(uintptr_t host_word) {
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, int fences, hipStream_t stream) {
+                           double timeout_s, int fences, int prepub, hipStream_t stream) {
   const int nranks = (int)regions.size();
   if (nranks < 1 || nranks > XG_MAX_RANKS) throw std::runtime_error("xgmi all-reduce: 1..8 ranks");
   if (rank < 0 || rank >= nranks) throw std::runtime_error("xgmi all-reduce: bad rank");
@@ -280,6 +292,7 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
   a.fences = fences;
+  a.prepub = prepub;
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, stream, a);
   HIP_CHECK(hipGetLastError());

@@ -17,6 +17,13 @@ struct ReduceArgs {
   int lo, hi;     // arena element range [lo, hi) handled by this launch (gradient bucket)
   int bookkeeping;  // 1: this launch also advances the cursor / epoch statistics
   long long* stamps = nullptr;  // diagnostic: per-block [start, end] s_memrealtime (grad_reduce)
+  // one-shot xGMI all-reduce hand-off (comm/xgmi_allreduce.hip): when set, the reduced
+  // gradients go straight into this rank's shared region (parity slot of the next
+  // all-reduce step, read from the group's counters) with system-coherent stores, so the
+  // all-reduce kernel skips its publish copy
+  unsigned char* xg_region = nullptr;
+  long long xg_slot_bytes = 0, xg_flag_bytes = 0;
+  const unsigned* xg_ctr = nullptr;
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

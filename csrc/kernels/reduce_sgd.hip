@@ -61,6 +61,10 @@ __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
 
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(ReduceArgs a) {
   reduce_stamp(a, 0);
+  if (a.xg_region != nullptr) {  // gradients -> the shared slot of the coming xGMI step
+    const unsigned step = a.xg_ctr[0] + 1u;
+    a.grad = reinterpret_cast<float*>(a.xg_region + a.xg_flag_bytes + (step & 1u) * a.xg_slot_bytes);
+  }
   grad_reduce_body(a);
   if (a.stamps != nullptr) __syncthreads();
   reduce_stamp(a, 1);

@@ -99,16 +99,23 @@ class XgmiGroup:
         self.fences = int(fences) if fences is not None else (0 if self.kind == "uncached" else 3)
 
     # -- launches --------------------------------------------------------------------------
+    def handoff(self) -> dict:
+        """grad_reduce kwargs that make it store the reduced gradients straight into this
+        rank's shared slot (then ``allreduce_sgd(..., prepublished=True)``)."""
+        return dict(xg_region=self.local, xg_slot_bytes=self.ext.xgmi_slot_bytes(self.capacity),
+                    xg_flag_bytes=self.ext.xgmi_flag_bytes(self.capacity), xg_ctr=self.ctr.data_ptr())
+
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, mom: torch.Tensor, shadow: torch.Tensor | None,
-                      lr: float, momentum: float, n: int | None = None) -> None:
-        """grad <- avg over ranks; momentum SGD on master/mom (+ bf16 shadow images)."""
+                      lr: float, momentum: float, n: int | None = None, prepublished: bool = False) -> None:
+        """grad <- avg over ranks; momentum SGD on master/mom (+ bf16 shadow images).
+        ``prepublished``: the gradients are already in the shared slot (``handoff``)."""
         n = grad.numel() if n is None else n
         s = torch.cuda.current_stream(grad.device).cuda_stream
         mode = 1 if shadow is not None else 2
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, n, grad.data_ptr(), grad.data_ptr(),
                                 master.data_ptr(), mom.data_ptr(), shadow.data_ptr() if shadow is not None else 0,
                                 lr, momentum, 1.0 / self.world, mode, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, self.fences, s)
+                                self.timeout_s, self.fences, int(prepublished), s)
 
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place average of a flat fp32 tensor."""
@@ -116,7 +123,7 @@ class XgmiGroup:
         s = torch.cuda.current_stream(t.device).cuda_stream
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, t.numel(), t.data_ptr(), t.data_ptr(),
                                 0, 0, 0, 0.0, 0.0, 1.0 / self.world, 0, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, self.fences, s)
+                                self.timeout_s, self.fences, 0, s)
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
@@ -188,7 +195,10 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
         ok, why = False, "a peer could not map the regions"
     else:
         comm.gather_scalars(0.0)
-    votes = comm.gather_scalars(1.0 if ok else 0.0)
+    votes = comm.gather_scalars(1.0 if ok else 0.0)  # (also: every peer finished reading our slots)
+    if grp is not None and all(v == 1.0 for v in votes):
+        with torch.cuda.device(comm.device):
+            grp.ext.xgmi_clear_slots(grp.local, grp.capacity)
     if os.environ.get("DNN_DEBUG_XGMI") == "1":
         print(f"[xgmi] gen {comm.generation} rank {comm.rank}/{comm.world} ok={ok} {why} votes={votes} "
               f"regions={[hex(r) for r in grp.regions] if grp is not None and ok else None} "

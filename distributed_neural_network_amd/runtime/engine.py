@@ -266,13 +266,13 @@ class HipEngine(Engine):
             self.batch_ids[:first].copy_(self.order[:first])
 
     # -- one step (launch sequence; also what graphs capture) ---------------------------
-    def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int) -> None:
+    def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int, **xg) -> None:
         self.ext.grad_reduce(self._p(self.a0), self._p(self.h1), self._p(self.h2), self._p(self.z1),
                              self._p(self.z2), self._p(self.z3), self._p(self.slab), self._p(self.loss),
                              self._p(self.correct), self.batch, self._p(self.master), self._p(self.grad),
                              self._p(self.mom), self._p(self.shadow), self._p(self.state), self._p(self.stats),
                              self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, self._p(self.order),
-                             self.order_len, self._p(self.batch_ids), s)
+                             self.order_len, self._p(self.batch_ids), s, **xg)
 
     def _launch_fused_reduce(self, fuse_sgd: int, s: int) -> None:
         """Fused step with the batch reduction (+ SGD when fuse_sgd) in the same launch."""
@@ -314,9 +314,10 @@ class HipEngine(Engine):
         if getattr(self.grad_sync, "fuses_sgd", False):
             # one-shot xGMI all-reduce: batch reduction -> [publish, 1 hop, rank-order sum,
             # momentum SGD, bf16 weight images] in ONE launch (parallel/xgmi.py)
-            self._reduce(0, 0, LAYOUT.total, 1, s)
-            self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum,
-                                         LAYOUT.total)
+            grp = self.grad_sync.group
+            self._reduce(0, 0, LAYOUT.total, 1, s, **grp.handoff())  # reduced grads -> shared slot
+            grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum, LAYOUT.total,
+                              prepublished=True)
             return
         mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
         if self.overlap:
