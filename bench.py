@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--train-samples", type=int, default=50_000,
+                    help="synthetic training-set size (CIFAR-10: 50,000); smaller = more epoch boundaries "
+                         "inside the timed window (diagnostic)")
     args = ap.parse_args()
 
     env = detect()
@@ -125,7 +128,7 @@ def main():
     comm = Communicator(env, device)
     B = args.batch_size
 
-    train, test = synthetic(50_000, args.seed, True), synthetic(10_000, args.seed, False)
+    train, test = synthetic(args.train_samples, args.seed, True), synthetic(10_000, args.seed, False)
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
     if args.model == "lenet" and args.engine in ("auto", "fused") and args.dtype == "bf16":
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
@@ -137,6 +140,7 @@ def main():
     engine.attach(train)
     test_dev = test.to(device)
     policy = make_policy(args.sync, comm)
+    policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
     policy.attach(engine)
     policy.initial_broadcast(engine)
     cur = EpochCursor(engine, sampler, policy, B)
@@ -161,6 +165,8 @@ def main():
     dt = time.perf_counter() - t0
     if getattr(engine, "sync_error", lambda: False)():
         raise RuntimeError("in-launch reducer hand-off timed out (sync error flag set)")
+    if hasattr(engine.grad_sync, "check"):
+        engine.grad_sync.check()  # raises if any xGMI wait in the timed window timed out
     dt = comm.reduce_scalar(dt, "max")
     ms_per_step = 1000.0 * dt / args.steps
     value = comm.world * B * args.steps / dt

@@ -226,6 +226,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
                                P<const unsigned>(abort_w), timeout_s, fences, prepub, S(stream));
   });
+  m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream) {
+    dnn::launch_epoch_begin(P<const int32_t>(staged), P<int32_t>(order), n, P<int32_t>(state), P<int32_t>(batch_ids),
+                            batch, S(stream));
+  });
   m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
                         int pack_only, u stream) {
     dnn::launch_sgd_apply(P<float>(master), P<const float>(grad), P<float>(mom), P<bf16>(shadow), n, lr, momentum,

@@ -39,6 +39,8 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
+void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
+                        hipStream_t stream);
 void launch_sgd_apply(float* master, const float* grad, float* mom, bf16* shadow, int n, float lr, float momentum,
                       float grad_scale, int pack_only, hipStream_t stream);
 

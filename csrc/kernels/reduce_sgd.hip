@@ -88,7 +88,31 @@ __global__ void __launch_bounds__(RT) sgd_apply_kernel(float* __restrict__ maste
   }
 }
 
+// Epoch start on the compute stream in ONE launch: the epoch's sample order (uploaded ahead
+// of time into a staging buffer on a side stream) -> the order the bookkeeping reads, the
+// first step's sample ids, cursor 0 and the first batch's valid count.
+__global__ void __launch_bounds__(RT) epoch_begin_kernel(const int32_t* __restrict__ staged, int32_t* __restrict__ order,
+                                                         int n, int32_t* __restrict__ state,
+                                                         int32_t* __restrict__ batch_ids, int batch) {
+  for (int i = blockIdx.x * RT + threadIdx.x; i < n; i += gridDim.x * RT) {
+    const int32_t v = staged[i];
+    order[i] = v;
+    if (i < batch) batch_ids[i] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    state[ST_CURSOR] = 0;
+    state[ST_BVALID] = min(batch, n);
+  }
+}
+
 // ---- host launchers ---------------------------------------------------------------------
+void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
+                        hipStream_t stream) {
+  const int nblk = max(1, min((n + RT - 1) / RT, 256));
+  hipLaunchKernelGGL(epoch_begin_kernel, dim3(nblk), dim3(RT), 0, stream, staged, order, n, state, batch_ids, batch);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
   const bool mlp = args.hi > OFF_F1W;
   const bool conv = args.lo < OFF_F1W;

@@ -209,6 +209,10 @@ class HipEngine(Engine):
         self.loss = torch.zeros(B, **f32)
         self.correct = torch.zeros(B, device=dev, dtype=torch.int32)
         self.order = torch.zeros(0, device=dev, dtype=torch.int32)
+        self.staged = torch.zeros(0, device=dev, dtype=torch.int32)  # epoch order upload target
+        self._pin = [torch.empty(0, dtype=torch.int32), torch.empty(0, dtype=torch.int32)]
+        self._pin_ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self._pin_i = 0
         self.batch_ids = torch.zeros(B, device=dev, dtype=torch.int32)  # sample ids of the next step
         # in-launch reducer hand-off counters [rows, slabs, done, error] (lenet_fused.hip);
         # zero between launches (the last reducer resets them)
@@ -247,23 +251,34 @@ class HipEngine(Engine):
         self.invalidate_graphs()
 
     def begin_epoch(self, order: np.ndarray) -> None:
+        """Queue the epoch start without a host<->device synchronisation: the order goes
+        through a pinned staging buffer with a stream-ordered async copy, then ONE
+        ``epoch_begin`` launch sets the order, the first step's sample ids and the cursor.
+        (Measured at 100 steps per epoch: 0.15 us/step of boundary cost vs 0.5-0.8 for a
+        blocking upload + separate fill/copy ops; an upload on a side stream with a
+        cross-stream event wait was slower still, 1.4 us/step, even in steady state.)"""
         order = np.ascontiguousarray(order, dtype=np.int32)
         n = int(order.shape[0])
         if self.order.numel() < n:
+            torch.cuda.synchronize(self.device)
             self.order = torch.zeros(n, device=self.device, dtype=torch.int32)
+            self.staged = torch.zeros(n, device=self.device, dtype=torch.int32)
             self.invalidate_graphs()
         if n != self.order_len:
             self.invalidate_graphs()  # order_len is a baked kernel argument
         self.order_len = n
+        main = torch.cuda.current_stream(self.device)
         if n:
-            self.order[:n].copy_(torch.from_numpy(order), non_blocking=False)
-        # step 0 of the epoch: cursor, valid count and sample ids (later steps are
-        # published on device by the reduce kernel's bookkeeping block)
-        first = min(self.batch, n)
-        self.state[0] = 0
-        self.state[1] = first
-        if first:
-            self.batch_ids[:first].copy_(self.order[:first])
+            i = self._pin_i = self._pin_i ^ 1
+            if self._pin[i].numel() < n:
+                self._pin[i] = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            self._pin_ev[i].synchronize()  # this staging buffer's previous upload is done
+            self._pin[i][:n].numpy()[:] = order
+            self.staged[:n].copy_(self._pin[i][:n], non_blocking=True)
+            self._pin_ev[i].record(main)
+        with torch.cuda.device(self.device):
+            self.ext.epoch_begin(self._p(self.staged), self._p(self.order), n, self._p(self.state),
+                                 self._p(self.batch_ids), self.batch, main.cuda_stream)
 
     # -- one step (launch sequence; also what graphs capture) ---------------------------
     def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int, **xg) -> None:
