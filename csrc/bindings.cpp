@@ -187,6 +187,24 @@ PYBIND11_MODULE(_dnn_hip, m) {
     a.batch_ids = P<int32_t>(batch_ids);
     dnn::launch_layer_bookkeeping(a, S(stream));
   });
+  m.def("conv_fwd", [](u x, u w, u bias, u y, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                       u stream) {
+    dnn::launch_conv_fwd(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(y), B, C, H, W, M, K,
+                         pad, bf16_ops, S(stream));
+  });
+  m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
+    int s = 1, cps = 1;
+    dnn::conv_wgrad_split(B, C, H, W, M, K, pad, &s, &cps);
+    return s;
+  });
+  m.def("conv_wgrad", [](u x, u dy, u part, u dw, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                         u stream) {
+    dnn::launch_conv_wgrad(P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), B, C, H, W, M, K, pad,
+                           bf16_ops, S(stream));
+  });
+  m.def("flip_weights", [](u w, int O, int C, int K, u wf, u stream) {
+    dnn::launch_flip_weights(P<const float>(w), O, C, K, P<float>(wf), S(stream));
+  });
   m.def("sgd_flat", [](u p, u g, u mom, long n, float lr, float momentum, float grad_scale, u stream) {
     dnn::launch_sgd_flat(P<float>(p), P<const float>(g), P<float>(mom), n, lr, momentum, grad_scale, S(stream));
   });

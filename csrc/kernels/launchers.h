@@ -67,6 +67,13 @@ void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* pa
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
                  int32_t* correct, float* dlogits, hipStream_t s);
 void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s);
+// implicit-GEMM convolution (conv_igemm.hip)
+void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W, int M,
+                     int K, int pad, int bf16_ops, hipStream_t s);
+void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S, int* cps);
+void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, int C, int H, int W, int M,
+                       int K, int pad, int bf16_ops, hipStream_t s);
+void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
 

@@ -30,6 +30,7 @@ HIP_SOURCES = [
     CSRC / "kernels" / "lenet_fused.hip",
     CSRC / "kernels" / "reduce_sgd.hip",
     CSRC / "kernels" / "layers.hip",
+    CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "comm" / "xgmi_allreduce.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"

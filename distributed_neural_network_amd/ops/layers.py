@@ -2,9 +2,9 @@
 
 Every op has two implementations with the SAME semantics:
 
-* on a ROCm device: the hand-written gfx950 kernels (``_dnn_hip``) for everything that is
-  not a plain GEMM, and the library GEMMs (hipBLASLt via ``torch.matmul``) for the
-  matrix products of Conv2d (im2col -> batched GEMM -> col2im) and Linear;
+* on a ROCm device: the hand-written gfx950 kernels (``_dnn_hip``) - Conv2d as
+  implicit-GEMM MFMA kernels (conv_igemm.hip), ReLU / pool / BatchNorm / loss / SGD in
+  layers.hip - and the library GEMMs (hipBLASLt via ``torch.matmul``) for Linear only;
 * on the CPU: plain PyTorch ops - the test double / CPU-only path (never used on a GPU:
   a missing extension there raises instead of silently falling back).
 
@@ -61,7 +61,12 @@ def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 # ---- Conv2d (stride 1, square kernel, zero padding) -------------------------------------------
 class Conv2dFn(torch.autograd.Function):
-    """``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
+    """On MI355X: implicit-GEMM MFMA kernels (csrc/kernels/conv_igemm.hip) - forward with the
+    bias in the epilogue, dgrad as the same kernel over dY with flipped weights, wgrad split
+    over workgroup slices + a fixed-order slice sum; fp32 or bf16 operands (converted while
+    staging to LDS).  On the CPU: unfold + matmul (the oracle).
+
+    ``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
     them (views of the engine's flat gradient arena) and autograd gets None for the
     parameters - no per-parameter accumulation kernels, no arena zeroing."""
 
@@ -71,42 +76,47 @@ class Conv2dFn(torch.autograd.Function):
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
         x = x.contiguous()
+        bf = int(gemm_dtype == torch.bfloat16)
         if _is_gpu(x):
-            cols = torch.empty(B, C * K * K, OH * OW, device=x.device, dtype=torch.float32)
-            _ext().im2col(_p(x), B, C, H, W, K, pad, _p(cols), _s(x))
+            y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
+            _ext().conv_fwd(_p(x), _p(w), _p(b), _p(y), B, C, H, W, Cout, K, pad, bf, _s(x))
         else:
             cols = F.unfold(x, K, padding=pad)
-        y = _gemm(w.reshape(Cout, -1), cols, gemm_dtype)  # [B, Cout, L]: NCHW directly
-        if _is_gpu(x):
-            _ext().bias_add(_p(y), _p(b), B, Cout, OH * OW, _s(x))
-        else:
-            y = y + b.view(1, Cout, 1)
-        ctx.save_for_backward(cols, w)
+            y = (_gemm(w.reshape(Cout, -1), cols, gemm_dtype) + b.view(1, Cout, 1)).view(B, Cout, OH, OW)
+        ctx.save_for_backward(x, w)
         ctx.shape = (B, C, H, W, K, pad, OH, OW)
         ctx.gemm_dtype = gemm_dtype
         ctx.gw, ctx.gb = gw, gb
-        return y.view(B, Cout, OH, OW)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        cols, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors
         B, C, H, W, K, pad, OH, OW = ctx.shape
         Cout = w.shape[0]
-        dy2 = dy.contiguous().view(B, Cout, OH * OW)
+        dy = dy.contiguous()
+        bf = int(ctx.gemm_dtype == torch.bfloat16)
         dw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
-        torch.sum(_gemm(dy2, cols.transpose(1, 2), ctx.gemm_dtype), 0, out=dw.view(Cout, -1))
         db = ctx.gb if ctx.gb is not None else torch.empty(Cout, device=dy.device, dtype=torch.float32)
-        if _is_gpu(dy2):
-            _ext().chan_sum(_p(dy2), B, Cout, OH * OW, _p(db), _p(_partials(dy2, B, Cout, OH * OW)), _s(dy2))
-        else:
-            db.copy_(dy2.sum((0, 2)))
         dx = None
-        if ctx.needs_input_grad[0]:
-            dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
-            if _is_gpu(dy):
+        if _is_gpu(dy):
+            ext, st = _ext(), _s(dy)
+            S = ext.conv_wgrad_slices(B, C, H, W, Cout, K, pad)
+            part = torch.empty(S * w.numel(), device=dy.device, dtype=torch.float32)
+            ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), B, C, H, W, Cout, K, pad, bf, st)
+            ext.chan_sum(_p(dy), B, Cout, OH * OW, _p(db), _p(_partials(dy, B, Cout, OH * OW)), st)
+            if ctx.needs_input_grad[0]:
+                wf = torch.empty(C, Cout, K, K, device=dy.device, dtype=torch.float32)
+                ext.flip_weights(_p(w), Cout, C, K, _p(wf), st)
                 dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
-                _ext().col2im(_p(dcols), B, C, H, W, K, pad, _p(dx), _s(dy))
-            else:
+                ext.conv_fwd(_p(dy), _p(wf), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf, st)
+        else:
+            cols = F.unfold(x, K, padding=pad)
+            dy2 = dy.view(B, Cout, OH * OW)
+            torch.sum(_gemm(dy2, cols.transpose(1, 2), ctx.gemm_dtype), 0, out=dw.view(Cout, -1))
+            db.copy_(dy2.sum((0, 2)))
+            if ctx.needs_input_grad[0]:
+                dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
             return dx, None, None, None, None, None, None

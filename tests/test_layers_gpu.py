@@ -30,8 +30,11 @@ def _both(fn, *tensors):
     return outs
 
 
-@pytest.mark.parametrize("B,C,H,K,pad,Cout", [(3, 3, 32, 5, 0, 6), (4, 6, 14, 5, 0, 16), (2, 8, 9, 3, 1, 5)])
+@pytest.mark.parametrize("B,C,H,K,pad,Cout", [(3, 3, 32, 5, 0, 6), (4, 6, 14, 5, 0, 16), (2, 8, 9, 3, 1, 5),
+                                               (16, 32, 16, 3, 1, 64), (33, 3, 32, 5, 0, 6), (5, 40, 8, 3, 1, 24)])
 def test_conv2d_fwd_bwd(B, C, H, K, pad, Cout):
+    """Implicit-GEMM conv (conv_igemm.hip) vs unfold + matmul; the larger shapes run the
+    wgrad with many slices (fixed-order slice sum) and partial M / N / K tiles."""
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, C, H, H, generator=g).requires_grad_()
     w = torch.randn(Cout, C, K, K, generator=g).requires_grad_()
@@ -43,6 +46,24 @@ def test_conv2d_fwd_bwd(B, C, H, K, pad, Cout):
     yg.backward(dy.to(DEV))
     for tc, tg in zip(ac, ag):
         _close(tg.grad, tc.grad)
+
+
+@pytest.mark.parametrize("B,C,H,K,pad,Cout", [(8, 32, 16, 3, 1, 64), (6, 3, 32, 5, 0, 6)])
+def test_conv2d_bf16_operands_track_fp32(B, C, H, K, pad, Cout):
+    """bf16 MFMA operands (fp32 accumulate): within bf16 rounding of the fp32 oracle."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, C, H, H, generator=g).requires_grad_()
+    w = torch.randn(Cout, C, K, K, generator=g).requires_grad_()
+    b = torch.randn(Cout, generator=g).requires_grad_()
+    yc = L.Conv2dFn.apply(x, w, b, pad, torch.float32)
+    xg, wg, bg = (t.detach().to(DEV).requires_grad_() for t in (x, w, b))
+    yg = L.Conv2dFn.apply(xg, wg, bg, pad, torch.bfloat16)
+    _close(yg, yc, 2e-2)
+    dy = torch.randn(yc.shape, generator=g)
+    yc.backward(dy)
+    yg.backward(dy.to(DEV))
+    for tc, tg in zip((x, w, b), (xg, wg, bg)):
+        _close(tg.grad, tc.grad, 2e-2)
 
 
 @pytest.mark.parametrize("shape", [(2, 6, 28, 28), (3, 4, 7, 9)])
