@@ -131,12 +131,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_ingest(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(ids), batch, per_img,
                        P<float>(out), P<int32_t>(lab_out), S(stream));
   });
-  m.def("im2col", [](u x, int B, int C, int H, int W, int K, int pad, u cols, u stream) {
-    dnn::launch_im2col(P<const float>(x), B, C, H, W, K, pad, P<float>(cols), S(stream));
-  });
-  m.def("col2im", [](u dcols, int B, int C, int H, int W, int K, int pad, u dx, u stream) {
-    dnn::launch_col2im(P<const float>(dcols), B, C, H, W, K, pad, P<float>(dx), S(stream));
-  });
   m.def("relu_pool_fwd", [](u x, int BC, int H, int W, u y, u code, u stream) {
     dnn::launch_relu_pool_fwd(P<const float>(x), BC, H, W, P<float>(y), P<uint8_t>(code), S(stream));
   });
@@ -146,9 +140,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("relu_fwd", [](u x, long n, u y, u stream) { dnn::launch_relu_fwd(P<const float>(x), n, P<float>(y), S(stream)); });
   m.def("relu_bwd", [](u dy, u y, long n, u dx, u stream) {
     dnn::launch_relu_bwd(P<const float>(dy), P<const float>(y), n, P<float>(dx), S(stream));
-  });
-  m.def("bias_add", [](u y, u bias, int B, int C, int L, u stream) {
-    dnn::launch_bias_add(P<float>(y), P<const float>(bias), B, C, L, S(stream));
   });
   m.def("chan_parts", [](int B, int L) { return dnn::chan_parts(B, L); });
   m.def("bn_fwd_train", [](u x, int B, int C, int L, u state, u gamma, u beta, float eps, float mom, u rmean,
@@ -187,20 +178,26 @@ PYBIND11_MODULE(_dnn_hip, m) {
     a.batch_ids = P<int32_t>(batch_ids);
     dnn::launch_layer_bookkeeping(a, S(stream));
   });
-  m.def("conv_fwd", [](u x, u w, u bias, u y, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
-                       u stream) {
-    dnn::launch_conv_fwd(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(y), B, C, H, W, M, K,
-                         pad, bf16_ops, S(stream));
+  m.def("conv_fwd", [](u x, u w, u bias, u y, u ws, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                       int flip, u stream) {
+    dnn::launch_conv_fwd(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(y), P<void>(ws), B, C, H,
+                         W, M, K, pad, bf16_ops, flip, S(stream));
+  });
+  m.def("conv_fwd_workspace", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int flip) {
+    return (long)dnn::conv_fwd_workspace(B, C, H, W, M, K, pad, bf16_ops, flip);
+  });
+  m.def("conv_fwd_fast", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+    return dnn::conv_fwd_fast(B, C, H, W, M, K, pad, bf16_ops);
   });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;
     dnn::conv_wgrad_split(B, C, H, W, M, K, pad, &s, &cps);
     return s;
   });
-  m.def("conv_wgrad", [](u x, u dy, u part, u dw, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
-                         u stream) {
-    dnn::launch_conv_wgrad(P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), B, C, H, W, M, K, pad,
-                           bf16_ops, S(stream));
+  m.def("conv_wgrad", [](u x, u dy, u part, u dw, u db, int B, int C, int H, int W, int M, int K, int pad,
+                         int bf16_ops, u stream) {
+    dnn::launch_conv_wgrad(P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), P<float>(db), B, C, H,
+                           W, M, K, pad, bf16_ops, S(stream));
   });
   m.def("flip_weights", [](u w, int O, int C, int K, u wf, u stream) {
     dnn::launch_flip_weights(P<const float>(w), O, C, K, P<float>(wf), S(stream));

@@ -9,9 +9,14 @@
 //   forward : y[b][m][p]  = sum_k W[m][k] * im2col(x)[k][(b, p)]  (+ bias[m])   M = Cout
 //   dgrad   : the same kernel on dY with the flipped, channel-transposed weights and
 //             pad' = K - 1 - pad (a stride-1 transposed convolution)              M = Cin
-//   wgrad   : dW[m][j]   = sum_r dY[m][r] * im2col(x)[j][r],  r = (b, p)  (B*OH*OW long):
-//             split over S workgroup slices into fp32 partials, then a fixed-order sum
-//             (deterministic, no float atomics)
+//   wgrad   : dW[m][j]   = sum_r dY[m][r] * im2col(x)[j][r],  r = (b, p)  (B*OH*OW long),
+//             with an all-ones row j = Kd appended so the bias gradient comes out of the
+//             same MFMAs: split over S workgroup slices into fp32 partials, then a
+//             fixed-order sum (deterministic, no float atomics)
+//
+// Forward and dgrad run on an LDS-patch kernel (conv_fwd_patch_kernel, below) whenever its
+// tiles fit the LDS budget - every zoo layer does - and on the general gather kernel
+// otherwise.
 //
 // Tiling: a workgroup (4 waves) owns a BM x 64 output tile (BM = 16/32/64 from M); wave w
 // owns columns [16 w, 16 w + 16) and all BM rows as BM/16 16x16 accumulators.  The
@@ -43,7 +48,9 @@ struct Geom {
 // KPT consecutive rows k0 .. k0+KPT-1 of im2col(x) at output position (b, oy, ox), with
 // k = (c, ky, kx); 0 outside the image and for k >= Kd.  One (c, ky, kx) decomposition per
 // call, then an incremental walk (no per-element integer division: the divisions were the
-// kernels' dominant VALU cost).
+// kernels' dominant VALU cost).  ONES: row k == Kd is all ones (the wgrad's bias column:
+// db[m] = sum_r dY[m][r] * 1 comes out of the same MFMAs as dW).
+template <bool ONES = false>
 __device__ __forceinline__ void gather_rows(const float* __restrict__ x, const Geom& g, int k0, int Kd, int b, int oy,
                                             int ox, bool valid, float (&v)[KPT]) {
   const int KK = g.K * g.K;
@@ -56,7 +63,7 @@ __device__ __forceinline__ void gather_rows(const float* __restrict__ x, const G
 #pragma unroll
   for (int e = 0; e < KPT; ++e) {
     const bool in = valid && k0 + e < Kd && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    v[e] = in ? x[off] : 0.f;
+    v[e] = in ? x[off] : ((ONES && valid && k0 + e == Kd) ? 1.f : 0.f);
     // advance k -> k + 1
     ++kx; ++ix; ++off;
     if (kx == g.K) {
@@ -213,7 +220,7 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
       const float a = dyb[(long)(mv ? m : 0) * OHW];
       av[e] = (mv && rv) ? a : 0.f;
     }
-    gather_rows(x, g, j0 + rowg, Kd, bb, oy, ox, rv, bv);
+    gather_rows<true>(x, g, j0 + rowg, Kd, bb, oy, ox, rv, bv);
   };
   if (r_begin < r_end) load(r_begin);
   for (long r0 = r_begin; r0 < r_end; r0 += BK) {
@@ -230,35 +237,37 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
 
   const int r16 = lane & 15, q = lane >> 4;
   const int j = j0 + wave * 16 + r16;
-  if (j < Kd) {
+  if (j <= Kd) {  // column Kd = the bias gradient
 #pragma unroll
     for (int i = 0; i < BM / 16; ++i) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int m = m0 + 16 * i + 4 * q + jj;
-        if (m < M) part[((long)s * M + m) * Kd + j] = acc[i][jj];
+        if (m < M) part[((long)s * M + m) * (Kd + 1) + j] = acc[i][jj];
       }
     }
   }
 }
 
 // dw[e] = sum_s part[s][e] in a fixed order (deterministic).  A workgroup owns 64
-// consecutive elements; wave w sums slices w, w+4, w+8, ... (8 loads in flight per
-// batch), then wave 0 adds the four wave sums in order.  Grid = n / 64 workgroups: the
+// consecutive elements; wave w of SW sums slices w, w+SW, ... (8 loads in flight per
+// batch), then wave 0 adds the SW wave sums in order.  Grid = n / 64 workgroups: the
 // earlier one-thread-per-element loop over all S slices was latency-bound at 26-56 us.
-__global__ void __launch_bounds__(CT) slice_sum_kernel(const float* __restrict__ part, int S, long n,
-                                                       float* __restrict__ out) {
-  __shared__ float red[4][64];
+// part rows are [M][Kd + 1]: column Kd goes to db, the rest to dw.
+constexpr int SW = 16;  // waves per slice-sum workgroup
+__global__ void __launch_bounds__(SW * 64) slice_sum_kernel(const float* __restrict__ part, int S, long n, int Kd,
+                                                            float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[SW][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + lane;
   const bool ev = e < n;
   const float* p = part + (ev ? e : 0);
   float acc = 0.f;
-  for (int s0 = wave; s0 < S; s0 += 32) {
+  for (int s0 = wave; s0 < S; s0 += 8 * SW) {
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int s = s0 + 4 * u;
+      const int s = s0 + SW * u;
       v[u] = s < S ? p[(long)s * n] : 0.f;
     }
 #pragma unroll
@@ -266,7 +275,14 @@ __global__ void __launch_bounds__(CT) slice_sum_kernel(const float* __restrict__
   }
   red[wave][lane] = acc;
   __syncthreads();
-  if (wave == 0 && ev) out[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (wave == 0 && ev) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < SW; ++w) v += red[w][lane];
+    const int m = (int)(e / (Kd + 1)), j = (int)(e - (long)m * (Kd + 1));
+    if (j < Kd) dw[(long)m * Kd + j] = v;
+    else db[m] = v;
+  }
 }
 
 // wf[c][o][ky][kx] = w[o][c][K-1-ky][K-1-kx]  (dgrad weights)
@@ -279,7 +295,243 @@ __global__ void __launch_bounds__(CT) flip_weights_kernel(const float* __restric
   }
 }
 
+// ---- fast forward / dgrad: LDS-resident input patch + packed weights ---------------------------
+// The general kernel above re-gathers every im2col element from global memory (K^2 reads
+// of each input value per M-tile).  This path stages, per 32-channel chunk, the input
+// rows a 64-position output tile needs as a zero-padded patch P[r][x][c] (channels
+// innermost) and the weights as A[tap][m][c], both in LDS.  With the reduction ordered
+// k = (ky, kx, c), the operand of one tap is then a plain shifted view of the patch: a
+// lane's eight consecutive k are eight consecutive channels of one patch pixel - one
+// ds_read_b128 - and no index arithmetic runs in the MFMA loop (a per-lane base plus a
+// wave-uniform tap offset).  Each input element is read from HBM/L2 once per tile.
+//   bf16: v_mfma_f32_16x16x32_bf16, one per (tap, 16-row subtile); 32-channel chunks
+//   fp32: v_mfma_f32_16x16x4f32, CCH / 4 per (tap, subtile); 8 / 16 / 32-channel chunks
+//         (the smallest that holds C: the reference LeNet has C = 3 and 6)
+constexpr int PNT = 64;  // output positions per workgroup tile (4 waves x 16 columns)
+
+template <bool BF16, int CCH>
+struct PatchT {
+  using T = typename std::conditional<BF16, bf16, float>::type;
+  // channel stride of one patch pixel / weight row: 80 B (bf16), 48 / 80 / 144 B (fp32) -
+  // 16-B aligned, and 16 consecutive pixels land on distinct 16-B bank groups
+  static constexpr int CCP = BF16 ? 40 : CCH + 4;
+};
+
+struct PGeom {
+  int B, C, H, W, K, pad, OH, OW, M;
+  int R, Wp, tiles, Cp, Mp;  // patch rows, padded width, tiles per image, padded C / M
+};
+
+// wp[(tap * Mp + m) * Cp + c] = w[m][c][ky][kx]            (forward)
+//                             = w[c][m][K-1-ky][K-1-kx]    (flip: dgrad, w is [C][M][K][K])
+// zero for m >= M or c >= C
+template <typename T>
+__global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restrict__ w, int M, int C, int K, int Mp,
+                                                          int Cp, int flip, T* __restrict__ wp) {
+  const int KK = K * K, n = KK * Mp * Cp;
+  for (int e = blockIdx.x * CT + threadIdx.x; e < n; e += gridDim.x * CT) {
+    const int c = e % Cp, m = (e / Cp) % Mp, tap = e / (Cp * Mp);
+    const int ky = tap / K, kx = tap - ky * K;
+    float v = 0.f;
+    if (m < M && c < C)
+      v = flip ? w[((c * M + m) * K + (K - 1 - ky)) * K + (K - 1 - kx)] : w[((m * C + c) * K + ky) * K + kx];
+    wp[e] = (T)v;
+  }
+}
+
+template <bool BF16, int BM, int CCH>
+__global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
+                                                            const typename PatchT<BF16, CCH>::T* __restrict__ wp,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            PGeom g) {
+  static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
+  using T = typename PatchT<BF16, CCH>::T;
+  constexpr int CCP = PatchT<BF16, CCH>::CCP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KK = g.K * g.K;
+  T* As = reinterpret_cast<T*>(smem);  // [KK][BM][CCP]
+  T* Ps = As + KK * BM * CCP;          // [R][Wp][CCP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, q = lane >> 4;
+  const int b = blockIdx.x / g.tiles, p0 = (blockIdx.x - b * g.tiles) * PNT;
+  const int m0 = blockIdx.y * BM;
+  const int OHW = g.OH * g.OW;
+  const int oy_lo = p0 / g.OW, iy0 = oy_lo - g.pad;
+
+  // this lane's output column (position) and its patch base
+  const int pn = p0 + wave * 16 + r16;
+  const int pc = min(pn, OHW - 1);
+  const int oy = pc / g.OW, ox = pc - oy * g.OW;
+  const int bbase = ((oy - oy_lo) * g.Wp + ox) * CCP + (BF16 ? 8 * q : q);
+
+  f32x4 acc[BM / 16];
+#pragma unroll
+  for (int i = 0; i < BM / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int prow = g.R * CCH;  // patch rows of a chunk: (c, r)
+  for (int c0 = 0; c0 < g.Cp; c0 += CCH) {
+    if (c0) __syncthreads();  // previous chunk's MFMAs are done with As / Ps
+    // Staging issues a batch of independent global loads before any LDS store, so a
+    // workgroup pays a few memory latencies per chunk instead of one per row.
+    // stage A: KK * BM rows of CCH channels, 16-B vectors, 4 in flight per thread
+    {
+      constexpr int VE = 16 / sizeof(T);  // elements per 16-B vector
+      constexpr int VPR = CCH / VE;       // vectors per row
+      const int nv = KK * BM * VPR;
+      for (int v0 = tid; v0 < nv; v0 += 4 * CT) {
+        uint4 val[4];
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+          const int v = min(v0 + u4 * CT, nv - 1);
+          const int row = v / VPR, u = v - row * VPR;  // row = tap * BM + m
+          const int tap = row / BM, m = row - tap * BM;
+          val[u4] = *reinterpret_cast<const uint4*>(wp + ((long)(tap * g.Mp + m0 + m) * g.Cp + c0 + u * VE));
+        }
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+          const int v = v0 + u4 * CT;
+          if (v < nv) {
+            const int row = v / VPR, u = v - row * VPR;
+            *reinterpret_cast<uint4*>(As + row * CCP + u * VE) = val[u4];
+          }
+        }
+      }
+    }
+    // stage the patch: wave-uniform (c, r) rows, lanes along x (coalesced global reads),
+    // PU rows per wave in flight
+    constexpr int PU = 8;
+    for (int xp0 = 0; xp0 < g.Wp; xp0 += 64) {
+      const int xp = xp0 + lane, ix = xp - g.pad;
+      const bool colok = xp < g.Wp && (unsigned)ix < (unsigned)g.W;
+      for (int row0 = wave; row0 < prow; row0 += 4 * PU) {
+        float v[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+          const int row = row0 + 4 * u;
+          const int c = row / g.R, r = row - c * g.R;
+          const int iy = iy0 + r;
+          const bool ok = row < prow && colok && c0 + c < g.C && (unsigned)iy < (unsigned)g.H;
+          v[u] = ok ? x[((long)(b * g.C + c0 + c) * g.H + iy) * g.W + ix] : 0.f;
+        }
+        if (xp < g.Wp) {
+#pragma unroll
+          for (int u = 0; u < PU; ++u) {
+            const int row = row0 + 4 * u;
+            if (row < prow) {
+              const int c = row / g.R, r = row - c * g.R;
+              Ps[(r * g.Wp + xp) * CCP + c] = (T)v[u];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int ky = 0; ky < g.K; ++ky) {
+      for (int kx = 0; kx < g.K; ++kx) {
+        const int tap = ky * g.K + kx;
+        const T* pb = Ps + bbase + (ky * g.Wp + kx) * CCP;
+        const T* ab = As + (tap * BM + r16) * CCP + (BF16 ? 8 * q : q);
+        if constexpr (BF16) {
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(pb);
+#pragma unroll
+          for (int i = 0; i < BM / 16; ++i) {
+            const bf16x8 av = *reinterpret_cast<const bf16x8*>(ab + 16 * i * CCP);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[i], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < CCH; kk += 4) {
+            const float bv = pb[kk];
+#pragma unroll
+            for (int i = 0; i < BM / 16; ++i)
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab[16 * i * CCP + kk], bv, acc[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue: acc[i][j] = D[16 i + 4 q + j][16 wave + r16]
+  if (pn < OHW) {
+#pragma unroll
+    for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + 16 * i + 4 * q + j;
+        if (m < g.M) y[((long)b * g.M + m) * OHW + pn] = acc[i][j] + (bias != nullptr ? bias[m] : 0.f);
+      }
+    }
+  }
+}
+
 int pick_bm(int M) { return M <= 16 ? 16 : (M <= 32 ? 32 : 64); }
+
+// LDS budget of the fast path (the default dynamic-LDS limit; >= 2 workgroups per CU)
+constexpr size_t kPatchLdsMax = 64 * 1024;
+
+struct FastPlan {
+  bool ok = false;
+  int bm = 16, gy = 1, cch = 32;
+  PGeom pg{};
+  size_t lds = 0, ws_bytes = 0;
+};
+
+FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
+  FastPlan f;
+  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  if (OH <= 0 || OW <= 0) return f;
+  const int OHW = OH * OW, tiles = (OHW + PNT - 1) / PNT;
+  int span = 1;  // most output rows one 64-position tile touches
+  for (int t = 0; t < tiles; ++t) {
+    const int lo = t * PNT, hi = std::min(OHW, lo + PNT) - 1;
+    span = std::max(span, hi / OW - lo / OW + 1);
+  }
+  const int R = span + K - 1, Wp = W + 2 * pad;
+  // M tile: <= 32 rows (enough workgroups on the small late layers), A fits the budget
+  int bm = M <= 16 ? 16 : 32;
+  const int cch = bf ? 32 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
+  const size_t es = bf ? 2 : 4, ccp = bf ? 40 : cch + 4;
+  auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp) * ccp * es; };
+  if (lds_of(bm) > kPatchLdsMax && bm == 32) bm = 16;
+  if (lds_of(bm) > kPatchLdsMax) return f;
+  f.ok = true;
+  f.bm = bm;
+  f.cch = cch;
+  f.gy = (M + bm - 1) / bm;
+  f.pg = PGeom{B, C, H, W, K, pad, OH, OW, M, R, Wp, tiles, (C + cch - 1) / cch * cch, f.gy * bm};
+  f.lds = lds_of(bm);
+  f.ws_bytes = (size_t)K * K * f.pg.Mp * f.pg.Cp * es;
+  return f;
+}
+
+template <bool BF16, int CCH>
+void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
+                 float* y, hipStream_t s) {
+  dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
+  if (f.bm == 16)
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+  else
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <bool BF16>
+void fast_dispatch(const FastPlan& f, const float* x, const float* w, int flip, const float* bias, float* y,
+                   void* ws, hipStream_t s) {
+  using T = typename std::conditional<BF16, bf16, float>::type;
+  const PGeom& g = f.pg;
+  T* wp = reinterpret_cast<T*>(ws);
+  const int n = g.K * g.K * g.Mp * g.Cp;
+  hipLaunchKernelGGL(pack_weights_kernel<T>, dim3(std::max(1, std::min((n + CT - 1) / CT, 1024))), dim3(CT), 0, s, w,
+                     g.M, g.C, g.K, g.Mp, g.Cp, flip, wp);
+  HIP_CHECK(hipGetLastError());
+  if constexpr (BF16) {
+    fast_launch<true, 32>(f, wp, x, bias, y, s);
+  } else {
+    if (f.cch == 8) fast_launch<false, 8>(f, wp, x, bias, y, s);
+    else if (f.cch == 16) fast_launch<false, 16>(f, wp, x, bias, y, s);
+    else fast_launch<false, 32>(f, wp, x, bias, y, s);
+  }
+}
 
 template <bool BF16>
 void fwd_dispatch(const float* x, const float* w, const float* bias, float* y, const Geom& g, int M, hipStream_t s) {
@@ -296,7 +548,7 @@ template <bool BF16>
 void wgrad_dispatch(const float* x, const float* dy, float* part, const Geom& g, int M, int S, int cps, hipStream_t s) {
   const int Kd = g.C * g.K * g.K;
   const int bm = pick_bm(M);
-  dim3 grid((unsigned)((Kd + BN - 1) / BN), (unsigned)((M + bm - 1) / bm), (unsigned)S);
+  dim3 grid((unsigned)((Kd + 1 + BN - 1) / BN), (unsigned)((M + bm - 1) / bm), (unsigned)S);  // + bias column
   if (bm == 16) hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 16>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
   else if (bm == 32) hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 32>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
   else hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 64>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
@@ -313,11 +565,38 @@ Geom geom(int B, int C, int H, int W, int K, int pad) {
 }
 }  // namespace
 
-void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W, int M,
-                     int K, int pad, int bf16_ops, hipStream_t s) {
+// Workspace bytes of launch_conv_fwd: the packed weights of the fast path, or the flipped
+// fp32 weights of the general path's dgrad (flip), else 0.
+size_t conv_fwd_workspace(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int flip) {
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (f.ok) return f.ws_bytes;
+  return flip ? (size_t)M * C * K * K * sizeof(float) : 0;
+}
+
+// y = conv(x, w) + bias.  flip = 0: w is [M][C][K][K] (forward).  flip = 1: w is the
+// forward weight [C][M][K][K] of the layer whose data gradient this computes (the kernel
+// flips and transposes it while packing).  ws: conv_fwd_workspace() bytes.
+void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y, void* ws, int B, int C, int H, int W,
+                     int M, int K, int pad, int bf16_ops, int flip, hipStream_t s) {
   const Geom g = geom(B, C, H, W, K, pad);
-  if (bf16_ops) fwd_dispatch<true>(x, w, bias, y, g, M, s);
-  else fwd_dispatch<false>(x, w, bias, y, g, M, s);
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (f.ok) {
+    if (bf16_ops) fast_dispatch<true>(f, x, w, flip, bias, y, ws, s);
+    else fast_dispatch<false>(f, x, w, flip, bias, y, ws, s);
+    return;
+  }
+  const float* wf = w;
+  if (flip) {  // general path: materialise the flipped weights [M][C][K][K] in the workspace
+    launch_flip_weights(w, C, M, K, reinterpret_cast<float*>(ws), s);
+    wf = reinterpret_cast<const float*>(ws);
+  }
+  if (bf16_ops) fwd_dispatch<true>(x, wf, bias, y, g, M, s);
+  else fwd_dispatch<false>(x, wf, bias, y, g, M, s);
+}
+
+// 1 when (B, C, H, W, M, K, pad, bf16) runs on the LDS-patch fast path (tests / profiling)
+int conv_fwd_fast(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+  return plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0).ok ? 1 : 0;
 }
 
 // slices for the wgrad split: enough workgroups to fill the chip, >= 4 chunks per slice
@@ -326,25 +605,29 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
   const long R = (long)B * g.OH * g.OW;
   const long chunks = (R + BK - 1) / BK;
   const int Kd = C * K * K, bm = pick_bm(M);
-  const long tiles = (long)((Kd + BN - 1) / BN) * ((M + bm - 1) / bm);
-  // ~512 workgroups, at most 64 slices (the fixed-order slice sum reads S partials per
-  // element), at least 2 chunks per slice
-  long want = std::max(1L, 512 / std::max(1L, tiles));
-  want = std::min({want, 64L, std::max(1L, chunks / 2)});
+  const long tiles = (long)((Kd + 1 + BN - 1) / BN) * ((M + bm - 1) / bm);
+  // ~1024 workgroups (4 per CU: a slice's chunks run back to back, so the chip must be
+  // full), at most 256 slices (the slice sum reads S partials per element), at least 4
+  // chunks per slice.  (A 64-slice cap left conv1's single tile with 64 workgroups of
+  // 16 serial chunks each: 45 us.)
+  long want = std::max(1L, 1024 / std::max(1L, tiles));
+  want = std::min({want, 256L, std::max(1L, chunks / 4)});
   const long per = (chunks + want - 1) / want;
   *cps = (int)per;
   *S = (int)((chunks + per - 1) / per);
 }
 
-void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, int C, int H, int W, int M,
-                       int K, int pad, int bf16_ops, hipStream_t s) {
+// dw [M][C][K][K] and db [M] from one MFMA pass; part: S * M * (C K^2 + 1) floats
+void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
+                       int M, int K, int pad, int bf16_ops, hipStream_t s) {
   const Geom g = geom(B, C, H, W, K, pad);
   int S = 1, cps = 1;
   conv_wgrad_split(B, C, H, W, M, K, pad, &S, &cps);
   if (bf16_ops) wgrad_dispatch<true>(x, dy, part, g, M, S, cps, s);
   else wgrad_dispatch<false>(x, dy, part, g, M, S, cps, s);
-  const long n = (long)M * C * K * K;
-  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(CT), 0, s, part, S, n, dw);
+  const int Kd = C * K * K;
+  const long n = (long)M * (Kd + 1);
+  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(SW * 64), 0, s, part, S, n, Kd, dw, db);
   HIP_CHECK(hipGetLastError());
 }
 

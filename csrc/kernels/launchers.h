@@ -47,13 +47,10 @@ void launch_sgd_apply(float* master, const float* grad, float* mom, bf16* shadow
 // ---- generic layer kernels (layers.hip) --------------------------------------------------
 void launch_ingest(const uint8_t* images, const int32_t* labels, const int32_t* ids, int batch, int per_img,
                    float* out, int32_t* lab_out, hipStream_t s);
-void launch_im2col(const float* x, int B, int C, int H, int W, int K, int pad, float* cols, hipStream_t s);
-void launch_col2im(const float* dcols, int B, int C, int H, int W, int K, int pad, float* dx, hipStream_t s);
 void launch_relu_pool_fwd(const float* x, int BC, int H, int W, float* y, uint8_t* code, hipStream_t s);
 void launch_relu_pool_bwd(const float* dy, const uint8_t* code, int BC, int H, int W, float* dx, hipStream_t s);
 void launch_relu_fwd(const float* x, long n, float* y, hipStream_t s);
 void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStream_t s);
-void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream_t s);
 int chan_parts(int B, int L);  // partitions per channel of the two-stage channel reductions
 void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
@@ -68,11 +65,13 @@ void launch_xent(const float* logits, const int32_t* labels, int B, int NC, cons
                  int32_t* correct, float* dlogits, hipStream_t s);
 void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s);
 // implicit-GEMM convolution (conv_igemm.hip)
-void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W, int M,
-                     int K, int pad, int bf16_ops, hipStream_t s);
+size_t conv_fwd_workspace(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int flip);
+int conv_fwd_fast(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
+void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y, void* ws, int B, int C, int H, int W,
+                     int M, int K, int pad, int bf16_ops, int flip, hipStream_t s);
 void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S, int* cps);
-void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, int C, int H, int W, int M,
-                       int K, int pad, int bf16_ops, hipStream_t s);
+void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
+                       int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);

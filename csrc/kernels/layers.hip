@@ -7,9 +7,8 @@
 // operands.  Capability parity: the ATen ops of SURVEY.md §2.5 K0-K23.
 //
 // Split of work (MI355X-first):
-//  * the GEMM-shaped parts of Conv2d / Linear go to the library GEMMs (hipBLASLt via
-//    torch.matmul): conv = im2col (here) -> batched GEMM -> col2im (here, a deterministic
-//    gather instead of an atomic scatter);
+//  * Conv2d is an implicit-GEMM MFMA kernel family of its own (conv_igemm.hip); Linear
+//    goes to the library GEMM (hipBLASLt via torch.matmul);
 //  * everything else is a hand-written kernel: ingest (u8 gather + ToTensor/Normalize),
 //    fused ReLU + 2x2 max-pool with a 2-bit argmax code (the same encoding as the fused
 //    kernel: 4 = no gradient), BatchNorm2d train/eval forward + backward with the tail
@@ -44,60 +43,17 @@ __global__ void __launch_bounds__(LT) ingest_kernel(const uint8_t* __restrict__ 
   if (e == 0) lab_out[b] = labels[sid];
 }
 
-// ---- im2col / col2im (stride 1, square kernel, zero padding) -----------------------
-// cols[b][(c*K + ky)*K + kx][oy*OW + ox] = x[b][c][oy+ky-pad][ox+kx-pad]
-__global__ void __launch_bounds__(LT) im2col_kernel(const float* __restrict__ x, int B, int C, int H, int W,
-                                                    int K, int pad, int OH, int OW, float* __restrict__ cols) {
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  const int L = OH * OW, CKK = C * K * K;
-  const long total = (long)B * CKK * L;
-  if (i >= total) return;
-  const int l = (int)(i % L);
-  const long r = i / L;
-  const int ck = (int)(r % CKK), b = (int)(r / CKK);
-  const int c = ck / (K * K), kk = ck - c * K * K, ky = kk / K, kx = kk - ky * K;
-  const int oy = l / OW, ox = l - oy * OW;
-  const int y = oy + ky - pad, xx = ox + kx - pad;
-  cols[i] = (y >= 0 && y < H && xx >= 0 && xx < W) ? x[(((size_t)b * C + c) * H + y) * W + xx] : 0.f;
-}
-
-// dx[b][c][y][x] = sum over (ky, kx) of dcols[b][(c,ky,kx)][(y-ky+pad, x-kx+pad)]: a gather
-// in a fixed (ky, kx) order - deterministic, no atomics.
-__global__ void __launch_bounds__(LT) col2im_kernel(const float* __restrict__ dcols, int B, int C, int H, int W,
-                                                    int K, int pad, int OH, int OW, float* __restrict__ dx) {
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  const long total = (long)B * C * H * W;
-  if (i >= total) return;
-  const int xx = (int)(i % W);
-  long r = i / W;
-  const int y = (int)(r % H);
-  r /= H;
-  const int c = (int)(r % C), b = (int)(r / C);
-  const int L = OH * OW, CKK = C * K * K;
-  float s = 0.f;
-  for (int ky = 0; ky < K; ++ky) {
-    const int oy = y - ky + pad;
-    if (oy < 0 || oy >= OH) continue;
-    for (int kx = 0; kx < K; ++kx) {
-      const int ox = xx - kx + pad;
-      if (ox < 0 || ox >= OW) continue;
-      s += dcols[((size_t)b * CKK + (c * K + ky) * K + kx) * L + oy * OW + ox];
-    }
-  }
-  dx[i] = s;
-}
-
 // ---- fused ReLU + 2x2 max-pool (stride 2, floor) with a 2-bit argmax code -------------
 // max_pool2d(relu(x)) == relu(max_pool2d(x)); code = first argmax (torch order) or 4 when
 // the max is <= 0 (no gradient reaches the input: ReLU and pool backward in one test).
 __global__ void __launch_bounds__(LT) relu_pool_fwd_kernel(const float* __restrict__ x, int BC, int H, int W,
                                                            float* __restrict__ y, uint8_t* __restrict__ code) {
   const int OH = H / 2, OW = W / 2;
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  if (i >= (long)BC * OH * OW) return;
-  const int ox = (int)(i % OW);
-  const long r = i / OW;
-  const int oy = (int)(r % OH), bc = (int)(r / OH);
+  const int i = blockIdx.x * LT + threadIdx.x;
+  if (i >= BC * OH * OW) return;
+  const unsigned r = (unsigned)i / (unsigned)OW;
+  const int ox = i - (int)r * OW;
+  const int bc = (int)(r / (unsigned)OH), oy = (int)r - bc * OH;
   const float* p = x + ((size_t)bc * H + 2 * oy) * W + 2 * ox;
   float best = p[0];
   int arg = 0;
@@ -112,16 +68,16 @@ __global__ void __launch_bounds__(LT) relu_pool_fwd_kernel(const float* __restri
 __global__ void __launch_bounds__(LT) relu_pool_bwd_kernel(const float* __restrict__ dy,
                                                            const uint8_t* __restrict__ code, int BC, int H, int W,
                                                            float* __restrict__ dx) {
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  if (i >= (long)BC * H * W) return;
+  const int i = blockIdx.x * LT + threadIdx.x;
+  if (i >= BC * H * W) return;
   const int OH = H / 2, OW = W / 2;
-  const int xx = (int)(i % W);
-  const long r = i / W;
-  const int y = (int)(r % H), bc = (int)(r / H);
+  const unsigned r = (unsigned)i / (unsigned)W;
+  const int xx = i - (int)r * W;
+  const int bc = (int)(r / (unsigned)H), y = (int)r - bc * H;
   const int oy = y >> 1, ox = xx >> 1;
   float v = 0.f;
   if (oy < OH && ox < OW) {
-    const long o = ((long)bc * OH + oy) * OW + ox;
+    const int o = (bc * OH + oy) * OW + ox;
     if (code[o] == (uint8_t)(((y & 1) << 1) | (xx & 1))) v = dy[o];
   }
   dx[i] = v;
@@ -136,14 +92,6 @@ __global__ void __launch_bounds__(LT) relu_bwd_kernel(const float* __restrict__ 
                                                       long n, float* __restrict__ dx) {
   const long i = (long)blockIdx.x * LT + threadIdx.x;
   if (i < n) dx[i] = y[i] > 0.f ? dy[i] : 0.f;
-}
-
-// ---- per-channel bias add (conv output [B][C][L]) ----------------------------------------
-__global__ void __launch_bounds__(LT) bias_add_kernel(float* __restrict__ y, const float* __restrict__ bias,
-                                                      int B, int C, int L) {
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  if (i >= (long)B * C * L) return;
-  y[i] += bias[(i / L) % C];
 }
 
 // ---- per-channel reductions over (batch, pixels): deterministic two-stage ---------------
@@ -191,13 +139,13 @@ __global__ void __launch_bounds__(LT) chan_partial_kernel(const float* __restric
   __shared__ double red[2 * (LT / 64)];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
-  const long n = (long)bv * L, chunk = ((long)B * L + P - 1) / P;
-  const long lo = (long)p * chunk, hi = min(n, lo + chunk);
+  const unsigned n = (unsigned)(bv * L), chunk = ((unsigned)(B * L) + P - 1) / P;
+  const unsigned lo = p * chunk, hi = min(n, lo + chunk);
   const float mu = MODE == 1 ? mean[c] : 0.f, is = MODE == 1 ? invstd[c] : 0.f;
   double s0 = 0.0, s1 = 0.0;
-  for (long t = lo + threadIdx.x; t < hi; t += LT) {
-    const long b = t / L, l = t - b * L;
-    const size_t o = ((size_t)b * C + c) * L + l;
+  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
+    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
+    const int o = (b * C + c) * L + l;
     const float v = a[o];
     s0 += (double)v;
     if (MODE == 0) s1 += (double)v * (double)v;
@@ -257,11 +205,11 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
   }
   __syncthreads();
   const float mean = st[0], invstd = st[1], g = gamma[c], bb = beta[c];
-  const long total = (long)B * L, chunk = (total + P - 1) / P;
-  const long lo = (long)p * chunk, hi = min(total, lo + chunk);
-  for (long t = lo + threadIdx.x; t < hi; t += LT) {
-    const long b = t / L, l = t - b * L;
-    const size_t o = ((size_t)b * C + c) * L + l;
+  const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
+  const unsigned lo = p * chunk, hi = min(total, lo + chunk);
+  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
+    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
+    const int o = (b * C + c) * L + l;
     y[o] = b < bv ? (x[o] - mean) * invstd * g + bb : 0.f;
   }
 }
@@ -272,9 +220,9 @@ __global__ void __launch_bounds__(LT) bn_fwd_eval_kernel(const float* __restrict
                                                          const float* __restrict__ running_mean,
                                                          const float* __restrict__ running_var,
                                                          float* __restrict__ y) {
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  if (i >= (long)B * C * L) return;
-  const int c = (int)((i / L) % C);
+  const int i = blockIdx.x * LT + threadIdx.x;
+  if (i >= B * C * L) return;
+  const int c = (int)(((unsigned)i / (unsigned)L) % (unsigned)C);
   y[i] = (x[i] - running_mean[c]) * rsqrtf(running_var[c] + eps) * gamma[c] + beta[c];
 }
 
@@ -303,11 +251,11 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
   __syncthreads();
   const float mdy = st[0], mdyx = st[1];
   const float mean = save_mean[c], invstd = save_invstd[c], g = gamma[c];
-  const long total = (long)B * L, chunk = (total + P - 1) / P;
-  const long lo = (long)p * chunk, hi = min(total, lo + chunk);
-  for (long t = lo + threadIdx.x; t < hi; t += LT) {
-    const long b = t / L, l = t - b * L;
-    const size_t o = ((size_t)b * C + c) * L + l;
+  const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
+  const unsigned lo = p * chunk, hi = min(total, lo + chunk);
+  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
+    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
+    const int o = (b * C + c) * L + l;
     dx[o] = b < bv ? g * invstd * (dy[o] - mdy - (x[o] - mean) * invstd * mdyx) : 0.f;
   }
 }
@@ -381,16 +329,6 @@ void launch_ingest(const uint8_t* images, const int32_t* labels, const int32_t* 
   if (n) hipLaunchKernelGGL(ingest_kernel, dim3(blocks(n)), dim3(LT), 0, s, images, labels, ids, batch, per_img, out,
                             lab_out);
 }
-void launch_im2col(const float* x, int B, int C, int H, int W, int K, int pad, float* cols, hipStream_t s) {
-  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
-  const long n = (long)B * C * K * K * OH * OW;
-  if (n) hipLaunchKernelGGL(im2col_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, B, C, H, W, K, pad, OH, OW, cols);
-}
-void launch_col2im(const float* dcols, int B, int C, int H, int W, int K, int pad, float* dx, hipStream_t s) {
-  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
-  const long n = (long)B * C * H * W;
-  if (n) hipLaunchKernelGGL(col2im_kernel, dim3(blocks(n)), dim3(LT), 0, s, dcols, B, C, H, W, K, pad, OH, OW, dx);
-}
 void launch_relu_pool_fwd(const float* x, int BC, int H, int W, float* y, uint8_t* code, hipStream_t s) {
   const long n = (long)BC * (H / 2) * (W / 2);
   if (n) hipLaunchKernelGGL(relu_pool_fwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, BC, H, W, y, code);
@@ -404,10 +342,6 @@ void launch_relu_fwd(const float* x, long n, float* y, hipStream_t s) {
 }
 void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStream_t s) {
   if (n) hipLaunchKernelGGL(relu_bwd_kernel, dim3(blocks(n)), dim3(LT), 0, s, dy, y, n, dx);
-}
-void launch_bias_add(float* y, const float* bias, int B, int C, int L, hipStream_t s) {
-  const long n = (long)B * C * L;
-  if (n) hipLaunchKernelGGL(bias_add_kernel, dim3(blocks(n)), dim3(LT), 0, s, y, bias, B, C, L);
 }
 int chan_parts(int B, int L) { return chan_parts_of(B, L); }
 

@@ -52,6 +52,11 @@ def _partials(t: torch.Tensor, B: int, C: int, L: int) -> torch.Tensor:
     return torch.empty(C * _ext().chan_parts(B, L) * 2, device=t.device, dtype=torch.float64)
 
 
+def _workspace(t: torch.Tensor, nbytes: int) -> torch.Tensor:
+    """Scratch bytes for a native launch (stream-ordered caching allocator: capture-safe)."""
+    return torch.empty(max(int(nbytes), 16), device=t.device, dtype=torch.uint8)
+
+
 def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Library GEMM with optional bf16 operands (fp32 accumulate / result)."""
     if dtype == torch.float32:
@@ -62,9 +67,10 @@ def _gemm(a: torch.Tensor, b: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 # ---- Conv2d (stride 1, square kernel, zero padding) -------------------------------------------
 class Conv2dFn(torch.autograd.Function):
     """On MI355X: implicit-GEMM MFMA kernels (csrc/kernels/conv_igemm.hip) - forward with the
-    bias in the epilogue, dgrad as the same kernel over dY with flipped weights, wgrad split
-    over workgroup slices + a fixed-order slice sum; fp32 or bf16 operands (converted while
-    staging to LDS).  On the CPU: unfold + matmul (the oracle).
+    bias in the epilogue (LDS-patch kernel with packed weights), dgrad as the same kernel
+    over dY with flipped weights, wgrad (+ the bias gradient as an all-ones im2col row)
+    split over workgroup slices + a fixed-order slice sum; fp32 or bf16 operands
+    (converted while staging to LDS).  On the CPU: unfold + matmul (the oracle).
 
     ``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
     them (views of the engine's flat gradient arena) and autograd gets None for the
@@ -78,8 +84,10 @@ class Conv2dFn(torch.autograd.Function):
         x = x.contiguous()
         bf = int(gemm_dtype == torch.bfloat16)
         if _is_gpu(x):
+            ext = _ext()
             y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
-            _ext().conv_fwd(_p(x), _p(w), _p(b), _p(y), B, C, H, W, Cout, K, pad, bf, _s(x))
+            ws = _workspace(x, ext.conv_fwd_workspace(B, C, H, W, Cout, K, pad, bf, 0))
+            ext.conv_fwd(_p(x), _p(w), _p(b), _p(y), _p(ws), B, C, H, W, Cout, K, pad, bf, 0, _s(x))
         else:
             cols = F.unfold(x, K, padding=pad)
             y = (_gemm(w.reshape(Cout, -1), cols, gemm_dtype) + b.view(1, Cout, 1)).view(B, Cout, OH, OW)
@@ -102,14 +110,14 @@ class Conv2dFn(torch.autograd.Function):
         if _is_gpu(dy):
             ext, st = _ext(), _s(dy)
             S = ext.conv_wgrad_slices(B, C, H, W, Cout, K, pad)
-            part = torch.empty(S * w.numel(), device=dy.device, dtype=torch.float32)
-            ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), B, C, H, W, Cout, K, pad, bf, st)
-            ext.chan_sum(_p(dy), B, Cout, OH * OW, _p(db), _p(_partials(dy, B, Cout, OH * OW)), st)
+            part = torch.empty(S * Cout * (C * K * K + 1), device=dy.device, dtype=torch.float32)
+            ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), _p(db), B, C, H, W, Cout, K, pad, bf, st)  # dW and db
             if ctx.needs_input_grad[0]:
-                wf = torch.empty(C, Cout, K, K, device=dy.device, dtype=torch.float32)
-                ext.flip_weights(_p(w), Cout, C, K, _p(wf), st)
+                # dgrad: the forward kernel over dY with the flipped, transposed weights
+                # (flip=1: packed from w inside the launch), pad' = K - 1 - pad
                 dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
-                ext.conv_fwd(_p(dy), _p(wf), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf, st)
+                ws = _workspace(dy, ext.conv_fwd_workspace(B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1))
+                ext.conv_fwd(_p(dy), _p(w), 0, _p(dx), _p(ws), B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1, st)
         else:
             cols = F.unfold(x, K, padding=pad)
             dy2 = dy.view(B, Cout, OH * OW)

@@ -69,12 +69,14 @@ class DropInjector:
 class Heartbeat:
     """Background heartbeat + watchdog over the rendezvous TCPStore."""
 
-    def __init__(self, comm: Communicator, period_s: float = 0.2, timeout_s: float = 3.0) -> None:
+    def __init__(self, comm: Communicator, period_s: float = 0.2, timeout_s: float | None = None) -> None:
         import torch.distributed as dist
 
         self.comm = comm
         self.period = period_s
-        self.timeout = timeout_s
+        # DNN_HEARTBEAT_TIMEOUT: seconds without a beat before a peer is declared dead (a
+        # loaded host can starve a live rank's beat thread for a few seconds)
+        self.timeout = float(os.environ.get("DNN_HEARTBEAT_TIMEOUT", "6.0")) if timeout_s is None else timeout_s
         self.dead: set[int] = set()
         self._stop = threading.Event()
         env = comm.env
@@ -133,8 +135,8 @@ def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0) -> 
         for r in comm.members:
             if st.check([f"{p}alive/{r}"]):
                 alive.append(r)
-            elif r in hb.dead or hb.stale(r):
-                pass
+            elif hb.stale(r):
+                pass  # dead (a rank the watchdog flagged but that is beating again is waited for)
             else:
                 undecided.append(r)
         if not undecided or time.time() > deadline:

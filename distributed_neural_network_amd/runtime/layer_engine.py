@@ -4,8 +4,8 @@ Same interface as ``HipEngine`` (attach / begin_epoch / run_steps / epoch_stats 
 evaluate_samples / master / grad / mom / grad_sync), so the trainer, every sync policy,
 fault recovery and checkpointing work unchanged.  Where the fused engine is one
 hand-scheduled kernel for the reference LeNet in bf16, this engine runs a layer stack
-(csrc/kernels/layers.hip + library GEMMs) in fp32 - bit-for-bit the reference's
-arithmetic class - or with bf16 GEMM operands, and supports BatchNorm.
+(csrc/kernels/layers.hip, conv_igemm.hip + library GEMMs for Linear) in fp32 - the
+reference's arithmetic class - or with bf16 convolution operands, and supports BatchNorm.
 
 MI355X design points kept from the fused engine:
   * flat fp32 parameter / gradient / momentum arenas; every layer op writes its parameter
@@ -139,7 +139,10 @@ class LayerEngine(Engine):
             elif isinstance(layer, zoo.Flatten):
                 x = x.reshape(x.shape[0], -1)
             elif isinstance(layer, zoo.FC):
-                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], dt, gw, gb)
+                # Linear stays fp32 in both modes: the fc GEMMs are < 0.3 GFLOP per step, and
+                # bf16 operands would cost six cast kernels per layer and step (measured:
+                # ~90 us per cifar-vgg step) for no MFMA gain at these sizes
+                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], torch.float32, gw, gb)
         return x
 
     def _ingest(self) -> None:

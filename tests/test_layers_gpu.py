@@ -31,10 +31,12 @@ def _both(fn, *tensors):
 
 
 @pytest.mark.parametrize("B,C,H,K,pad,Cout", [(3, 3, 32, 5, 0, 6), (4, 6, 14, 5, 0, 16), (2, 8, 9, 3, 1, 5),
-                                               (16, 32, 16, 3, 1, 64), (33, 3, 32, 5, 0, 6), (5, 40, 8, 3, 1, 24)])
+                                               (16, 32, 16, 3, 1, 64), (33, 3, 32, 5, 0, 6), (5, 40, 8, 3, 1, 24),
+                                               (2, 20, 12, 7, 3, 40)])
 def test_conv2d_fwd_bwd(B, C, H, K, pad, Cout):
     """Implicit-GEMM conv (conv_igemm.hip) vs unfold + matmul; the larger shapes run the
-    wgrad with many slices (fixed-order slice sum) and partial M / N / K tiles."""
+    wgrad with many slices (fixed-order slice sum) and partial M / N / K tiles; the 7x7
+    layer does not fit the LDS-patch kernel and runs the general gather kernel."""
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, C, H, H, generator=g).requires_grad_()
     w = torch.randn(Cout, C, K, K, generator=g).requires_grad_()
@@ -46,6 +48,19 @@ def test_conv2d_fwd_bwd(B, C, H, K, pad, Cout):
     yg.backward(dy.to(DEV))
     for tc, tg in zip(ac, ag):
         _close(tg.grad, tc.grad)
+
+
+def test_conv_fast_path_covers_zoo_layers():
+    """Every zoo conv layer (forward and dgrad, fp32 and bf16) runs on the LDS-patch kernel;
+    the 7x7 test layer above does not (it exercises the general kernel)."""
+    ext = L._ext()
+    for (C, H, K, pad, M) in [(3, 32, 5, 0, 6), (6, 14, 5, 0, 16), (3, 32, 3, 1, 32), (32, 32, 3, 1, 32),
+                              (32, 16, 3, 1, 64), (64, 16, 3, 1, 64)]:
+        OH = H + 2 * pad - K + 1
+        for bf in (0, 1):
+            assert ext.conv_fwd_fast(64, C, H, H, M, K, pad, bf) == 1
+            assert ext.conv_fwd_fast(64, M, OH, OH, C, K, K - 1 - pad, bf) == 1
+    assert ext.conv_fwd_fast(2, 20, 12, 12, 40, 7, 3, 0) == 0
 
 
 @pytest.mark.parametrize("B,C,H,K,pad,Cout", [(8, 32, 16, 3, 1, 64), (6, 3, 32, 5, 0, 6)])
