@@ -308,6 +308,8 @@ __global__ void __launch_bounds__(CT) flip_weights_kernel(const float* __restric
 //   fp32: v_mfma_f32_16x16x4f32, CCH / 4 per (tap, subtile); 8 / 16 / 32-channel chunks
 //         (the smallest that holds C: the reference LeNet has C = 3 and 6)
 constexpr int PNT = 64;  // output positions per workgroup tile (4 waves x 16 columns)
+constexpr int AV = 6;    // weight vectors per thread in a chunk's register batch
+constexpr int PV = 20;   // patch elements per thread in a chunk's register batch
 
 template <bool BF16, int CCH>
 struct PatchT {
@@ -367,64 +369,97 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
 #pragma unroll
   for (int i = 0; i < BM / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int prow = g.R * CCH;  // patch rows of a chunk: (c, r)
+  // Staging of one chunk = ONE batch of independent global loads per thread (weights: AV
+  // 16-B vectors, patch: PV scalars, flat indices so all 64 lanes of every wave load),
+  // held in registers and stored to LDS after the previous chunk's MFMAs; the next
+  // chunk's batch is issued right after the barrier, so its latency overlaps the MFMAs.
+  // (The earlier row-per-wave staging paid ~8 serial memory latencies per chunk and left
+  // lanes >= Wp idle: 36-41 us per 16x16-layer launch.)  Shapes whose chunk exceeds the
+  // register batch stage the remainder directly (a slower, still correct path).
+  constexpr int VE = 16 / sizeof(T);  // elements per 16-B vector
+  constexpr int VPR = CCH / VE;       // vectors per weight row
+  const int nv = KK * BM * VPR;       // weight vectors per chunk
+  const int np = g.R * CCH * g.Wp;    // patch elements per chunk: (r, c, xp), xp fastest
+  // flat patch index e = tid + i * CT -> (row = r * CCH + c, xp), walked incrementally
+  const int dq = CT / g.Wp, dr = CT - dq * g.Wp;
+  const int row_t = tid / g.Wp, xp_t = tid - row_t * g.Wp;
+
+  // Per-thread offsets are chunk-invariant and hoisted (32-bit, one VGPR per element);
+  // a chunk adds c0.  Patch loads are raw buffer loads over image b: positions in the
+  // zero padding, rows past R and channels past C get an offset >= num_records, which the
+  // hardware returns as 0 - no per-element exec masks.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x) + (long)b * g.C * g.H * g.W, 0, g.C * g.H * g.W * (int)sizeof(float), 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;  // >= num_records for every chunk (C*H*W*4 < 2^31)
+  const unsigned cstep = (unsigned)(g.H * g.W * (int)sizeof(float));  // bytes per channel
+  // LDS destinations are hoisted too; out-of-range entries go to a dummy slot past the
+  // patch (Ps + R*Wp*CCP), so the stores need no exec masks either.
+  const int dummy = (int)(Ps - As) + g.R * g.Wp * CCP;
+  int aoff[AV], adst[AV], pdst[PV];
+  unsigned poff[PV];
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    const int v = min(tid + i * CT, nv - 1);
+    const int row = v / VPR, u = v - row * VPR;  // row = tap * BM + m (compile-time divisors)
+    const int tap = row / BM, m = row - tap * BM;
+    aoff[i] = (tap * g.Mp + m0 + m) * g.Cp + u * VE;
+    adst[i] = tid + i * CT < nv ? row * CCP + u * VE : dummy;
+  }
+  {
+    int row = row_t, xp = xp_t;
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
+      const bool ok = r < g.R && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      poff[i] = ok ? (unsigned)(((c * g.H + iy) * g.W + ix) * (int)sizeof(float)) : OOB;
+      pdst[i] = r < g.R ? (int)(Ps - As) + (r * g.Wp + xp) * CCP + c : dummy;
+      xp += dr; row += dq;
+      if (xp >= g.Wp) { xp -= g.Wp; ++row; }
+    }
+  }
+  uint4 areg[AV];
+  float preg[PV];
+  auto p_val = [&](int row, int xp, int c0) {  // remainder path
+    const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
+    const bool ok = r < g.R && c0 + c < g.C && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    return ok ? x[((long)(b * g.C + c0 + c) * g.H + iy) * g.W + ix] : 0.f;
+  };
+  auto p_store = [&](int row, int xp, float v) {
+    const int r = row / CCH, c = row - r * CCH;
+    if (r < g.R) Ps[(r * g.Wp + xp) * CCP + c] = (T)v;
+  };
+  auto load_batch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) areg[i] = *reinterpret_cast<const uint4*>(wp + aoff[i] + c0);
+    const unsigned cb = (unsigned)c0 * cstep;
+#pragma unroll
+    for (int i = 0; i < PV; ++i)
+      preg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(poff[i] + cb), 0, 0));
+  };
+  auto store_batch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) *reinterpret_cast<uint4*>(As + adst[i]) = areg[i];
+#pragma unroll
+    for (int i = 0; i < PV; ++i) As[pdst[i]] = (T)preg[i];
+    // remainder beyond the register batch (large kernels / wide images only)
+    for (int v = tid + AV * CT; v < nv; v += CT) {
+      const int row = v / VPR, u = v - row * VPR;
+      const int tap = row / BM, m = row - tap * BM;
+      *reinterpret_cast<uint4*>(As + row * CCP + u * VE) =
+          *reinterpret_cast<const uint4*>(wp + (tap * g.Mp + m0 + m) * g.Cp + u * VE + c0);
+    }
+    for (int e = tid + PV * CT; e < np; e += CT) {
+      const int row = e / g.Wp, xp = e - row * g.Wp;
+      p_store(row, xp, p_val(row, xp, c0));
+    }
+  };
+
+  load_batch(0);
   for (int c0 = 0; c0 < g.Cp; c0 += CCH) {
     if (c0) __syncthreads();  // previous chunk's MFMAs are done with As / Ps
-    // Staging issues a batch of independent global loads before any LDS store, so a
-    // workgroup pays a few memory latencies per chunk instead of one per row.
-    // stage A: KK * BM rows of CCH channels, 16-B vectors, 4 in flight per thread
-    {
-      constexpr int VE = 16 / sizeof(T);  // elements per 16-B vector
-      constexpr int VPR = CCH / VE;       // vectors per row
-      const int nv = KK * BM * VPR;
-      for (int v0 = tid; v0 < nv; v0 += 4 * CT) {
-        uint4 val[4];
-#pragma unroll
-        for (int u4 = 0; u4 < 4; ++u4) {
-          const int v = min(v0 + u4 * CT, nv - 1);
-          const int row = v / VPR, u = v - row * VPR;  // row = tap * BM + m
-          const int tap = row / BM, m = row - tap * BM;
-          val[u4] = *reinterpret_cast<const uint4*>(wp + ((long)(tap * g.Mp + m0 + m) * g.Cp + c0 + u * VE));
-        }
-#pragma unroll
-        for (int u4 = 0; u4 < 4; ++u4) {
-          const int v = v0 + u4 * CT;
-          if (v < nv) {
-            const int row = v / VPR, u = v - row * VPR;
-            *reinterpret_cast<uint4*>(As + row * CCP + u * VE) = val[u4];
-          }
-        }
-      }
-    }
-    // stage the patch: wave-uniform (c, r) rows, lanes along x (coalesced global reads),
-    // PU rows per wave in flight
-    constexpr int PU = 8;
-    for (int xp0 = 0; xp0 < g.Wp; xp0 += 64) {
-      const int xp = xp0 + lane, ix = xp - g.pad;
-      const bool colok = xp < g.Wp && (unsigned)ix < (unsigned)g.W;
-      for (int row0 = wave; row0 < prow; row0 += 4 * PU) {
-        float v[PU];
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-          const int row = row0 + 4 * u;
-          const int c = row / g.R, r = row - c * g.R;
-          const int iy = iy0 + r;
-          const bool ok = row < prow && colok && c0 + c < g.C && (unsigned)iy < (unsigned)g.H;
-          v[u] = ok ? x[((long)(b * g.C + c0 + c) * g.H + iy) * g.W + ix] : 0.f;
-        }
-        if (xp < g.Wp) {
-#pragma unroll
-          for (int u = 0; u < PU; ++u) {
-            const int row = row0 + 4 * u;
-            if (row < prow) {
-              const int c = row / g.R, r = row - c * g.R;
-              Ps[(r * g.Wp + xp) * CCP + c] = (T)v[u];
-            }
-          }
-        }
-      }
-    }
+    store_batch(c0);
     __syncthreads();
+    if (c0 + CCH < g.Cp) load_batch(c0 + CCH);  // in flight during this chunk's MFMAs
     for (int ky = 0; ky < g.K; ++ky) {
       for (int kx = 0; kx < g.K; ++kx) {
         const int tap = ky * g.K + kx;
@@ -490,7 +525,7 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
   int bm = M <= 16 ? 16 : 32;
   const int cch = bf ? 32 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
   const size_t es = bf ? 2 : 4, ccp = bf ? 40 : cch + 4;
-  auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp) * ccp * es; };
+  auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp + 1) * ccp * es; };  // + dummy slot
   if (lds_of(bm) > kPatchLdsMax && bm == 32) bm = 16;
   if (lds_of(bm) > kPatchLdsMax) return f;
   f.ok = true;
