@@ -189,6 +189,20 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("conv_fwd_fast", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
     return dnn::conv_fwd_fast(B, C, H, W, M, K, pad, bf16_ops);
   });
+  // jobs: [(w, dst, B, C, H, W, M, K, pad, bf16_ops, flip), ...]
+  m.def("conv_pack_all", [](std::vector<std::tuple<u, u, int, int, int, int, int, int, int, int, int>> jobs, u stream) {
+    std::vector<dnn::ConvPackJob> js;
+    for (const auto& t : jobs)
+      js.push_back(dnn::ConvPackJob{P<const float>(std::get<0>(t)), P<void>(std::get<1>(t)), std::get<2>(t),
+                                    std::get<3>(t), std::get<4>(t), std::get<5>(t), std::get<6>(t), std::get<7>(t),
+                                    std::get<8>(t), std::get<9>(t), std::get<10>(t)});
+    dnn::launch_conv_pack_all(js.data(), (int)js.size(), S(stream));
+  });
+  m.def("conv_fwd_packed", [](u x, u wp, u bias, u y, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                              u stream) {
+    dnn::launch_conv_fwd_packed(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y), B, C, H, W, M,
+                                K, pad, bf16_ops, S(stream));
+  });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;
     dnn::conv_wgrad_split(B, C, H, W, M, K, pad, &s, &cps);

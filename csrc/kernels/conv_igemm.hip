@@ -308,8 +308,11 @@ __global__ void __launch_bounds__(CT) flip_weights_kernel(const float* __restric
 //   fp32: v_mfma_f32_16x16x4f32, CCH / 4 per (tap, subtile); 8 / 16 / 32-channel chunks
 //         (the smallest that holds C: the reference LeNet has C = 3 and 6)
 constexpr int PNT = 64;  // output positions per workgroup tile (4 waves x 16 columns)
-constexpr int AV = 6;    // weight vectors per thread in a chunk's register batch
-constexpr int PV = 20;   // patch elements per thread in a chunk's register batch
+// register batch of one chunk per thread: AV 16-B weight vectors, PV patch elements - sized
+// per channel chunk so the small-C (LeNet) variants keep their occupancy
+template <int CCH> struct Batch { static constexpr int AV = 6, PV = 20; };     // 32-ch chunks (vgg)
+template <> struct Batch<16> { static constexpr int AV = 7, PV = 13; };        // lenet conv2 dgrad
+template <> struct Batch<8> { static constexpr int AV = 4, PV = 8; };          // lenet conv1 / conv2
 
 template <bool BF16, int CCH>
 struct PatchT {
@@ -378,6 +381,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   // register batch stage the remainder directly (a slower, still correct path).
   constexpr int VE = 16 / sizeof(T);  // elements per 16-B vector
   constexpr int VPR = CCH / VE;       // vectors per weight row
+  constexpr int AV = Batch<CCH>::AV, PV = Batch<CCH>::PV;
   const int nv = KK * BM * VPR;       // weight vectors per chunk
   const int np = g.R * CCH * g.Wp;    // patch elements per chunk: (r, c, xp), xp fastest
   // flat patch index e = tid + i * CT -> (row = r * CCH + c, xp), walked incrementally
@@ -664,6 +668,74 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   const long n = (long)M * (Kd + 1);
   hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(SW * 64), 0, s, part, S, n, Kd, dw, db);
   HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+constexpr int kMaxPack = 16;
+struct PackItem {
+  const float* w;
+  void* dst;
+  int M, C, K, Mp, Cp, flip, bf;
+};
+struct PackSet {
+  PackItem it[kMaxPack];
+  int start[kMaxPack + 1];  // element prefix sums
+  int n;
+};
+
+// every job's packed image in one grid-stride launch (same element map as pack_weights_kernel)
+__global__ void __launch_bounds__(CT) pack_multi_kernel(const PackSet ps) {
+  const int total = ps.start[ps.n];
+  for (int e = blockIdx.x * CT + threadIdx.x; e < total; e += gridDim.x * CT) {
+    int j = 0;
+    while (j + 1 < ps.n && e >= ps.start[j + 1]) ++j;
+    const PackItem& p = ps.it[j];
+    const int l = e - ps.start[j];
+    const int c = l % p.Cp, m = (l / p.Cp) % p.Mp, tap = l / (p.Cp * p.Mp);
+    const int ky = tap / p.K, kx = tap - ky * p.K;
+    float v = 0.f;
+    if (m < p.M && c < p.C)
+      v = p.flip ? p.w[((c * p.M + m) * p.K + (p.K - 1 - ky)) * p.K + (p.K - 1 - kx)]
+                 : p.w[((m * p.C + c) * p.K + ky) * p.K + kx];
+    if (p.bf) reinterpret_cast<bf16*>(p.dst)[l] = (bf16)v;
+    else reinterpret_cast<float*>(p.dst)[l] = v;
+  }
+}
+}  // namespace
+
+void launch_conv_pack_all(const ConvPackJob* jobs, int n, hipStream_t s) {
+  for (int j0 = 0; j0 < n; j0 += kMaxPack) {
+    PackSet ps{};
+    ps.n = std::min(kMaxPack, n - j0);
+    ps.start[0] = 0;
+    for (int j = 0; j < ps.n; ++j) {
+      const ConvPackJob& J = jobs[j0 + j];
+      const FastPlan f = plan_fast(J.B, J.C, J.H, J.W, J.M, J.K, J.pad, J.bf16_ops != 0);
+      if (!f.ok) throw std::runtime_error("conv_pack_all: layer is not on the LDS-patch path");
+      // (forward: w is [M][C][K][K]; flip: w is the layer's [C][M][K][K], as in launch_conv_fwd)
+      ps.it[j] = PackItem{J.w, J.dst, f.pg.M, f.pg.C, f.pg.K, f.pg.Mp, f.pg.Cp, J.flip, J.bf16_ops != 0};
+      ps.start[j + 1] = ps.start[j] + f.pg.K * f.pg.K * f.pg.Mp * f.pg.Cp;
+    }
+    const int total = ps.start[ps.n];
+    hipLaunchKernelGGL(pack_multi_kernel, dim3(std::max(1, std::min((total + CT - 1) / CT, 2048))), dim3(CT), 0, s,
+                       ps);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, float* y, int B, int C, int H, int W,
+                            int M, int K, int pad, int bf16_ops, hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (!f.ok) throw std::runtime_error("conv_fwd_packed: layer is not on the LDS-patch path");
+  if (bf16_ops) {
+    fast_launch<true, 32>(f, reinterpret_cast<const bf16*>(wp), x, bias, y, s);
+  } else {
+    const float* w = reinterpret_cast<const float*>(wp);
+    if (f.cch == 8) fast_launch<false, 8>(f, w, x, bias, y, s);
+    else if (f.cch == 16) fast_launch<false, 16>(f, w, x, bias, y, s);
+    else fast_launch<false, 32>(f, w, x, bias, y, s);
+  }
 }
 
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s) {

@@ -73,6 +73,18 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
                        int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s);
+// Weight packing for the LDS-patch path, hoisted out of the convolutions: one launch packs
+// the forward (flip = 0) and dgrad (flip = 1) images of every fast-path layer of a step
+// (geometry = the launch_conv_fwd call the image is for); launch_conv_fwd_packed then
+// skips its per-call pack kernel.
+struct ConvPackJob {
+  const float* w;
+  void* dst;  // conv_fwd_workspace(B, C, H, W, M, K, pad, bf16_ops, flip) bytes
+  int B, C, H, W, M, K, pad, bf16_ops, flip;
+};
+void launch_conv_pack_all(const ConvPackJob* jobs, int n, hipStream_t s);
+void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, float* y, int B, int C, int H, int W,
+                            int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
 

@@ -72,12 +72,14 @@ class Conv2dFn(torch.autograd.Function):
     split over workgroup slices + a fixed-order slice sum; fp32 or bf16 operands
     (converted while staging to LDS).  On the CPU: unfold + matmul (the oracle).
 
+    ``packed``: (forward image, dgrad image) from the engine's once-per-step
+    ``conv_pack_all`` launch (either may be None: packed per call).
     ``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
     them (views of the engine's flat gradient arena) and autograd gets None for the
     parameters - no per-parameter accumulation kernels, no arena zeroing."""
 
     @staticmethod
-    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None):
+    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -86,8 +88,11 @@ class Conv2dFn(torch.autograd.Function):
         if _is_gpu(x):
             ext = _ext()
             y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
-            ws = _workspace(x, ext.conv_fwd_workspace(B, C, H, W, Cout, K, pad, bf, 0))
-            ext.conv_fwd(_p(x), _p(w), _p(b), _p(y), _p(ws), B, C, H, W, Cout, K, pad, bf, 0, _s(x))
+            if packed is not None and packed[0] is not None:  # image packed by the engine's conv_pack_all
+                ext.conv_fwd_packed(_p(x), _p(packed[0]), _p(b), _p(y), B, C, H, W, Cout, K, pad, bf, _s(x))
+            else:
+                ws = _workspace(x, ext.conv_fwd_workspace(B, C, H, W, Cout, K, pad, bf, 0))
+                ext.conv_fwd(_p(x), _p(w), _p(b), _p(y), _p(ws), B, C, H, W, Cout, K, pad, bf, 0, _s(x))
         else:
             cols = F.unfold(x, K, padding=pad)
             y = (_gemm(w.reshape(Cout, -1), cols, gemm_dtype) + b.view(1, Cout, 1)).view(B, Cout, OH, OW)
@@ -95,6 +100,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.shape = (B, C, H, W, K, pad, OH, OW)
         ctx.gemm_dtype = gemm_dtype
         ctx.gw, ctx.gb = gw, gb
+        ctx.packed = packed
         return y
 
     @staticmethod
@@ -116,8 +122,12 @@ class Conv2dFn(torch.autograd.Function):
                 # dgrad: the forward kernel over dY with the flipped, transposed weights
                 # (flip=1: packed from w inside the launch), pad' = K - 1 - pad
                 dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
-                ws = _workspace(dy, ext.conv_fwd_workspace(B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1))
-                ext.conv_fwd(_p(dy), _p(w), 0, _p(dx), _p(ws), B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1, st)
+                if ctx.packed is not None and ctx.packed[1] is not None:
+                    ext.conv_fwd_packed(_p(dy), _p(ctx.packed[1]), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf,
+                                        st)
+                else:
+                    ws = _workspace(dy, ext.conv_fwd_workspace(B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1))
+                    ext.conv_fwd(_p(dy), _p(w), 0, _p(dx), _p(ws), B, Cout, OH, OW, C, K, K - 1 - pad, bf, 1, st)
         else:
             cols = F.unfold(x, K, padding=pad)
             dy2 = dy.view(B, Cout, OH * OW)
@@ -127,8 +137,8 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None
+            return dx, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 # ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------

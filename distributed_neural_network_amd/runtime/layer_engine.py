@@ -71,6 +71,39 @@ class LayerEngine(Engine):
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._warm = False
+        self._packed: dict[str, tuple] = {}
+        self._pack_jobs: list[tuple] = []
+        if self.gpu:
+            self._plan_weight_packing()
+
+    def _plan_weight_packing(self) -> None:
+        """Persistent packed weight images of every LDS-patch convolution (forward and, except
+        for the input layer, dgrad), refreshed by ONE conv_pack_all launch per forward instead
+        of a pack kernel inside each convolution (7 launches per cifar-vgg step).  The images
+        do not depend on the batch size, so the eval forward uses them too."""
+        ext, B = self.ext, self.batch
+        bf = int(self.gemm_dtype == torch.bfloat16)
+        H = W = 32
+        first = True
+        for layer in self.spec:
+            if isinstance(layer, zoo.Conv):
+                n, C, M, K, pad = layer.name, layer.cin, layer.cout, layer.k, layer.pad
+                OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+                w = self.P[f"{n}.weight"].data_ptr()
+                fwd = dgr = None
+                if ext.conv_fwd_fast(B, C, H, W, M, K, pad, bf):
+                    fwd = torch.empty(ext.conv_fwd_workspace(B, C, H, W, M, K, pad, bf, 0), device=self.device,
+                                      dtype=torch.uint8)
+                    self._pack_jobs.append((w, fwd.data_ptr(), B, C, H, W, M, K, pad, bf, 0))
+                if not first and ext.conv_fwd_fast(B, M, OH, OW, C, K, K - 1 - pad, bf):
+                    dgr = torch.empty(ext.conv_fwd_workspace(B, M, OH, OW, C, K, K - 1 - pad, bf, 1),
+                                      device=self.device, dtype=torch.uint8)
+                    self._pack_jobs.append((w, dgr.data_ptr(), B, M, OH, OW, C, K, K - 1 - pad, bf, 1))
+                self._packed[n] = (fwd, dgr)
+                first = False
+                H, W = OH, OW
+            elif isinstance(layer, zoo.ReluPool):
+                H, W = H // 2, W // 2
 
     # -- parameters / checkpoints ------------------------------------------------------------
     def state_dict(self):
@@ -124,11 +157,13 @@ class LayerEngine(Engine):
         flat gradient arena (views ``G``), so backward leaves ``grad`` complete with no
         accumulation or zeroing kernels."""
         P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
+        if self._pack_jobs:
+            self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
         for layer in self.spec:
             n = getattr(layer, "name", "")
             gw, gb = (G[f"{n}.weight"], G[f"{n}.bias"]) if (training and n) else (None, None)
             if isinstance(layer, zoo.Conv):
-                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb)
+                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, self._packed.get(n))
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
                                           Bf[f"{n}.running_var"], state, training, layer.eps, layer.momentum, gw, gb)
