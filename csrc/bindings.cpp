@@ -158,6 +158,20 @@ PYBIND11_MODULE(_dnn_hip, m) {
                        P<const float>(smean), P<const float>(sinvstd), P<float>(dx), P<float>(dgamma),
                        P<float>(dbeta), P<double>(part), S(stream));
   });
+  m.def("bn_act_fwd_train", [](u x, int B, int C, int H, int W, u state, u gamma, u beta, float eps, float mom,
+                               u rmean, u rvar, u y, u code, u smean, u sinvstd, u part, int act, u stream) {
+    dnn::launch_bn_act_fwd_train(P<const float>(x), B, C, H, W, P<const int32_t>(state), P<const float>(gamma),
+                                 P<const float>(beta), eps, mom, P<float>(rmean), P<float>(rvar), P<float>(y),
+                                 P<uint8_t>(code), P<float>(smean), P<float>(sinvstd), P<double>(part), act,
+                                 S(stream));
+  });
+  m.def("bn_act_bwd", [](u dy, u x, int B, int C, int H, int W, u state, u gamma, u beta, u smean, u sinvstd, u code,
+                         u dx, u dgamma, u dbeta, u part, int act, u stream) {
+    dnn::launch_bn_act_bwd(P<const float>(dy), P<const float>(x), B, C, H, W, P<const int32_t>(state),
+                           P<const float>(gamma), P<const float>(beta), P<const float>(smean), P<const float>(sinvstd),
+                           P<const uint8_t>(code), P<float>(dx), P<float>(dgamma), P<float>(dbeta), P<double>(part),
+                           act, S(stream));
+  });
   m.def("chan_sum", [](u a, int B, int C, int L, u out, u part, u stream) {
     dnn::launch_chan_sum(P<const float>(a), B, C, L, P<float>(out), P<double>(part), S(stream));
   });

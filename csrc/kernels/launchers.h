@@ -60,6 +60,16 @@ void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma,
 void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                    const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
                    hipStream_t s);
+// BatchNorm2d (training) fused with the activation that follows it: act 0 none, 1 ReLU,
+// 2 ReLU + 2x2 max-pool (y is [B][C][H/2][W/2] + the 2-bit argmax code).  The backward
+// takes the gradient of the ACTIVATION output (pooled for act 2).
+void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const int32_t* state, const float* gamma,
+                             const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
+                             float* smean, float* sinvstd, double* part, int act, hipStream_t s);
+void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
+                       const float* gamma, const float* beta, const float* smean, const float* sinvstd,
+                       const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
+                       hipStream_t s);
 void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s);
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
                  int32_t* correct, float* dlogits, hipStream_t s);

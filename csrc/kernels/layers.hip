@@ -129,27 +129,65 @@ __device__ __forceinline__ void block_sum2_d(double& s0, double& s1, double* red
   }
 }
 
+// BatchNorm affine output with an explicit rounding sequence: the fused BN+ReLU backward
+// recomputes it to rebuild the ReLU mask, and must get the forward's exact sign.
+__device__ __forceinline__ float bn_affine(float x, float mean, float invstd, float g, float bb) {
+  return __fmaf_rn(__fmul_rn(__fsub_rn(x, mean), invstd), g, bb);
+}
+
+// Activation fused after BatchNorm (ACT): 0 none, 1 ReLU, 2 ReLU + 2x2 max-pool (2-bit code).
+// Gradient reaching the BN output at element o = (b, c, l) of the [B][C][L = H*W] plane:
+// ACT 1 re-derives the ReLU mask from x; ACT 2 routes the pooled gradient through the code.
+struct ActArgs {
+  const float* beta;     // ACT 1
+  const uint8_t* code;   // ACT 2: [B][C][H/2][W/2]
+  int W;                 // ACT 2
+};
+template <int ACT>
+__device__ __forceinline__ float act_grad(const float* __restrict__ dy, const ActArgs& aa, int b, int C, int c,
+                                          int L, int l, int o, float xv, float mean, float invstd, float g) {
+  if constexpr (ACT == 0) {
+    return dy[o];
+  } else if constexpr (ACT == 1) {
+    return bn_affine(xv, mean, invstd, g, aa.beta[c]) > 0.f ? dy[o] : 0.f;
+  } else {
+    const int W = aa.W, OH = (L / W) >> 1, OW = W >> 1;
+    const int yy = l / W, xx = l - yy * W, oy = yy >> 1, ox = xx >> 1;
+    if (oy >= OH || ox >= OW) return 0.f;
+    const int po = ((b * C + c) * OH + oy) * OW + ox;
+    return aa.code[po] == (uint8_t)(((yy & 1) << 1) | (xx & 1)) ? dy[po] : 0.f;
+  }
+}
+
 // MODE 0: (sum x, sum x^2)   MODE 1: (sum dy, sum dy * xhat)   MODE 2: (sum a, 0)
-template <int MODE>
+template <int MODE, int ACT = 0>
 __global__ void __launch_bounds__(LT) chan_partial_kernel(const float* __restrict__ a, const float* __restrict__ x,
                                                           int B, int C, int L, const int32_t* __restrict__ state,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part, const float* __restrict__ gamma = nullptr,
+                                                          ActArgs aa = ActArgs{}) {
   __shared__ double red[2 * (LT / 64)];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
   const unsigned n = (unsigned)(bv * L), chunk = ((unsigned)(B * L) + P - 1) / P;
   const unsigned lo = p * chunk, hi = min(n, lo + chunk);
   const float mu = MODE == 1 ? mean[c] : 0.f, is = MODE == 1 ? invstd[c] : 0.f;
+  const float g = (MODE == 1 && ACT == 1) ? gamma[c] : 0.f;
   double s0 = 0.0, s1 = 0.0;
   for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
     const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
     const int o = (b * C + c) * L + l;
-    const float v = a[o];
-    s0 += (double)v;
-    if (MODE == 0) s1 += (double)v * (double)v;
-    if (MODE == 1) s1 += (double)v * (double)((x[o] - mu) * is);
+    if constexpr (MODE == 1) {
+      const float xv = x[o];
+      const float v = act_grad<ACT>(a, aa, b, C, c, L, l, o, xv, mu, is, g);
+      s0 += (double)v;
+      s1 += (double)v * (double)((xv - mu) * is);
+    } else {
+      const float v = a[o];
+      s0 += (double)v;
+      if (MODE == 0) s1 += (double)v * (double)v;
+    }
   }
   block_sum2_d(s0, s1, red);
   if (threadIdx.x == 0) {
@@ -172,6 +210,7 @@ __device__ __forceinline__ void merge_parts(const double* part, int c, int P, do
 // captured step must not pollute them), biased variance for the normalisation, unbiased
 // for the running estimate (torch semantics, momentum m).  Grid (P, C) like the partials:
 // each block merges its channel's partials, then normalises its slice.
+template <int ACT>
 __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restrict__ x, int B, int C, int L,
                                                             const int32_t* __restrict__ state,
                                                             const float* __restrict__ gamma,
@@ -180,7 +219,8 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
                                                             float* __restrict__ running_var, float* __restrict__ y,
                                                             float* __restrict__ save_mean,
                                                             float* __restrict__ save_invstd,
-                                                            const double* __restrict__ part) {
+                                                            const double* __restrict__ part, int W,
+                                                            uint8_t* __restrict__ code) {
   __shared__ float st[2];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
@@ -205,12 +245,42 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
   }
   __syncthreads();
   const float mean = st[0], invstd = st[1], g = gamma[c], bb = beta[c];
-  const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
-  const unsigned lo = p * chunk, hi = min(total, lo + chunk);
-  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
-    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
-    const int o = (b * C + c) * L + l;
-    y[o] = b < bv ? (x[o] - mean) * invstd * g + bb : 0.f;
+  if constexpr (ACT == 2) {
+    // BN -> ReLU -> 2x2 max-pool: one pooled output per thread (4 BN values, first max wins,
+    // code 4 = max <= 0), exactly relu_pool_fwd_kernel applied to the BN output
+    const int H = L / W, OH = H >> 1, OW = W >> 1, OL = OH * OW;
+    const unsigned total = (unsigned)(B * OL), chunk = (total + P - 1) / P;
+    const unsigned lo = p * chunk, hi = min(total, lo + chunk);
+    for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
+      const int b = (int)(t / (unsigned)OL), pl = (int)t - b * OL;
+      const int oy = pl / OW, ox = pl - oy * OW;
+      const int po = (b * C + c) * OL + pl;
+      float out = 0.f;
+      uint8_t cd = 4;
+      if (b < bv) {
+        const float* xp = x + ((long)(b * C + c) * H + 2 * oy) * W + 2 * ox;
+        float best = bn_affine(xp[0], mean, invstd, g, bb);
+        int arg = 0;
+        const float v1 = bn_affine(xp[1], mean, invstd, g, bb), v2 = bn_affine(xp[W], mean, invstd, g, bb),
+                    v3 = bn_affine(xp[W + 1], mean, invstd, g, bb);
+        if (v1 > best) { best = v1; arg = 1; }
+        if (v2 > best) { best = v2; arg = 2; }
+        if (v3 > best) { best = v3; arg = 3; }
+        out = fmaxf(best, 0.f);
+        cd = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+      }
+      y[po] = out;
+      code[po] = cd;
+    }
+  } else {
+    const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
+    const unsigned lo = p * chunk, hi = min(total, lo + chunk);
+    for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
+      const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
+      const int o = (b * C + c) * L + l;
+      const float v = bn_affine(x[o], mean, invstd, g, bb);
+      y[o] = b < bv ? (ACT == 1 ? fmaxf(v, 0.f) : v) : 0.f;
+    }
   }
 }
 
@@ -226,6 +296,7 @@ __global__ void __launch_bounds__(LT) bn_fwd_eval_kernel(const float* __restrict
   y[i] = (x[i] - running_mean[c]) * rsqrtf(running_var[c] + eps) * gamma[c] + beta[c];
 }
 
+template <int ACT>
 __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           int B, int C, int L, const int32_t* __restrict__ state,
                                                           const float* __restrict__ gamma,
@@ -233,7 +304,7 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
                                                           const float* __restrict__ save_invstd,
                                                           float* __restrict__ dx, float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta,
-                                                          const double* __restrict__ part) {
+                                                          const double* __restrict__ part, ActArgs aa) {
   __shared__ float st[2];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
   const int bv = valid_count(state, B);
@@ -256,7 +327,9 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
   for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
     const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
     const int o = (b * C + c) * L + l;
-    dx[o] = b < bv ? g * invstd * (dy[o] - mdy - (x[o] - mean) * invstd * mdyx) : 0.f;
+    const float xv = x[o];
+    const float d = act_grad<ACT>(dy, aa, b, C, c, L, l, o, xv, mean, invstd, g);
+    dx[o] = b < bv ? g * invstd * (d - mdy - (xv - mean) * invstd * mdyx) : 0.f;
   }
 }
 
@@ -351,9 +424,27 @@ void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* sta
   if (!C) return;
   const dim3 grid(chan_parts_of(B, L), C);
   hipLaunchKernelGGL(chan_partial_kernel<0>, grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr, nullptr,
-                     part);
-  hipLaunchKernelGGL(bn_apply_train_kernel, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
-                     rvar, y, smean, sinvstd, part);
+                     part, nullptr, ActArgs{});
+  hipLaunchKernelGGL(bn_apply_train_kernel<0>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
+                     rvar, y, smean, sinvstd, part, 1, nullptr);
+}
+void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const int32_t* state, const float* gamma,
+                             const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
+                             float* smean, float* sinvstd, double* part, int act, hipStream_t s) {
+  if (!C) return;
+  const int L = H * W;
+  const dim3 grid(chan_parts_of(B, L), C);
+  hipLaunchKernelGGL(chan_partial_kernel<0>, grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr, nullptr,
+                     part, nullptr, ActArgs{});
+  if (act == 1)
+    hipLaunchKernelGGL(bn_apply_train_kernel<1>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
+                       rvar, y, smean, sinvstd, part, W, nullptr);
+  else if (act == 2)
+    hipLaunchKernelGGL(bn_apply_train_kernel<2>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
+                       rvar, y, smean, sinvstd, part, W, code);
+  else
+    hipLaunchKernelGGL(bn_apply_train_kernel<0>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
+                       rvar, y, smean, sinvstd, part, W, nullptr);
 }
 void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
                         const float* rmean, const float* rvar, float* y, hipStream_t s) {
@@ -366,15 +457,36 @@ void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const i
                    hipStream_t s) {
   if (!C) return;
   const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL(chan_partial_kernel<1>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd, part);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
-                     dgamma, dbeta, part);
+  hipLaunchKernelGGL((chan_partial_kernel<1, 0>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd, part,
+                     gamma, ActArgs{});
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
+                     dgamma, dbeta, part, ActArgs{});
+}
+template <int ACT>
+static void bn_act_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                       const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
+                       ActArgs aa, hipStream_t s) {
+  const dim3 grid(chan_parts_of(B, L), C);
+  hipLaunchKernelGGL((chan_partial_kernel<1, ACT>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd,
+                     part, gamma, aa);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<ACT>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd,
+                     dx, dgamma, dbeta, part, aa);
+}
+void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
+                       const float* gamma, const float* beta, const float* smean, const float* sinvstd,
+                       const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
+                       hipStream_t s) {
+  if (!C) return;
+  const ActArgs aa{beta, code, W};
+  if (act == 1) bn_act_bwd<1>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
+  else if (act == 2) bn_act_bwd<2>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
+  else bn_act_bwd<0>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
 }
 void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s) {
   if (!C) return;
   const int P = chan_parts_of(B, L);
   hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(P, C), dim3(LT), 0, s, a, nullptr, B, C, L, nullptr, nullptr,
-                     nullptr, part);
+                     nullptr, part, nullptr, ActArgs{});
   hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, part, C, P, out);
 }
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,

@@ -314,6 +314,57 @@ class BatchNorm2dFn(torch.autograd.Function):
         return (dx, dgamma, dbeta) + none9
 
 
+class BatchNormActFn(torch.autograd.Function):
+    """BatchNorm2d (training statistics, tail-masked) fused with the activation after it -
+    act 1: ReLU, act 2: ReLU + 2x2 max-pool (2-bit argmax code) - MI355X only.  Forward: the
+    statistics pass, then one kernel that normalises AND activates (and pools); backward:
+    the ReLU mask is re-derived from x (bit-exact affine recompute) or the pooled gradient
+    is routed through the code inside the two BN backward kernels.  Saves the activation
+    kernels and one full read + write of the activation per direction (the separate
+    ReluFn / ReluPoolFn path is the CPU oracle and the eval path)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, state, eps: float, momentum: float, act: int,
+                ggamma=None, gbeta=None):
+        B, C, H, W = x.shape
+        x = x.contiguous()
+        ext = _ext()
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        if act == 2:
+            y = torch.empty(B, C, H // 2, W // 2, device=x.device, dtype=torch.float32)
+            code = torch.empty(B, C, H // 2, W // 2, device=x.device, dtype=torch.uint8)
+        else:
+            y = torch.empty_like(x)
+            code = torch.zeros(0, device=x.device, dtype=torch.uint8)
+        part = _partials(x, B, C, H * W)
+        ext.bn_act_fwd_train(_p(x), B, C, H, W, _p(state) if state is not None else 0, _p(gamma), _p(beta), eps,
+                             momentum, _p(running_mean), _p(running_var), _p(y), _p(code) if act == 2 else 0,
+                             _p(mean), _p(invstd), _p(part), act, _s(x))
+        ctx.act = act
+        ctx.gg, ctx.gb = ggamma, gbeta
+        ctx.save_for_backward(x, gamma, beta, mean, invstd, code, state if state is not None else torch.zeros(0))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, mean, invstd, code, state = ctx.saved_tensors
+        state = state if state.numel() else None
+        B, C, H, W = x.shape
+        dy = dy.contiguous()
+        inplace = ctx.gg is not None
+        dx = torch.empty_like(x)
+        dgamma = ctx.gg if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
+        dbeta = ctx.gb if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
+        _ext().bn_act_bwd(_p(dy), _p(x), B, C, H, W, _p(state) if state is not None else 0, _p(gamma), _p(beta),
+                          _p(mean), _p(invstd), _p(code) if ctx.act == 2 else 0, _p(dx), _p(dgamma), _p(dbeta),
+                          _p(_partials(dy, B, C, H * W)), ctx.act, _s(dy))
+        none8 = (None,) * 8
+        if inplace:
+            return (dx, None, None) + none8
+        return (dx, dgamma, dbeta) + none8
+
+
 # ---- softmax cross-entropy (mean over the valid batch) + accuracy ----------------------------
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, state: torch.Tensor | None, want_grad: bool = True):
     """Returns (per-sample loss [B], per-sample correct [B] int32, dlogits [B, NC] or None)."""

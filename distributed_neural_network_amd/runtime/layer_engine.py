@@ -159,10 +159,21 @@ class LayerEngine(Engine):
         P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
         if self._pack_jobs:
             self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
-        for layer in self.spec:
+        fuse_act = training and self.gpu  # BN + following ReLU / ReLU-pool in one op (MI355X training)
+        skip = False
+        for i, layer in enumerate(self.spec):
+            if skip:  # activation already applied by the fused BatchNorm
+                skip = False
+                continue
             n = getattr(layer, "name", "")
             gw, gb = (G[f"{n}.weight"], G[f"{n}.bias"]) if (training and n) else (None, None)
-            if isinstance(layer, zoo.Conv):
+            nxt = self.spec[i + 1] if i + 1 < len(self.spec) else None
+            if fuse_act and isinstance(layer, zoo.BN) and isinstance(nxt, (zoo.Relu, zoo.ReluPool)):
+                act = 2 if isinstance(nxt, zoo.ReluPool) else 1
+                x = L.BatchNormActFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
+                                           Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb)
+                skip = True
+            elif isinstance(layer, zoo.Conv):
                 x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, self._packed.get(n))
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],

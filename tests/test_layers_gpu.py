@@ -128,6 +128,33 @@ def test_batchnorm_train_masked_and_eval(bvalid):
     assert float(outs[1][0][bvalid:].abs().sum()) == 0.0  # padded tail masked out
 
 
+@pytest.mark.parametrize("act,bvalid,hw", [(1, 6, 7), (2, 6, 8), (2, 4, 7), (1, 3, 6)])
+def test_batchnorm_act_fused_matches_composition(act, bvalid, hw):
+    """BatchNormActFn (BN + ReLU / ReLU-pool in the BN kernels) == BatchNorm2dFn followed by
+    ReluFn / ReluPoolFn (CPU oracle composition), tail-masked, odd sizes (pool floor)."""
+    g = torch.Generator().manual_seed(7)
+    B, C = 6, 5
+    x = torch.randn(B, C, hw, hw, generator=g)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.5
+    rm0, rv0 = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    outs = []
+    for dev in ("cpu", DEV):
+        xs, gs, bs = (t.detach().to(dev).requires_grad_() for t in (x, gamma, beta))
+        rm, rv = rm0.clone().to(dev), rv0.clone().to(dev)
+        st = torch.tensor([0, bvalid, 0, 0], dtype=torch.int32, device=dev)
+        if dev == "cpu":
+            y = L.BatchNorm2dFn.apply(xs, gs, bs, rm, rv, st, True, 1e-5, 0.1)
+            y = L.ReluPoolFn.apply(y) if act == 2 else L.ReluFn.apply(y)
+        else:
+            y = L.BatchNormActFn.apply(xs, gs, bs, rm, rv, st, 1e-5, 0.1, act)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(dev)
+        y.backward(dy)
+        outs.append((y, xs.grad, gs.grad, bs.grad, rm, rv))
+    for c, gg in zip(*outs):
+        _close(gg, c, 2e-5)
+    assert float(outs[1][0][bvalid:].abs().sum()) == 0.0  # padded tail masked out
+
+
 def test_cross_entropy_masked():
     g = torch.Generator().manual_seed(4)
     z = torch.randn(9, 10, generator=g)
