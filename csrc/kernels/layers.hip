@@ -15,6 +15,9 @@
 //    batch masked out of the statistics, fused softmax cross-entropy forward + backward +
 //    accuracy, step bookkeeping (shared with the fused path), flat momentum SGD.
 //  * every reduction is a fixed-order tree (no float atomics): bitwise reproducible.
+#include <cstdint>
+#include <initializer_list>
+
 #include "reduce_common.h"
 
 namespace dnn {
@@ -95,15 +98,59 @@ __global__ void __launch_bounds__(LT) relu_bwd_kernel(const float* __restrict__ 
 }
 
 // ---- per-channel reductions over (batch, pixels): deterministic two-stage ---------------
-// Stage 1: grid (P, C) blocks, block (p, c) reduces a fixed slice of channel c's B*L plane
-// into fp64 partials; stage 2 merges the P partials of a channel in a fixed order.  The
-// slicing depends only on (B, L), never on the valid count, so graph replays and tail
-// batches reduce in the same order (bitwise reproducible).  fp64 partial sums make the
-// one-pass E[x^2] - E[x]^2 variance safe.
+// Stage 1: grid (P, C) blocks; block (p, c) owns channel c's planes of samples
+// [p * ppb, (p + 1) * ppb) (ppb = planes per block, ~2048 elements) and reduces them into
+// fp64 partials; stage 2 merges a channel's P partials in a fixed order.  The split depends
+// only on (B, L), never on the valid count, so graph replays and tail batches reduce in the
+// same order (bitwise reproducible).  fp64 partial sums make the one-pass E[x^2] - E[x]^2
+// variance safe.  Threads walk (plane, vector) pairs incrementally - no per-element integer
+// division - and move float4 vectors when the plane allows it (VW = 4; host-checked).
+__host__ __device__ inline int chan_ppb(int B, int L) {
+  const int p = (2048 + L - 1) / L;
+  return p < 1 ? 1 : (p > B ? (B > 0 ? B : 1) : p);
+}
 __host__ __device__ inline int chan_parts_of(int B, int L) {
-  const long n = (long)B * L;
-  const int p = (int)((n + 4095) / 4096);
-  return p < 1 ? 1 : (p > 64 ? 64 : p);
+  const int ppb = chan_ppb(B, L);
+  const int P = (B + ppb - 1) / ppb;
+  return P < 1 ? 1 : P;
+}
+
+// f(b, l, o) for every VW-vector (plane b of channel c, first pixel l, element offset o) of
+// planes [b0, b1); thread t takes vectors t, t + LT, ...
+template <int VW, typename F>
+__device__ __forceinline__ void plane_walk(int b0, int b1, int C, int c, int L, F&& f) {
+  const int LV = L / VW;
+  if (b1 <= b0 || LV <= 0) return;
+  const int n = (b1 - b0) * LV;
+  const int dq = LT / LV, dr = LT - dq * LV;
+  int q = (int)threadIdx.x / LV, r = (int)threadIdx.x - q * LV;
+  for (int t = threadIdx.x; t < n; t += LT) {
+    const int l = r * VW;
+    f(b0 + q, l, ((b0 + q) * C + c) * L + l);  // 32-bit: B*C*L < 2^31 (host check)
+    r += dr;
+    q += dq;
+    if (r >= LV) { r -= LV; ++q; }
+  }
+}
+
+template <int VW>
+__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&v)[VW]) {
+  if constexpr (VW == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) v[j] = p[j];
+  }
+}
+template <int VW>
+__device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[VW]) {
+  if constexpr (VW == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) p[j] = v[j];
+  }
 }
 
 __device__ __forceinline__ void block_sum2_d(double& s0, double& s1, double* red) {
@@ -136,59 +183,76 @@ __device__ __forceinline__ float bn_affine(float x, float mean, float invstd, fl
 }
 
 // Activation fused after BatchNorm (ACT): 0 none, 1 ReLU, 2 ReLU + 2x2 max-pool (2-bit code).
-// Gradient reaching the BN output at element o = (b, c, l) of the [B][C][L = H*W] plane:
-// ACT 1 re-derives the ReLU mask from x; ACT 2 routes the pooled gradient through the code.
 struct ActArgs {
   const float* beta;     // ACT 1
   const uint8_t* code;   // ACT 2: [B][C][H/2][W/2]
-  int W;                 // ACT 2
+  int W, OH;             // ACT 2: plane width, pooled height (H / 2)
 };
-template <int ACT>
-__device__ __forceinline__ float act_grad(const float* __restrict__ dy, const ActArgs& aa, int b, int C, int c,
-                                          int L, int l, int o, float xv, float mean, float invstd, float g) {
-  if constexpr (ACT == 0) {
-    return dy[o];
-  } else if constexpr (ACT == 1) {
-    return bn_affine(xv, mean, invstd, g, aa.beta[c]) > 0.f ? dy[o] : 0.f;
+// Gradient reaching the BN output at the VW pixels (b, c, l..l+VW-1), element offset o:
+// ACT 0 reads dy; ACT 1 re-derives the ReLU mask from x; ACT 2 routes the pooled gradient
+// through the code (VW pixels share one image row: W % VW == 0, host-checked).
+template <int ACT, int VW>
+__device__ __forceinline__ void grad_in(const float* __restrict__ dy, const ActArgs& aa, int b, int C, int c, int l,
+                                        int o, const float (&xv)[VW], float mean, float invstd, float g,
+                                        float (&d)[VW]) {
+  if constexpr (ACT == 2) {
+    const int W = aa.W, OW = W >> 1;
+    const int yy = l / W, xx0 = l - yy * W, oy = yy >> 1;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const int xx = xx0 + j, ox = xx >> 1;
+      d[j] = 0.f;
+      if (oy < aa.OH && ox < OW) {
+        const int po = ((b * C + c) * aa.OH + oy) * OW + ox;
+        if (aa.code[po] == (uint8_t)(((yy & 1) << 1) | (xx & 1))) d[j] = dy[po];
+      }
+    }
   } else {
-    const int W = aa.W, OH = (L / W) >> 1, OW = W >> 1;
-    const int yy = l / W, xx = l - yy * W, oy = yy >> 1, ox = xx >> 1;
-    if (oy >= OH || ox >= OW) return 0.f;
-    const int po = ((b * C + c) * OH + oy) * OW + ox;
-    return aa.code[po] == (uint8_t)(((yy & 1) << 1) | (xx & 1)) ? dy[po] : 0.f;
+    ldv<VW>(dy + o, d);
+    if constexpr (ACT == 1) {
+      const float bb = aa.beta[c];
+#pragma unroll
+      for (int j = 0; j < VW; ++j)
+        if (!(bn_affine(xv[j], mean, invstd, g, bb) > 0.f)) d[j] = 0.f;
+    }
   }
 }
 
-// MODE 0: (sum x, sum x^2)   MODE 1: (sum dy, sum dy * xhat)   MODE 2: (sum a, 0)
-template <int MODE, int ACT = 0>
+// MODE 0: (sum x, sum x^2)   MODE 1: (sum dz, sum dz * xhat), dz = grad_in<ACT>   MODE 2: (sum a, 0)
+template <int MODE, int ACT, int VW>
 __global__ void __launch_bounds__(LT) chan_partial_kernel(const float* __restrict__ a, const float* __restrict__ x,
                                                           int B, int C, int L, const int32_t* __restrict__ state,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
-                                                          double* __restrict__ part, const float* __restrict__ gamma = nullptr,
-                                                          ActArgs aa = ActArgs{}) {
+                                                          double* __restrict__ part, const float* __restrict__ gamma,
+                                                          ActArgs aa) {
   __shared__ double red[2 * (LT / 64)];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
-  const int bv = valid_count(state, B);
-  const unsigned n = (unsigned)(bv * L), chunk = ((unsigned)(B * L) + P - 1) / P;
-  const unsigned lo = p * chunk, hi = min(n, lo + chunk);
+  const int bv = valid_count(state, B), ppb = chan_ppb(B, L);
+  const int b0 = p * ppb, b1 = min(min(B, b0 + ppb), bv);  // valid planes only
   const float mu = MODE == 1 ? mean[c] : 0.f, is = MODE == 1 ? invstd[c] : 0.f;
   const float g = (MODE == 1 && ACT == 1) ? gamma[c] : 0.f;
   double s0 = 0.0, s1 = 0.0;
-  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
-    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
-    const int o = (b * C + c) * L + l;
+  plane_walk<VW>(b0, b1, C, c, L, [&](int b, int l, int o) {
     if constexpr (MODE == 1) {
-      const float xv = x[o];
-      const float v = act_grad<ACT>(a, aa, b, C, c, L, l, o, xv, mu, is, g);
-      s0 += (double)v;
-      s1 += (double)v * (double)((xv - mu) * is);
+      float xv[VW], d[VW];
+      ldv<VW>(x + o, xv);
+      grad_in<ACT, VW>(a, aa, b, C, c, l, o, xv, mu, is, g, d);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        s0 += (double)d[j];
+        s1 += (double)d[j] * (double)((xv[j] - mu) * is);
+      }
     } else {
-      const float v = a[o];
-      s0 += (double)v;
-      if (MODE == 0) s1 += (double)v * (double)v;
+      float v[VW];
+      ldv<VW>(a + o, v);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        s0 += (double)v[j];
+        if (MODE == 0) s1 += (double)v[j] * (double)v[j];
+      }
     }
-  }
+  });
   block_sum2_d(s0, s1, red);
   if (threadIdx.x == 0) {
     part[((size_t)c * P + p) * 2] = s0;
@@ -209,8 +273,8 @@ __device__ __forceinline__ void merge_parts(const double* part, int c, int P, do
 // Training: batch statistics over the VALID samples only (the padded tail batch of a
 // captured step must not pollute them), biased variance for the normalisation, unbiased
 // for the running estimate (torch semantics, momentum m).  Grid (P, C) like the partials:
-// each block merges its channel's partials, then normalises its slice.
-template <int ACT>
+// each block merges its channel's partials, then normalises (and activates) its planes.
+template <int ACT, int VW>
 __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restrict__ x, int B, int C, int L,
                                                             const int32_t* __restrict__ state,
                                                             const float* __restrict__ gamma,
@@ -223,7 +287,7 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
                                                             uint8_t* __restrict__ code) {
   __shared__ float st[2];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
-  const int bv = valid_count(state, B);
+  const int bv = valid_count(state, B), ppb = chan_ppb(B, L);
   if (threadIdx.x == 0) {
     double s0, s1;
     merge_parts(part, c, P, s0, s1);
@@ -245,19 +309,16 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
   }
   __syncthreads();
   const float mean = st[0], invstd = st[1], g = gamma[c], bb = beta[c];
+  const int b0 = p * ppb, b1 = min(B, b0 + ppb);  // every plane: the padded tail is written as 0
   if constexpr (ACT == 2) {
     // BN -> ReLU -> 2x2 max-pool: one pooled output per thread (4 BN values, first max wins,
     // code 4 = max <= 0), exactly relu_pool_fwd_kernel applied to the BN output
-    const int H = L / W, OH = H >> 1, OW = W >> 1, OL = OH * OW;
-    const unsigned total = (unsigned)(B * OL), chunk = (total + P - 1) / P;
-    const unsigned lo = p * chunk, hi = min(total, lo + chunk);
-    for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
-      const int b = (int)(t / (unsigned)OL), pl = (int)t - b * OL;
-      const int oy = pl / OW, ox = pl - oy * OW;
-      const int po = (b * C + c) * OL + pl;
+    const int H = L / W, OH = H >> 1, OW = W >> 1;
+    plane_walk<1>(b0, b1, C, c, OH * OW, [&](int b, int pl, int po) {
       float out = 0.f;
       uint8_t cd = 4;
       if (b < bv) {
+        const int oy = pl / OW, ox = pl - oy * OW;
         const float* xp = x + ((long)(b * C + c) * H + 2 * oy) * W + 2 * ox;
         float best = bn_affine(xp[0], mean, invstd, g, bb);
         int arg = 0;
@@ -271,16 +332,23 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
       }
       y[po] = out;
       code[po] = cd;
-    }
+    });
   } else {
-    const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
-    const unsigned lo = p * chunk, hi = min(total, lo + chunk);
-    for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
-      const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
-      const int o = (b * C + c) * L + l;
-      const float v = bn_affine(x[o], mean, invstd, g, bb);
-      y[o] = b < bv ? (ACT == 1 ? fmaxf(v, 0.f) : v) : 0.f;
-    }
+    plane_walk<VW>(b0, b1, C, c, L, [&](int b, int l, int o) {
+      float v[VW];
+      if (b < bv) {
+        ldv<VW>(x + o, v);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          v[j] = bn_affine(v[j], mean, invstd, g, bb);
+          if (ACT == 1) v[j] = fmaxf(v[j], 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) v[j] = 0.f;
+      }
+      stv<VW>(y + o, v);
+    });
   }
 }
 
@@ -296,7 +364,7 @@ __global__ void __launch_bounds__(LT) bn_fwd_eval_kernel(const float* __restrict
   y[i] = (x[i] - running_mean[c]) * rsqrtf(running_var[c] + eps) * gamma[c] + beta[c];
 }
 
-template <int ACT>
+template <int ACT, int VW>
 __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           int B, int C, int L, const int32_t* __restrict__ state,
                                                           const float* __restrict__ gamma,
@@ -307,7 +375,7 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
                                                           const double* __restrict__ part, ActArgs aa) {
   __shared__ float st[2];
   const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
-  const int bv = valid_count(state, B);
+  const int bv = valid_count(state, B), ppb = chan_ppb(B, L);
   if (threadIdx.x == 0) {
     double s0, s1;
     merge_parts(part, c, P, s0, s1);
@@ -322,15 +390,21 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
   __syncthreads();
   const float mdy = st[0], mdyx = st[1];
   const float mean = save_mean[c], invstd = save_invstd[c], g = gamma[c];
-  const unsigned total = (unsigned)(B * L), chunk = (total + P - 1) / P;
-  const unsigned lo = p * chunk, hi = min(total, lo + chunk);
-  for (unsigned t = lo + threadIdx.x; t < hi; t += LT) {
-    const int b = (int)(t / (unsigned)L), l = (int)t - b * L;  // 32-bit: B*C*L < 2^31 (host check)
-    const int o = (b * C + c) * L + l;
-    const float xv = x[o];
-    const float d = act_grad<ACT>(dy, aa, b, C, c, L, l, o, xv, mean, invstd, g);
-    dx[o] = b < bv ? g * invstd * (d - mdy - (xv - mean) * invstd * mdyx) : 0.f;
-  }
+  const int b0 = p * ppb, b1 = min(B, b0 + ppb);
+  plane_walk<VW>(b0, b1, C, c, L, [&](int b, int l, int o) {
+    float r[VW];
+    if (b < bv) {
+      float xv[VW], d[VW];
+      ldv<VW>(x + o, xv);
+      grad_in<ACT, VW>(dy, aa, b, C, c, l, o, xv, mean, invstd, g, d);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) r[j] = g * invstd * (d[j] - mdy - (xv[j] - mean) * invstd * mdyx);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) r[j] = 0.f;
+    }
+    stv<VW>(dx + o, r);
+  });
 }
 
 // per-channel sum of a [B][C][L] tensor (conv bias gradient): stage 2
@@ -418,33 +492,44 @@ void launch_relu_bwd(const float* dy, const float* y, long n, float* dx, hipStre
 }
 int chan_parts(int B, int L) { return chan_parts_of(B, L); }
 
+// float4 vectors when every plane row allows it (pool-routed gradients also need W % 4)
+static bool vec4_ok(int L, int W, int act, std::initializer_list<const void*> ptrs) {
+  if (L % 4 != 0 || (act == 2 && W % 4 != 0)) return false;
+  for (const void* p : ptrs)
+    if (p != nullptr && reinterpret_cast<uintptr_t>(p) % 16 != 0) return false;
+  return true;
+}
+template <int ACT, int VW>
+static void bn_fwd_launch(const float* x, int B, int C, int L, int W, const int32_t* state, const float* gamma,
+                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
+                          float* smean, float* sinvstd, double* part, hipStream_t s) {
+  const dim3 grid(chan_parts_of(B, L), C);
+  hipLaunchKernelGGL((chan_partial_kernel<0, 0, VW>), grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr,
+                     nullptr, part, nullptr, ActArgs{});
+  hipLaunchKernelGGL((bn_apply_train_kernel<ACT, VW>), grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m,
+                     rmean, rvar, y, smean, sinvstd, part, W, code);
+}
 void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
                          float* sinvstd, double* part, hipStream_t s) {
   if (!C) return;
-  const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL(chan_partial_kernel<0>, grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr, nullptr,
-                     part, nullptr, ActArgs{});
-  hipLaunchKernelGGL(bn_apply_train_kernel<0>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
-                     rvar, y, smean, sinvstd, part, 1, nullptr);
+  if (vec4_ok(L, 1, 0, {x, y}))
+    bn_fwd_launch<0, 4>(x, B, C, L, 1, state, gamma, beta, eps, m, rmean, rvar, y, nullptr, smean, sinvstd, part, s);
+  else
+    bn_fwd_launch<0, 1>(x, B, C, L, 1, state, gamma, beta, eps, m, rmean, rvar, y, nullptr, smean, sinvstd, part, s);
 }
 void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const int32_t* state, const float* gamma,
                              const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
                              float* smean, float* sinvstd, double* part, int act, hipStream_t s) {
   if (!C) return;
   const int L = H * W;
-  const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL(chan_partial_kernel<0>, grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr, nullptr,
-                     part, nullptr, ActArgs{});
-  if (act == 1)
-    hipLaunchKernelGGL(bn_apply_train_kernel<1>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
-                       rvar, y, smean, sinvstd, part, W, nullptr);
-  else if (act == 2)
-    hipLaunchKernelGGL(bn_apply_train_kernel<2>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
-                       rvar, y, smean, sinvstd, part, W, code);
-  else
-    hipLaunchKernelGGL(bn_apply_train_kernel<0>, grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m, rmean,
-                       rvar, y, smean, sinvstd, part, W, nullptr);
+  const bool v4 = vec4_ok(L, W, act == 2 ? 0 : act, {x, act == 2 ? nullptr : y});  // (pooled output: scalar)
+#define BN_FWD(A, V) bn_fwd_launch<A, V>(x, B, C, L, W, state, gamma, beta, eps, m, rmean, rvar, y, code, smean, \
+                                          sinvstd, part, s)
+  if (act == 1) { if (v4) BN_FWD(1, 4); else BN_FWD(1, 1); }
+  else if (act == 2) { if (v4) BN_FWD(2, 4); else BN_FWD(2, 1); }
+  else { if (v4) BN_FWD(0, 4); else BN_FWD(0, 1); }
+#undef BN_FWD
 }
 void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma, const float* beta, float eps,
                         const float* rmean, const float* rvar, float* y, hipStream_t s) {
@@ -452,41 +537,44 @@ void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma,
   if (n) hipLaunchKernelGGL(bn_fwd_eval_kernel, dim3(blocks(n)), dim3(LT), 0, s, x, B, C, L, gamma, beta, eps, rmean,
                             rvar, y);
 }
-void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
-                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
-                   hipStream_t s) {
-  if (!C) return;
-  const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL((chan_partial_kernel<1, 0>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd, part,
-                     gamma, ActArgs{});
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd, dx,
-                     dgamma, dbeta, part, ActArgs{});
-}
-template <int ACT>
+template <int ACT, int VW>
 static void bn_act_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                        const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
                        ActArgs aa, hipStream_t s) {
   const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL((chan_partial_kernel<1, ACT>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd,
+  hipLaunchKernelGGL((chan_partial_kernel<1, ACT, VW>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd,
                      part, gamma, aa);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<ACT>, grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean, sinvstd,
-                     dx, dgamma, dbeta, part, aa);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, VW>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean,
+                     sinvstd, dx, dgamma, dbeta, part, aa);
+}
+void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
+                   const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
+                   hipStream_t s) {
+  if (!C) return;
+  if (vec4_ok(L, 1, 0, {dy, x, dx}))
+    bn_act_bwd<0, 4>(dy, x, B, C, L, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, ActArgs{}, s);
+  else
+    bn_act_bwd<0, 1>(dy, x, B, C, L, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, ActArgs{}, s);
 }
 void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
                        const float* gamma, const float* beta, const float* smean, const float* sinvstd,
                        const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
                        hipStream_t s) {
   if (!C) return;
-  const ActArgs aa{beta, code, W};
-  if (act == 1) bn_act_bwd<1>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
-  else if (act == 2) bn_act_bwd<2>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
-  else bn_act_bwd<0>(dy, x, B, C, H * W, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s);
+  const int L = H * W;
+  const ActArgs aa{beta, code, W, H / 2};
+  const bool v4 = vec4_ok(L, W, act, {act == 2 ? nullptr : dy, x, dx});
+#define BN_BWD(A, V) bn_act_bwd<A, V>(dy, x, B, C, L, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s)
+  if (act == 1) { if (v4) BN_BWD(1, 4); else BN_BWD(1, 1); }
+  else if (act == 2) { if (v4) BN_BWD(2, 4); else BN_BWD(2, 1); }
+  else { if (v4) BN_BWD(0, 4); else BN_BWD(0, 1); }
+#undef BN_BWD
 }
 void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s) {
   if (!C) return;
   const int P = chan_parts_of(B, L);
-  hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(P, C), dim3(LT), 0, s, a, nullptr, B, C, L, nullptr, nullptr,
-                     nullptr, part, nullptr, ActArgs{});
+  hipLaunchKernelGGL((chan_partial_kernel<2, 0, 1>), dim3(P, C), dim3(LT), 0, s, a, nullptr, B, C, L, nullptr,
+                     nullptr, nullptr, part, nullptr, ActArgs{});
   hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, part, C, P, out);
 }
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
