@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
   }
 }
 
-template <bool BF16, int BM, int CCH>
+template <bool BF16, int BM, int CCH, bool V4>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
                                                             const typename PatchT<BF16, CCH>::T* __restrict__ wp,
                                                             const float* __restrict__ bias, float* __restrict__ y,
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
     aoff[i] = (tap * g.Mp + m0 + m) * g.Cp + u * VE;
     adst[i] = tid + i * CT < nv ? row * CCP + u * VE : dummy;
   }
-  {
+  if constexpr (!V4) {
     int row = row_t, xp = xp_t;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
@@ -421,8 +421,39 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       if (xp >= g.Wp) { xp -= g.Wp; ++row; }
     }
   }
+  // V4 (W % 4 == 0): the patch moves as float4 groups of 4 image pixels (4x fewer loads and
+  // offset computations - the scalar path's per-element address math was ~900 of the
+  // kernel's ~1000 VALU instructions per wave); the x-padding columns are zeroed once.
+  constexpr int PG = 6;               // float4 groups per thread in the register batch
+  const int G = g.W >> 2;             // groups per patch row
+  const int ng = V4 ? g.R * CCH * G : 0;
+  const unsigned gq0 = V4 ? (unsigned)tid / (unsigned)G : 0u;
+  const int gdq = V4 ? CT / G : 0, gdr = V4 ? CT - gdq * G : 0;
+  unsigned goff[PG];
+  int gdst[PG];
+  if constexpr (V4) {
+    unsigned row = gq0;
+    int gx = tid - (int)gq0 * G;
+#pragma unroll
+    for (int i = 0; i < PG; ++i) {
+      const unsigned r = row / CCH, c = row & (CCH - 1);
+      const int iy = iy0 + (int)r;
+      const bool ok = r < (unsigned)g.R && (unsigned)iy < (unsigned)g.H;
+      goff[i] = ok ? (unsigned)(((int)c * g.H + iy) * g.W + 4 * gx) * 4u : OOB;
+      gdst[i] = r < (unsigned)g.R ? (int)(Ps - As) + ((int)r * g.Wp + 4 * gx + g.pad) * CCP + (int)c : dummy;
+      gx += gdr; row += gdq;
+      if (gx >= G) { gx -= G; ++row; }
+    }
+    // x-padding columns: always zero, never written by the group loads
+    const int pc = g.Wp - g.W, nz = g.R * pc * CCH;
+    for (int e = tid; e < nz; e += CT) {
+      const int c = e % CCH, rp = e / CCH, r = rp / pc, k = rp - r * pc;
+      Ps[(r * g.Wp + (k < g.pad ? k : g.W + k)) * CCP + c] = (T)0.f;
+    }
+  }
   uint4 areg[AV];
   float preg[PV];
+  float4 greg[PG];
   auto p_val = [&](int row, int xp, int c0) {  // remainder path
     const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
     const bool ok = r < g.R && c0 + c < g.C && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
@@ -436,15 +467,39 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < AV; ++i) areg[i] = *reinterpret_cast<const uint4*>(wp + aoff[i] + c0);
     const unsigned cb = (unsigned)c0 * cstep;
+    if constexpr (V4) {
 #pragma unroll
-    for (int i = 0; i < PV; ++i)
-      preg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(poff[i] + cb), 0, 0));
+      for (int i = 0; i < PG; ++i)
+        greg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(goff[i] + cb), 0, 0));
+    } else {
+#pragma unroll
+      for (int i = 0; i < PV; ++i)
+        preg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(poff[i] + cb), 0, 0));
+    }
   };
   auto store_batch = [&](int c0) {
 #pragma unroll
     for (int i = 0; i < AV; ++i) *reinterpret_cast<uint4*>(As + adst[i]) = areg[i];
+    if constexpr (V4) {
 #pragma unroll
-    for (int i = 0; i < PV; ++i) As[pdst[i]] = (T)preg[i];
+      for (int i = 0; i < PG; ++i) {
+        As[gdst[i]] = (T)greg[i].x;
+        As[gdst[i] + CCP] = (T)greg[i].y;
+        As[gdst[i] + 2 * CCP] = (T)greg[i].z;
+        As[gdst[i] + 3 * CCP] = (T)greg[i].w;
+      }
+      for (int e = tid + PG * CT; e < ng; e += CT) {  // remainder groups
+        const int row = e / G, gx = e - row * G, r = row / CCH, c = row - r * CCH, iy = iy0 + r;
+        const bool ok = r < g.R && c0 + c < g.C && (unsigned)iy < (unsigned)g.H;
+        const float* src = x + ((long)(b * g.C + c0 + c) * g.H + iy) * g.W + 4 * gx;
+        T* dst = Ps + (r * g.Wp + 4 * gx + g.pad) * CCP + c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k * CCP] = (T)(ok ? src[k] : 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PV; ++i) As[pdst[i]] = (T)preg[i];
+    }
     // remainder beyond the register batch (large kernels / wide images only)
     for (int v = tid + AV * CT; v < nv; v += CT) {
       const int row = v / VPR, u = v - row * VPR;
@@ -452,7 +507,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       *reinterpret_cast<uint4*>(As + row * CCP + u * VE) =
           *reinterpret_cast<const uint4*>(wp + (tap * g.Mp + m0 + m) * g.Cp + u * VE + c0);
     }
-    for (int e = tid + PV * CT; e < np; e += CT) {
+    for (int e = V4 ? np : tid + PV * CT; e < np; e += CT) {
       const int row = e / g.Wp, xp = e - row * g.Wp;
       p_store(row, xp, p_val(row, xp, c0));
     }
@@ -529,7 +584,7 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
   int bm = M <= 16 ? 16 : 32;
   const int cch = bf ? 32 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
   const size_t es = bf ? 2 : 4, ccp = bf ? 40 : cch + 4;
-  auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp + 1) * ccp * es; };  // + dummy slot
+  auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp + 4) * ccp * es; };  // + dummy pixels
   if (lds_of(bm) > kPatchLdsMax && bm == 32) bm = 16;
   if (lds_of(bm) > kPatchLdsMax) return f;
   f.ok = true;
@@ -542,15 +597,22 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
   return f;
 }
 
+template <bool BF16, int CCH, bool V4>
+void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
+                   float* y, hipStream_t s) {
+  dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
+  if (f.bm == 16)
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+  else
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+  HIP_CHECK(hipGetLastError());
+}
+// float4 patch groups when image rows are whole 16-B vectors
 template <bool BF16, int CCH>
 void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                  float* y, hipStream_t s) {
-  dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
-  if (f.bm == 16)
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
-  else
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
-  HIP_CHECK(hipGetLastError());
+  if (f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) fast_launch_v<BF16, CCH, true>(f, wp, x, bias, y, s);
+  else fast_launch_v<BF16, CCH, false>(f, wp, x, bias, y, s);
 }
 
 template <bool BF16>
