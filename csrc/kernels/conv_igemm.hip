@@ -16,7 +16,10 @@
 //
 // Forward and dgrad run on an LDS-patch kernel (conv_fwd_patch_kernel, below) whenever its
 // tiles fit the LDS budget - every zoo layer does - and on the general gather kernel
-// otherwise.
+// otherwise.  Its weight images are packed once per step for all layers
+// (launch_conv_pack_all), and its input patch moves as float4 pixel groups when image rows
+// are whole 16-B vectors.  (An LDS-patch wgrad was measured and lost to the gather kernel
+// below: profiles/r1_wgrad_patch_experiment.txt.)
 //
 // Tiling: a workgroup (4 waves) owns a BM x 64 output tile (BM = 16/32/64 from M); wave w
 // owns columns [16 w, 16 w + 16) and all BM rows as BM/16 16x16 accumulators.  The
