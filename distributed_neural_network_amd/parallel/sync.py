@@ -97,7 +97,25 @@ def assert_replicas_identical(comm: Communicator, engine) -> None:
     a, b = replica_checksums(engine)
     sa, sb = comm.gather_scalars(a), comm.gather_scalars(b)
     if len(set(sa)) != 1 or len(set(sb)) != 1:
-        raise RuntimeError(f"replicas diverged: parameter checksums per rank {sa} / {sb}")
+        raise RuntimeError(f"replicas diverged: parameter checksums per rank {sa} / {sb}; "
+                           f"rank {comm.rank}: {_divergence_report(comm, engine)}")
+
+
+def _divergence_report(comm: Communicator, engine) -> str:
+    """Where this rank's arena differs from rank 0's (collective: every rank calls it)."""
+    mine = engine.master.detach().float().cpu()
+    ref = mine.clone()
+    try:
+        comm.broadcast_(ref, 0)
+    except Exception as e:  # diagnostics only
+        return f"(no report: {e})"
+    bad = (mine != ref).nonzero().flatten()
+    if bad.numel() == 0:
+        return "arena equals rank 0's"
+    i = int(bad[0])
+    same_multiset = bool(torch.equal(mine.sort().values, ref.sort().values))
+    return (f"{bad.numel()} of {mine.numel()} elements differ from rank 0, indices {int(bad[0])}..{int(bad[-1])}, "
+            f"first: {float(mine[i])} vs {float(ref[i])}, permutation of rank 0's values: {same_multiset}")
 
 
 class StepAllReduce(SyncPolicy):
