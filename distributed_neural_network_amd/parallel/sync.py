@@ -83,9 +83,11 @@ class SyncPolicy:
 
 def replica_checksums(engine) -> tuple[float, float]:
     """(sum, position-weighted sum) of the fp32 parameter arena in fp64: equal on two
-    ranks iff (with overwhelming probability) their arenas are bit-identical."""
-    m = engine.master.detach().double()
-    w = torch.arange(1, m.numel() + 1, device=m.device, dtype=torch.float64).remainder_(9973).add_(1)
+    ranks iff (with overwhelming probability) their arenas are bit-identical.  Computed on a
+    host copy: the check itself allocates no device temporaries (a GPU-side version once
+    reported a mismatch between bit-identical arenas: profiles/r1_xcd_map_experiment.txt)."""
+    m = engine.master.detach().to("cpu", torch.float64)
+    w = torch.arange(1, m.numel() + 1, dtype=torch.float64).remainder_(9973).add_(1)
     return float(m.sum()), float((m * w).sum())
 
 
