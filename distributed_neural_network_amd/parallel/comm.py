@@ -205,9 +205,16 @@ class Communicator:
         self.aborted = True
         try:
             pg = dist.distributed_c10d._get_default_group()
-            be = pg._get_backend(self.device) if self.backend == "nccl" else None
-            if be is not None and hasattr(be, "abort"):
-                be.abort()
+            if self.backend == "nccl":
+                be = pg._get_backend(self.device)
+                if be is not None and hasattr(be, "abort"):
+                    be.abort()
+            elif hasattr(pg, "abort"):
+                # gloo: close the pairs so a collective still pending on the dead peer (or on
+                # a survivor blocked the same way) fails now - destroy_process_group would
+                # otherwise wait for it up to the group timeout, and two survivors can each
+                # wait on the other's pending ring step
+                pg.abort()
         except Exception:
             pass
         try:

@@ -123,6 +123,15 @@ class Heartbeat:
         self._thread.join(timeout=2.0)
 
 
+def announce_alive(comm: Communicator) -> None:
+    """Mark this rank alive for generation g's agreement.  Called BEFORE tearing the broken
+    group down: destroying a gloo group can block until a collective pending on the dead
+    peer times out (~30 s), and a survivor that announced itself only afterwards used to
+    miss the agreement deadline and get excluded."""
+    assert comm.store is not None
+    comm.store.set(f"dnn/recover/{comm.generation}/alive/{comm.orig_rank}", "1")
+
+
 def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0) -> list[int]:
     """Survivors of generation g agree on the member list of generation g+1."""
     assert comm.store is not None

@@ -25,7 +25,7 @@ import torch
 
 from ..data import EpochSampler, get_splits
 from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
-from ..parallel.fault import DropInjector, Heartbeat, agree_survivors, simulate_failure
+from ..parallel.fault import DropInjector, Heartbeat, agree_survivors, announce_alive, simulate_failure
 from ..runtime import eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
 from ..utils.metrics import Run
@@ -115,6 +115,7 @@ class Trainer:
         # tear our side of the broken group down FIRST: closing its sockets/communicator
         # fails the collectives peers may still be blocked in on us (a gloo ring peer would
         # otherwise sit in recv until our reform, past the agreement deadline)
+        announce_alive(self.comm)
         self.comm.abort()
         members = agree_survivors(self.comm, self.hb)
         if self.comm.orig_rank not in members:
