@@ -155,3 +155,23 @@ def test_rank_drop_reforms_and_finishes(tmp_path, sync):
     assert "[fault] post-recovery epoch 1:" in r.stdout
     sd, side = checkpoint.load(str(tmp_path / "ck.pt"))
     assert side["epoch"] == 2 and side["world"] == 2
+
+
+def test_survivor_agreement_counts_early_announcements():
+    """A survivor that announced itself before tearing its group down (announce_alive) is in
+    the next generation even if it has not reached agree_survivors yet; a stale rank is not."""
+    import time
+    from types import SimpleNamespace
+
+    import torch.distributed as dist
+
+    from distributed_neural_network_amd.parallel.fault import agree_survivors, announce_alive
+
+    store = dist.TCPStore("127.0.0.1", 0, 1, is_master=True, wait_for_workers=False)
+    mk = lambda r: SimpleNamespace(store=store, generation=3, orig_rank=r, members=[0, 1, 2])
+    hb = SimpleNamespace(stale=lambda r: r == 2)
+    announce_alive(mk(1))  # rank 1 is still blocked in its group teardown
+    t0 = time.time()
+    assert agree_survivors(mk(0), hb, wait_s=5.0) == [0, 1]
+    assert time.time() - t0 < 2.0  # nobody undecided: no waiting for the deadline
+    assert agree_survivors(mk(1), hb, wait_s=5.0) == [0, 1]  # the late survivor reads the same list
