@@ -47,14 +47,17 @@ def _local(arena, data, idx, batch, epochs_orders, lr=0.05, momentum=0.9, reset=
     return eng
 
 
-def test_step_allreduce_equals_big_batch(tmp_path):
-    got = _run_worker(tmp_path, "step-allreduce", 2, n=192, batch=16, epochs=1)
-    assert torch.allclose(got[0], got[1], atol=0, rtol=0)  # replicas stay bitwise identical
+@pytest.mark.parametrize("world", [2, 4])
+def test_step_allreduce_equals_big_batch(tmp_path, world):
+    got = _run_worker(tmp_path, "step-allreduce", world, n=192, batch=16, epochs=1)
+    for r in range(1, world):
+        assert torch.allclose(got[0], got[r], atol=0, rtol=0)  # replicas stay bitwise identical
     data = synthetic(192, 3)
-    # single process, batch 32: step t takes shard0[16t:16t+16] + shard1[16t:16t+16]
-    order = np.concatenate([np.concatenate([np.arange(16 * t, 16 * t + 16), 96 + np.arange(16 * t, 16 * t + 16)])
-                            for t in range(6)]).astype(np.int32)
-    ref = _local(init_arena(seed=100), data, None, 32, [order])
+    # single process, batch 16 * world: step t takes shard_r[16t:16t+16] of every rank r
+    shard = 192 // world
+    order = np.concatenate([np.concatenate([shard * r + np.arange(16 * t, 16 * t + 16) for r in range(world)])
+                            for t in range(shard // 16)]).astype(np.int32)
+    ref = _local(init_arena(seed=100), data, None, 16 * world, [order])
     assert torch.allclose(got[0], ref.master, atol=2e-6), float((got[0] - ref.master).abs().max())
 
 
