@@ -1,5 +1,6 @@
 # A/B of the standalone grad_reduce work-group size (DNN_REDUCE_WAVES = 4, 2, 1 waves per group):
 # exactness tests, headline bench and per-kernel stats for each.  usage: bash tools/gpu_reduce_ab.sh
+# (the DNN_REDUCE_WAVES knob was reverted after this A/B: profiles/r1_reduce_wg_size_experiment.txt)
 set -e
 mkdir -p gpurun_out/rab
 R=$PWD
