@@ -145,15 +145,17 @@ def main():
     policy.initial_broadcast(engine)
     cur = EpochCursor(engine, sampler, policy, B)
 
-    # warmup: captures every chunk graph, runs W real steps
+    # untimed set-up: capture every chunk graph, first-call costs of the eval path (kernel,
+    # D2H, host ops), then the W warmup steps LAST, so the timed window starts on a busy,
+    # clocked-up GPU right behind them (a host-side gap here shows up in short runs)
     cur._next_epoch()
     engine.prepare_graphs()
-    cur.run(args.warmup)
-    if not args.no_epoch:  # first-call costs of the eval path (kernel, D2H, host ops) stay untimed
+    if not args.no_epoch:
         wl, wc = engine.evaluate_samples(test_dev, 0, len(test))
         wl2, wc2 = torch.zeros_like(wl), torch.zeros_like(wc, dtype=torch.float32)
         comm.allreduce_(wl2, "sum")
         eval_metrics(wl + wl2, wc.float() + wc2, B)
+    cur.run(args.warmup)
     comm.barrier()
     torch.cuda.synchronize(device)
 

@@ -27,6 +27,7 @@ void rccl_destroy(uintptr_t comm);
 std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
+std::string xgmi_device_id();
 void xgmi_free(uintptr_t p);
 std::pair<uintptr_t, uintptr_t> xgmi_abort_word();
 void xgmi_set_abort(uintptr_t host_word, unsigned v);
@@ -40,6 +41,8 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
 long long xgmi_slot_bytes(long long capacity);
 void xgmi_clear_slots(uintptr_t region, long long capacity);
 long long xgmi_flag_bytes(long long capacity);
+// runtime/graph_exec.cpp
+void graph_upload(uintptr_t exec, uintptr_t stream);
 }  // namespace dnn
 
 namespace py = pybind11;
@@ -253,6 +256,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("xgmi_open", [](py::bytes h) { return dnn::xgmi_open(std::string(h)); });
   m.def("xgmi_close", &dnn::xgmi_close);
+  m.def("xgmi_device_id", &dnn::xgmi_device_id);
+  m.def("graph_upload", &dnn::graph_upload, py::arg("exec"), py::arg("stream"));
   m.def("xgmi_free", &dnn::xgmi_free);
   m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
   m.def("xgmi_set_abort", &dnn::xgmi_set_abort);

@@ -235,6 +235,16 @@ uintptr_t xgmi_open(const std::string& handle) {
   return reinterpret_cast<uintptr_t>(p);
 }
 
+// physical identity of the current device ("domain:bus:device.function"): ranks that share
+// one GPU (single-GPU rehearsals) and ranks on distinct GPUs need different fence defaults
+std::string xgmi_device_id() {
+  int dev = 0;
+  xcheck(hipGetDevice(&dev), "hipGetDevice");
+  char buf[64] = {0};
+  xcheck(hipDeviceGetPCIBusId(buf, sizeof(buf) - 1, dev), "hipDeviceGetPCIBusId");
+  return std::string(buf);
+}
+
 void xgmi_close(uintptr_t p) {
   if (p) (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p));
 }

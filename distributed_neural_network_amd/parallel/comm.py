@@ -95,6 +95,55 @@ class Communicator:
                                 timeout=self.timeout, **kwargs)
         self.aborted = False
 
+    # -- liveness (fault.Heartbeat installs ``watch``) -------------------------------------
+    def lost(self) -> list[int]:
+        """Members the heartbeat watchdog has declared dead (original rank ids)."""
+        watch = self.watch
+        if watch is None:
+            return []
+        return sorted(set(watch()) & set(self.members))
+
+    def check_alive(self) -> None:
+        """Raise ``CommError`` on the calling (main) thread if a member was declared dead.
+
+        The watchdog thread only FLAGS a dead peer (and releases xGMI flag waits through the
+        host-mapped abort word); every teardown - ncclCommAbort, process-group destruction -
+        happens on the main thread in ``Trainer._recover``, never concurrently with a graph
+        replay or a collective the main thread is issuing."""
+        lost = self.lost()
+        if lost:
+            raise CommError(f"peer rank(s) {lost} lost (heartbeat stale)")
+
+    def wait_device(self, poll_s: float = 50e-6) -> None:
+        """Wait for this rank's queued GPU work without blocking uninterruptibly.
+
+        A collective whose peer died spins on the GPU until its communicator is aborted, so
+        ``torch.cuda.synchronize`` could block the main thread forever.  With a liveness
+        watch installed, the wait polls an event and raises ``CommError`` as soon as a member
+        is declared dead; the caller then aborts on this thread (``Trainer._recover``)."""
+        if self.device.type != "cuda":
+            return
+        if self.watch is None or not self.distributed:
+            torch.cuda.synchronize(self.device)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        while not ev.query():
+            self.check_alive()
+            time.sleep(poll_s)
+
+    def signal_lost(self) -> None:
+        """Watchdog-thread side of a peer loss: only thread-safe, non-blocking actions.  The
+        xGMI abort word is a host-mapped word that in-flight kernels poll - setting it
+        releases their bounded flag waits, so the GPU drains and the main thread's
+        ``wait_device`` returns or raises."""
+        xg = getattr(self, "xgmi", None)
+        if xg is not None:
+            try:
+                xg.abort()
+            except Exception:
+                pass
+
     # -- collectives ---------------------------------------------------------------------
     def _avg_op(self):
         return dist.ReduceOp.AVG if self.backend == "nccl" else None
@@ -172,6 +221,8 @@ class Communicator:
         t = torch.tensor([float(x)], dtype=torch.float64,
                          device=self.device if self.backend == "nccl" else "cpu")
         self.allreduce_(t, op)
+        if self.backend == "nccl":
+            self.wait_device()  # interruptible: the D2H read below would block on a dead peer
         return float(t.item())
 
     def gather_scalars(self, x: float) -> list[float]:
@@ -182,11 +233,16 @@ class Communicator:
         t = torch.zeros(self.world, dtype=torch.float64, device=dev)
         t[self.rank] = float(x)
         self.allreduce_(t, "sum")
+        if self.backend == "nccl":
+            self.wait_device()
         return [float(v) for v in t.cpu().tolist()]
 
     # -- fault handling --------------------------------------------------------------------
     def abort(self) -> None:
-        """Tear down the current communicator without waiting for peers."""
+        """Tear down the current communicator without waiting for peers.  Main thread only
+        (the watchdog thread calls ``signal_lost``): it aborts the native RCCL communicator
+        that captured step graphs use and destroys the process group, so nothing may be
+        replaying or issuing collectives concurrently."""
         xg = getattr(self, "xgmi", None)
         if xg is not None:
             try:

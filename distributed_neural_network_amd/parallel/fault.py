@@ -11,9 +11,12 @@ Capability parity:
       - ``DropInjector``: ``--drop-rank R --drop-at-epoch E [--drop-at-step S]`` makes
         rank R die hard (``os._exit``, no cleanup) at that point;
       - ``Heartbeat``: every rank stamps ``hb/<rank>`` in the rendezvous TCPStore from
-        a background thread; a watchdog marks a rank dead when its stamp goes stale
-        and aborts the communicator so nobody stays blocked in a collective (gloo
-        collectives also fail fast with a CommError on a closed peer socket);
+        a background thread; a watchdog marks a rank dead when its stamp goes stale.
+        The thread only flags it (and sets the xGMI abort word, which in-flight kernels
+        poll); the main thread notices between graph replays and in its interruptible
+        waits (``Communicator.check_alive`` / ``wait_device``), raises ``CommError`` and
+        aborts RCCL / the process group itself, so no teardown ever races a replay or a
+        collective (gloo collectives also fail fast on a closed peer socket);
       - ``agree_survivors``: the survivors agree on the new member list through the
         store (first survivor to win a compare_set is the leader and publishes it);
       - the trainer then re-forms the communicator over the survivors
@@ -110,10 +113,10 @@ class Heartbeat:
                     if r != self.comm.orig_rank and r not in self.dead and self.stale(r):
                         self.dead.add(r)
                         print(f"[fault] watchdog: rank {r} heartbeat stale > {self.timeout}s", flush=True)
-                        if self.comm.backend == "nccl":
-                            self.comm.abort()  # unblock collectives spinning on a dead peer
-                        elif getattr(self.comm, "xgmi", None) is not None:
-                            self.comm.xgmi.abort()  # xGMI flag waits (host collectives fail by themselves)
+                        # flag only: the main thread sees ``comm.lost()`` between graph
+                        # replays / in its interruptible waits and does every teardown
+                        # (ncclCommAbort, group destruction) itself in Trainer._recover
+                        self.comm.signal_lost()
             except Exception:
                 pass
 

@@ -22,7 +22,7 @@ from typing import Callable, Optional
 import torch
 
 from ..ops import native
-from .comm import Communicator, split_buckets
+from .comm import CommError, Communicator, split_buckets
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
@@ -46,19 +46,29 @@ class RcclComm:
         if c.rank == 0:
             c.store.set(key, self.ext.rccl_unique_id())
         uid = c.store.get(key)
-        self.handle = self.ext.rccl_init(uid, c.world, c.rank, c.device.index)
+        try:
+            self.handle = self.ext.rccl_init(uid, c.world, c.rank, c.device.index)
+        except RuntimeError as e:
+            raise CommError(f"ncclCommInitRank failed: {e}") from e
         self.generation = c.generation
 
     def allreduce_(self, t: torch.Tensor, op: str = "avg", stream: Optional[torch.cuda.Stream] = None) -> None:
         assert t.is_contiguous() and t.device.type == "cuda"
+        if not self.handle:
+            raise CommError("RCCL communicator was aborted (a peer was lost)")
         s = (stream or torch.cuda.current_stream(t.device)).cuda_stream
-        self.ext.rccl_allreduce(self.handle, t.data_ptr(), t.numel(), _DT[t.dtype],
-                                {"sum": 0, "avg": 1, "max": 2}[op], s)
+        try:
+            self.ext.rccl_allreduce(self.handle, t.data_ptr(), t.numel(), _DT[t.dtype],
+                                    {"sum": 0, "avg": 1, "max": 2}[op], s)
+        except RuntimeError as e:  # ncclAllReduce launch error (e.g. ncclRemoteError after a peer died)
+            raise CommError(f"ncclAllReduce failed: {e}") from e
 
     def healthy(self) -> bool:
         return self.handle != 0 and self.ext.rccl_async_error(self.handle) == 0
 
     def abort(self) -> None:
+        """ncclCommAbort: releases RCCL kernels spinning on a dead peer.  Main thread only
+        (Communicator.abort from Trainer._recover); never concurrent with a replay."""
         if self.handle:
             self.ext.rccl_abort(self.handle)
             self.handle = 0

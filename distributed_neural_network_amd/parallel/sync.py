@@ -21,7 +21,7 @@ import time
 
 import torch
 
-from .comm import Communicator, GradAllReduce
+from .comm import CommError, Communicator, GradAllReduce
 
 SYNC_MODES = ("step-allreduce", "epoch-avg", "parent")
 
@@ -55,7 +55,7 @@ class SyncPolicy:
         if buf is not None:
             self.comm.broadcast_(buf, src=0)
         engine.params_changed()
-        engine.synchronize()
+        self.comm.wait_device()
         self.comm_time += time.perf_counter() - t0
 
     def epoch_start(self, engine, epoch: int) -> None:
@@ -180,9 +180,16 @@ class StepAllReduce(SyncPolicy):
     lazy_check = False  # True: the caller checks the xGMI error word itself (bench: once, at the end)
 
     def epoch_end(self, engine, epoch: int) -> None:
-        check = getattr(engine.grad_sync, "check", None)
-        if check is not None and not self.lazy_check:
-            check()  # a timed-out / aborted xGMI wait surfaces here as a CommError (one D2H sync)
+        failed = getattr(engine.grad_sync, "failed", None)
+        if failed is not None and not self.lazy_check:
+            # a timed-out / aborted xGMI wait sets a sticky word on the rank that waited; the
+            # ranks agree on it (one tiny collective per epoch), so EVERY rank raises and
+            # enters recovery together - a late but live straggler included, which then
+            # counts as alive and the recovery becomes a retry, not an exclusion
+            votes = self.comm.gather_scalars(1.0 if failed() else 0.0)
+            if any(v != 0.0 for v in votes):
+                bad = [i for i, v in enumerate(votes) if v != 0.0]
+                raise CommError(f"xGMI all-reduce wait failed on rank(s) {bad} in epoch {epoch}")
         super().epoch_end(engine, epoch)
 
 
@@ -201,7 +208,7 @@ class EpochAverage(SyncPolicy):
         self.comm.allreduce_(engine.master, "avg")
         self.sync_buffers(engine)
         engine.params_changed()
-        engine.synchronize()
+        self.comm.wait_device()
         self.comm_time += time.perf_counter() - t0
 
 
@@ -230,7 +237,7 @@ class ParentAverage(EpochAverage):
             engine.master.div_(self.comm.world - 1)
         self.sync_buffers(engine, trainers_only=True)
         engine.params_changed()
-        engine.synchronize()
+        self.comm.wait_device()
         self.comm_time += time.perf_counter() - t0
 
 

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import itertools
 import os
+import socket
 import sys
 
 import torch
@@ -35,6 +36,20 @@ MAX_RANKS = 8
 _ids = itertools.count()
 
 
+def _local_world() -> int | None:
+    """Ranks on this node according to the launcher (torchrun, OpenMPI, MPICH/Intel MPI,
+    Slurm); None when no launcher says.  Only a hint: ``build_group`` decides single-node
+    from a hostname all-gather through the store, which every launcher supports."""
+    for name in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"):
+        v = os.environ.get(name)
+        if v:
+            return int(v)
+    v = os.environ.get("SLURM_NTASKS_PER_NODE", "")
+    if v.isdigit():
+        return int(v)
+    return None
+
+
 def wanted(comm: Communicator) -> bool:
     """xGMI path requested and applicable (DNN_ALLREDUCE=rccl forces RCCL)."""
     choice = os.environ.get("DNN_ALLREDUCE", "xgmi")
@@ -44,24 +59,40 @@ def wanted(comm: Communicator) -> bool:
         return False
     if comm.world > MAX_RANKS:
         return False
-    local = os.environ.get("LOCAL_WORLD_SIZE")
-    return local is None or int(local) == comm.env.world  # single node only
+    local = _local_world()
+    return local is None or local >= comm.env.world  # launcher says multi-node: RCCL
+
+
+def wait_timeout(comm: Communicator) -> float:
+    """Bound of one flag wait.  A live straggler (``--failure-duration`` sleeps before its
+    epoch) must not be mistaken for a dead peer: the bound covers the longest injected
+    sleep twice over, plus the base minute."""
+    return 60.0 + 2.0 * float(getattr(comm, "straggler_s", 0.0) or 0.0)
 
 
 class XgmiGroup:
     """IPC-mapped regions of every rank + the per-rank launch state."""
 
-    def __init__(self, comm: Communicator, capacity: int, timeout_s: float = 60.0) -> None:
+    def __init__(self, comm: Communicator, capacity: int, timeout_s: float | None = None,
+                 device_ids: list[str] | None = None) -> None:
         assert comm.store is not None
         self.comm = comm
         self.ext = native.hip()
         self.capacity = int(capacity)
-        self.timeout_s = float(timeout_s)
+        self.timeout_s = wait_timeout(comm) if timeout_s is None else float(timeout_s)
         self.rank, self.world = comm.rank, comm.world
         self.generation = comm.generation
-        dev = comm.device
         self.opened: list[int] = []
         self.local = 0
+        self.abort_host = 0
+        try:
+            self._setup(comm, device_ids)
+        except BaseException:
+            self.close()  # a half-built group must not leak peer mappings, its region or the abort word
+            raise
+
+    def _setup(self, comm: Communicator, device_ids: list[str] | None) -> None:
+        dev = comm.device
         self.abort_host, self.abort_dev = self.ext.xgmi_abort_word()
         nb = self.ext.xgmi_max_blocks(self.capacity)
         self.ctr = torch.zeros(nb + 1, device=dev, dtype=torch.int32)
@@ -92,11 +123,18 @@ class XgmiGroup:
                 regions.append(p)
         self.regions = regions
         # The shared bytes always move with sc0 sc1 (system-coherent) accesses, and the flag
-        # is stored only after the data stores were acknowledged.  In uncached (fine-grained)
-        # regions that is the whole hand-off; a cached fallback region also gets the
-        # system-scope release/acquire fences (bit 0 / bit 1; measured cost 0.6 us per step).
+        # is stored only after the data stores were acknowledged.  With every rank on ONE
+        # device and uncached regions that is the whole hand-off (measured on one MI355X with
+        # up to 8 ranks).  Across distinct GPUs the hand-off also gets the system-scope
+        # release/acquire fences (bit 0 / bit 1; measured cost 0.6 us per step) until a
+        # multi-GPU --check-sync run validates the fence-free variant there; a cached
+        # fallback region always gets them.  DNN_XGMI_FENCES overrides.
+        self.devices = len(set(device_ids)) if device_ids else 1
         fences = os.environ.get("DNN_XGMI_FENCES")
-        self.fences = int(fences) if fences is not None else (0 if self.kind == "uncached" else 3)
+        if fences is not None:
+            self.fences = int(fences)
+        else:
+            self.fences = 0 if (self.kind == "uncached" and self.devices == 1) else 3
 
     # -- launches --------------------------------------------------------------------------
     def handoff(self) -> dict:
@@ -127,6 +165,8 @@ class XgmiGroup:
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
+        if self.comm.watch is not None:
+            self.comm.wait_device()  # the D2H read below must not block on a stuck peer
         return bool(self.ctr[-1].item())
 
     def check(self) -> None:
@@ -176,11 +216,32 @@ class XgmiGroup:
             self.abort_host = 0
 
 
+def _topology(comm: Communicator) -> tuple[bool, list[str]]:
+    """Collective: (all ranks on this host?, physical device id per rank).  Every rank reads
+    every rank's entry, so all reach the same decision (no launcher variable needed)."""
+    assert comm.store is not None
+    key = f"dnn/xgmi/g{comm.generation}/topo{next(_ids)}"
+    try:
+        with torch.cuda.device(comm.device):
+            dev_id = native.hip().xgmi_device_id()
+    except Exception:
+        dev_id = f"?{comm.rank}"
+    comm.store.set(f"{key}/{comm.rank}", f"{socket.gethostname()}|{dev_id}")
+    entries = [comm.store.get(f"{key}/{r}").decode() for r in range(comm.world)]
+    hosts = {e.split("|", 1)[0] for e in entries}
+    return len(hosts) == 1, [e for e in entries]
+
+
 def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
     """Collective: every rank builds + self-tests the group, and all agree on the outcome."""
+    single_node, device_ids = _topology(comm)
+    if not single_node:
+        if comm.rank == 0:
+            print("[xgmi] ranks span several hosts: per-step all-reduce over RCCL", file=sys.stderr, flush=True)
+        return None
     grp, ok, why = None, True, ""
     try:
-        grp = XgmiGroup(comm, capacity)
+        grp = XgmiGroup(comm, capacity, device_ids=device_ids)
     except Exception as e:  # IPC export/import refused, etc.
         ok, why = False, f"{type(e).__name__}: {e}"
     # agree that every rank mapped every region BEFORE any rank launches a self-test
@@ -232,6 +293,9 @@ class XgmiGradSync:
 
     def check(self) -> None:
         self.group.check()
+
+    def failed(self) -> bool:
+        return self.group.failed()
 
 
 __all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "wanted"]

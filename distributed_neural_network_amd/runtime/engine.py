@@ -86,6 +86,11 @@ class Engine:
         self.grad_sync: GradSync | None = None
         self.train: Split | None = None
         self.order_len = 0
+        # liveness check between graph replays / steps (Trainer installs
+        # Communicator.check_alive): raises CommError on the main thread when the heartbeat
+        # watchdog has flagged a dead peer, instead of queueing more work behind a
+        # collective that can no longer complete
+        self.poll: Optional[Callable[[], None]] = None
 
     # -- parameters --------------------------------------------------------------------
     def state_dict(self):
@@ -136,6 +141,8 @@ class CpuEngine(Engine):
     def run_steps(self, n: int) -> None:
         assert self.train is not None
         for _ in range(n):
+            if self.poll is not None:
+                self.poll()
             lo = self._cursor * self.batch
             idx = torch.from_numpy(self._order[lo:lo + self.batch].astype(np.int64))
             self._cursor += 1
@@ -377,9 +384,12 @@ class HipEngine(Engine):
     def run_steps(self, n: int) -> None:
         if n <= 0:
             return
+        poll = self.poll
         if not self.use_graphs:
             with torch.cuda.device(self.device):
                 for _ in range(n):
+                    if poll is not None:
+                        poll()
                     self._launch_step()
             return
         # binary decomposition over power-of-two chunk graphs: <= log2(chunk)+n/chunk replays
@@ -388,6 +398,8 @@ class HipEngine(Engine):
             if reps:
                 g = self._graph(k)
                 for _ in range(reps):
+                    if poll is not None:
+                        poll()
                     g.replay()
 
     def epoch_stats(self, reset: bool = True) -> StepStats:

@@ -284,10 +284,13 @@ class LayerEngine(Engine):
     def run_steps(self, n: int) -> None:
         if n <= 0:
             return
+        poll = self.poll
         if not self.use_graphs:
             ctx = torch.cuda.device(self.device) if self.gpu else _Null()
             with ctx:
                 for _ in range(n):
+                    if poll is not None:
+                        poll()
                     self._launch_step()
             self.num_batches_tracked += n
             return
@@ -298,6 +301,8 @@ class LayerEngine(Engine):
             if reps:
                 g = self._graph(k)
                 for _ in range(reps):
+                    if poll is not None:
+                        poll()
                     g.replay()
             k //= 2
         self.num_batches_tracked += total

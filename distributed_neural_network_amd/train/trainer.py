@@ -59,6 +59,8 @@ class Trainer:
             # (the reference's anti-scaling mechanism, Project_Report.pdf p.3 §5.3)
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // self.env.world))
         self.comm = Communicator(self.env, self.device)
+        # longest injected straggler sleep: bounded collective waits must outlast it
+        self.comm.straggler_s = cfg.failure_duration if cfg.failure_probability > 0 else 0.0
         self.rank0 = self.comm.orig_rank == 0
         self.drop = DropInjector(cfg.drop_rank, cfg.drop_at_epoch, cfg.drop_at_step)
         self.hb: Optional[Heartbeat] = Heartbeat(self.comm) if self.comm.distributed else None
@@ -93,6 +95,7 @@ class Trainer:
             full[0, lo:hi] = loss.to(dev)
             full[1, lo:hi] = corr.to(dev).float()
             self.comm.allreduce_(full, "sum")
+            self.comm.wait_device()
             loss, corr = full[0], full[1]
         return eval_metrics(loss, corr, self.cfg.batch_size)
 
@@ -103,10 +106,10 @@ class Trainer:
         lim = self.drop.step_limit(self.comm.orig_rank, epoch)
         if lim is not None and lim <= n:
             self.engine.run_steps(lim)
-            self.engine.synchronize()
+            self.comm.wait_device()
             self.drop.die(self.comm.orig_rank, epoch, lim)
         self.engine.run_steps(n)
-        self.engine.synchronize()
+        self.comm.wait_device()  # interruptible: raises CommError if a peer is declared dead
 
     def _recover(self, epoch: int, snap: tuple[torch.Tensor, torch.Tensor], err: Exception) -> None:
         t0 = time.perf_counter()
@@ -138,9 +141,15 @@ class Trainer:
         self.recoveries.append(rec)
         self.rank0 = self.comm.rank == 0
         if self.comm.rank == 0:
-            print(f"[fault] rank(s) {dead} dropped in epoch {epoch}; communicator re-formed "
-                  f"(generation {self.comm.generation}, {self.comm.world} ranks) in {dt:.3f} s; "
-                  f"data re-partitioned, epoch restarted from the last consistent parameters", flush=True)
+            if dead:
+                print(f"[fault] rank(s) {dead} dropped in epoch {epoch}; communicator re-formed "
+                      f"(generation {self.comm.generation}, {self.comm.world} ranks) in {dt:.3f} s; "
+                      f"data re-partitioned, epoch restarted from the last consistent parameters", flush=True)
+            else:
+                # every member is alive (e.g. an xGMI wait timed out behind a straggler):
+                # a retry - fresh communicator generation, same members, epoch redone
+                print(f"[fault] collective failure in epoch {epoch} with every rank alive; communicator "
+                      f"re-created (generation {self.comm.generation}) in {dt:.3f} s, epoch retried", flush=True)
         self.run_log.record(event="recovery", **rec)
 
     # -- main ------------------------------------------------------------------------------
@@ -158,7 +167,7 @@ class Trainer:
             self.engine.attach(self.train)
             self.test = self.test.to(self.device)
             self.engine.synchronize()
-        self.timers._sync = self.engine.synchronize
+        self.timers._sync = self.comm.wait_device if self.comm.distributed else self.engine.synchronize
         self.policy = make_policy(c.sync if self.comm.distributed else "step-allreduce", self.comm,
                                   c.momentum_reset)
         if c.mode == "single":
@@ -166,6 +175,8 @@ class Trainer:
         self.policy.bucket_kb = c.bucket_kb
         self.policy.attach(self.engine)
         self.sampler = self._sampler()
+        if self.hb is not None:
+            self.engine.poll = self.comm.check_alive  # between graph replays (main thread)
 
         start_epoch = 0
         if c.resume:
@@ -214,9 +225,14 @@ class Trainer:
                     dev = self.device if self.comm.backend == "nccl" else torch.device("cpu")
                     tt = tot.to(dev)
                     self.comm.allreduce_(tt, "sum")
+                    self.comm.wait_device()
                     tot = tt.cpu()
                 self.timers.add(PhaseTimers.COMM_PARENT if self.rank0 else PhaseTimers.COMM_CHILDREN,
                                 time.perf_counter() - t0)
+                # evaluated inside the recovery scope (its metric all-reduce can meet a dead
+                # peer too); the lines are printed below in the reference's order
+                with self.timers.phase(PhaseTimers.EVAL):
+                    val_loss, val_acc = self._evaluate()
             except CommError as e:
                 if not self.comm.distributed or self.hb is None:
                     raise
@@ -235,8 +251,6 @@ class Trainer:
                 avg = loss_sum / (10.0 * trainers) if c.compat else loss_sum / max(batches, 1)
                 self._say(f"Global Average Training Loss: {avg}")
                 self._say("evaluating model")
-            with self.timers.phase(PhaseTimers.EVAL):
-                val_loss, val_acc = self._evaluate()
             if c.mode == "single":
                 print("Validation Accuracy: %.2f %%" % val_acc, flush=True)
                 print("Validation Loss: %.3f" % val_loss, flush=True)

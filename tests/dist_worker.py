@@ -12,8 +12,35 @@ from distributed_neural_network_amd.parallel import Communicator, make_policy  #
 from distributed_neural_network_amd.runtime import CpuEngine  # noqa: E402
 
 
+def failvote(out: str) -> None:
+    """Only rank 1's (fake) one-shot all-reduce reports a failed wait: the epoch-end vote must
+    raise CommError on EVERY rank, so all of them enter recovery together."""
+    from distributed_neural_network_amd.parallel import CommError
+
+    comm = Communicator(device="cpu")
+
+    class _Sync:
+        def failed(self):
+            return comm.rank == 1
+
+    eng = CpuEngine(batch=4, arena=init_arena(seed=0))
+    policy = make_policy("step-allreduce", comm)
+    policy.attach(eng)
+    eng.grad_sync = _Sync()
+    try:
+        policy.epoch_end(eng, 0)
+        raised = ""
+    except CommError as e:
+        raised = str(e)
+    with open(os.path.join(out, f"vote{comm.rank}.txt"), "w") as f:
+        f.write(raised)
+    comm.close()
+
+
 def main(mode: str, out: str, n: int, batch: int, epochs: int) -> None:
     torch.set_num_threads(1)
+    if mode == "failvote":
+        return failvote(out)
     comm = Communicator(device="cpu")
     data = synthetic(n, 3)
     eng = CpuEngine(batch=batch, lr=0.05, momentum=0.9, arena=init_arena(seed=comm.rank + 100))  # differ on purpose
