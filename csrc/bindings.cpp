@@ -10,6 +10,7 @@
 #include <vector>
 #include <string>
 
+#include "comm/xgmi_layout.h"
 #include "kernels/launchers.h"
 
 
@@ -32,15 +33,11 @@ void xgmi_free(uintptr_t p);
 std::pair<uintptr_t, uintptr_t> xgmi_abort_word();
 void xgmi_set_abort(uintptr_t host_word, unsigned v);
 void xgmi_free_abort_word(uintptr_t host_word);
-int xgmi_max_blocks(long long capacity);
-long long xgmi_region_bytes(long long capacity);
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
                            double timeout_s, int fences, int prepub, hipStream_t stream);
-long long xgmi_slot_bytes(long long capacity);
 void xgmi_clear_slots(uintptr_t region, long long capacity);
-long long xgmi_flag_bytes(long long capacity);
 // runtime/graph_exec.cpp
 void graph_upload(uintptr_t exec, uintptr_t stream);
 }  // namespace dnn
@@ -110,7 +107,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, u xg_region, long long xg_slot_bytes, long long xg_flag_bytes,
-                          u xg_ctr) {
+                          u xg_ctr, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
+                          u xp_err, u xp_abort, double xp_timeout_s, int xp_fences, float xp_scale) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -121,13 +119,34 @@ PYBIND11_MODULE(_dnn_hip, m) {
     a.xg_slot_bytes = xg_slot_bytes;
     a.xg_flag_bytes = xg_flag_bytes;
     a.xg_ctr = P<const unsigned>(xg_ctr);
+    if (!xp_regions.empty()) {
+      if ((int)xp_regions.size() > dnn::XG_MAX_RANKS || xp_rank < 0 || xp_rank >= (int)xp_regions.size())
+        throw std::runtime_error("grad_reduce exchange: 1..8 ranks, rank in range");
+      if (lo != 0 || hi < dnn::ARENA || xp_capacity < dnn::ARENA || !xp_ctr || !xp_err || !xp_abort)
+        throw std::runtime_error("grad_reduce exchange: whole arena, region capacity >= arena, counters set");
+      for (size_t r = 0; r < xp_regions.size(); ++r) a.xp_region[r] = P<unsigned char>(xp_regions[r]);
+      a.xp_rank = xp_rank;
+      a.xp_nranks = (int)xp_regions.size();
+      a.xp_ctr = P<unsigned>(xp_ctr);
+      a.xp_err = P<unsigned>(xp_err);
+      a.xp_abort = P<const unsigned>(xp_abort);
+      a.xp_timeout_ticks = (long long)(xp_timeout_s * 1.0e8);
+      a.xp_fences = xp_fences;
+      a.xp_scale = xp_scale;
+      a.xp_slot_bytes = dnn::xgmi_slot_bytes(xp_capacity);
+      a.xp_flag_bytes = dnn::xgmi_flag_bytes(xp_capacity);
+      a.xp_flag_off = dnn::xgmi_xp_flag_off(xp_capacity);
+    }
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
      py::arg("loss"), py::arg("correct"), py::arg("batch"), py::arg("master"), py::arg("grad"), py::arg("mom"),
      py::arg("shadow"), py::arg("state"), py::arg("stats"), py::arg("lr"), py::arg("momentum"),
      py::arg("grad_scale"), py::arg("fuse_sgd"), py::arg("lo"), py::arg("hi"), py::arg("bookkeeping"),
      py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
-     py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0);
+     py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0,
+     py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
+     py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
+     py::arg("xp_fences") = 3, py::arg("xp_scale") = 1.0f);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
@@ -265,6 +284,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_max_blocks", &dnn::xgmi_max_blocks);
   m.def("xgmi_region_bytes", &dnn::xgmi_region_bytes);
   m.def("xgmi_slot_bytes", &dnn::xgmi_slot_bytes);
+  m.def("xgmi_xp_max_blocks", []() { return dnn::XP_MAX_BLOCKS; });
+  m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
   m.def("xgmi_clear_slots", &dnn::xgmi_clear_slots);
   m.def("xgmi_flag_bytes", &dnn::xgmi_flag_bytes);
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,

@@ -34,11 +34,10 @@
 #include <string>
 
 #include "../kernels/common.h"
+#include "xgmi_layout.h"
 
 namespace dnn {
 
-constexpr int XG_MAX_RANKS = 8;
-constexpr int XG_CHUNK = 1024;  // elements per workgroup
 constexpr int XG_THREADS = 256;
 constexpr int XG_PER_THREAD = XG_CHUNK / XG_THREADS;  // 4
 
@@ -159,8 +158,8 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
     if (a.mode == 0) {
       a.out[e] = gr;
     } else {
-      const float m = a.momentum * m_old[k] + gr;
-      const float p = p_old[k] - a.lr * m;
+      float p, m;
+      sgd_update(gr, p_old[k], m_old[k], a.lr, a.momentum, p, m);
       a.mom[e] = m;
       a.master[e] = p;
       if (a.mode == 1) write_shadow(a.shadow, e, p);
@@ -175,19 +174,7 @@ namespace {
 void xcheck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
-long long round_up(long long x, long long m) { return (x + m - 1) / m * m; }
 }  // namespace
-
-int xgmi_max_blocks(long long capacity) { return (int)((capacity + XG_CHUNK - 1) / XG_CHUNK); }
-long long xgmi_flag_bytes(long long capacity) {
-  return round_up((long long)XG_MAX_RANKS * xgmi_max_blocks(capacity) * 4, 4096);
-}
-long long xgmi_slot_bytes(long long capacity) {
-  return round_up((long long)xgmi_max_blocks(capacity) * XG_CHUNK * 4, 4096);
-}
-long long xgmi_region_bytes(long long capacity) {
-  return xgmi_flag_bytes(capacity) + 2 * xgmi_slot_bytes(capacity);
-}
 
 // Allocates this rank's shared region (zeroed) and returns (device pointer, IPC handle
 // bytes, memory kind).  Uncached (fine-grained) memory first; plain device memory if the

@@ -79,6 +79,16 @@ __device__ __forceinline__ void write_shadow(bf16* __restrict__ sh, int e, float
   }
 }
 
+// momentum SGD (torch.optim.SGD, dampening 0): m <- momentum * m + g; p <- p - lr * m.
+// Both steps are explicit fmas, so every kernel that applies the update (batch reduction,
+// xGMI all-reduce, one-launch exchange) rounds identically and replicas stay bit-identical
+// whichever path produced them.
+__device__ __forceinline__ void sgd_update(float g, float p_old, float m_old, float lr, float momentum, float& p,
+                                           float& m) {
+  m = __builtin_fmaf(momentum, m_old, g);
+  p = __builtin_fmaf(-lr, m, p_old);
+}
+
 // ---- device step state (int32 words) -------------------------------------------------
 // [0] cursor: step index within the epoch (advanced by the reduce kernel)
 // [1] bvalid: valid samples of the current batch (written by the fused kernel)

@@ -1,6 +1,7 @@
 // Host-side launch API of the gfx950 kernels (used by csrc/bindings.cpp).
 #pragma once
 #include "common.h"
+#include "../comm/xgmi_layout.h"
 
 namespace dnn {
 
@@ -24,6 +25,21 @@ struct ReduceArgs {
   unsigned char* xg_region = nullptr;
   long long xg_slot_bytes = 0, xg_flag_bytes = 0;
   const unsigned* xg_ctr = nullptr;
+  // one-launch xGMI all-reduce (xp_nranks > 0; region layout: comm/xgmi_layout.h): every
+  // reduction block stores its reduced elements into this rank's slot, pushes a step flag
+  // for its block into every peer's flag table B, waits for the same block of every peer,
+  // sums the N values in rank order, scales by xp_scale and applies momentum SGD + the bf16
+  // images itself - the batch reduction and the all-reduce in ONE launch, with no hand-off
+  // between blocks of this GPU (each block exchanges exactly the elements it reduced).
+  unsigned char* xp_region[XG_MAX_RANKS] = {};
+  int xp_rank = 0, xp_nranks = 0;
+  unsigned* xp_ctr = nullptr;          // [XP_MAX_BLOCKS] per-block step counters (local)
+  unsigned* xp_err = nullptr;          // sticky error word (shared with the group's all-reduce kernel)
+  const unsigned* xp_abort = nullptr;  // host-mapped abort word (fault watchdog)
+  long long xp_timeout_ticks = 0;      // s_memrealtime ticks (100 MHz)
+  long long xp_slot_bytes = 0, xp_flag_bytes = 0, xp_flag_off = 0;
+  int xp_fences = 3;                   // bit 0: system release before the flag push, bit 1: acquire after
+  float xp_scale = 1.f;                // 1 / N
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
@@ -39,6 +55,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
+int grad_reduce_blocks();  // grid of a whole-arena grad_reduce launch (with bookkeeping)
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
                         hipStream_t stream);
 void launch_sgd_apply(float* master, const float* grad, float* mom, bf16* shadow, int n, float lr, float momentum,

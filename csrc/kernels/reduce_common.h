@@ -32,8 +32,8 @@ struct Src {
 __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs a) {
   g *= a.grad_scale;
   if (a.fuse_sgd) {
-    const float m = a.momentum * m_old + g;
-    const float p = p_old - a.lr * m;
+    float p, m;
+    sgd_update(g, p_old, m_old, a.lr, a.momentum, p, m);
     a.mom[e] = m;
     a.master[e] = p;
     write_shadow(a.shadow, e, p);
@@ -45,6 +45,28 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
   }
 }
 
+// Where a lane's reduced elements go (at most 4 per lane; j is a compile-time index once the
+// callers' loops are unrolled, so the exchange sink's arrays stay in registers).
+//  * DirectSink: finish at once (local SGD step, or gradient output).
+//  * XpSink (one-launch xGMI all-reduce, reduce_sgd.hip): the gradient goes to this rank's
+//    shared slot now (system-coherent store); the update runs after the block's exchange.
+struct DirectSink {
+  __device__ __forceinline__ void put(int, int e, float g, float p, float m, const ReduceArgs& a) {
+    sgd_finish(e, g, p, m, a);
+  }
+};
+struct XpSink {
+  unsigned* own;  // this rank's slot of the step
+  int e[4] = {0, 0, 0, 0};
+  float g[4] = {0.f, 0.f, 0.f, 0.f}, p[4], m[4];
+  bool v[4] = {false, false, false, false};
+  __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
+    g_ *= a.grad_scale;
+    e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
+    __hip_atomic_store(own + e_, __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+};
+
 // fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
 // output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).
 template <int LAYER> struct Fc;
@@ -55,8 +77,8 @@ constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
 constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
 constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
 
-template <int LAYER, bool COH>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
+template <int LAYER, bool COH, class Sink>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
   using L = Fc<LAYER>;
   const Src<COH> z(LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3), a.batch * L::ZLD);
   const Src<COH> x(LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2), a.batch * L::XLD);
@@ -100,8 +122,13 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + 4 * kq + j;
-    if (o < L::O && iv) sgd_finish(e[j], acc[j], pv[j], mv[j], a);
+    if (o < L::O && iv) sk.put(j, e[j], acc[j], pv[j], mv[j], a);
   }
+}
+template <int LAYER, bool COH>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
+  DirectSink d;
+  fc_tile<LAYER, COH>(t, a, d);
 }
 
 // Column sums (fc biases: sum_b z[b][o]; conv slab columns: sum_b slab[b][j]) with SPLIT = 4
@@ -132,8 +159,8 @@ __device__ __forceinline__ float column_sum_split(const Src<COH>& src, int ld, i
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
-template <bool COH>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
+template <bool COH, class Sink>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
@@ -147,7 +174,12 @@ __device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
   const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
   const float g = column_sum_split(src, ld, cc, a.batch, q);  // every lane shuffles: no early exit
-  if (t < FCB_SLOTS && col < n && q == 0) sgd_finish(dst, g, pv, mv, a);
+  if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
+}
+template <bool COH>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
+  DirectSink d;
+  fcb_task<COH>(t, a, d);
 }
 
 constexpr int CONV_ELEMS = SLAB;
@@ -158,14 +190,19 @@ __device__ __forceinline__ int conv_dst(int e) {
   if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
   return OFF_C2B + (e - SLAB_C2B);
 }
-template <bool COH>
-__device__ __forceinline__ void conv_task(int t, const ReduceArgs a) {
+template <bool COH, class Sink>
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs a, Sink& sk) {
   const Src<COH> src(a.slab, a.batch * SLAB);
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
   const float g = column_sum_split(src, SLAB, e, a.batch, q);
-  if (t < CONV_SLOTS && q == 0) sgd_finish(dst, g, pv, mv, a);
+  if (t < CONV_SLOTS && q == 0) sk.put(0, dst, g, pv, mv, a);
+}
+template <bool COH>
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs a) {
+  DirectSink d;
+  conv_task<COH>(t, a, d);
 }
 
 // Epoch statistics of the step that just ran + publication of the next step's cursor,

@@ -21,33 +21,117 @@ static_assert(RT % SPLIT == 0, "split column lanes stay inside a wave");
 
 
 
-__device__ __forceinline__ void grad_reduce_body(const ReduceArgs& a) {
-  // block roles: [MLP tile blocks][MLP bias block][conv element blocks][bookkeeping]
+// One launch's blocks: [MLP tile blocks][MLP bias blocks][conv element blocks][bookkeeping].
+// Returns true (block-uniform) when this block reduced arena elements.
+template <class Sink>
+__device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk) {
   const bool mlp = a.hi > OFF_F1W;
   const bool conv = a.lo < OFF_F1W;
   int blk = blockIdx.x;
   if (mlp) {
     if (blk < TILE_BLOCKS) {
       const int t = blk * 4 + (threadIdx.x >> 6);
-      if (t < FC_T0) fc_tile<0, false>(t, a);
-      else if (t < FC_T0 + FC_T1) fc_tile<1, false>(t - FC_T0, a);
-      else if (t < FC_TILES) fc_tile<2, false>(t - FC_T0 - FC_T1, a);
-      return;
+      if (t < FC_T0) fc_tile<0, false>(t, a, sk);
+      else if (t < FC_T0 + FC_T1) fc_tile<1, false>(t - FC_T0, a, sk);
+      else if (t < FC_TILES) fc_tile<2, false>(t - FC_T0 - FC_T1, a, sk);
+      return true;
     }
     blk -= TILE_BLOCKS;
     constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
     if (blk < FB) {
-      fcb_task<false>(blk * RT + threadIdx.x, a);
-      return;
+      fcb_task<false>(blk * RT + threadIdx.x, a, sk);
+      return true;
     }
     blk -= FB;
   }
   if (conv) {
     constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
-    if (blk < CB) { conv_task<false>(blk * RT + threadIdx.x, a); return; }
+    if (blk < CB) { conv_task<false>(blk * RT + threadIdx.x, a, sk); return true; }
     blk -= CB;
   }
   if (a.bookkeeping && blk == 0 && threadIdx.x < 64) bookkeeping<false>(a, threadIdx.x);
+  return false;
+}
+
+constexpr int GRAD_REDUCE_BLOCKS =
+    TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT + (CONV_SLOTS + RT - 1) / RT + 1;
+static_assert(GRAD_REDUCE_BLOCKS <= XP_MAX_BLOCKS, "exchange flag table B has a column per reduce block");
+int grad_reduce_blocks() { return GRAD_REDUCE_BLOCKS; }
+
+__device__ __forceinline__ unsigned xp_ld(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The one-launch all-reduce exchange of ONE block (same protocol as xgmi_allreduce_kernel,
+// per reduce block instead of per 1024-element slice):
+//   publish - the block's gradients are already in the own slot (XpSink::put, system-
+//             coherent stores); drain them, then push this block's step flag into EVERY
+//             peer's flag table B (remote stores; the peer polls locally);
+//   wait    - lanes 0..N-1 poll the N flags of this block (bounded: timeout / abort word ->
+//             sticky error word, never a hang);
+//   reduce  - every lane reads its elements from all N slots (7 links at once), sums in RANK
+//             ORDER (bit-identical replicas), scales by 1/N, applies momentum SGD + images.
+// Double buffering by step parity is safe for the same reason as in the slice kernel: block b
+// overwrites its elements of slot (s & 1) at step s + 2 only after every peer's block b
+// published step s + 1, which each does after finishing its step s reads of those elements.
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int par = step & 1u;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own slot stores acknowledged
+  __syncthreads();
+  if (tid < 64) {
+    if (a.xp_fences & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid < a.xp_nranks && tid != a.xp_rank) {
+      unsigned* flags = reinterpret_cast<unsigned*>(a.xp_region[tid] + a.xp_flag_off);
+      __hip_atomic_store(flags + a.xp_rank * XP_MAX_BLOCKS + b, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (tid < a.xp_nranks && tid != a.xp_rank && !failed) {
+    const unsigned* f = reinterpret_cast<const unsigned*>(a.xp_region[a.xp_rank] + a.xp_flag_off) +
+                        tid * XP_MAX_BLOCKS + b;
+    const long long t0 = wall_clock64();
+    int spins = 0;
+    while ((int)(xp_ld(f) - step) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255) == 0) {
+        if (wall_clock64() - t0 > a.xp_timeout_ticks || xp_ld(a.xp_abort) != 0u) {
+          __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+    }
+  }
+  if (tid < 64 && (a.xp_fences & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // every peer load in flight before the first use (invalid lanes read element 0: harmless)
+  float v[XG_MAX_RANKS][4];
+#pragma unroll
+  for (int r = 0; r < XG_MAX_RANKS; ++r) {
+    if (r < a.xp_nranks) {
+      const unsigned* src = reinterpret_cast<const unsigned*>(a.xp_region[r] + a.xp_flag_bytes + par * a.xp_slot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[r][j] = r == a.xp_rank ? sk.g[j] : __uint_as_float(xp_ld(src + sk.e[j]));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!sk.v[j]) continue;
+    float s = v[0][j];
+#pragma unroll
+    for (int r = 1; r < XG_MAX_RANKS; ++r)
+      if (r < a.xp_nranks) s += v[r][j];
+    const float gr = s * a.xp_scale;
+    float p, m;
+    sgd_update(gr, sk.p[j], sk.m[j], a.lr, a.momentum, p, m);
+    a.mom[sk.e[j]] = m;
+    a.master[sk.e[j]] = p;
+    write_shadow(a.shadow, sk.e[j], p);
+  }
+  __syncthreads();
+  if (tid == 0) a.xp_ctr[b] = step;
 }
 
 // diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
@@ -59,13 +143,25 @@ __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
   }
 }
 
-__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(ReduceArgs a) {
+__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(const ReduceArgs a) {
   reduce_stamp(a, 0);
-  if (a.xg_region != nullptr) {  // gradients -> the shared slot of the coming xGMI step
-    const unsigned step = a.xg_ctr[0] + 1u;
-    a.grad = reinterpret_cast<float*>(a.xg_region + a.xg_flag_bytes + (step & 1u) * a.xg_slot_bytes);
+  if (a.xp_nranks > 0) {  // one-launch all-reduce: reduce -> exchange -> SGD, per block
+    // (the arguments are only read on this path: the per-lane region index then reads the
+    //  kernel-argument segment directly instead of a private copy of the whole struct)
+    const unsigned step = a.xp_ctr[blockIdx.x] + 1u;
+    const bool failed = *a.xp_err != 0u;
+    XpSink sk;
+    sk.own = reinterpret_cast<unsigned*>(a.xp_region[a.xp_rank] + a.xp_flag_bytes + (step & 1u) * a.xp_slot_bytes);
+    if (grad_reduce_body(a, sk)) xp_exchange(a, sk, step, failed);
+  } else {
+    ReduceArgs d_args = a;
+    if (a.xg_region != nullptr) {  // gradients -> the shared slot of the coming xGMI step
+      const unsigned step = a.xg_ctr[0] + 1u;
+      d_args.grad = reinterpret_cast<float*>(a.xg_region + a.xg_flag_bytes + (step & 1u) * a.xg_slot_bytes);
+    }
+    DirectSink d;
+    grad_reduce_body(d_args, d);
   }
-  grad_reduce_body(a);
   if (a.stamps != nullptr) __syncthreads();
   reduce_stamp(a, 1);
 }
@@ -79,8 +175,8 @@ __global__ void __launch_bounds__(RT) sgd_apply_kernel(float* __restrict__ maste
   for (int e = blockIdx.x * RT + threadIdx.x; e < n; e += gridDim.x * RT) {
     float p = master[e];
     if (!pack_only) {
-      const float m = momentum * mom[e] + grad[e] * grad_scale;
-      p -= lr * m;
+      float m;
+      sgd_update(grad[e] * grad_scale, p, mom[e], lr, momentum, p, m);
       mom[e] = m;
       master[e] = p;
     }
@@ -121,6 +217,10 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
   if (conv) nblk += (CONV_SLOTS + RT - 1) / RT;
   if (args.bookkeeping) nblk += 1;
   if (nblk == 0) return;
+  // the exchange waits on the same block of every peer: every block must be resident at once
+  // (<= XP_MAX_BLOCKS blocks of RT threads, one per CU of the 256) and take the whole arena
+  if (args.xp_nranks > 0 && (nblk > XP_MAX_BLOCKS || !mlp || !conv))
+    throw std::runtime_error("grad_reduce exchange needs the whole-arena grid");
   hipLaunchKernelGGL(grad_reduce_kernel, dim3(nblk), dim3(RT), 0, stream, args);
   HIP_CHECK(hipGetLastError());
 }

@@ -129,9 +129,20 @@ class StepAllReduce(SyncPolicy):
             engine.grad_sync = None
         elif (xg := self._xgmi_group(engine)) is not None:
             # GPU hot path on one node: one-shot xGMI all-reduce fused with the optimizer
-            from .xgmi import XgmiGradSync
+            from .xgmi import XgmiGradSync, one_launch_wanted
 
             engine.grad_sync = XgmiGradSync(xg)
+            xg.one_launch = False
+            if one_launch_wanted() and hasattr(engine, "selftest_exchange"):
+                # batch reduction + all-reduce + SGD in ONE launch, once it has matched the
+                # two-launch path bit for bit on every rank (all ranks get the same vote)
+                xg.one_launch = engine.selftest_exchange(xg, self.comm)
+                if not xg.one_launch and self.comm.rank == 0:
+                    import sys
+
+                    print("[xgmi] one-launch exchange self-test failed: two-launch all-reduce", file=sys.stderr,
+                          flush=True)
+                engine.invalidate_graphs()
         elif self.comm.backend == "nccl":
             # GPU hot path: native RCCL communicator, all-reduce launched on the engine stream
             from .rccl import NativeGradAllReduce, RcclComm

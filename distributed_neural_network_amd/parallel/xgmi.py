@@ -63,6 +63,14 @@ def wanted(comm: Communicator) -> bool:
     return local is None or local >= comm.env.world  # launcher says multi-node: RCCL
 
 
+def one_launch_wanted() -> bool:
+    """The fused engine's one-launch exchange (DNN_XGMI_ONE_LAUNCH=0 keeps two launches)."""
+    v = os.environ.get("DNN_XGMI_ONE_LAUNCH", "1")
+    if v not in ("0", "1"):
+        raise ValueError(f"DNN_XGMI_ONE_LAUNCH must be 0 or 1, not {v!r}")
+    return v == "1"
+
+
 def wait_timeout(comm: Communicator) -> float:
     """Bound of one flag wait.  A live straggler (``--failure-duration`` sleeps before its
     epoch) must not be mistaken for a dead peer: the bound covers the longest injected
@@ -95,7 +103,12 @@ class XgmiGroup:
         dev = comm.device
         self.abort_host, self.abort_dev = self.ext.xgmi_abort_word()
         nb = self.ext.xgmi_max_blocks(self.capacity)
-        self.ctr = torch.zeros(nb + 1, device=dev, dtype=torch.int32)
+        self.ctr = torch.zeros(nb + 1, device=dev, dtype=torch.int32)  # [per-slice steps | error word]
+        # per-block step counters of the one-launch exchange inside grad_reduce (flag table B)
+        self.xp_ctr = torch.zeros(self.ext.xgmi_xp_max_blocks(), device=dev, dtype=torch.int32)
+        # set once the exchange matched the two-launch path bit for bit on every rank
+        # (HipEngine.selftest_exchange, run by the step-allreduce policy)
+        self.one_launch = False
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
         # on a key that never comes
@@ -142,6 +155,19 @@ class XgmiGroup:
         rank's shared slot (then ``allreduce_sgd(..., prepublished=True)``)."""
         return dict(xg_region=self.local, xg_slot_bytes=self.ext.xgmi_slot_bytes(self.capacity),
                     xg_flag_bytes=self.ext.xgmi_flag_bytes(self.capacity), xg_ctr=self.ctr.data_ptr())
+
+    def exchange(self) -> dict:
+        """grad_reduce kwargs of the one-launch all-reduce: every reduction block publishes its
+        reduced elements, exchanges them with the same block of every peer and applies the
+        averaged update itself (no separate all-reduce launch, no hand-off inside the GPU)."""
+        err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
+        return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
+                    xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
+                    xp_timeout_s=self.timeout_s, xp_fences=self.fences, xp_scale=1.0 / self.world)
+
+    def clear_error(self) -> None:
+        """Reset the sticky error word (only after every rank's kernels have drained)."""
+        self.ctr[-1].zero_()
 
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, mom: torch.Tensor, shadow: torch.Tensor | None,
                       lr: float, momentum: float, n: int | None = None, prepublished: bool = False) -> None:
@@ -298,4 +324,4 @@ class XgmiGradSync:
         return self.group.failed()
 
 
-__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "wanted"]
+__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "one_launch_wanted", "wanted"]

@@ -24,6 +24,8 @@ epoch ends.
 """
 from __future__ import annotations
 
+import os
+import sys
 from dataclasses import dataclass
 from typing import Callable, Optional, Protocol
 
@@ -334,9 +336,15 @@ class HipEngine(Engine):
             self._reduce(1, 0, LAYOUT.total, 1, s)
             return
         if getattr(self.grad_sync, "fuses_sgd", False):
-            # one-shot xGMI all-reduce: batch reduction -> [publish, 1 hop, rank-order sum,
-            # momentum SGD, bf16 weight images] in ONE launch (parallel/xgmi.py)
             grp = self.grad_sync.group
+            if grp.one_launch:
+                # one-launch all-reduce: each reduction block reduces its elements over the
+                # batch, exchanges them with the same block of every peer over xGMI (1 hop)
+                # and applies the averaged momentum-SGD update + bf16 images itself
+                self._reduce(1, 0, LAYOUT.total, 1, s, **grp.exchange())
+                return
+            # two launches: batch reduction -> shared slot; one-shot xGMI all-reduce kernel
+            # [flags, 1 hop, rank-order sum, momentum SGD, bf16 weight images] (parallel/xgmi.py)
             self._reduce(0, 0, LAYOUT.total, 1, s, **grp.handoff())  # reduced grads -> shared slot
             grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum, LAYOUT.total,
                               prepublished=True)
@@ -354,8 +362,65 @@ class HipEngine(Engine):
         self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
                            LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
 
+    def selftest_exchange(self, grp, comm, steps: int = 2) -> bool:
+        """Collective: does the one-launch all-reduce (``grp.exchange()``) reproduce the
+        two-launch path (reduce -> shared slot, xGMI all-reduce kernel) BIT FOR BIT on every
+        rank?  Random per-rank reduction inputs, both parity slots; the engine's parameters,
+        optimizer state and buffers are restored afterwards.  Every rank returns the same vote."""
+        dev = self.device
+        bufs = [self.a0, self.h1, self.h2, self.z1, self.z2, self.z3, self.slab]
+        saved = [t.clone() for t in bufs + [self.master, self.mom, self.shadow]]
+        gen = torch.Generator().manual_seed(1009 + 7 * comm.rank)
+        with torch.no_grad():
+            for t in bufs:
+                t.copy_(torch.randn(t.shape, generator=gen))
+            # arena padding stays zero, as in training (the two-launch kernel updates every
+            # element of its slices, the exchange only the real parameters)
+            real = LAYOUT.pad_mask().float()
+            p0 = (torch.randn(self.master.shape, generator=torch.Generator().manual_seed(3)) * 0.1 * real).to(dev)
+            m0 = (torch.randn(self.master.shape, generator=torch.Generator().manual_seed(4)) * 0.01 * real).to(dev)
+        results, err = [], False
+        timeout, grp.timeout_s = grp.timeout_s, min(grp.timeout_s, 10.0)
+        for one_launch in (False, True):
+            if not err:
+                try:
+                    with torch.cuda.device(dev):
+                        self.master.copy_(p0)
+                        self.mom.copy_(m0)
+                        self.params_changed()
+                        s = self._stream()
+                        for _ in range(steps):
+                            if one_launch:
+                                self._reduce(1, 0, LAYOUT.total, 0, s, **grp.exchange())
+                            else:
+                                self._reduce(0, 0, LAYOUT.total, 0, s, **grp.handoff())
+                                grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
+                                                  self.momentum, LAYOUT.total, prepublished=True)
+                        torch.cuda.synchronize(dev)
+                        results.append((self.master.cpu(), self.mom.cpu(), self.shadow.cpu()))
+                except Exception as e:
+                    err = True
+                    why = f"{type(e).__name__}: {e}"
+            comm.gather_scalars(0.0)  # (every rank) done with these slots before they are reused
+        grp.timeout_s = timeout
+        ok = not err and not grp.failed() and all(torch.equal(x, y) for x, y in zip(*results))
+        if not ok and os.environ.get("DNN_DEBUG_XGMI") == "1":
+            if not err:
+                why = "wait failed" if grp.failed() else "mismatch in " + str(
+                    [name for name, (x, y) in zip(("master", "mom", "shadow"), zip(*results)) if not torch.equal(x, y)])
+            print(f"[xgmi] rank {comm.rank}: exchange self-test: {why}", file=sys.stderr, flush=True)
+        votes = comm.gather_scalars(1.0 if ok else 0.0)
+        if not all(v == 1.0 for v in votes):
+            grp.clear_error()  # the two-launch path must not inherit a failed wait of this test
+        with torch.no_grad():
+            for t, v in zip(bufs + [self.master, self.mom, self.shadow], saved):
+                t.copy_(v)
+        torch.cuda.synchronize(dev)
+        return all(v == 1.0 for v in votes)
+
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, self.grad_sync is not None, self.overlap, self.in_launch_reduce, self.order_len)
+        key = (nsteps, self.grad_sync is not None, self.overlap, self.in_launch_reduce, self.order_len,
+               getattr(getattr(self.grad_sync, "group", None), "one_launch", None))
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.

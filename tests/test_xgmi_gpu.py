@@ -21,8 +21,9 @@ def _py(code, env_extra, timeout=300):
 
 
 def test_xgmi_one_rank_matches_local_sgd():
-    """World size 1 with forced collectives: batch reduce -> xGMI kernel (publish, flag,
-    gather, SGD + bf16 images) must reproduce the fused local-SGD step bitwise."""
+    """World size 1 with forced collectives: the one-launch exchange (grad_reduce publishes,
+    flags, gathers, applies SGD + bf16 images) and the two-launch path (batch reduce -> xGMI
+    kernel) must both reproduce the fused local-SGD step bitwise."""
     code = r'''
 import numpy as np, torch
 from distributed_neural_network_amd.data import synthetic
@@ -35,7 +36,10 @@ comm = Communicator(device=torch.device("cuda", 0))
 data = synthetic(1000, 5)
 a = init_arena(seed=9)
 res = []
-for sync_on, graphs, inl in [(False, True, False), (True, True, False), (True, False, False), (True, True, True)]:
+import os
+for sync_on, graphs, inl, one in [(False, True, False, "1"), (True, True, False, "1"), (True, False, False, "1"),
+                                  (True, True, True, "1"), (True, True, False, "0")]:
+    os.environ["DNN_XGMI_ONE_LAUNCH"] = one
     eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, in_launch_reduce=inl)
     pol = make_policy("step-allreduce", comm)
     pol.attach(eng)
@@ -43,6 +47,7 @@ for sync_on, graphs, inl in [(False, True, False), (True, True, False), (True, F
         eng.grad_sync = None
     else:
         assert isinstance(eng.grad_sync, XgmiGradSync), type(eng.grad_sync)
+        assert eng.grad_sync.group.one_launch == (one == "1"), "exchange self-test failed"
     eng.attach(data); eng.begin_epoch(np.arange(1000, dtype=np.int32)); eng.run_steps(16)
     torch.cuda.synchronize()
     if sync_on:
@@ -81,16 +86,18 @@ for ep in range(2):
     eng.synchronize()
     pol.epoch_end(eng, ep)
 kind = type(eng.grad_sync).__name__
-torch.save({"master": eng.master.cpu(), "kind": kind}, os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
+one = bool(getattr(getattr(eng.grad_sync, "group", None), "one_launch", False))
+torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one},
+           os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
 comm.close()
 '''
 
 
-def _two_ranks(tmp_path, allreduce, graphs, port):
-    out = tmp_path / allreduce
+def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1"):
+    out = tmp_path / f"{allreduce}{one_launch}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
-               OUT=str(out), GRAPHS=graphs)
+               OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch)
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -102,13 +109,19 @@ def _two_ranks(tmp_path, allreduce, graphs, port):
 
 
 def test_xgmi_two_ranks_match_host_allreduce(tmp_path):
-    """2 ranks on the box's GPU: the IPC one-shot all-reduce + fused SGD keeps the replicas
-    bit-identical and matches the gloo all-reduce + sgd_apply path."""
+    """2 ranks on the box's GPU: the one-launch exchange (reduce + xGMI all-reduce + SGD in
+    grad_reduce) keeps the replicas bit-identical, equals the two-launch path bit for bit and
+    matches the gloo all-reduce + sgd_apply path."""
     import torch
 
     xg, r = _two_ranks(tmp_path, "xgmi", "1", 29641)
     assert xg[0]["kind"] == "XgmiGradSync", r.stderr[-2000:]
+    assert xg[0]["one_launch"] and xg[1]["one_launch"], r.stderr[-2000:]  # exchange self-test passed
     assert torch.equal(xg[0]["master"], xg[1]["master"])
+    # the two-launch path (reduce -> slot, all-reduce kernel) gives the same bits
+    two, r2 = _two_ranks(tmp_path, "xgmi", "1", 29645, one_launch="0")
+    assert two[0]["kind"] == "XgmiGradSync" and not two[0]["one_launch"], r2.stderr[-2000:]
+    assert torch.equal(two[0]["master"], xg[0]["master"]) and torch.equal(two[1]["master"], xg[1]["master"])
     host, _ = _two_ranks(tmp_path, "rccl", "0", 29643)  # DNN_BACKEND=gloo: host all-reduce, eager
     assert host[0]["kind"] == "GradAllReduce"
     assert torch.equal(host[0]["master"], host[1]["master"])
