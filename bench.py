@@ -9,8 +9,9 @@ with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step
     python bench.py [--gpus N] [--steps K] [--warmup W] [--sync step-allreduce|epoch-avg]
 
 Synchronisation defaults to a per-step gradient all-reduce inside the step hipGraph: on
-one node the one-shot xGMI all-reduce kernel fused with the SGD update (every rank reads
-all peers' 248 KB gradients over the xGMI mesh in one hop; parallel/xgmi.py), or native
+one node a one-hop exchange over the xGMI mesh inside the batch-reduction kernel, fused with
+the SGD update (every reduction block reads the same block of all peers' gradients;
+parallel/xgmi.py, kernels/reduce_sgd.hip), or native
 RCCL (DNN_ALLREDUCE=rccl, multi-node, or if the xGMI self-test fails).  --sync epoch-avg runs the reference algorithm
 (data_parallelism_train.py:185-254): local SGD over the rank's shard with a fresh momentum
 buffer per epoch and an RCCL parameter all-reduce at every epoch end (epoch boundaries fall
@@ -70,12 +71,17 @@ class EpochCursor:
 
 
 def _allreduce_kind(engine) -> str | None:
-    """Which per-step gradient all-reduce ran: xgmi (one-shot IPC kernel fused with SGD),
-    rccl (native ncclAllReduce), torch-pg (host process group), or None (one rank)."""
+    """Which per-step gradient all-reduce ran: xgmi-one-launch (the batch-reduction kernel
+    exchanges its blocks over xGMI and applies SGD), xgmi-two-launch (reduction, then the
+    one-shot IPC all-reduce kernel fused with SGD), rccl (native ncclAllReduce), torch-pg
+    (host process group), or None (one rank)."""
     gs = getattr(engine, "grad_sync", None)
     if gs is None:
         return None
-    return {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
+    kind = {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
+    if kind == "xgmi":  # one launch: batch reduction + exchange + SGD in grad_reduce
+        kind = "xgmi-one-launch" if gs.group.one_launch else "xgmi-two-launch"
+    return kind
 
 
 def _reserve_stdout() -> int:

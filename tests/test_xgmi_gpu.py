@@ -139,4 +139,4 @@ def test_bench_two_ranks_xgmi(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
-    assert out["n_gpus"] == 2 and out["config"]["allreduce"] == "xgmi", out
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] == "xgmi-one-launch", out
