@@ -65,17 +65,18 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("fused_train",
         [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
-           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
+           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage) {
           dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order),
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
-                                  P<long long>(stamps), nullptr, nullptr, S(stream));
+                                  P<long long>(stamps), nullptr, nullptr, P<const int32_t>(next_ids),
+                                  P<unsigned char>(stage), S(stream));
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
-        py::arg("stream"), py::arg("stamps") = 0);
+        py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0);
   // fused training step WITH the in-launch reducer workgroups (batch reduction + SGD)
   m.def("fused_train_reduce",
         [](u images, u labels, u batch_ids, int batch, u state, u master, u shadow, u a0, u h1, u h2, u z1, u z2,
@@ -90,7 +91,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
-                                  P<long long>(stamps), &r, P<unsigned>(sync), S(stream));
+                                  P<long long>(stamps), &r, P<unsigned>(sync), nullptr, nullptr, S(stream));
         },
         py::arg("images"), py::arg("labels"), py::arg("batch_ids"), py::arg("batch"), py::arg("state"),
         py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"),
@@ -108,7 +109,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, u xg_region, long long xg_slot_bytes, long long xg_flag_bytes,
                           u xg_ctr, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
-                          u xp_err, u xp_abort, double xp_timeout_s, int xp_fences, float xp_scale) {
+                          u xp_err, u xp_abort, double xp_timeout_s, int xp_fences, float xp_scale, u next_ids) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -119,6 +120,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     a.xg_slot_bytes = xg_slot_bytes;
     a.xg_flag_bytes = xg_flag_bytes;
     a.xg_ctr = P<const unsigned>(xg_ctr);
+    a.next_ids = P<int32_t>(next_ids);
     if (!xp_regions.empty()) {
       if ((int)xp_regions.size() > dnn::XG_MAX_RANKS || xp_rank < 0 || xp_rank >= (int)xp_regions.size())
         throw std::runtime_error("grad_reduce exchange: 1..8 ranks, rank in range");
@@ -146,7 +148,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
-     py::arg("xp_fences") = 3, py::arg("xp_scale") = 1.0f);
+     py::arg("xp_fences") = 3, py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
@@ -295,10 +297,13 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
                                P<const unsigned>(abort_w), timeout_s, fences, prepub, S(stream));
   });
-  m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream) {
+  m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream, u images, u labels,
+                          u next_ids, u stage) {
     dnn::launch_epoch_begin(P<const int32_t>(staged), P<int32_t>(order), n, P<int32_t>(state), P<int32_t>(batch_ids),
-                            batch, S(stream));
-  });
+                            batch, P<const uint8_t>(images), P<const int32_t>(labels), P<int32_t>(next_ids),
+                            P<unsigned char>(stage), S(stream));
+  }, py::arg("staged"), py::arg("order"), py::arg("n"), py::arg("state"), py::arg("batch_ids"), py::arg("batch"),
+     py::arg("stream"), py::arg("images") = 0, py::arg("labels") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0);
   m.def("sgd_apply", [](u master, u grad, u mom, u shadow, int n, float lr, float momentum, float grad_scale,
                         int pack_only, u stream) {
     dnn::launch_sgd_apply(P<float>(master), P<const float>(grad), P<float>(mom), P<bf16>(shadow), n, lr, momentum,

@@ -18,6 +18,8 @@ struct ReduceArgs {
   int lo, hi;     // arena element range [lo, hi) handled by this launch (gradient bucket)
   int bookkeeping;  // 1: this launch also advances the cursor / epoch statistics
   long long* stamps = nullptr;  // diagnostic: per-block [start, end] s_memrealtime (grad_reduce)
+  int32_t* next_ids = nullptr;  // bookkeeping: also publish the sample ids TWO steps ahead (-1: none),
+                                // read by the fused kernel's image staging
   // one-shot xGMI all-reduce hand-off (comm/xgmi_allreduce.hip): when set, the reduced
   // gradients go straight into this rank's shared region (parity slot of the next
   // all-reduce step, read from the group's counters) with system-coherent stores, so the
@@ -46,7 +48,7 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const ReduceArgs* ra, unsigned* sync,
-                        hipStream_t stream);
+                        const int32_t* next_ids, unsigned char* stage, hipStream_t stream);
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);
@@ -57,6 +59,7 @@ void init_kernels();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
 int grad_reduce_blocks();  // grid of a whole-arena grad_reduce launch (with bookkeeping)
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
+                        const uint8_t* images, const int32_t* labels, int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream);
 void launch_sgd_apply(float* master, const float* grad, float* mom, bf16* shadow, int n, float lr, float momentum,
                       float grad_scale, int pack_only, hipStream_t stream);

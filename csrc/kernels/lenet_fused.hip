@@ -328,7 +328,8 @@ __device__ __forceinline__ void reducer_block(int r, const ReduceArgs ra, unsign
 }
 
 // INL: in-launch reducer variant (extra reducer workgroups, write-through hand-off stores)
-template <bool TRAIN, bool INL>
+// STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
+template <bool TRAIN, bool INL, bool STAGED = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -340,7 +341,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
     float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
-    long long* __restrict__ stamps, const ReduceArgs ra, unsigned* __restrict__ sync) {
+    long long* __restrict__ stamps, const ReduceArgs ra, unsigned* __restrict__ sync,
+    const int32_t* __restrict__ next_ids,  // TRAIN + stage: sample ids of the NEXT step (-1: none)
+    unsigned char* __restrict__ stage) {   // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
+  // stage (optional): block b of step c stores the image + label of step c + 1's sample b
+  // there during phase F (next_ids: published two steps ahead by the reduce kernel's
+  // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
+  // address - one dependent load level (batch id -> image) off the start of phase A.
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // per-block diagnostic trace (stamps != nullptr): stamps[16 + 4 * block + k], k = 0 start,
   // 1 rows published, 2 end, 3 XCC id
@@ -370,9 +377,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // than cursor -> order -> sample.
   int bvalid = 1, sample = 0;
   bool valid;
+  uint4 st_im = make_uint4(0, 0, 0, 0);
+  int st_label = 0;
+  uint4* const stage_im = reinterpret_cast<uint4*>(stage);
+  int32_t* const stage_lab = reinterpret_cast<int32_t*>(stage + (size_t)batch * IMG);
+  constexpr bool staged = TRAIN && STAGED;
   if (TRAIN) {
+    if constexpr (staged) {  // issued first: independent of every other load of the kernel
+      st_im = stage_im[(size_t)b * (IMG / 16) + min(tid, IMG / 16 - 1)];
+      st_label = stage_lab[b];
+    } else {
+      sample = order[b];  // `order` = the published batch ids [batch]
+    }
     bvalid = state[ST_BVALID];
-    sample = order[b];  // `order` = the published batch ids [batch]
     valid = b < bvalid;
   } else {
     const long gidx = (long)base_index + b;
@@ -401,8 +418,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     return;
   }
-  const int label = labels[sample];
+  int label;
   const uint8_t* img = images + (size_t)sample * IMG;
+  if constexpr (staged) label = st_label;
+  else label = labels[sample];
 
   bf16* fc1s = reinterpret_cast<bf16*>(smem + L_REGA);
   bf16x8* R1 = reinterpret_cast<bf16x8*>(smem + L_REGB);
@@ -432,7 +451,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // then the conv B fragments and biases, whose latency hides behind the R1 record build;
   // they are consumed before the fc1 LDS-DMA is issued (hipcc would otherwise drain the
   // DMA at their first use, or under-count vmcnt for them).
-  const uint4 im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
+  uint4 im;
+  if constexpr (staged) im = st_im;
+  else im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
 #pragma unroll
   for (int sk = 0; sk < 4; ++sk) bw1[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W1F)[(4 * sk + fg) * 16 + fr];
@@ -908,6 +929,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 
   STAMP(6);
   // ============ phase F: conv1 weight gradient ==========================================
+  // Waves 5-7 (no conv1-wgrad MFMAs) also stage the NEXT step's image + label: the sample
+  // id is loaded under the F1 row build, the image under the F2 MMAs; the values live only
+  // in those waves' branch, away from the register peak of the MFMA waves.
+  int ns_next = -1;
   unsigned char* DY1 = smem + L_REGA + A_DY1;  // bf16 [6] x [28][32] (channel stride DY1_CH bytes)
   float* RS1 = reinterpret_cast<float*>(smem + L_REGA + A_RS1);
   if (tid < 168) {  // one dY1 row per thread: unpool dP1 by CODE1, ReLU-masked
@@ -937,10 +962,22 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     RS1[c * 28 + y] = rs;
   } else {
+    if (staged && wave >= 5) {  // a vector load: the lgkmcnt(0) of the barriers does not wait for it
+      const int32_t* p = next_ids + b;
+      asm volatile("" : "+v"(p));
+      ns_next = *p;
+    }
     for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, R1, r1_row(t), r1_q(t));  // R2 dead
   }
   lds_barrier();
   STAMP(10);
+  if (staged && wave >= 5 && ns_next >= 0) {
+    const int t = tid - 320;  // 192 threads x 16 B = one image
+    const uint4 v = reinterpret_cast<const uint4*>(images + (size_t)ns_next * IMG)[t];
+    const int lab = t == 0 ? labels[ns_next] : 0;
+    stage_im[(size_t)b * (IMG / 16) + t] = v;
+    if (t == 0) stage_lab[b] = lab;
+  }
   if (wave == 7) {  // conv1 bias gradient: 8 lanes per channel over its 28 row sums
     const int c = min(lane >> 3, 5), part = lane & 7;
     float t = 0.f;
@@ -1002,6 +1039,8 @@ void init_kernels() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<false, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
+  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   done = true;
 }
 
@@ -1009,15 +1048,18 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const ReduceArgs* ra, unsigned* sync,
-                        hipStream_t stream) {
+                        const int32_t* next_ids, unsigned char* stage, hipStream_t stream) {
   init_kernels();
+  if (stage != nullptr && (next_ids == nullptr || (ra && sync)))
+    throw std::runtime_error("fused_train: staging needs next_ids and separate reduce launches");
   ReduceArgs r{};
   if (ra) r = *ra;
   const int grid = batch + (ra && sync ? RED_BLOCKS : 0);
-  auto* kern = (ra && sync) ? &lenet_fused_kernel<true, true> : &lenet_fused_kernel<true, false>;
+  auto* kern = (ra && sync) ? &lenet_fused_kernel<true, true>
+                            : (stage ? &lenet_fused_kernel<true, false, true> : &lenet_fused_kernel<true, false>);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, order_len, batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss,
-                     correct, stamps, r, ra ? sync : nullptr);
+                     correct, stamps, r, ra ? sync : nullptr, next_ids, stage);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1028,7 +1070,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct, nullptr, ReduceArgs{}, nullptr);
+                     nullptr, nullptr, nullptr, loss, correct, nullptr, ReduceArgs{}, nullptr, nullptr, nullptr);
   HIP_CHECK(hipGetLastError());
 }
 

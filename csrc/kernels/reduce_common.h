@@ -231,6 +231,12 @@ __device__ __forceinline__ void bookkeeping(const ReduceArgs a, int lane) {
       const long g = base + b;
       a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
     }
+    if (a.next_ids != nullptr) {  // and the step after it (image staging, lenet_fused.hip)
+      for (int b = lane; b < a.batch; b += 64) {
+        const long g = base + a.batch + b;
+        a.next_ids[b] = g < a.order_len ? a.order[g] : -1;
+      }
+    }
     const long rem = (long)a.order_len - base;
     const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
     if (lane == 0) {

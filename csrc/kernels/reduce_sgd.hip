@@ -187,13 +187,32 @@ __global__ void __launch_bounds__(RT) sgd_apply_kernel(float* __restrict__ maste
 // Epoch start on the compute stream in ONE launch: the epoch's sample order (uploaded ahead
 // of time into a staging buffer on a side stream) -> the order the bookkeeping reads, the
 // first step's sample ids, cursor 0 and the first batch's valid count.
+// With image staging (stage != nullptr): also the ids of step 1 (next_ids) and step 0's images
+// + labels in the stage buffer, which the fused kernel reads instead of chasing its batch id.
 __global__ void __launch_bounds__(RT) epoch_begin_kernel(const int32_t* __restrict__ staged, int32_t* __restrict__ order,
                                                          int n, int32_t* __restrict__ state,
-                                                         int32_t* __restrict__ batch_ids, int batch) {
+                                                         int32_t* __restrict__ batch_ids, int batch,
+                                                         const uint8_t* __restrict__ images,
+                                                         const int32_t* __restrict__ labels,
+                                                         int32_t* __restrict__ next_ids,
+                                                         unsigned char* __restrict__ stage) {
   for (int i = blockIdx.x * RT + threadIdx.x; i < n; i += gridDim.x * RT) {
     const int32_t v = staged[i];
     order[i] = v;
     if (i < batch) batch_ids[i] = v;
+  }
+  if (stage != nullptr) {
+    constexpr int V = IMG / 16;  // 16-B vectors per image
+    for (int i = blockIdx.x * RT + threadIdx.x; i < batch * V; i += gridDim.x * RT) {
+      const int b = i / V, k = i - b * V;
+      if (b < n) {
+        const int s = staged[b];
+        reinterpret_cast<uint4*>(stage)[i] = reinterpret_cast<const uint4*>(images + (size_t)s * IMG)[k];
+        if (k == 0) reinterpret_cast<int32_t*>(stage + (size_t)batch * IMG)[b] = labels[s];
+      }
+    }
+    for (int b = blockIdx.x * RT + threadIdx.x; b < batch; b += gridDim.x * RT)
+      next_ids[b] = batch + b < n ? staged[batch + b] : -1;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     state[ST_CURSOR] = 0;
@@ -203,9 +222,13 @@ __global__ void __launch_bounds__(RT) epoch_begin_kernel(const int32_t* __restri
 
 // ---- host launchers ---------------------------------------------------------------------
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
+                        const uint8_t* images, const int32_t* labels, int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream) {
-  const int nblk = max(1, min((n + RT - 1) / RT, 256));
-  hipLaunchKernelGGL(epoch_begin_kernel, dim3(nblk), dim3(RT), 0, stream, staged, order, n, state, batch_ids, batch);
+  if (stage != nullptr && (images == nullptr || labels == nullptr || next_ids == nullptr))
+    throw std::runtime_error("epoch_begin: staging needs the images, labels and next_ids");
+  const int nblk = max(1, min((max(n, batch * (IMG / 16)) + RT - 1) / RT, 256));
+  hipLaunchKernelGGL(epoch_begin_kernel, dim3(nblk), dim3(RT), 0, stream, staged, order, n, state, batch_ids, batch,
+                     images, labels, next_ids, stage);
   HIP_CHECK(hipGetLastError());
 }
 

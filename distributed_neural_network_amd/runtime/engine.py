@@ -189,7 +189,8 @@ class HipEngine(Engine):
 
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
-                 use_graphs: bool = True, overlap: bool = False, in_launch_reduce: bool = False) -> None:
+                 use_graphs: bool = True, overlap: bool = False, in_launch_reduce: bool = False,
+                 stage_images: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if not torch.cuda.is_available():
             raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -223,6 +224,15 @@ class HipEngine(Engine):
         self._pin_ev = [torch.cuda.Event(), torch.cuda.Event()]
         self._pin_i = 0
         self.batch_ids = torch.zeros(B, device=dev, dtype=torch.int32)  # sample ids of the next step
+        # next step's images + labels, staged by the fused kernel of the current step
+        # ([B][3072] u8 | [B] int32; lenet_fused.hip), so a step's image load has no
+        # dependency on its sample ids (stage_images=False / DNN_STAGE_IMAGES=0 turns it off)
+        if stage_images is None:
+            stage_images = os.environ.get("DNN_STAGE_IMAGES", "1") != "0"
+        self.stage = (torch.zeros(B * (3072 + 4), device=dev, dtype=torch.uint8)
+                      if stage_images and not in_launch_reduce else None)
+        self.next_ids = torch.full((B,), -1, device=dev, dtype=torch.int32)  # ids two steps ahead
+        self._staged = False  # stage holds this epoch's step-0 batch (set by begin_epoch)
         # in-launch reducer hand-off counters [rows, slabs, done, error] (lenet_fused.hip);
         # zero between launches (the last reducer resets them)
         self.sync = torch.zeros(4, device=dev, dtype=torch.int32)
@@ -257,6 +267,7 @@ class HipEngine(Engine):
     # -- data ---------------------------------------------------------------------------
     def attach(self, train: Split) -> None:
         self.train = train.to(self.device)
+        self._staged = False  # the stage holds images of the previous split until begin_epoch
         self.invalidate_graphs()
 
     def begin_epoch(self, order: np.ndarray) -> None:
@@ -285,9 +296,15 @@ class HipEngine(Engine):
             self._pin[i][:n].numpy()[:] = order
             self.staged[:n].copy_(self._pin[i][:n], non_blocking=True)
             self._pin_ev[i].record(main)
+        staged = self.stage is not None and self.train is not None and n > 0
+        if staged != self._staged:
+            self.invalidate_graphs()  # the stage pointer is a baked kernel argument
+        self._staged = staged
+        st = dict(images=self._p(self.train.images), labels=self._p(self.train.labels),
+                  next_ids=self._p(self.next_ids), stage=self._p(self.stage)) if staged else {}
         with torch.cuda.device(self.device):
             self.ext.epoch_begin(self._p(self.staged), self._p(self.order), n, self._p(self.state),
-                                 self._p(self.batch_ids), self.batch, main.cuda_stream)
+                                 self._p(self.batch_ids), self.batch, main.cuda_stream, **st)
 
     # -- one step (launch sequence; also what graphs capture) ---------------------------
     def _reduce(self, fuse_sgd: int, lo: int, hi: int, bookkeeping: int, s: int, **xg) -> None:
@@ -296,7 +313,8 @@ class HipEngine(Engine):
                              self._p(self.correct), self.batch, self._p(self.master), self._p(self.grad),
                              self._p(self.mom), self._p(self.shadow), self._p(self.state), self._p(self.stats),
                              self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, self._p(self.order),
-                             self.order_len, self._p(self.batch_ids), s, **xg)
+                             self.order_len, self._p(self.batch_ids), s,
+                             next_ids=self._p(self.next_ids) if self._staged else 0, **xg)
 
     def _launch_fused_reduce(self, fuse_sgd: int, s: int) -> None:
         """Fused step with the batch reduction (+ SGD when fuse_sgd) in the same launch."""
@@ -331,7 +349,9 @@ class HipEngine(Engine):
                              self.order_len, self.batch, self._p(self.state), self._p(self.master),
                              self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
                              self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
-                             self._p(self.loss), self._p(self.correct), s)
+                             self._p(self.loss), self._p(self.correct), s,
+                             next_ids=self._p(self.next_ids) if self._staged else 0,
+                             stage=self._p(self.stage) if self._staged else 0)
         if self.grad_sync is None:
             self._reduce(1, 0, LAYOUT.total, 1, s)
             return
@@ -420,7 +440,7 @@ class HipEngine(Engine):
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
         key = (nsteps, self.grad_sync is not None, self.overlap, self.in_launch_reduce, self.order_len,
-               getattr(getattr(self.grad_sync, "group", None), "one_launch", None))
+               getattr(getattr(self.grad_sync, "group", None), "one_launch", None), self._staged)
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.

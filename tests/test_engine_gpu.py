@@ -48,6 +48,32 @@ def test_in_launch_reducers_match_separate_reduce_kernel():
     assert int(e2.sync.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("graphs", [True, False])
+def test_staged_images_match_batch_id_path(graphs):
+    """Image staging (the fused kernel of step c stores step c + 1's images; epoch_begin
+    stages step 0) must give the same bits as loading every image through its batch id:
+    shuffled epochs, a tail batch, steps past the end of an epoch, a new epoch mid-chunk."""
+    data = synthetic(1000, 9)
+    a = init_arena(seed=8)
+    rng = np.random.default_rng(0)
+    orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
+    res = []
+    for stage in (False, True):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=8, use_graphs=graphs, stage_images=stage)
+        eng.attach(data)
+        stats = []
+        for ep, order in enumerate(orders):
+            eng.begin_epoch(order)
+            eng.run_steps(16 + (ep == 1) * 3)  # epoch 1 runs 3 steps past its end (no-ops)
+            stats.append(eng.epoch_stats())
+        torch.cuda.synchronize()
+        assert (eng.stage is not None) == stage
+        res.append((eng.master.cpu(), eng.mom.cpu(), stats))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for s0, s1 in zip(res[0][2], res[1][2]):
+        assert s0.loss_sum == s1.loss_sum and s0.correct == s1.correct and s0.samples == s1.samples == 1000
+
+
 def test_deterministic_run_to_run():
     data = synthetic(512, 2)
     a = init_arena(seed=4)

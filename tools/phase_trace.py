@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-phase timeline of the fused training kernel (diagnostic).
 
-Launches the fused kernel with its stamp buffer enabled: block 0 / thread 0 records
+Launches the fused kernel (the image-staged variant unless DNN_STAGE_IMAGES=0) with its
+stamp buffer enabled: block 0 / thread 0 records
 s_memrealtime (100 MHz) at each phase boundary.  Prints the median over repeats of
 each phase's duration in microseconds, plus the whole-kernel wall time from events.
 """
@@ -46,10 +47,11 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
                 stamps=stamps.data_ptr())
         else:
             e = eng
+            st = dict(next_ids=e._p(e.next_ids), stage=e._p(e.stage)) if e._staged else {}
             e.ext.fused_train(e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.order_len, e.batch,
                               e._p(e.state), e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2),
                               e._p(e.z1), e._p(e.z2), e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct),
-                              e._stream(), stamps=stamps.data_ptr())
+                              e._stream(), stamps=stamps.data_ptr(), **st)
         ev1.record()
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
