@@ -109,7 +109,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, u xg_region, long long xg_slot_bytes, long long xg_flag_bytes,
                           u xg_ctr, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
-                          u xp_err, u xp_abort, double xp_timeout_s, int xp_fences, float xp_scale, u next_ids) {
+                          u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -133,11 +133,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_err = P<unsigned>(xp_err);
       a.xp_abort = P<const unsigned>(xp_abort);
       a.xp_timeout_ticks = (long long)(xp_timeout_s * 1.0e8);
-      a.xp_fences = xp_fences;
       a.xp_scale = xp_scale;
-      a.xp_slot_bytes = dnn::xgmi_slot_bytes(xp_capacity);
-      a.xp_flag_bytes = dnn::xgmi_flag_bytes(xp_capacity);
-      a.xp_flag_off = dnn::xgmi_xp_flag_off(xp_capacity);
+      a.xp_gslot_off = dnn::xgmi_gslot_off(xp_capacity);
+      a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
     }
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
@@ -148,7 +146,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
-     py::arg("xp_fences") = 3, py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
+     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {

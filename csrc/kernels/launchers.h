@@ -28,19 +28,19 @@ struct ReduceArgs {
   long long xg_slot_bytes = 0, xg_flag_bytes = 0;
   const unsigned* xg_ctr = nullptr;
   // one-launch xGMI all-reduce (xp_nranks > 0; region layout: comm/xgmi_layout.h): every
-  // reduction block stores its reduced elements into this rank's slot, pushes a step flag
-  // for its block into every peer's flag table B, waits for the same block of every peer,
-  // sums the N values in rank order, scales by xp_scale and applies momentum SGD + the bf16
-  // images itself - the batch reduction and the all-reduce in ONE launch, with no hand-off
-  // between blocks of this GPU (each block exchanges exactly the elements it reduced).
+  // reduction block stores each reduced element into this rank's granule slot as ONE 8-byte
+  // {value, step} word, reads the same element's granule from every peer until its tag shows
+  // this step, sums the N values in rank order, scales by xp_scale and applies momentum SGD +
+  // the bf16 images itself - the batch reduction and the all-reduce in ONE launch, with no
+  // hand-off between blocks of this GPU and no flag (each block exchanges exactly the
+  // elements it reduced; the tag travels in the same atomic word as the value).
   unsigned char* xp_region[XG_MAX_RANKS] = {};
   int xp_rank = 0, xp_nranks = 0;
   unsigned* xp_ctr = nullptr;          // [XP_MAX_BLOCKS] per-block step counters (local)
   unsigned* xp_err = nullptr;          // sticky error word (shared with the group's all-reduce kernel)
   const unsigned* xp_abort = nullptr;  // host-mapped abort word (fault watchdog)
   long long xp_timeout_ticks = 0;      // s_memrealtime ticks (100 MHz)
-  long long xp_slot_bytes = 0, xp_flag_bytes = 0, xp_flag_off = 0;
-  int xp_fences = 3;                   // bit 0: system release before the flag push, bit 1: acquire after
+  long long xp_gslot_off = 0, xp_gslot_bytes = 0;
   float xp_scale = 1.f;                // 1 / N
 };
 

@@ -49,21 +49,23 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
 // callers' loops are unrolled, so the exchange sink's arrays stay in registers).
 //  * DirectSink: finish at once (local SGD step, or gradient output).
 //  * XpSink (one-launch xGMI all-reduce, reduce_sgd.hip): the gradient goes to this rank's
-//    shared slot now (system-coherent store); the update runs after the block's exchange.
+//    granule slot now as one 8-byte {value, step} word (system-coherent store); the update
+//    runs after the lane has read the same element from every peer.
 struct DirectSink {
   __device__ __forceinline__ void put(int, int e, float g, float p, float m, const ReduceArgs& a) {
     sgd_finish(e, g, p, m, a);
   }
 };
 struct XpSink {
-  unsigned* own;  // this rank's slot of the step
+  unsigned long long* own;  // this rank's granule slot of the step
+  unsigned long long tag;   // step << 32
   int e[4] = {0, 0, 0, 0};
   float g[4] = {0.f, 0.f, 0.f, 0.f}, p[4], m[4];
   bool v[4] = {false, false, false, false};
   __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
     g_ *= a.grad_scale;
     e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
-    __hip_atomic_store(own + e_, __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 };
 

@@ -55,65 +55,62 @@ __device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk) 
 
 constexpr int GRAD_REDUCE_BLOCKS =
     TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT + (CONV_SLOTS + RT - 1) / RT + 1;
-static_assert(GRAD_REDUCE_BLOCKS <= XP_MAX_BLOCKS, "exchange flag table B has a column per reduce block");
+static_assert(GRAD_REDUCE_BLOCKS <= XP_MAX_BLOCKS, "one exchange step counter per reduce block");
 int grad_reduce_blocks() { return GRAD_REDUCE_BLOCKS; }
 
-__device__ __forceinline__ unsigned xp_ld(const unsigned* p) {
+__device__ __forceinline__ unsigned long long xp_ld(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The one-launch all-reduce exchange of ONE block (same protocol as xgmi_allreduce_kernel,
-// per reduce block instead of per 1024-element slice):
-//   publish - the block's gradients are already in the own slot (XpSink::put, system-
-//             coherent stores); drain them, then push this block's step flag into EVERY
-//             peer's flag table B (remote stores; the peer polls locally);
-//   wait    - lanes 0..N-1 poll the N flags of this block (bounded: timeout / abort word ->
-//             sticky error word, never a hang);
-//   reduce  - every lane reads its elements from all N slots (7 links at once), sums in RANK
-//             ORDER (bit-identical replicas), scales by 1/N, applies momentum SGD + images.
-// Double buffering by step parity is safe for the same reason as in the slice kernel: block b
-// overwrites its elements of slot (s & 1) at step s + 2 only after every peer's block b
-// published step s + 1, which each does after finishing its step s reads of those elements.
+// The one-launch all-reduce exchange of ONE lane's (<= 4) reduced elements.  Each element
+// was stored as a granule {value, step} (XpSink::put); the lane reads the same element's
+// granule from every peer's slot over xGMI (7 links at once, every load in flight before the
+// first check) until each tag shows this step, sums the N values in RANK ORDER (bit-identical
+// replicas), scales by 1/N and applies momentum SGD + the bf16 images.  The value and its tag
+// are one 8-byte atomic word, so no flag, fence or barrier orders anything: a tag match IS
+// the data.  Waits are bounded (timeout / abort word -> sticky error word, never a hang).
+// Double buffering by step parity: the owner overwrites its element e of slot (s & 1) at step
+// s + 2 only after it read every peer's step s + 1 granule of e, which each peer wrote only
+// after it had read the owner's step s granule of e.
+// NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
+// group does not pay for 8 ranks' loads in flight.
+template <int NR>
 __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
-  const int b = blockIdx.x, tid = threadIdx.x;
   const int par = step & 1u;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own slot stores acknowledged
-  __syncthreads();
-  if (tid < 64) {
-    if (a.xp_fences & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (tid < a.xp_nranks && tid != a.xp_rank) {
-      unsigned* flags = reinterpret_cast<unsigned*>(a.xp_region[tid] + a.xp_flag_off);
-      __hip_atomic_store(flags + a.xp_rank * XP_MAX_BLOCKS + b, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  float v[NR][4];
+  unsigned pending = 0;  // bit 4 r + j: granule (r, j) still to read
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[r][j] = sk.g[j];
+      if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
     }
-  }
-  if (tid < a.xp_nranks && tid != a.xp_rank && !failed) {
-    const unsigned* f = reinterpret_cast<const unsigned*>(a.xp_region[a.xp_rank] + a.xp_flag_off) +
-                        tid * XP_MAX_BLOCKS + b;
-    const long long t0 = wall_clock64();
-    int spins = 0;
-    while ((int)(xp_ld(f) - step) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 255) == 0) {
-        if (wall_clock64() - t0 > a.xp_timeout_ticks || xp_ld(a.xp_abort) != 0u) {
-          __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
+  const long long t0 = wall_clock64();
+  while (pending != 0u) {
+    unsigned long long x[NR][4];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const unsigned long long* src =
+          reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src + sk.e[j]);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((pending & (1u << (4 * r + j))) && (unsigned)(x[r][j] >> 32) == step) {
+          v[r][j] = __uint_as_float((unsigned)x[r][j]);
+          pending &= ~(1u << (4 * r + j));
         }
-      }
-    }
-  }
-  if (tid < 64 && (a.xp_fences & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // every peer load in flight before the first use (invalid lanes read element 0: harmless)
-  float v[XG_MAX_RANKS][4];
-#pragma unroll
-  for (int r = 0; r < XG_MAX_RANKS; ++r) {
-    if (r < a.xp_nranks) {
-      const unsigned* src = reinterpret_cast<const unsigned*>(a.xp_region[r] + a.xp_flag_bytes + par * a.xp_slot_bytes);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[r][j] = r == a.xp_rank ? sk.g[j] : __uint_as_float(xp_ld(src + sk.e[j]));
+    if (pending == 0u || failed) break;
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > a.xp_timeout_ticks || __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
     }
   }
 #pragma unroll
@@ -121,7 +118,7 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
     if (!sk.v[j]) continue;
     float s = v[0][j];
 #pragma unroll
-    for (int r = 1; r < XG_MAX_RANKS; ++r)
+    for (int r = 1; r < NR; ++r)
       if (r < a.xp_nranks) s += v[r][j];
     const float gr = s * a.xp_scale;
     float p, m;
@@ -130,8 +127,6 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
     a.master[sk.e[j]] = p;
     write_shadow(a.shadow, sk.e[j], p);
   }
-  __syncthreads();
-  if (tid == 0) a.xp_ctr[b] = step;
 }
 
 // diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
@@ -143,16 +138,24 @@ __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
   }
 }
 
+// NR = 1: local reduction (+ SGD, or gradients out); NR = 2 / 4 / 8: the one-launch
+// exchange for groups of up to NR ranks (separate instances keep the local step's registers
+// at its own need).
+template <int NR>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(const ReduceArgs a) {
   reduce_stamp(a, 0);
-  if (a.xp_nranks > 0) {  // one-launch all-reduce: reduce -> exchange -> SGD, per block
+  if constexpr (NR > 1) {  // one-launch all-reduce: reduce -> exchange -> SGD, per lane
     // (the arguments are only read on this path: the per-lane region index then reads the
     //  kernel-argument segment directly instead of a private copy of the whole struct)
     const unsigned step = a.xp_ctr[blockIdx.x] + 1u;
     const bool failed = *a.xp_err != 0u;
     XpSink sk;
-    sk.own = reinterpret_cast<unsigned*>(a.xp_region[a.xp_rank] + a.xp_flag_bytes + (step & 1u) * a.xp_slot_bytes);
-    if (grad_reduce_body(a, sk)) xp_exchange(a, sk, step, failed);
+    sk.own = reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                   (step & 1u) * a.xp_gslot_bytes);
+    sk.tag = (unsigned long long)step << 32;
+    if (grad_reduce_body(a, sk)) xp_exchange<NR>(a, sk, step, failed);
+    __syncthreads();  // every thread read this block's counter before it advances
+    if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;
   } else {
     ReduceArgs d_args = a;
     if (a.xg_region != nullptr) {  // gradients -> the shared slot of the coming xGMI step
@@ -240,11 +243,16 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
   if (conv) nblk += (CONV_SLOTS + RT - 1) / RT;
   if (args.bookkeeping) nblk += 1;
   if (nblk == 0) return;
-  // the exchange waits on the same block of every peer: every block must be resident at once
-  // (<= XP_MAX_BLOCKS blocks of RT threads, one per CU of the 256) and take the whole arena
+  // the exchange waits on the same elements of every peer, which the same block reduces there:
+  // every block must be resident at once (<= XP_MAX_BLOCKS blocks of RT threads, at most one
+  // per CU of the 256) and the launch must take the whole arena
   if (args.xp_nranks > 0 && (nblk > XP_MAX_BLOCKS || !mlp || !conv))
     throw std::runtime_error("grad_reduce exchange needs the whole-arena grid");
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3(nblk), dim3(RT), 0, stream, args);
+  const int nr = args.xp_nranks;
+  if (nr > XG_MAX_RANKS) throw std::runtime_error("grad_reduce exchange: at most 8 ranks");
+  auto* kern = nr == 0 ? &grad_reduce_kernel<1>
+                       : (nr <= 2 ? &grad_reduce_kernel<2> : (nr <= 4 ? &grad_reduce_kernel<4> : &grad_reduce_kernel<8>));
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(RT), 0, stream, args);
   HIP_CHECK(hipGetLastError());
 }
 

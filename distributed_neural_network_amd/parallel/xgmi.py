@@ -157,13 +157,15 @@ class XgmiGroup:
                     xg_flag_bytes=self.ext.xgmi_flag_bytes(self.capacity), xg_ctr=self.ctr.data_ptr())
 
     def exchange(self) -> dict:
-        """grad_reduce kwargs of the one-launch all-reduce: every reduction block publishes its
-        reduced elements, exchanges them with the same block of every peer and applies the
-        averaged update itself (no separate all-reduce launch, no hand-off inside the GPU)."""
+        """grad_reduce kwargs of the one-launch all-reduce: every reduction lane publishes its
+        reduced elements as {value, step} granules, reads the same elements' granules from
+        every peer and applies the averaged update itself (no separate all-reduce launch, no
+        hand-off inside the GPU, no flag: the step tag travels in the value's atomic word, so
+        this path needs no fences on any topology)."""
         err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
         return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
                     xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
-                    xp_timeout_s=self.timeout_s, xp_fences=self.fences, xp_scale=1.0 / self.world)
+                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world)
 
     def clear_error(self) -> None:
         """Reset the sticky error word (only after every rank's kernels have drained)."""
