@@ -36,8 +36,7 @@ void xgmi_free_abort_word(uintptr_t host_word);
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, int fences, int prepub, hipStream_t stream);
-void xgmi_clear_slots(uintptr_t region, long long capacity);
+                           double timeout_s, hipStream_t stream);
 // runtime/graph_exec.cpp
 void graph_upload(uintptr_t exec, uintptr_t stream);
 }  // namespace dnn
@@ -107,8 +106,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("grad_reduce", [](u a0, u h1, u h2, u z1, u z2, u z3, u slab, u loss, u correct, int batch, u master,
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
-                          u stream, u stamps, u xg_region, long long xg_slot_bytes, long long xg_flag_bytes,
-                          u xg_ctr, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
+                          u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
                           u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
@@ -116,10 +114,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
                       P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order), order_len,
                       P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping,
                       P<long long>(stamps)};
-    a.xg_region = P<unsigned char>(xg_region);
-    a.xg_slot_bytes = xg_slot_bytes;
-    a.xg_flag_bytes = xg_flag_bytes;
-    a.xg_ctr = P<const unsigned>(xg_ctr);
     a.next_ids = P<int32_t>(next_ids);
     if (!xp_regions.empty()) {
       if ((int)xp_regions.size() > dnn::XG_MAX_RANKS || xp_rank < 0 || xp_rank >= (int)xp_regions.size())
@@ -134,7 +128,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_abort = P<const unsigned>(xp_abort);
       a.xp_timeout_ticks = (long long)(xp_timeout_s * 1.0e8);
       a.xp_scale = xp_scale;
-      a.xp_gslot_off = dnn::xgmi_gslot_off(xp_capacity);
+      a.xp_gslot_off = dnn::xgmi_xp_off(xp_capacity);
       a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
     }
     dnn::launch_grad_reduce(a, S(stream));
@@ -143,7 +137,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("shadow"), py::arg("state"), py::arg("stats"), py::arg("lr"), py::arg("momentum"),
      py::arg("grad_scale"), py::arg("fuse_sgd"), py::arg("lo"), py::arg("hi"), py::arg("bookkeeping"),
      py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
-     py::arg("xg_region") = 0, py::arg("xg_slot_bytes") = 0, py::arg("xg_flag_bytes") = 0, py::arg("xg_ctr") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
      py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
@@ -283,17 +276,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);
   m.def("xgmi_max_blocks", &dnn::xgmi_max_blocks);
   m.def("xgmi_region_bytes", &dnn::xgmi_region_bytes);
-  m.def("xgmi_slot_bytes", &dnn::xgmi_slot_bytes);
+  m.def("xgmi_gslot_bytes", &dnn::xgmi_gslot_bytes);
   m.def("xgmi_xp_max_blocks", []() { return dnn::XP_MAX_BLOCKS; });
   m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
-  m.def("xgmi_clear_slots", &dnn::xgmi_clear_slots);
-  m.def("xgmi_flag_bytes", &dnn::xgmi_flag_bytes);
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
-                             double timeout_s, int fences, int prepub, u stream) {
+                             double timeout_s, u stream) {
     dnn::launch_xgmi_allreduce(regions, rank, capacity, n, P<const float>(grad), P<float>(out), P<float>(master),
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
-                               P<const unsigned>(abort_w), timeout_s, fences, prepub, S(stream));
+                               P<const unsigned>(abort_w), timeout_s, S(stream));
   });
   m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream, u images, u labels,
                           u next_ids, u stage) {

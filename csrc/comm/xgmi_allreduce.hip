@@ -7,22 +7,26 @@
 // (RCCL) pays 2 (N-1) dependent hops over single xGMI links.  An 8x MI355X node is a full
 // xGMI mesh (7 links per GPU), so this kernel does it in ONE hop instead:
 //
-//   1. publish - every workgroup copies its 1024-element slice of the local gradient into
-//      this rank's shared region (double-buffered by step parity), then pushes a step
-//      flag into EVERY peer's region (remote stores over xGMI; the peer polls locally);
-//   2. wait    - lanes 0..N-1 poll the N flags of this slice in local memory;
-//   3. reduce  - the workgroup reads the slice from all N regions (7 xGMI links in
-//      parallel), sums them in RANK ORDER (so every replica computes bit-identical
-//      values - no float atomics, deterministic run to run), scales by 1/N and applies
-//      the momentum-SGD update + the bf16 weight-image refresh (the work sgd_apply does
-//      after an RCCL all-reduce), or writes the averaged gradient (plain all-reduce).
+//   1. publish - every workgroup writes its 1024-element slice of the local gradient into
+//      this rank's shared region as data-tagged granules: ONE 8-byte {fp32 value, step}
+//      word per element (double-buffered by step parity);
+//   2. gather  - every lane reads its elements' granules from all N regions (7 xGMI links
+//      in parallel, every load in flight before the first check) until each tag shows the
+//      current step: the value and its tag are one atomic word, so no flag, fence or barrier
+//      has to order the hand-off - on one device and across GPUs alike;
+//   3. reduce  - sums them in RANK ORDER (so every replica computes bit-identical values - no
+//      float atomics, deterministic run to run), scales by 1/N and applies the momentum-SGD
+//      update + the bf16 weight-image refresh (the work sgd_apply does after an RCCL
+//      all-reduce), or writes the averaged gradient (plain all-reduce).
 //
 // Regions come from hipExtMallocWithFlags(hipDeviceMallocUncached) and are shared with
-// hipIpcGetMemHandle / hipIpcOpenMemHandle (dmabuf IPC); every access to shared bytes is
-// a system-scope atomic (sc0 sc1), ordered by system-scope release/acquire fences around
-// the flag hand-off.  Double buffering makes one flag per slice and step enough: a rank
-// overwrites slot (s & 1) at step s + 2 only after every peer published step s + 1, which
-// each does only after finishing its step s reads.
+// hipIpcGetMemHandle / hipIpcOpenMemHandle (dmabuf IPC); every access to shared bytes is a
+// system-scope 64-bit atomic (sc0 sc1).  Double buffering by parity makes the tags safe: a
+// rank overwrites element e of slot (s & 1) at step s + 2 only after it read every peer's
+// step s + 1 granule of e, which each peer wrote only after reading this rank's step s one.
+// (The one-launch path - kernels/reduce_sgd.hip xp_exchange - is the same protocol run by
+// the batch-reduction lanes on their own elements; this kernel is its two-launch fallback
+// and the all-reduce of the generic layer engine.)
 //
 // Never hangs: a wait that exceeds the timeout (or sees the host abort word set - the
 // fault watchdog sets it when a peer dies) sets a sticky error word and the kernel
@@ -45,9 +49,7 @@ struct XgmiArgs {
   unsigned char* region[XG_MAX_RANKS];  // every rank's shared region, mapped here (own included)
   int rank, nranks;
   int n;                 // elements to reduce
-  int max_blocks;        // flag rows per writer (capacity / XG_CHUNK)
-  long long slot_bytes;  // bytes per parity slot
-  long long flag_bytes;  // bytes of the flag area at the start of a region
+  long long gslot_bytes; // bytes per parity slot of granules
   const float* grad;     // local input
   float* out;            // mode 0: averaged gradient (may alias grad)
   float* master;
@@ -56,20 +58,17 @@ struct XgmiArgs {
   float lr, momentum, scale;
   int mode;                 // 0: all-reduce (avg) -> out; 1: + momentum SGD + bf16 shadow; 2: + SGD (no shadow)
   unsigned* ctr;            // local: [max_blocks] per-workgroup step counters, [max_blocks] error word
+  int max_blocks;
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  int fences;               // bit 0: system release before the flag push, bit 1: system acquire after the wait
-  int prepub;               // 1: the previous kernel (grad_reduce) already stored this step's gradients in
-                            //    the own slot (system-coherent): no publish copy, flags go out at once
 };
 
-__device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
+__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
+// NR: group-size bucket (2, 4, 8 >= nranks; 1 for a 1-rank group) sizing the register arrays
+template <int NR>
 __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   unsigned* err_w = a.ctr + a.max_blocks;
@@ -77,95 +76,85 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   const bool failed = a.ctr[a.max_blocks] != 0u;
   const int par = step & 1u;
   const int lo = b * XG_CHUNK;
+  const unsigned long long tag = (unsigned long long)step << 32;
   auto slot = [&](int r) {
-    return reinterpret_cast<unsigned*>(a.region[r] + a.flag_bytes + par * a.slot_bytes);
+    return reinterpret_cast<unsigned long long*>(a.region[r] + par * a.gslot_bytes);
   };
 
-  // 1. publish this slice (system-coherent stores), then release + push the step flag
-  // (the optimizer state is local and only this thread touches it: prefetch it now, so the
-  //  update after the wait costs no extra memory latency)
-  const unsigned* g = reinterpret_cast<const unsigned*>(a.grad);
-  unsigned mine[XG_PER_THREAD];
+  // 1. publish this slice as granules (the optimizer state is local and only this thread
+  //    touches it: prefetch it now, so the update after the gather costs no extra latency)
+  float v[NR][XG_PER_THREAD];
   float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
-  unsigned* my_slot = slot(a.rank);
+  int e[XG_PER_THREAD];
+  unsigned long long* mine = slot(a.rank);
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
-    const int e = min(lo + k * XG_THREADS + tid, a.n - 1);
-    mine[k] = a.prepub ? ld_sys(my_slot + e) : g[e];
+    e[k] = min(lo + k * XG_THREADS + tid, a.n - 1);
+    const float g = a.grad[e[k]];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) v[r][k] = g;
     if (a.mode != 0) {
-      p_old[k] = a.master[e];
-      m_old[k] = a.mom[e];
+      p_old[k] = a.master[e[k]];
+      m_old[k] = a.mom[e[k]];
     }
-  }
-  if (!a.prepub) {
-#pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k) {
-      const int e = lo + k * XG_THREADS + tid;
-      if (e < a.n) st_sys(my_slot + e, mine[k]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (tid < 64) {
-    if (a.fences & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-    if (tid < a.nranks && tid != a.rank) {  // (own data stays in registers: no own flag)
-      unsigned* flags = reinterpret_cast<unsigned*>(a.region[tid]);
-      st_sys(flags + a.rank * a.max_blocks + b, step);
-    }
+    if (lo + k * XG_THREADS + tid < a.n)
+      __hip_atomic_store(mine + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 
-  // 2. wait for the N flags of this slice (bounded)
-  if (tid < a.nranks && tid != a.rank && !failed) {
-    const unsigned* f = reinterpret_cast<const unsigned*>(a.region[a.rank]) + tid * a.max_blocks + b;
-    const long long t0 = wall_clock64();
-    int spins = 0;
-    while ((int)(ld_sys(f) - step) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 255) == 0) {
-        if (wall_clock64() - t0 > a.timeout_ticks || ld_sys(a.abort_w) != 0u) {
-          st_sys(err_w, 1u);
-          break;
+  // 2. gather every peer's granules of these elements until their tags show this step
+  unsigned pending = 0;  // bit 4 r + k
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k)
+      if (r < a.nranks && r != a.rank && lo + k * XG_THREADS + tid < a.n) pending |= 1u << (4 * r + k);
+  const long long t0 = wall_clock64();
+  while (pending != 0u) {
+    unsigned long long x[NR][XG_PER_THREAD];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const unsigned long long* src = slot(r);
+#pragma unroll
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if (pending & (1u << (4 * r + k))) x[r][k] = ld_sys64(src + e[k]);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if ((pending & (1u << (4 * r + k))) && (unsigned)(x[r][k] >> 32) == step) {
+          v[r][k] = __uint_as_float((unsigned)x[r][k]);
+          pending &= ~(1u << (4 * r + k));
         }
-      }
+    if (pending == 0u || failed) break;
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > a.timeout_ticks ||
+        __hip_atomic_load(a.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      __hip_atomic_store(err_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
     }
   }
-  if (tid < 64 && (a.fences & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // 3. gather all ranks' slices (every load in flight before the first use), sum in rank order
-  float v[XG_MAX_RANKS][XG_PER_THREAD];
-#pragma unroll
-  for (int r = 0; r < XG_MAX_RANKS; ++r) {
-    if (r < a.nranks) {
-      const unsigned* src = slot(r);
-#pragma unroll
-      for (int k = 0; k < XG_PER_THREAD; ++k) {
-        const int e = min(lo + k * XG_THREADS + tid, a.n - 1);
-        v[r][k] = __uint_as_float(r == a.rank ? mine[k] : ld_sys(src + e));
-      }
-    }
-  }
+  // 3. rank-order sum, scale, optimizer
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
-    const int e = lo + k * XG_THREADS + tid;
-    if (e >= a.n) continue;
+    if (lo + k * XG_THREADS + tid >= a.n) continue;
     float s = v[0][k];
 #pragma unroll
-    for (int r = 1; r < XG_MAX_RANKS; ++r)
+    for (int r = 1; r < NR; ++r)
       if (r < a.nranks) s += v[r][k];
     const float gr = s * a.scale;
     if (a.mode == 0) {
-      a.out[e] = gr;
+      a.out[e[k]] = gr;
     } else {
       float p, m;
       sgd_update(gr, p_old[k], m_old[k], a.lr, a.momentum, p, m);
-      a.mom[e] = m;
-      a.master[e] = p;
-      if (a.mode == 1) write_shadow(a.shadow, e, p);
+      a.mom[e[k]] = m;
+      a.master[e[k]] = p;
+      if (a.mode == 1) write_shadow(a.shadow, e[k], p);
     }
   }
-  __syncthreads();
+  __syncthreads();  // every thread read this workgroup's counter before it advances
   if (tid == 0) a.ctr[b] = step;
 }
 
@@ -203,14 +192,6 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity) {
   }
   xcheck(e, "hipIpcGetMemHandle");
   return {reinterpret_cast<uintptr_t>(p), std::string(h.reserved, HIP_IPC_HANDLE_SIZE), kind};
-}
-
-// zero both data slots (keeps the flags): elements a pre-published step never writes (arena
-// padding) must read as 0 after the self-test filled the slots
-void xgmi_clear_slots(uintptr_t region, long long capacity) {
-  xcheck(hipMemset(reinterpret_cast<unsigned char*>(region) + xgmi_flag_bytes(capacity), 0,
-                   2 * xgmi_slot_bytes(capacity)), "hipMemset(xgmi slots)");
-  xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }
 
 uintptr_t xgmi_open(const std::string& handle) {
@@ -261,21 +242,20 @@ void xgmi_free_abort_word(uintptr_t host_word) {
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, int fences, int prepub, hipStream_t stream) {
+                           double timeout_s, hipStream_t stream) {
   const int nranks = (int)regions.size();
   if (nranks < 1 || nranks > XG_MAX_RANKS) throw std::runtime_error("xgmi all-reduce: 1..8 ranks");
   if (rank < 0 || rank >= nranks) throw std::runtime_error("xgmi all-reduce: bad rank");
   if (n <= 0 || n > capacity) throw std::runtime_error("xgmi all-reduce: n exceeds the region capacity");
   if (mode < 0 || mode > 2) throw std::runtime_error("xgmi all-reduce: bad mode");
   if (mode == 1 && n > ARENA) throw std::runtime_error("xgmi all-reduce: shadow mode is for the fused arena");
+  static_assert(XG_PER_THREAD * XG_MAX_RANKS <= 32, "pending mask bits");
   XgmiArgs a{};
   for (int r = 0; r < nranks; ++r) a.region[r] = reinterpret_cast<unsigned char*>(regions[r]);
   a.rank = rank;
   a.nranks = nranks;
   a.n = n;
-  a.max_blocks = xgmi_max_blocks(capacity);
-  a.slot_bytes = xgmi_slot_bytes(capacity);
-  a.flag_bytes = xgmi_flag_bytes(capacity);
+  a.gslot_bytes = xgmi_gslot_bytes(capacity);
   a.grad = grad;
   a.out = out;
   a.master = master;
@@ -286,12 +266,14 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.scale = scale;
   a.mode = mode;
   a.ctr = ctr;
+  a.max_blocks = xgmi_max_blocks(capacity);
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
-  a.fences = fences;
-  a.prepub = prepub;
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;
-  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, stream, a);
+  auto* kern = nranks == 1 ? &xgmi_allreduce_kernel<1>
+                           : (nranks <= 2 ? &xgmi_allreduce_kernel<2>
+                                          : (nranks <= 4 ? &xgmi_allreduce_kernel<4> : &xgmi_allreduce_kernel<8>));
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(XG_THREADS), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 

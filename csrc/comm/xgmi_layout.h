@@ -1,20 +1,15 @@
-// Layout of one rank's IPC-shared xGMI region, shared by the one-shot all-reduce kernel
-// (xgmi_allreduce.hip, the two-launch path) and the one-launch exchange inside grad_reduce
-// (kernels/reduce_sgd.hip).
+// Layout of one rank's IPC-shared xGMI region, shared by the one-launch exchange inside
+// grad_reduce (kernels/reduce_sgd.hip) and the one-shot all-reduce kernel
+// (xgmi_allreduce.hip: the two-launch fallback and the layer engine's all-reduce).
 //
-//   [flag table: XG_MAX_RANKS x max_blocks words]  step flags of xgmi_allreduce_kernel,
-//                                                  row = writer rank, column = its workgroup
-//   [slot 0 | slot 1]                              fp32 gradient slots of the two-launch path,
-//                                                  alternated by step parity
-//   [granule slot 0 | granule slot 1]              one 8-byte granule per arena element for the
-//                                                  one-launch exchange: {fp32 value, step tag},
-//                                                  written by ONE 64-bit store, so a reader that
-//                                                  sees the tag also sees the value (no flag, no
-//                                                  ordering between two stores to rely on)
+//   [slot 0 | slot 1]        granules of xgmi_allreduce_kernel (step = its per-workgroup counters)
+//   [slot 0 | slot 1]        granules of the grad_reduce exchange (step = its per-block counters)
 //
-// A flag word is written only by its writer rank (remote store over xGMI) and polled only by
-// the region's owner (local load); a granule is written only by the region's owner and read
-// by the peers (remote loads).
+// A granule is one 8-byte word per element: {fp32 value, step}, written by ONE 64-bit store
+// of the region's owner and read by the peers (remote loads); slots alternate by step parity.
+// A reader that sees the tag also sees the value - no flag, and no ordering between two stores
+// to rely on.  The two paths count steps independently, so each has its own slots (a tag of
+// one could otherwise match a stale granule of the other).
 #pragma once
 
 namespace dnn {
@@ -25,19 +20,8 @@ constexpr int XP_MAX_BLOCKS = 128;   // grad_reduce blocks that take part in the
 
 inline long long xg_round_up(long long x, long long m) { return (x + m - 1) / m * m; }
 inline int xgmi_max_blocks(long long capacity) { return (int)((capacity + XG_CHUNK - 1) / XG_CHUNK); }
-inline long long xgmi_flag_bytes(long long capacity) {
-  return xg_round_up((long long)XG_MAX_RANKS * xgmi_max_blocks(capacity) * 4, 4096);
-}
-inline long long xgmi_slot_bytes(long long capacity) {
-  return xg_round_up((long long)xgmi_max_blocks(capacity) * XG_CHUNK * 4, 4096);
-}
-// granule slots of the one-launch exchange
-inline long long xgmi_gslot_off(long long capacity) {
-  return xgmi_flag_bytes(capacity) + 2 * xgmi_slot_bytes(capacity);
-}
 inline long long xgmi_gslot_bytes(long long capacity) { return xg_round_up(capacity * 8, 4096); }
-inline long long xgmi_region_bytes(long long capacity) {
-  return xgmi_gslot_off(capacity) + 2 * xgmi_gslot_bytes(capacity);
-}
+inline long long xgmi_xp_off(long long capacity) { return 2 * xgmi_gslot_bytes(capacity); }  // exchange slots
+inline long long xgmi_region_bytes(long long capacity) { return 4 * xgmi_gslot_bytes(capacity); }
 
 }  // namespace dnn

@@ -20,13 +20,6 @@ struct ReduceArgs {
   long long* stamps = nullptr;  // diagnostic: per-block [start, end] s_memrealtime (grad_reduce)
   int32_t* next_ids = nullptr;  // bookkeeping: also publish the sample ids TWO steps ahead (-1: none),
                                 // read by the fused kernel's image staging
-  // one-shot xGMI all-reduce hand-off (comm/xgmi_allreduce.hip): when set, the reduced
-  // gradients go straight into this rank's shared region (parity slot of the next
-  // all-reduce step, read from the group's counters) with system-coherent stores, so the
-  // all-reduce kernel skips its publish copy
-  unsigned char* xg_region = nullptr;
-  long long xg_slot_bytes = 0, xg_flag_bytes = 0;
-  const unsigned* xg_ctr = nullptr;
   // one-launch xGMI all-reduce (xp_nranks > 0; region layout: comm/xgmi_layout.h): every
   // reduction block stores each reduced element into this rank's granule slot as ONE 8-byte
   // {value, step} word, reads the same element's granule from every peer until its tag shows

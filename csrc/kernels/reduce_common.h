@@ -37,9 +37,6 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
     a.mom[e] = m;
     a.master[e] = p;
     write_shadow(a.shadow, e, p);
-  } else if (a.xg_region != nullptr) {
-    __hip_atomic_store(reinterpret_cast<unsigned*>(a.grad) + e, __float_as_uint(g), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
     a.grad[e] = g;
   }

@@ -157,13 +157,8 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     __syncthreads();  // every thread read this block's counter before it advances
     if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;
   } else {
-    ReduceArgs d_args = a;
-    if (a.xg_region != nullptr) {  // gradients -> the shared slot of the coming xGMI step
-      const unsigned step = a.xg_ctr[0] + 1u;
-      d_args.grad = reinterpret_cast<float*>(a.xg_region + a.xg_flag_bytes + (step & 1u) * a.xg_slot_bytes);
-    }
     DirectSink d;
-    grad_reduce_body(d_args, d);
+    grad_reduce_body(a, d);
   }
   if (a.stamps != nullptr) __syncthreads();
   reduce_stamp(a, 1);

@@ -135,33 +135,17 @@ class XgmiGroup:
                 self.opened.append(p)
                 regions.append(p)
         self.regions = regions
-        # The shared bytes always move with sc0 sc1 (system-coherent) accesses, and the flag
-        # is stored only after the data stores were acknowledged.  With every rank on ONE
-        # device and uncached regions that is the whole hand-off (measured on one MI355X with
-        # up to 8 ranks).  Across distinct GPUs the hand-off also gets the system-scope
-        # release/acquire fences (bit 0 / bit 1; measured cost 0.6 us per step) until a
-        # multi-GPU --check-sync run validates the fence-free variant there; a cached
-        # fallback region always gets them.  DNN_XGMI_FENCES overrides.
+        # Every shared byte moves as part of a {value, step} granule written and read with
+        # single 64-bit system-scope atomics (csrc/comm/xgmi_layout.h): a reader that sees the
+        # step sees the value, so the hand-off needs no flag and no fence on any topology.
         self.devices = len(set(device_ids)) if device_ids else 1
-        fences = os.environ.get("DNN_XGMI_FENCES")
-        if fences is not None:
-            self.fences = int(fences)
-        else:
-            self.fences = 0 if (self.kind == "uncached" and self.devices == 1) else 3
 
     # -- launches --------------------------------------------------------------------------
-    def handoff(self) -> dict:
-        """grad_reduce kwargs that make it store the reduced gradients straight into this
-        rank's shared slot (then ``allreduce_sgd(..., prepublished=True)``)."""
-        return dict(xg_region=self.local, xg_slot_bytes=self.ext.xgmi_slot_bytes(self.capacity),
-                    xg_flag_bytes=self.ext.xgmi_flag_bytes(self.capacity), xg_ctr=self.ctr.data_ptr())
-
     def exchange(self) -> dict:
         """grad_reduce kwargs of the one-launch all-reduce: every reduction lane publishes its
         reduced elements as {value, step} granules, reads the same elements' granules from
         every peer and applies the averaged update itself (no separate all-reduce launch, no
-        hand-off inside the GPU, no flag: the step tag travels in the value's atomic word, so
-        this path needs no fences on any topology)."""
+        hand-off inside the GPU, no flag: the step tag travels in the value's atomic word)."""
         err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
         return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
                     xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
@@ -172,16 +156,15 @@ class XgmiGroup:
         self.ctr[-1].zero_()
 
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, mom: torch.Tensor, shadow: torch.Tensor | None,
-                      lr: float, momentum: float, n: int | None = None, prepublished: bool = False) -> None:
-        """grad <- avg over ranks; momentum SGD on master/mom (+ bf16 shadow images).
-        ``prepublished``: the gradients are already in the shared slot (``handoff``)."""
+                      lr: float, momentum: float, n: int | None = None) -> None:
+        """grad <- avg over ranks; momentum SGD on master/mom (+ bf16 shadow images)."""
         n = grad.numel() if n is None else n
         s = torch.cuda.current_stream(grad.device).cuda_stream
         mode = 1 if shadow is not None else 2
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, n, grad.data_ptr(), grad.data_ptr(),
                                 master.data_ptr(), mom.data_ptr(), shadow.data_ptr() if shadow is not None else 0,
                                 lr, momentum, 1.0 / self.world, mode, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, self.fences, int(prepublished), s)
+                                self.timeout_s, s)
 
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place average of a flat fp32 tensor."""
@@ -189,7 +172,7 @@ class XgmiGroup:
         s = torch.cuda.current_stream(t.device).cuda_stream
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, t.numel(), t.data_ptr(), t.data_ptr(),
                                 0, 0, 0, 0.0, 0.0, 1.0 / self.world, 0, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, self.fences, 0, s)
+                                self.timeout_s, s)
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
@@ -284,14 +267,11 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
         ok, why = False, "a peer could not map the regions"
     else:
         comm.gather_scalars(0.0)
-    votes = comm.gather_scalars(1.0 if ok else 0.0)  # (also: every peer finished reading our slots)
-    if grp is not None and all(v == 1.0 for v in votes):
-        with torch.cuda.device(comm.device):
-            grp.ext.xgmi_clear_slots(grp.local, grp.capacity)
+    votes = comm.gather_scalars(1.0 if ok else 0.0)
     if os.environ.get("DNN_DEBUG_XGMI") == "1":
         print(f"[xgmi] gen {comm.generation} rank {comm.rank}/{comm.world} ok={ok} {why} votes={votes} "
               f"regions={[hex(r) for r in grp.regions] if grp is not None and ok else None} "
-              f"kind={getattr(grp, 'kind', None)} fences={getattr(grp, 'fences', None)}", file=sys.stderr, flush=True)
+              f"kind={getattr(grp, 'kind', None)} devices={getattr(grp, 'devices', None)}", file=sys.stderr, flush=True)
     if all(v == 1.0 for v in votes):
         return grp
     if grp is not None:

@@ -363,11 +363,10 @@ class HipEngine(Engine):
                 # and applies the averaged momentum-SGD update + bf16 images itself
                 self._reduce(1, 0, LAYOUT.total, 1, s, **grp.exchange())
                 return
-            # two launches: batch reduction -> shared slot; one-shot xGMI all-reduce kernel
-            # [flags, 1 hop, rank-order sum, momentum SGD, bf16 weight images] (parallel/xgmi.py)
-            self._reduce(0, 0, LAYOUT.total, 1, s, **grp.handoff())  # reduced grads -> shared slot
-            grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum, LAYOUT.total,
-                              prepublished=True)
+            # two launches: batch reduction -> grad; one-shot xGMI all-reduce kernel [publish,
+            # 1 hop, rank-order sum, momentum SGD, bf16 weight images] (parallel/xgmi.py)
+            self._reduce(0, 0, LAYOUT.total, 1, s)
+            grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr, self.momentum, LAYOUT.total)
             return
         mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
         if self.overlap:
@@ -384,7 +383,7 @@ class HipEngine(Engine):
 
     def selftest_exchange(self, grp, comm, steps: int = 2) -> bool:
         """Collective: does the one-launch all-reduce (``grp.exchange()``) reproduce the
-        two-launch path (reduce -> shared slot, xGMI all-reduce kernel) BIT FOR BIT on every
+        two-launch path (batch reduce, then the xGMI all-reduce kernel) BIT FOR BIT on every
         rank?  Random per-rank reduction inputs, both parity slots; the engine's parameters,
         optimizer state and buffers are restored afterwards.  Every rank returns the same vote."""
         dev = self.device
@@ -413,9 +412,9 @@ class HipEngine(Engine):
                             if one_launch:
                                 self._reduce(1, 0, LAYOUT.total, 0, s, **grp.exchange())
                             else:
-                                self._reduce(0, 0, LAYOUT.total, 0, s, **grp.handoff())
+                                self._reduce(0, 0, LAYOUT.total, 0, s)
                                 grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
-                                                  self.momentum, LAYOUT.total, prepublished=True)
+                                                  self.momentum, LAYOUT.total)
                         torch.cuda.synchronize(dev)
                         results.append((self.master.cpu(), self.mom.cpu(), self.shadow.cpu()))
                 except Exception as e:
