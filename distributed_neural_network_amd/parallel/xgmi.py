@@ -1,21 +1,27 @@
-"""One-shot xGMI all-reduce for the per-step gradient (csrc/comm/xgmi_allreduce.hip).
+"""One-hop xGMI all-reduce for the per-step gradient (csrc/comm/xgmi_allreduce.hip and the
+one-launch exchange in csrc/kernels/reduce_sgd.hip).
 
 Why a second collective path next to RCCL: the step-allreduce gradient is 248 KB, so the
 collective is pure latency.  RCCL's ring (or tree) walks 2 (N-1) dependent hops over
 single links; an 8x MI355X node is a full xGMI mesh, so one hop suffices: every rank
-publishes its gradient in an IPC-shared region, pushes a step flag to each peer, and
-reads all N regions over the 7 links at once.  The kernel sums in rank order (replicas
-stay bit-identical), scales by 1/N and applies the momentum-SGD update in the same launch
-- it replaces ``ncclAllReduce`` + ``sgd_apply`` inside the captured step graph.
+publishes its gradient in an IPC-shared region as {value, step} granules (one 64-bit word
+per element) and reads the same elements from all N regions over the 7 links at once,
+until every tag shows the current step.  The sum runs in rank order (replicas stay
+bit-identical), is scaled by 1/N and feeds the momentum-SGD update in the same launch - it
+replaces ``ncclAllReduce`` + ``sgd_apply`` inside the captured step graph.  With the fused
+engine the exchange runs inside the batch-reduction kernel itself (``exchange()``): one
+launch for reduce + all-reduce + SGD.
 
 Scope: one node (all ranks share the xGMI mesh), 1..8 ranks, a GPU engine.  At set-up the
-group runs a self-test (three steps against a known pattern: both parity slots, all
-flags) and every rank votes through the process group; if any rank fails (IPC refused,
-wrong sums, timeout), every rank falls back to the native RCCL path together.
-RCCL stays the transport for everything else (broadcast, epoch averaging, eval metrics).
+group runs a self-test (random data, both parity slots, exact against a host rank-order
+sum) and every rank votes through the process group; if any rank fails (IPC refused,
+wrong sums, timeout), every rank falls back to the native RCCL path together.  The engine
+then checks the one-launch exchange against the two-launch path (``HipEngine.
+selftest_exchange``).  RCCL stays the transport for everything else (broadcast, epoch
+averaging, eval metrics).
 
-Fault tolerance: the kernel's flag wait is bounded (timeout, plus a host-mapped abort
-word the fault watchdog sets through ``Communicator.abort``); a failed wait sets a sticky
+Fault tolerance: every granule wait is bounded (timeout, plus a host-mapped abort word the
+fault watchdog sets through ``Communicator.signal_lost``); a failed wait sets a sticky
 device error word instead of hanging, and ``check()`` raises ``CommError`` at the next
 epoch boundary, which the trainer's recovery path handles like any other comm failure.
 After ``Communicator.reform`` the group is rebuilt over the survivors.
@@ -72,7 +78,7 @@ def one_launch_wanted() -> bool:
 
 
 def wait_timeout(comm: Communicator) -> float:
-    """Bound of one flag wait.  A live straggler (``--failure-duration`` sleeps before its
+    """Bound of one granule wait.  A live straggler (``--failure-duration`` sleeps before its
     epoch) must not be mistaken for a dead peer: the bound covers the longest injected
     sleep twice over, plus the base minute."""
     return 60.0 + 2.0 * float(getattr(comm, "straggler_s", 0.0) or 0.0)
