@@ -454,9 +454,11 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       Ps[(r * g.Wp + (k < g.pad ? k : g.W + k)) * CCP + c] = (T)0.f;
     }
   }
-  uint4 areg[AV];
+  // native vector types, not HIP's uint4 / float4 structs: arrays of those were copied to
+  // scratch memory (112 B per lane) instead of living in registers
+  u32x4 areg[AV];
   float preg[PV];
-  float4 greg[PG];
+  f32x4 greg[PG];
   auto p_val = [&](int row, int xp, int c0) {  // remainder path
     const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
     const bool ok = r < g.R && c0 + c < g.C && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
@@ -468,12 +470,12 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   };
   auto load_batch = [&](int c0) {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) areg[i] = *reinterpret_cast<const uint4*>(wp + aoff[i] + c0);
+    for (int i = 0; i < AV; ++i) areg[i] = *reinterpret_cast<const u32x4*>(wp + aoff[i] + c0);
     const unsigned cb = (unsigned)c0 * cstep;
     if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < PG; ++i)
-        greg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(goff[i] + cb), 0, 0));
+        greg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(goff[i] + cb), 0, 0));
     } else {
 #pragma unroll
       for (int i = 0; i < PV; ++i)
@@ -482,14 +484,14 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   };
   auto store_batch = [&](int c0) {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) *reinterpret_cast<uint4*>(As + adst[i]) = areg[i];
+    for (int i = 0; i < AV; ++i) *reinterpret_cast<u32x4*>(As + adst[i]) = areg[i];
     if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < PG; ++i) {
-        As[gdst[i]] = (T)greg[i].x;
-        As[gdst[i] + CCP] = (T)greg[i].y;
-        As[gdst[i] + 2 * CCP] = (T)greg[i].z;
-        As[gdst[i] + 3 * CCP] = (T)greg[i].w;
+        As[gdst[i]] = (T)greg[i][0];
+        As[gdst[i] + CCP] = (T)greg[i][1];
+        As[gdst[i] + 2 * CCP] = (T)greg[i][2];
+        As[gdst[i] + 3 * CCP] = (T)greg[i][3];
       }
       for (int e = tid + PG * CT; e < ng; e += CT) {  // remainder groups
         const int row = e / G, gx = e - row * G, r = row / CCH, c = row - r * CCH, iy = iy0 + r;
@@ -507,8 +509,8 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
     for (int v = tid + AV * CT; v < nv; v += CT) {
       const int row = v / VPR, u = v - row * VPR;
       const int tap = row / BM, m = row - tap * BM;
-      *reinterpret_cast<uint4*>(As + row * CCP + u * VE) =
-          *reinterpret_cast<const uint4*>(wp + (tap * g.Mp + m0 + m) * g.Cp + u * VE + c0);
+      *reinterpret_cast<u32x4*>(As + row * CCP + u * VE) =
+          *reinterpret_cast<const u32x4*>(wp + (tap * g.Mp + m0 + m) * g.Cp + u * VE + c0);
     }
     for (int e = V4 ? np : tid + PV * CT; e < np; e += CT) {
       const int row = e / g.Wp, xp = e - row * g.Wp;

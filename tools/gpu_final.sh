@@ -8,6 +8,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
   > gpurun_out/final/t.log 2>&1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/final/bench.json 2> gpurun_out/final/bench.err
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/final/bench_k20.json 2> gpurun_out/final/bench_k20.err
 for m in "cifar-vgg bf16" "cifar-vgg fp32" "lenet-bn fp32" "lenet fp32"; do set -- $m
   timeout -k 10 300 python bench.py --model $1 --dtype $2 --engine layers --steps 300 --warmup 30 --no-epoch \
     > gpurun_out/final/b_$1_$2.json 2> gpurun_out/final/b_$1_$2.err
