@@ -4,12 +4,25 @@ import csv
 import glob
 import sys
 
+# usage: python tools/pmc_summary.py ROOT [KERNEL_PATTERN] - ROOT holds one directory per
+# counter pass, each with the CSV output (run_counter_collection.csv) or the rocpd database
+# (run_results.db) that rocprofv3 writes
 root, pattern = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "lenet_fused_kernelILb1"
 agg = collections.defaultdict(list)
 for f in glob.glob(f"{root}/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if pattern in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for f in glob.glob(f"{root}/*/run_results.db"):
+    import sqlite3
+
+    db = sqlite3.connect(f)
+    per = collections.defaultdict(float)  # (dispatch, counter) -> value summed over its instances
+    for name, disp, cname, val in db.execute("select name, dispatch_id, counter_name, counter_value from pmc_events"):
+        if pattern in name:
+            per[(disp, cname)] += float(val)
+    for (_, cname), v in per.items():
+        agg[cname].append(v)
 med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
 for k in sorted(med):
     print(f"{k:28s} median {med[k]:12.4g}  (n={len(agg[k])})")
