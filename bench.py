@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--diag-windows", type=int, default=0,
+                    help="diagnostic: time this many extra K-step windows after the reported one (stderr)")
     ap.add_argument("--train-samples", type=int, default=50_000,
                     help="synthetic training-set size (CIFAR-10: 50,000); smaller = more epoch boundaries "
                          "inside the timed window (diagnostic)")
@@ -165,16 +167,37 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(device)
 
+    diag = args.diag_windows > 0
+    if diag:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
     t0 = time.perf_counter()
     cur.run(args.steps)
+    if diag:
+        ev[1].record()
     torch.cuda.synchronize(device)
     comm.barrier()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
+    if diag:
+        print(f"[bench] reported window: {1e6 * dt / args.steps:.2f} us/step wall, "
+              f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
     if getattr(engine, "sync_error", lambda: False)():
         raise RuntimeError("in-launch reducer hand-off timed out (sync error flag set)")
     if hasattr(engine.grad_sync, "check"):
         engine.grad_sync.check()  # raises if any xGMI wait in the timed window timed out
+    for _ in range(args.diag_windows):  # diagnostic only: the reported window is the first one
+        comm.barrier()
+        torch.cuda.synchronize(device)
+        ev[0].record()
+        t1 = time.perf_counter()
+        cur.run(args.steps)
+        ev[1].record()
+        torch.cuda.synchronize(device)
+        comm.barrier()
+        torch.cuda.synchronize(device)
+        print(f"[bench] extra window: {1e6 * (time.perf_counter() - t1) / args.steps:.2f} us/step wall, "
+              f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
     dt = comm.reduce_scalar(dt, "max")
     ms_per_step = 1000.0 * dt / args.steps
     value = comm.world * B * args.steps / dt
