@@ -157,7 +157,12 @@ def main():
     # D2H, host ops), then the W warmup steps LAST, so the timed window starts on a busy,
     # clocked-up GPU right behind them (a host-side gap here shows up in short runs)
     cur._next_epoch()
-    engine.prepare_graphs()
+    if isinstance(engine, HipEngine):
+        # the timed window as ONE graph replay when it fits in the current epoch (a 20-step
+        # window: one launch instead of 16 + 4; profiles/r2/window/)
+        engine.prepare_graphs(exact=(args.steps,) if args.steps <= min(512, cur.left - args.warmup) else ())
+    else:
+        engine.prepare_graphs()
     if not args.no_epoch:
         wl, wc = engine.evaluate_samples(test_dev, 0, len(test))
         wl2, wc2 = torch.zeros_like(wl), torch.zeros_like(wc, dtype=torch.float32)
