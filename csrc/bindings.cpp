@@ -141,6 +141,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
      py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
   m.def("init", []() { dnn::init_kernels(); });
+  // ---- Linear layers on MFMA (kernels/linear.hip) ----
+  m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {
+    dnn::launch_linear_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), B, K, N, relu,
+                           S(stream));
+  });
+  m.def("linear_dgrad", [](u dy, u y, u w, u dx, int B, int K, int N, u stream) {
+    dnn::launch_linear_dgrad(P<const float>(dy), P<const float>(y), P<const float>(w), P<float>(dx), B, K, N,
+                             S(stream));
+  });
+  m.def("linear_wgrad", [](u dy, u y, u x, u dw, u db, int B, int K, int N, u stream) {
+    dnn::launch_linear_wgrad(P<const float>(dy), P<const float>(y), P<const float>(x), P<float>(dw), P<float>(db), B,
+                             K, N, S(stream));
+  });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
     dnn::launch_ingest(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(ids), batch, per_img,

@@ -110,5 +110,13 @@ void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, f
                             int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
+// Linear layers on MFMA (linear.hip): y = act(x W^T + b); dx = dz W; dW = dz^T x, db = sum_b dz,
+// dz = dy masked by y > 0 when y != nullptr (fused ReLU)
+void launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int B, int K, int N, int relu,
+                       hipStream_t s);
+void launch_linear_dgrad(const float* dy, const float* y, const float* w, float* dx, int B, int K, int N,
+                         hipStream_t s);
+void launch_linear_wgrad(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N,
+                         hipStream_t s);
 
 }  // namespace dnn

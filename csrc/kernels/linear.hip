@@ -1,0 +1,150 @@
+// Linear layers of the generic layer engine on MFMA (gfx950): forward, data gradient and
+// weight + bias gradient of y = x W^T + b, with an optional fused ReLU.
+//
+// Capability parity: aten::addmm / mm / sum(dim 0) / relu / threshold_backward of the fc layers
+//  for any zoo model (lenet: 400-120-84-10, cifar-vgg:
+// 4096-256-10) at batch B.  These GEMMs are tiny (B = 64 rows), so the library GEMM picked
+// single-workgroup tiles that ran 5-19 us each (profiles/r2/linear/); here every 16 x 16
+// output tile is its own workgroup, the reduction is split over up to 16 waves of it and
+// summed in a fixed order through LDS (deterministic, no atomics), and every operand load of a
+// 16-step batch is in flight before its first MFMA.
+//
+//   forward : y[b][n]  = act(sum_k x[b][k] W[n][k] + bias[n])        act = ReLU if relu
+//   dgrad   : dx[b][k] = sum_n dz[b][n] W[n][k]                       dz = dy * (y > 0) if relu
+//   wgrad   : dW[n][k] = sum_b dz[b][n] x[b][k],  db[n] = sum_b dz[b][n]  (the "ones" column k = K)
+//
+// All three are C[M][N] = sum_k A(m, k) B(k, n) on v_mfma_f32_16x16x4_f32 (exact fp32
+// products, fp32 accumulation: the layer engine's Linear math stays fp32 in both dtype modes)
+// with strided operand views; A may carry the ReLU mask of a saved activation.
+#include <algorithm>
+#include <stdexcept>
+
+#include "launchers.h"
+
+namespace dnn {
+namespace {
+
+constexpr int LIN_MAX_WAVES = 16;
+
+struct GemmArgs {
+  const float* a;  long a_m, a_k;   // A(m, k) = a[m * a_m + k * a_k]
+  const float* am;                  // optional ReLU mask source: A(m, k) *= (am[same index] > 0)
+  const float* b;  long b_k, b_n;   // B(k, n) = b[k * b_k + n * b_n];  n == ones_col -> 1
+  float* c;        long c_m;        // C[m][n] = c[m * c_m + n] for n < N
+  float* c_ones;                    // C[m][ones_col] -> c_ones[m]  (bias gradient)
+  const float* bias;                // + bias[n]
+  int M, N, K, ones_col;            // ones_col = -1: none
+  int relu;                         // forward: ReLU on the output
+  int kpw;                          // reduction elements per wave (multiple of 64)
+};
+
+// one 16 x 16 output tile per workgroup; wave w reduces k in [w kpw, (w + 1) kpw).  Every
+// operand load of a 16-step batch is unconditional (clamped, in-bounds address) and issued
+// before the first MFMA; out-of-range and masked operands are zeroed by selects afterwards
+// (a load under a per-element branch made the compiler wait for it at the branch join:
+// 16-32 serial memory latencies per batch).  MASK: A is multiplied by (am > 0).
+template <bool MASK>
+__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(GemmArgs g) {
+  __shared__ f32x4 red[LIN_MAX_WAVES][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  const int m = m0 + i, n = n0 + i;
+  const bool mv = m < g.M, nv = n < g.N, ones = n == g.ones_col;
+  const long ma = (long)min(m, g.M - 1) * g.a_m, nb = (long)min(n, g.N - 1) * g.b_n;
+  const int k_lo = wave * g.kpw, k_hi = min(g.K, k_lo + g.kpw);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = k_lo; k0 < k_hi; k0 += 64) {
+    float av[16], bv[16], mk[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const long kc = min(k0 + 4 * s + kq, g.K - 1);
+      av[s] = g.a[ma + kc * g.a_k];
+      if constexpr (MASK) mk[s] = g.am[ma + kc * g.a_k];
+      bv[s] = g.b[kc * g.b_k + nb];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all 32 (48) loads in flight before the first use
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool kin = k0 + 4 * s + kq < k_hi;
+      bool aon = kin && mv;
+      if constexpr (MASK) aon = aon && mk[s] > 0.f;
+      av[s] = aon ? av[s] : 0.f;
+      bv[s] = kin ? (ones ? 1.f : (nv ? bv[s] : 0.f)) : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  f32x4 sum = red[0][lane];
+  for (int w = 1; w < nw; ++w) sum += red[w][lane];  // fixed order: deterministic
+  // lane (i, kq) holds C[m0 + 4 kq + r][n0 + i], r = 0..3
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mm = m0 + 4 * kq + r;
+    if (mm >= g.M) continue;
+    float v = sum[r];
+    if (ones) {
+      g.c_ones[mm] = v;
+      continue;
+    }
+    if (!nv) continue;
+    if (g.bias != nullptr) v += g.bias[n];
+    if (g.relu) v = fmaxf(v, 0.f);
+    g.c[(long)mm * g.c_m + n] = v;
+  }
+}
+
+void launch(GemmArgs g, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0 || g.K <= 0) throw std::runtime_error("linear: empty GEMM");
+  const int ncols = g.ones_col >= 0 ? g.ones_col + 1 : g.N;
+  // waves per tile: one 64-deep batch each (all of a tile's loads in flight at once), at most
+  // 16 waves; longer reductions loop
+  const int nw = std::max(1, std::min(LIN_MAX_WAVES, (g.K + 63) / 64));
+  g.kpw = ((g.K + nw - 1) / nw + 63) / 64 * 64;
+  const int used = (g.K + g.kpw - 1) / g.kpw;
+  dim3 grid((unsigned)((ncols + 15) / 16), (unsigned)((g.M + 15) / 16));
+  if (g.am != nullptr) hipLaunchKernelGGL(small_gemm_kernel<true>, grid, dim3(64 * used), 0, s, g);
+  else hipLaunchKernelGGL(small_gemm_kernel<false>, grid, dim3(64 * used), 0, s, g);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+// y[B][N] = act(x[B][K] W[N][K]^T + b)
+void launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int B, int K, int N, int relu,
+                       hipStream_t s) {
+  GemmArgs g{};
+  g.a = x; g.a_m = K; g.a_k = 1;
+  g.b = w; g.b_k = 1; g.b_n = K;
+  g.c = y; g.c_m = N;
+  g.bias = b;
+  g.M = B; g.N = N; g.K = K; g.ones_col = -1; g.relu = relu;
+  launch(g, s);
+}
+
+// dx[B][K] = dz[B][N] W[N][K], dz = dy masked by y > 0 when y != nullptr (fused ReLU)
+void launch_linear_dgrad(const float* dy, const float* y, const float* w, float* dx, int B, int K, int N,
+                         hipStream_t s) {
+  GemmArgs g{};
+  g.a = dy; g.am = y; g.a_m = N; g.a_k = 1;
+  g.b = w; g.b_k = K; g.b_n = 1;
+  g.c = dx; g.c_m = K;
+  g.M = B; g.N = K; g.K = N; g.ones_col = -1;
+  launch(g, s);
+}
+
+// dW[N][K] = dz^T x, db[N] = sum_b dz[b][n] (dz as in dgrad)
+void launch_linear_wgrad(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N,
+                         hipStream_t s) {
+  GemmArgs g{};
+  g.a = dy; g.am = y; g.a_m = 1; g.a_k = N;  // A(m = n, k = b) = dz[b][n]
+  g.b = x; g.b_k = K; g.b_n = 1;             // B(k = b, n = k') = x[b][k'],  k' == K: 1
+  g.c = dw; g.c_m = K; g.c_ones = db;
+  g.M = N; g.N = K; g.K = B; g.ones_col = K;
+  launch(g, s);
+}
+
+}  // namespace dnn

@@ -31,6 +31,7 @@ HIP_SOURCES = [
     CSRC / "kernels" / "reduce_sgd.hip",
     CSRC / "kernels" / "layers.hip",
     CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "linear.hip",
     CSRC / "comm" / "xgmi_allreduce.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"

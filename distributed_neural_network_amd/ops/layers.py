@@ -19,6 +19,8 @@ CrossEntropyLoss (mean), SGD-momentum.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -205,22 +207,80 @@ class ReluFn(torch.autograd.Function):
 
 
 # ---- Linear ---------------------------------------------------------------------------------
+# GEMMs up to this many multiply-adds run on the hand-written MFMA kernels (linear.hip); the
+# library GEMM only wins on the large ones (cifar-vgg fc1, 64 x 4096 x 256: 7 us vs 17-31 us),
+# while it runs the small ones as single-workgroup tiles (lenet fc1 forward: 19 us vs 5-9 us;
+# profiles/r2/linear/).  DNN_LINEAR_MFMA_MAX overrides (0: library everywhere).
+LINEAR_MFMA_MAX_MACS = int(os.environ.get("DNN_LINEAR_MFMA_MAX", 16 << 20))
+
+
 class LinearFn(torch.autograd.Function):
-    """y = x W^T + b; fp32 GEMMs carry the bias in the GEMM epilogue (addmm).  ``gw`` /
-    ``gb``: gradient arena views written in place (see Conv2dFn)."""
+    """y = act(x W^T + b), act = ReLU when ``relu`` (the following zoo ReLU fused in).
+
+    GPU: hand-written MFMA kernels (csrc/kernels/linear.hip) for every GEMM of at most
+    ``LINEAR_MFMA_MAX_MACS`` multiply-adds: forward with bias + ReLU in the epilogue; backward
+    as ONE data-gradient and ONE weight-gradient launch, the bias gradient coming out of the
+    weight-gradient MFMAs (an all-ones column) and the ReLU mask applied on the operand loads
+    (no relu / threshold_backward / sum kernels).  Larger GEMMs use the library GEMM.  fp32
+    operands and accumulation in both dtype modes (``gemm_dtype`` only affects the CPU
+    oracle path).  CPU: addmm / mm (+ relu).  ``gw`` / ``gb``: gradient arena views written
+    in place (see Conv2dFn)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gemm_dtype: torch.dtype, gw=None, gb=None):
-        ctx.save_for_backward(x, w)
+    def forward(ctx, x, w, b, gemm_dtype: torch.dtype, gw=None, gb=None, relu: bool = False):
         ctx.gemm_dtype = gemm_dtype
-        ctx.gw, ctx.gb = gw, gb
+        ctx.gw, ctx.gb, ctx.relu = gw, gb, relu
+        if _is_gpu(x):
+            x = x.contiguous()
+            B, K = x.shape
+            N = w.shape[0]
+            if B * K * N <= LINEAR_MFMA_MAX_MACS:
+                y = torch.empty(B, N, device=x.device, dtype=torch.float32)
+                _ext().linear_fwd(_p(x), _p(w), _p(b), _p(y), B, K, N, int(relu), _s(x))
+            else:
+                y = torch.addmm(b, x, w.t())
+                if relu:
+                    y.relu_()
+            ctx.save_for_backward(x, w, y if relu else None)
+            return y
         if gemm_dtype == torch.float32:
-            return torch.addmm(b, x, w.t())
-        return _gemm(x, w.t(), gemm_dtype) + b
+            y = torch.addmm(b, x, w.t())
+        else:
+            y = _gemm(x, w.t(), gemm_dtype) + b
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
+        if _is_gpu(dy):
+            dy = dy.contiguous()
+            B, K = x.shape
+            N = w.shape[0]
+            ext, st = _ext(), _s(dy)
+            small = B * K * N <= LINEAR_MFMA_MAX_MACS
+            gw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
+            gb = ctx.gb if ctx.gb is not None else torch.empty(N, device=dy.device, dtype=torch.float32)
+            dx = None
+            if small:
+                ym = _p(y) if y is not None else 0
+                if ctx.needs_input_grad[0]:
+                    dx = torch.empty(B, K, device=dy.device, dtype=torch.float32)
+                    ext.linear_dgrad(_p(dy), ym, _p(w), _p(dx), B, K, N, st)
+                ext.linear_wgrad(_p(dy), ym, _p(x), _p(gw), _p(gb), B, K, N, st)
+            else:
+                dz = dy * (y > 0) if y is not None else dy
+                if ctx.needs_input_grad[0]:
+                    dx = torch.mm(dz, w)
+                torch.mm(dz.t(), x, out=gw)
+                torch.sum(dz, 0, out=gb)
+            if ctx.gw is not None:
+                return dx, None, None, None, None, None, None
+            return dx, gw, gb, None, None, None, None
+        if y is not None:
+            dy = dy * (y > 0)
         dx = _gemm(dy, w, ctx.gemm_dtype) if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
             if ctx.gemm_dtype == torch.float32:
@@ -228,8 +288,8 @@ class LinearFn(torch.autograd.Function):
             else:
                 ctx.gw.copy_(_gemm(dy.t(), x, ctx.gemm_dtype))
             torch.sum(dy, 0, out=ctx.gb)
-            return dx, None, None, None, None, None
-        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None, None, None
+            return dx, None, None, None, None, None, None
+        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None, None, None, None
 
 
 # ---- BatchNorm2d (train: masked batch statistics; eval: running statistics) -----------------

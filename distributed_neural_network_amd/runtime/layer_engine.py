@@ -185,10 +185,11 @@ class LayerEngine(Engine):
             elif isinstance(layer, zoo.Flatten):
                 x = x.reshape(x.shape[0], -1)
             elif isinstance(layer, zoo.FC):
-                # Linear stays fp32 in both modes: the fc GEMMs are < 0.3 GFLOP per step, and
-                # bf16 operands would cost six cast kernels per layer and step (measured:
-                # ~90 us per cifar-vgg step) for no MFMA gain at these sizes
-                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], torch.float32, gw, gb)
+                # Linear stays fp32 in both modes: the fc GEMMs are < 0.3 GFLOP per step (fp32
+                # MFMA, linear.hip); on the GPU a following ReLU is fused into it
+                relu = self.gpu and isinstance(nxt, zoo.Relu)
+                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], torch.float32, gw, gb, relu)
+                skip = relu
         return x
 
     def _ingest(self) -> None:

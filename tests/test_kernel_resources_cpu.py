@@ -14,7 +14,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["kernels/lenet_fused.hip", "kernels/reduce_sgd.hip", "kernels/layers.hip", "kernels/conv_igemm.hip",
-           "comm/xgmi_allreduce.hip"]
+           "kernels/linear.hip", "comm/xgmi_allreduce.hip"]
 
 
 def _resources(src, tmp):
@@ -36,7 +36,7 @@ def _resources(src, tmp):
 
 @pytest.mark.skipif(not shutil.which(HIPCC), reason="hipcc not available")
 def test_no_kernel_uses_scratch(tmp_path):
-    with ThreadPoolExecutor(4) as ex:
+    with ThreadPoolExecutor(2) as ex:
         res = list(ex.map(lambda s: _resources(s, str(tmp_path)), SOURCES))
     found = {k: v for r in res for k, v in r.items()}
     assert len(found) > 40, f"resource remarks not parsed: {len(found)} kernels"

@@ -81,6 +81,36 @@ def test_conv2d_bf16_operands_track_fp32(B, C, H, K, pad, Cout):
         _close(tg.grad, tc.grad, 2e-2)
 
 
+@pytest.mark.parametrize("B,K,N", [(64, 400, 120), (64, 120, 84), (3, 84, 10), (64, 4096, 256), (17, 130, 33),
+                                   (1, 5, 1)])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("arena", [False, True])
+@pytest.mark.parametrize("mfma_max", [None, 0])
+def test_linear_mfma_fwd_bwd(B, K, N, relu, arena, mfma_max, monkeypatch):
+    """linear.hip (forward + bias + fused ReLU, data gradient, weight gradient with the bias
+    gradient from the all-ones column, ReLU mask on the operand loads) vs the fp32 CPU path;
+    arena=True writes the parameter gradients into preallocated views (the engine's mode)."""
+    if mfma_max is not None:  # 0: the library-GEMM path for every size
+        monkeypatch.setattr(L, "LINEAR_MFMA_MAX_MACS", mfma_max)
+    else:  # the MFMA kernels for every size
+        monkeypatch.setattr(L, "LINEAR_MFMA_MAX_MACS", 1 << 40)
+    torch.manual_seed(B * 131 + K + N)
+    x = torch.randn(B, K, requires_grad=True)
+    w = torch.randn(N, K, requires_grad=True) / K ** 0.5
+    b = torch.randn(N, requires_grad=True)
+    g = torch.randn(B, N)
+    res = []
+    for dev in ("cpu", DEV):
+        xx, ww, bb = (t.detach().to(dev).requires_grad_(True) for t in (x, w, b))
+        gw = torch.full((N, K), float("nan"), device=dev) if arena else None
+        gb = torch.full((N,), float("nan"), device=dev) if arena else None
+        y = L.LinearFn.apply(xx, ww, bb, torch.float32, gw, gb, relu)
+        y.backward(g.to(dev))
+        res.append((y, xx.grad, gw if arena else ww.grad, gb if arena else bb.grad))
+    for c, d in zip(res[0], res[1]):
+        _close(d, c, 2e-5)
+
+
 @pytest.mark.parametrize("shape", [(2, 6, 28, 28), (3, 4, 7, 9)])
 def test_relu_pool_fwd_bwd(shape):
     g = torch.Generator().manual_seed(1)
