@@ -131,3 +131,30 @@ def test_split_buckets():
     from distributed_neural_network_amd.parallel.comm import split_buckets
     assert split_buckets([(0, 10)], 0) == [(0, 10)]
     assert split_buckets([(0, 10), (10, 13)], 4) == [(0, 4), (4, 8), (8, 10), (10, 13)]
+
+
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("arena", [False, True])
+def test_linear_fn_cpu_matches_nn_linear(relu, arena):
+    """LinearFn's CPU path (the oracle of linear.hip) with and without the fused ReLU, with
+    gradients into arena views or returned, equals nn.Linear (+ F.relu) under autograd."""
+    from distributed_neural_network_amd.ops import layers as L
+
+    torch.manual_seed(3)
+    lin = torch.nn.Linear(37, 11)
+    x = torch.randn(5, 37, requires_grad=True)
+    g = torch.randn(5, 11)
+    y_ref = lin(x)
+    if relu:
+        y_ref = F.relu(y_ref)
+    y_ref.backward(g)
+    x2 = x.detach().clone().requires_grad_(True)
+    w2, b2 = lin.weight.detach().clone().requires_grad_(True), lin.bias.detach().clone().requires_grad_(True)
+    gw = torch.zeros_like(w2) if arena else None
+    gb = torch.zeros_like(b2) if arena else None
+    y = L.LinearFn.apply(x2, w2, b2, torch.float32, gw, gb, relu)
+    y.backward(g)
+    assert torch.allclose(y, y_ref, atol=1e-6)
+    assert torch.allclose(x2.grad, x.grad, atol=1e-6)
+    assert torch.allclose(gw if arena else w2.grad, lin.weight.grad, atol=1e-6)
+    assert torch.allclose(gb if arena else b2.grad, lin.bias.grad, atol=1e-6)
