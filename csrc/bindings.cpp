@@ -154,6 +154,16 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_linear_wgrad(P<const float>(dy), P<const float>(y), P<const float>(x), P<float>(dw), P<float>(db), B,
                              K, N, S(stream));
   });
+  m.def("linear_fwd_xent", [](u x, u w, u b, u y, u labels, u state, u loss, u correct, u dlogits, int B, int K,
+                              int N, u stream) {
+    dnn::launch_linear_fwd_xent(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
+                                P<const int32_t>(labels), P<const int32_t>(state), P<float>(loss), P<int32_t>(correct),
+                                P<float>(dlogits), B, K, N, S(stream));
+  });
+  m.def("linear_bwd", [](u dy, u y, u w, u x, u dx, u dw, u db, int B, int K, int N, u stream) {
+    dnn::launch_linear_bwd(P<const float>(dy), P<const float>(y), P<const float>(w), P<const float>(x), P<float>(dx),
+                           P<float>(dw), P<float>(db), B, K, N, S(stream));
+  });
   // ---- generic layer kernels (kernels/layers.hip), used by runtime/layer_engine.py ----
   m.def("ingest", [](u images, u labels, u ids, int batch, int per_img, u out, u lab_out, u stream) {
     dnn::launch_ingest(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(ids), batch, per_img,
@@ -207,8 +217,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_xent(P<const float>(logits), P<const int32_t>(labels), B, NC, P<const int32_t>(state), P<float>(loss),
                      P<int32_t>(correct), P<float>(dlogits), S(stream));
   });
-  m.def("layer_bookkeeping", [](u loss, u correct, int batch, u state, u stats, u order, int order_len,
-                                u batch_ids, u stream) {
+  auto book_args = [](u loss, u correct, int batch, u state, u stats, u order, int order_len, u batch_ids) {
     dnn::ReduceArgs a{};
     a.loss = P<const float>(loss);
     a.correct = P<const int32_t>(correct);
@@ -218,7 +227,26 @@ PYBIND11_MODULE(_dnn_hip, m) {
     a.order = P<const int32_t>(order);
     a.order_len = order_len;
     a.batch_ids = P<int32_t>(batch_ids);
-    dnn::launch_layer_bookkeeping(a, S(stream));
+    return a;
+  };
+  m.def("layer_bookkeeping", [book_args](u loss, u correct, int batch, u state, u stats, u order, int order_len,
+                                         u batch_ids, u stream) {
+    dnn::launch_layer_bookkeeping(book_args(loss, correct, batch, state, stats, order, order_len, batch_ids),
+                                  S(stream));
+  });
+  // SGD + packed conv-weight images + bookkeeping (loss == 0: no bookkeeping) in one launch
+  m.def("sgd_tail", [book_args](u p, u g, u mom, long n, float lr, float momentum, float grad_scale,
+                                std::vector<std::tuple<u, u, int, int, int, int, int, int, int, int, int>> jobs,
+                                u arena, u loss, u correct, int batch, u state, u stats, u order, int order_len,
+                                u batch_ids, u stream) {
+    std::vector<dnn::ConvPackJob> js;
+    for (const auto& t : jobs)
+      js.push_back(dnn::ConvPackJob{P<const float>(std::get<0>(t)), P<void>(std::get<1>(t)), std::get<2>(t),
+                                    std::get<3>(t), std::get<4>(t), std::get<5>(t), std::get<6>(t), std::get<7>(t),
+                                    std::get<8>(t), std::get<9>(t), std::get<10>(t)});
+    const dnn::ReduceArgs a = book_args(loss, correct, batch, state, stats, order, order_len, batch_ids);
+    dnn::launch_sgd_tail(P<float>(p), P<const float>(g), P<float>(mom), n, lr, momentum, grad_scale, js.data(),
+                         (int)js.size(), P<const float>(arena), loss != 0 ? &a : nullptr, S(stream));
   });
   m.def("conv_fwd", [](u x, u w, u bias, u y, u ws, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
                        int flip, u stream) {

@@ -790,6 +790,12 @@ void launch_conv_pack_all(const ConvPackJob* jobs, int n, hipStream_t s) {
   }
 }
 
+void conv_pack_geometry(const ConvPackJob& J, int* M, int* C, int* K, int* Mp, int* Cp) {
+  const FastPlan f = plan_fast(J.B, J.C, J.H, J.W, J.M, J.K, J.pad, J.bf16_ops != 0);
+  if (!f.ok) throw std::runtime_error("conv_pack_geometry: layer is not on the LDS-patch path");
+  *M = f.pg.M; *C = f.pg.C; *K = f.pg.K; *Mp = f.pg.Mp; *Cp = f.pg.Cp;
+}
+
 void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, float* y, int B, int C, int H, int W,
                             int M, int K, int pad, int bf16_ops, hipStream_t s) {
   geom(B, C, H, W, K, pad);

@@ -110,6 +110,22 @@ void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, f
                             int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
+// element map of a packed conv-weight image (the LDS-patch plan of the job's layer)
+void conv_pack_geometry(const ConvPackJob& job, int* M, int* C, int* K, int* Mp, int* Cp);
+// conv-weight images the SGD tail refreshes (weight offset in the arena, packed destination)
+struct PackScatter {
+  static constexpr int kMax = 16;
+  struct Item {
+    long off, len;
+    void* dst;
+    int M, C, K, Mp, Cp, flip, bf;
+  } it[kMax];
+  int n;
+};
+// SGD + packed conv-weight images (jobs: conv_pack_all's list; arena: the parameter arena the
+// jobs' weights live in) + the step bookkeeping (book != nullptr) in one launch
+void launch_sgd_tail(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     const ConvPackJob* jobs, int njobs, const float* arena, const ReduceArgs* book, hipStream_t s);
 // Linear layers on MFMA (linear.hip): y = act(x W^T + b); dx = dz W; dW = dz^T x, db = sum_b dz,
 // dz = dy masked by y > 0 when y != nullptr (fused ReLU)
 void launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int B, int K, int N, int relu,
@@ -118,5 +134,10 @@ void launch_linear_dgrad(const float* dy, const float* y, const float* w, float*
                          hipStream_t s);
 void launch_linear_wgrad(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N,
                          hipStream_t s);
+void launch_linear_fwd_xent(const float* x, const float* w, const float* b, float* y, const int32_t* labels,
+                            const int32_t* state, float* loss, int32_t* correct, float* dlogits, int B, int K, int N,
+                            hipStream_t s);
+void launch_linear_bwd(const float* dy, const float* y, const float* w, const float* x, float* dx, float* dw,
+                       float* db, int B, int K, int N, hipStream_t s);
 
 }  // namespace dnn

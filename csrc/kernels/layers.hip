@@ -455,15 +455,51 @@ __global__ void __launch_bounds__(LT) xent_kernel(const float* __restrict__ logi
 __global__ void __launch_bounds__(64) layer_bookkeeping_kernel(ReduceArgs a) { bookkeeping<false>(a, threadIdx.x); }
 
 // ---- flat momentum SGD over an arena (no bf16 shadow: generic models) -------------------------
+// torch.optim.SGD (dampening 0, no nesterov) with the explicit fmas of sgd_update, so the
+// value a packed conv-weight image receives below is bit-identical to the arena's.
 __global__ void __launch_bounds__(LT) sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, long n, float lr, float momentum,
                                                       float grad_scale) {
   const long i = (long)blockIdx.x * LT + threadIdx.x;
   if (i >= n) return;
-  const float gi = g[i] * grad_scale;
-  const float mi = momentum * m[i] + gi;  // torch.optim.SGD: dampening 0, no nesterov
-  m[i] = mi;
-  p[i] -= lr * mi;
+  float pn, mn;
+  sgd_update(g[i] * grad_scale, p[i], m[i], lr, momentum, pn, mn);
+  m[i] = mn;
+  p[i] = pn;
+}
+
+// The step's tail in ONE launch: momentum SGD over the arena; every updated conv weight is also
+// stored into the layer's packed forward / dgrad images (the next step's conv kernels read
+// those: no pack launch at the next step's start); the last workgroup runs the step
+// bookkeeping (epoch loss / accuracy, cursor, next batch ids).
+template <bool BOOK>
+__global__ void __launch_bounds__(LT) sgd_tail_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, long n, float lr, float momentum,
+                                                      float grad_scale, const PackScatter ps, const ReduceArgs book) {
+  if (BOOK && blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < 64) bookkeeping<false>(book, threadIdx.x);
+    return;
+  }
+  const long i = (long)blockIdx.x * LT + threadIdx.x;
+  if (i >= n) return;
+  float pn, mn;
+  sgd_update(g[i] * grad_scale, p[i], m[i], lr, momentum, pn, mn);
+  m[i] = mn;
+  p[i] = pn;
+  for (int j = 0; j < ps.n; ++j) {
+    const PackScatter::Item& it = ps.it[j];
+    const long l = i - it.off;
+    if (l < 0 || l >= it.len) continue;
+    // layer weight [Cout][Cin][K][K]; the image holds (m, c, ky, kx) = (o, ci, y, x), or
+    // (ci, o, K-1-y, K-1-x) for the flipped dgrad image (launch_conv_pack_all's element map)
+    const int KK = it.K * it.K, cin = it.flip ? it.M : it.C;
+    const int x = (int)(l % it.K), y = (int)((l / it.K) % it.K), ci = (int)((l / KK) % cin), o = (int)(l / ((long)KK * cin));
+    const int mm = it.flip ? ci : o, cc = it.flip ? o : ci;
+    const int tap = it.flip ? (it.K - 1 - y) * it.K + (it.K - 1 - x) : y * it.K + x;
+    const long d = ((long)tap * it.Mp + mm) * it.Cp + cc;
+    if (it.bf) reinterpret_cast<bf16*>(it.dst)[d] = (bf16)pn;
+    else reinterpret_cast<float*>(it.dst)[d] = pn;
+  }
 }
 
 inline unsigned blocks(long n) { return (unsigned)((n + LT - 1) / LT); }
@@ -588,6 +624,31 @@ void launch_layer_bookkeeping(const ReduceArgs& a, hipStream_t s) {
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s) {
   if (n) hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks(n)), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale);
+}
+
+void launch_sgd_tail(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     const ConvPackJob* jobs, int njobs, const float* arena, const ReduceArgs* book, hipStream_t s) {
+  PackScatter ps{};
+  if (njobs > PackScatter::kMax) throw std::runtime_error("sgd_tail: too many packed conv images");
+  for (int j = 0; j < njobs; ++j) {
+    const ConvPackJob& J = jobs[j];
+    PackScatter::Item& it = ps.it[ps.n++];
+    conv_pack_geometry(J, &it.M, &it.C, &it.K, &it.Mp, &it.Cp);
+    it.off = J.w - arena;
+    it.len = (long)it.M * it.C * it.K * it.K;
+    if (it.off < 0 || it.off + it.len > n) throw std::runtime_error("sgd_tail: packed weight outside the arena");
+    it.dst = J.dst;
+    it.flip = J.flip;
+    it.bf = J.bf16_ops;
+  }
+  const unsigned nb = blocks(n) + (book != nullptr ? 1u : 0u);
+  if (book != nullptr)
+    hipLaunchKernelGGL(sgd_tail_kernel<true>, dim3(nb), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
+                       *book);
+  else
+    hipLaunchKernelGGL(sgd_tail_kernel<false>, dim3(nb), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
+                       ReduceArgs{});
+  HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dnn

@@ -36,23 +36,83 @@ struct GemmArgs {
   int M, N, K, ones_col;            // ones_col = -1: none
   int relu;                         // forward: ReLU on the output
   int kpw;                          // reduction elements per wave (multiple of 64)
+  int ncols;                        // output columns incl. the ones column (set by prepare)
+  // fused softmax cross-entropy on the forward output (logits; N <= 16 classes, one column tile)
+  const int32_t* labels;            // [M]
+  const int32_t* state;             // device step state: samples >= state[ST_BVALID] are padding
+  float* loss;                      // [M] per-sample loss (0 for padding)
+  int32_t* correct;                 // [M] argmax == label (first maximum wins, like torch.argmax)
+  float* dlogits;                   // [M][N] (softmax - onehot) / valid samples (0 for padding)
 };
+
+// Softmax cross-entropy of the 4 rows m = m0 + 4 kq + r of a logits tile (n0 = 0, N <= 16): the
+// 16 lanes of a kq group hold one row, so its max / first argmax / exp-sum are butterfly
+// reductions over those lanes (xor shuffles: every lane ends with the bit-identical value -
+// fp32 max and add are commutative).  Loss = max + log(sum exp) - z[label]; the whole wave
+// runs this (no lane leaves before a shuffle).
+__device__ __forceinline__ void xent_rows(const GemmArgs& g, const f32x4& sum, const int (&lab)[4], int bvalid, int m0,
+                                          int i, int kq, int lane) {
+  const bool nv = i < g.N;
+  const float bias = (g.bias != nullptr && nv) ? g.bias[i] : 0.f;
+  const float inv = bvalid > 0 ? 1.f / (float)bvalid : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mm = m0 + 4 * kq + r;
+    const float z = nv ? sum[r] + bias : -INFINITY;
+    float mx = z;
+    int am = nv ? i : 16;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const float o = __shfl_xor(mx, off);
+      const int oa = __shfl_xor(am, off);
+      if (o > mx || (o == mx && oa < am)) { mx = o; am = oa; }
+    }
+    const float e = nv ? expf(z - mx) : 0.f;
+    float se = e;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) se += __shfl_xor(se, off);
+    const int y = lab[r];
+    const float zy = __shfl(z, (lane & ~15) | (y & 15));
+    if (mm < g.M) {
+      const bool valid = mm < bvalid;
+      if (nv) {
+        g.c[(long)mm * g.c_m + i] = z;
+        g.dlogits[(long)mm * g.N + i] = valid ? (e / se - (i == y ? 1.f : 0.f)) * inv : 0.f;
+      }
+      if (i == 0) {
+        g.loss[mm] = valid ? mx + logf(se) - zy : 0.f;
+        g.correct[mm] = (valid && am == y) ? 1 : 0;
+      }
+    }
+  }
+}
 
 // one 16 x 16 output tile per workgroup; wave w reduces k in [w kpw, (w + 1) kpw).  Every
 // operand load of a 16-step batch is unconditional (clamped, in-bounds address) and issued
 // before the first MFMA; out-of-range and masked operands are zeroed by selects afterwards
 // (a load under a per-element branch made the compiler wait for it at the branch join:
-// 16-32 serial memory latencies per batch).  MASK: A is multiplied by (am > 0).
-template <bool MASK>
-__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(GemmArgs g) {
-  __shared__ f32x4 red[LIN_MAX_WAVES][64];
+// 16-32 serial memory latencies per batch).  MASK: A is multiplied by (am > 0).  XENT: the
+// tile holds whole rows of logits and wave 0 finishes the softmax cross-entropy (forward and
+// backward) of its 16 samples in the epilogue (see xent_rows).
+template <bool MASK, bool XENT = false>
+__device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4 (&red)[LIN_MAX_WAVES][64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
   const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  if (m0 >= g.M || n0 >= g.ncols) return;  // whole workgroup: outside this GEMM's tile grid
   const int m = m0 + i, n = n0 + i;
   const bool mv = m < g.M, nv = n < g.N, ones = n == g.ones_col;
   const long ma = (long)min(m, g.M - 1) * g.a_m, nb = (long)min(n, g.N - 1) * g.b_n;
   const int k_lo = wave * g.kpw, k_hi = min(g.K, k_lo + g.kpw);
+  // XENT: the step state and the 4 labels of this lane's rows are in flight with the operands
+  int bvalid = g.M, lab[4] = {0, 0, 0, 0};
+  if constexpr (XENT) {
+    if (wave == 0) {
+      bvalid = g.state != nullptr ? min(g.state[ST_BVALID], g.M) : g.M;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lab[r] = g.labels[min(m0 + 4 * kq + r, g.M - 1)];
+    }
+  }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int k0 = k_lo; k0 < k_hi; k0 += 64) {
     float av[16], bv[16], mk[16];
@@ -81,6 +141,10 @@ __global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(GemmArgs
   f32x4 sum = red[0][lane];
   for (int w = 1; w < nw; ++w) sum += red[w][lane];  // fixed order: deterministic
   // lane (i, kq) holds C[m0 + 4 kq + r][n0 + i], r = 0..3
+  if constexpr (XENT) {
+    xent_rows(g, sum, lab, bvalid, m0, i, kq, lane);
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int mm = m0 + 4 * kq + r;
@@ -97,18 +161,66 @@ __global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(GemmArgs
   }
 }
 
-void launch(GemmArgs g, hipStream_t s) {
+// blockIdx.z selects the GEMM: the data and weight gradients of one layer share a launch (both
+// only read dz, x and W).  Waves past a GEMM's own reduction split get an empty k range and
+// add exact zeros to the fixed-order sum.
+template <bool MASK>
+__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(const GemmArgs g0, const GemmArgs g1) {
+  __shared__ f32x4 red[LIN_MAX_WAVES][64];
+  if (blockIdx.z == 0) small_gemm_tile<MASK>(g0, red);
+  else small_gemm_tile<MASK>(g1, red);
+}
+
+__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_xent_kernel(const GemmArgs g) {
+  __shared__ f32x4 red[LIN_MAX_WAVES][64];
+  small_gemm_tile<false, true>(g, red);
+}
+
+// waves per tile: one 64-deep batch each (all of a tile's loads in flight at once), at most
+// 16 waves; longer reductions loop.  Returns the waves this GEMM uses.
+int prepare(GemmArgs& g) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) throw std::runtime_error("linear: empty GEMM");
-  const int ncols = g.ones_col >= 0 ? g.ones_col + 1 : g.N;
-  // waves per tile: one 64-deep batch each (all of a tile's loads in flight at once), at most
-  // 16 waves; longer reductions loop
+  g.ncols = g.ones_col >= 0 ? g.ones_col + 1 : g.N;
   const int nw = std::max(1, std::min(LIN_MAX_WAVES, (g.K + 63) / 64));
   g.kpw = ((g.K + nw - 1) / nw + 63) / 64 * 64;
-  const int used = (g.K + g.kpw - 1) / g.kpw;
-  dim3 grid((unsigned)((ncols + 15) / 16), (unsigned)((g.M + 15) / 16));
-  if (g.am != nullptr) hipLaunchKernelGGL(small_gemm_kernel<true>, grid, dim3(64 * used), 0, s, g);
-  else hipLaunchKernelGGL(small_gemm_kernel<false>, grid, dim3(64 * used), 0, s, g);
+  return (g.K + g.kpw - 1) / g.kpw;
+}
+
+// one launch for one GEMM, or for two (same MASK) in grid z = 0 / 1
+void launch(GemmArgs g0, const GemmArgs* g1p, hipStream_t s) {
+  int waves = prepare(g0);
+  unsigned gx = (unsigned)((g0.ncols + 15) / 16), gy = (unsigned)((g0.M + 15) / 16), gz = 1;
+  GemmArgs g1 = g0;
+  if (g1p != nullptr) {
+    g1 = *g1p;
+    if ((g1.am != nullptr) != (g0.am != nullptr)) throw std::runtime_error("linear: paired GEMMs differ in masking");
+    waves = std::max(waves, prepare(g1));
+    gx = std::max(gx, (unsigned)((g1.ncols + 15) / 16));
+    gy = std::max(gy, (unsigned)((g1.M + 15) / 16));
+    gz = 2;
+  }
+  const dim3 grid(gx, gy, gz), block(64 * waves);
+  if (g0.am != nullptr) hipLaunchKernelGGL(small_gemm_kernel<true>, grid, block, 0, s, g0, g1);
+  else hipLaunchKernelGGL(small_gemm_kernel<false>, grid, block, 0, s, g0, g1);
   HIP_CHECK(hipGetLastError());
+}
+
+GemmArgs dgrad_args(const float* dy, const float* y, const float* w, float* dx, int B, int K, int N) {
+  GemmArgs g{};
+  g.a = dy; g.am = y; g.a_m = N; g.a_k = 1;
+  g.b = w; g.b_k = K; g.b_n = 1;
+  g.c = dx; g.c_m = K;
+  g.M = B; g.N = K; g.K = N; g.ones_col = -1;
+  return g;
+}
+
+GemmArgs wgrad_args(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N) {
+  GemmArgs g{};
+  g.a = dy; g.am = y; g.a_m = 1; g.a_k = N;  // A(m = n, k = b) = dz[b][n]
+  g.b = x; g.b_k = K; g.b_n = 1;             // B(k = b, n = k') = x[b][k'],  k' == K: 1
+  g.c = dw; g.c_m = K; g.c_ones = db;
+  g.M = N; g.N = K; g.K = B; g.ones_col = K;
+  return g;
 }
 
 }  // namespace
@@ -122,29 +234,48 @@ void launch_linear_fwd(const float* x, const float* w, const float* b, float* y,
   g.c = y; g.c_m = N;
   g.bias = b;
   g.M = B; g.N = N; g.K = K; g.ones_col = -1; g.relu = relu;
-  launch(g, s);
+  launch(g, nullptr, s);
+}
+
+// logits[B][N] = x W^T + b with the softmax cross-entropy of every row fused in (N <= 16)
+void launch_linear_fwd_xent(const float* x, const float* w, const float* b, float* y, const int32_t* labels,
+                            const int32_t* state, float* loss, int32_t* correct, float* dlogits, int B, int K, int N,
+                            hipStream_t s) {
+  if (N > 16) throw std::runtime_error("linear_fwd_xent: more than 16 classes");
+  GemmArgs g{};
+  g.a = x; g.a_m = K; g.a_k = 1;
+  g.b = w; g.b_k = 1; g.b_n = K;
+  g.c = y; g.c_m = N;
+  g.bias = b;
+  g.M = B; g.N = N; g.K = K; g.ones_col = -1;
+  g.labels = labels; g.state = state; g.loss = loss; g.correct = correct; g.dlogits = dlogits;
+  const int waves = prepare(g);
+  hipLaunchKernelGGL(small_gemm_xent_kernel, dim3(1, (unsigned)((B + 15) / 16)), dim3(64 * waves), 0, s, g);
+  HIP_CHECK(hipGetLastError());
 }
 
 // dx[B][K] = dz[B][N] W[N][K], dz = dy masked by y > 0 when y != nullptr (fused ReLU)
 void launch_linear_dgrad(const float* dy, const float* y, const float* w, float* dx, int B, int K, int N,
                          hipStream_t s) {
-  GemmArgs g{};
-  g.a = dy; g.am = y; g.a_m = N; g.a_k = 1;
-  g.b = w; g.b_k = K; g.b_n = 1;
-  g.c = dx; g.c_m = K;
-  g.M = B; g.N = K; g.K = N; g.ones_col = -1;
-  launch(g, s);
+  launch(dgrad_args(dy, y, w, dx, B, K, N), nullptr, s);
 }
 
 // dW[N][K] = dz^T x, db[N] = sum_b dz[b][n] (dz as in dgrad)
 void launch_linear_wgrad(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N,
                          hipStream_t s) {
-  GemmArgs g{};
-  g.a = dy; g.am = y; g.a_m = 1; g.a_k = N;  // A(m = n, k = b) = dz[b][n]
-  g.b = x; g.b_k = K; g.b_n = 1;             // B(k = b, n = k') = x[b][k'],  k' == K: 1
-  g.c = dw; g.c_m = K; g.c_ones = db;
-  g.M = N; g.N = K; g.K = B; g.ones_col = K;
-  launch(g, s);
+  launch(wgrad_args(dy, y, x, dw, db, B, K, N), nullptr, s);
+}
+
+// both gradients of one layer in ONE launch (dx == nullptr: weight gradient only)
+void launch_linear_bwd(const float* dy, const float* y, const float* w, const float* x, float* dx, float* dw,
+                       float* db, int B, int K, int N, hipStream_t s) {
+  const GemmArgs gw = wgrad_args(dy, y, x, dw, db, B, K, N);
+  if (dx == nullptr) {
+    launch(gw, nullptr, s);
+    return;
+  }
+  const GemmArgs gd = dgrad_args(dy, y, w, dx, B, K, N);
+  launch(gd, &gw, s);
 }
 
 }  // namespace dnn

@@ -214,12 +214,23 @@ class ReluFn(torch.autograd.Function):
 LINEAR_MFMA_MAX_MACS = int(os.environ.get("DNN_LINEAR_MFMA_MAX", 16 << 20))
 
 
+class XentFusion:
+    """Request + result of a softmax cross-entropy fused into the last Linear's forward (GPU,
+    no ReLU, at most 16 classes, MFMA path): set ``labels`` / ``state`` before the forward;
+    afterwards ``out`` is (per-sample loss, per-sample correct, dlogits) exactly as
+    ``cross_entropy`` returns them, or None when the layer could not fuse it."""
+
+    def __init__(self, labels: torch.Tensor, state: torch.Tensor | None) -> None:
+        self.labels, self.state = labels, state
+        self.out = None
+
+
 class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b), act = ReLU when ``relu`` (the following zoo ReLU fused in).
 
     GPU: hand-written MFMA kernels (csrc/kernels/linear.hip) for every GEMM of at most
     ``LINEAR_MFMA_MAX_MACS`` multiply-adds: forward with bias + ReLU in the epilogue; backward
-    as ONE data-gradient and ONE weight-gradient launch, the bias gradient coming out of the
+    as ONE launch for the data and weight gradients (grid z picks the GEMM), the bias gradient coming out of the
     weight-gradient MFMAs (an all-ones column) and the ReLU mask applied on the operand loads
     (no relu / threshold_backward / sum kernels).  Larger GEMMs use the library GEMM.  fp32
     operands and accumulation in both dtype modes (``gemm_dtype`` only affects the CPU
@@ -227,14 +238,25 @@ class LinearFn(torch.autograd.Function):
     in place (see Conv2dFn)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gemm_dtype: torch.dtype, gw=None, gb=None, relu: bool = False):
+    def forward(ctx, x, w, b, gemm_dtype: torch.dtype, gw=None, gb=None, relu: bool = False,
+                xent: XentFusion | None = None):
         ctx.gemm_dtype = gemm_dtype
         ctx.gw, ctx.gb, ctx.relu = gw, gb, relu
         if _is_gpu(x):
             x = x.contiguous()
             B, K = x.shape
             N = w.shape[0]
-            if B * K * N <= LINEAR_MFMA_MAX_MACS:
+            if xent is not None and not relu and N <= 16 and B * K * N <= LINEAR_MFMA_MAX_MACS:
+                # logits + softmax cross-entropy (loss, accuracy, dlogits) in one launch
+                y = torch.empty(B, N, device=x.device, dtype=torch.float32)
+                loss = torch.empty(B, device=x.device, dtype=torch.float32)
+                corr = torch.empty(B, device=x.device, dtype=torch.int32)
+                dl = torch.empty(B, N, device=x.device, dtype=torch.float32)
+                st = _p(xent.state) if xent.state is not None else 0
+                _ext().linear_fwd_xent(_p(x), _p(w), _p(b), _p(y), _p(xent.labels), st, _p(loss), _p(corr), _p(dl),
+                                       B, K, N, _s(x))
+                xent.out = (loss, corr, dl)
+            elif B * K * N <= LINEAR_MFMA_MAX_MACS:
                 y = torch.empty(B, N, device=x.device, dtype=torch.float32)
                 _ext().linear_fwd(_p(x), _p(w), _p(b), _p(y), B, K, N, int(relu), _s(x))
             else:
@@ -264,12 +286,12 @@ class LinearFn(torch.autograd.Function):
             gw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
             gb = ctx.gb if ctx.gb is not None else torch.empty(N, device=dy.device, dtype=torch.float32)
             dx = None
-            if small:
+            if small:  # data + weight (+ bias) gradients in ONE launch
                 ym = _p(y) if y is not None else 0
                 if ctx.needs_input_grad[0]:
                     dx = torch.empty(B, K, device=dy.device, dtype=torch.float32)
-                    ext.linear_dgrad(_p(dy), ym, _p(w), _p(dx), B, K, N, st)
-                ext.linear_wgrad(_p(dy), ym, _p(x), _p(gw), _p(gb), B, K, N, st)
+                ext.linear_bwd(_p(dy), ym, _p(w), _p(x), _p(dx) if dx is not None else 0, _p(gw), _p(gb), B, K, N,
+                               st)
             else:
                 dz = dy * (y > 0) if y is not None else dy
                 if ctx.needs_input_grad[0]:
@@ -277,8 +299,8 @@ class LinearFn(torch.autograd.Function):
                 torch.mm(dz.t(), x, out=gw)
                 torch.sum(dz, 0, out=gb)
             if ctx.gw is not None:
-                return dx, None, None, None, None, None, None
-            return dx, gw, gb, None, None, None, None
+                return dx, None, None, None, None, None, None, None
+            return dx, gw, gb, None, None, None, None, None
         if y is not None:
             dy = dy * (y > 0)
         dx = _gemm(dy, w, ctx.gemm_dtype) if ctx.needs_input_grad[0] else None
@@ -288,8 +310,8 @@ class LinearFn(torch.autograd.Function):
             else:
                 ctx.gw.copy_(_gemm(dy.t(), x, ctx.gemm_dtype))
             torch.sum(dy, 0, out=ctx.gb)
-            return dx, None, None, None, None, None, None
-        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None, None, None, None
+            return dx, None, None, None, None, None, None, None
+        return dx, _gemm(dy.t(), x, ctx.gemm_dtype), dy.sum(0), None, None, None, None, None
 
 
 # ---- BatchNorm2d (train: masked batch statistics; eval: running statistics) -----------------

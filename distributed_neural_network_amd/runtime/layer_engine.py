@@ -152,12 +152,15 @@ class LayerEngine(Engine):
             self.batch_ids[:first].copy_(self.order[:first])
 
     # -- model ------------------------------------------------------------------------------------
-    def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None, pack: bool = True,
+                xent: L.XentFusion | None = None) -> torch.Tensor:
         """Layer stack.  Training: every op writes its parameter gradients straight into the
         flat gradient arena (views ``G``), so backward leaves ``grad`` complete with no
-        accumulation or zeroing kernels."""
+        accumulation or zeroing kernels.  ``pack``: refresh the packed conv-weight images
+        from the arena first (False: the previous step's SGD tail already stored them).
+        ``xent``: offered to the last layer, which may fuse the loss (``xent.out``)."""
         P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
-        if self._pack_jobs:
+        if pack and self._pack_jobs:
             self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
         fuse_act = training and self.gpu  # BN + following ReLU / ReLU-pool in one op (MI355X training)
         skip = False
@@ -188,7 +191,9 @@ class LayerEngine(Engine):
                 # Linear stays fp32 in both modes: the fc GEMMs are < 0.3 GFLOP per step (fp32
                 # MFMA, linear.hip); on the GPU a following ReLU is fused into it
                 relu = self.gpu and isinstance(nxt, zoo.Relu)
-                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], torch.float32, gw, gb, relu)
+                last = nxt is None
+                x = L.LinearFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], torch.float32, gw, gb, relu,
+                                     xent if last else None)
                 skip = relu
         return x
 
@@ -223,23 +228,42 @@ class LayerEngine(Engine):
         self.state[0] = nxt
         self.state[1] = max(0, min(self.batch, self.order_len - base))
 
-    def _launch_step(self) -> None:
+    def _fused_sgd(self) -> bool:
+        return self.grad_sync is not None and getattr(self.grad_sync, "fuses_sgd", False)
+
+    def _launch_step(self, first: bool = True) -> None:
+        """One training step.  ``first``: the first step of a launch sequence (graph chunk or
+        eager call) - it packs the conv-weight images from the arena, which may have changed
+        since the last step (epoch averaging, checkpoint load, recovery); later steps find
+        them refreshed by the previous step's SGD tail."""
         assert self.train is not None
         self._ingest()
-        logits = self.forward(self.x, True, self.state)
-        loss, corr, dl = L.cross_entropy(logits, self.labels, self.state)
+        tail = self.gpu and not self._fused_sgd()
+        xent = L.XentFusion(self.labels, self.state) if self.gpu else None
+        logits = self.forward(self.x, True, self.state, pack=first or not tail, xent=xent)
+        if xent is not None and xent.out is not None:
+            loss, corr, dl = xent.out  # fused into the last Linear's launch
+        else:
+            loss, corr, dl = L.cross_entropy(logits, self.labels, self.state)
         logits.backward(dl)  # writes every parameter gradient into self.grad (no zeroing needed)
-        if self.grad_sync is not None and getattr(self.grad_sync, "fuses_sgd", False):
-            # one-shot xGMI all-reduce with the momentum-SGD update in the same launch
+        if self._fused_sgd():
+            # one-shot xGMI all-reduce with the momentum-SGD update in the same launch (the next
+            # step packs its conv weights itself: pack=True above)
             self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, None, self.lr, self.momentum,
                                          self.play.total)
+        elif self.gpu:
+            if self.grad_sync is not None:
+                self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
+            # SGD + the next step's packed conv weights + bookkeeping: one launch
+            self.ext.sgd_tail(self.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.play.total,
+                              self.lr, self.momentum, 1.0, self._pack_jobs, self.master.data_ptr(), loss.data_ptr(),
+                              corr.data_ptr(), self.batch, self.state.data_ptr(), self.stats.data_ptr(),
+                              self.order.data_ptr(), self.order_len, self.batch_ids.data_ptr(),
+                              torch.cuda.current_stream(self.device).cuda_stream)
             return
-        if self.grad_sync is not None:
-            self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
-        if self.gpu:
-            self.ext.sgd_flat(self.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.play.total,
-                              self.lr, self.momentum, 1.0, torch.cuda.current_stream(self.device).cuda_stream)
         else:
+            if self.grad_sync is not None:
+                self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
             with torch.no_grad():
                 self.mom.mul_(self.momentum).add_(self.grad)
                 self.master.sub_(self.lr * self.mom)
@@ -254,8 +278,8 @@ class LayerEngine(Engine):
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(nsteps):
-                    self._launch_step()
+                for i in range(nsteps):
+                    self._launch_step(first=i == 0)
             torch.cuda.synchronize(self.device)
             self._graphs[key] = g
         return g
@@ -267,8 +291,8 @@ class LayerEngine(Engine):
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(2):
-                self._launch_step()
+            for i in range(2):
+                self._launch_step(first=i == 0)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         for t, v in zip((self.master, self.mom, self.buffers, self.state, self.stats, self.batch_ids), saved):
@@ -289,10 +313,10 @@ class LayerEngine(Engine):
         if not self.use_graphs:
             ctx = torch.cuda.device(self.device) if self.gpu else _Null()
             with ctx:
-                for _ in range(n):
+                for i in range(n):
                     if poll is not None:
                         poll()
-                    self._launch_step()
+                    self._launch_step(first=i == 0)
             self.num_batches_tracked += n
             return
         k = self.graph_chunk

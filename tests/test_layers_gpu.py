@@ -196,6 +196,63 @@ def test_cross_entropy_masked():
         _close(a.float(), b.float(), 1e-5)
 
 
+@pytest.mark.parametrize("B,K,N,bvalid", [(64, 84, 10, 64), (64, 84, 10, 40), (9, 256, 10, 7), (33, 17, 16, 33),
+                                          (5, 3, 1, 5)])
+def test_linear_fused_cross_entropy(B, K, N, bvalid):
+    """linear_fwd_xent (logits + softmax CE + accuracy + dlogits in one launch) vs the CPU
+    Linear + cross_entropy oracle; the padded tail (>= bvalid) must come out as zeros, and the
+    backward through the same LinearFn must still give the parameter gradients."""
+    torch.manual_seed(B * 7 + K + N + bvalid)
+    x = torch.randn(B, K)
+    w = torch.randn(N, K) / K ** 0.5
+    b = torch.randn(N)
+    lab = torch.randint(0, N, (B,), dtype=torch.int32)
+    x[1] = x[0]  # a repeated row: equal logits
+    st = torch.tensor([0, bvalid, 0, 0], dtype=torch.int32)
+    zc = L.LinearFn.apply(x, w, b, torch.float32)
+    ref = L.cross_entropy(zc, lab, st)
+    xg, wg, bg = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    fx = L.XentFusion(lab.to(DEV), st.to(DEV))
+    gw, gb = torch.full((N, K), float("nan"), device=DEV), torch.full((N,), float("nan"), device=DEV)
+    zg = L.LinearFn.apply(xg, wg, bg, torch.float32, gw, gb, False, fx)
+    assert fx.out is not None
+    _close(zg, zc, 2e-5)
+    loss, corr, dl = fx.out
+    _close(loss, ref[0], 2e-5)
+    _close(dl, ref[2], 2e-6)
+    assert torch.equal(corr.cpu(), ref[1])
+    assert float(loss[bvalid:].abs().sum()) == 0.0 and float(dl[bvalid:].abs().sum()) == 0.0
+    zg.backward(dl)
+    zc2 = L.LinearFn.apply(x.requires_grad_(True), w.requires_grad_(True), b.requires_grad_(True), torch.float32)
+    zc2.backward(ref[2])
+    _close(xg.grad, x.grad, 2e-5)
+    _close(gw, w.grad, 2e-5)
+    _close(gb, b.grad, 2e-5)
+
+
+@pytest.mark.parametrize("model,dtype", [("lenet", "fp32"), ("cifar-vgg", "bf16"), ("lenet-bn", "fp32")])
+def test_sgd_tail_refreshes_packed_conv_images(model, dtype):
+    """After steps whose conv-weight images come from the SGD tail (no pack launch), the images
+    must equal a fresh conv_pack_all of the updated arena bit for bit."""
+    data = synthetic(300, 2).to(DEV)
+    eng = LayerEngine(batch=32, model=model, device=DEV, gemm_dtype=dtype, use_graphs=True, graph_chunk=4, seed=3)
+    eng.attach(data)
+    eng.begin_epoch(np.arange(300, dtype=np.int32))
+    eng.run_steps(7)
+    torch.cuda.synchronize()
+    imgs = [(v[0].clone() if v[0] is not None else None, v[1].clone() if v[1] is not None else None)
+            for v in eng._packed.values()]
+    assert eng._pack_jobs
+    eng.ext.conv_pack_all(eng._pack_jobs, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for (f0, d0), (f1, d1) in zip(imgs, eng._packed.values()):
+        for a, b in ((f0, f1), (d0, d1)):
+            if a is not None:
+                assert torch.equal(a, b)
+    st = eng.epoch_stats()
+    assert st.batches == 7 and st.samples == 7 * 32
+
+
 def test_ingest_and_sgd_flat():
     data = synthetic(50, 5).to(DEV)
     eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)

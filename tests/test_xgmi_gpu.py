@@ -64,6 +64,45 @@ print("OK")
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
+def test_xgmi_one_rank_layer_engine_matches_local_sgd():
+    """The layer engine on a 1-rank xGMI group (all-reduce fused with SGD) must equal its local
+    SGD tail bitwise, and still advance the step cursor and the epoch statistics (the fused
+    path once skipped the bookkeeping: every step re-ran the first batch)."""
+    code = r'''
+import numpy as np, torch
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.parallel import Communicator, make_policy
+from distributed_neural_network_amd.parallel.xgmi import XgmiGradSync
+from distributed_neural_network_amd.runtime.layer_engine import LayerEngine
+torch.cuda.set_device(0)
+comm = Communicator(device=torch.device("cuda", 0))
+data = synthetic(1000, 5)
+res = []
+for sync_on, graphs in [(False, True), (True, True), (True, False)]:
+    eng = LayerEngine(batch=64, model="lenet", seed=4, device="cuda", graph_chunk=4, use_graphs=graphs)
+    pol = make_policy("step-allreduce", comm)
+    pol.attach(eng)
+    if not sync_on:
+        eng.grad_sync = None
+    else:
+        assert isinstance(eng.grad_sync, XgmiGradSync), type(eng.grad_sync)
+    eng.attach(data); eng.begin_epoch(np.arange(1000, dtype=np.int32)); eng.run_steps(16)
+    torch.cuda.synchronize()
+    if sync_on:
+        pol.epoch_end(eng, 0)
+    res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats(), int(eng.state[0])))
+for m, mo, st, cur in res:
+    assert st.samples == 1000 and st.batches == 16 and cur == 16, (st, cur)
+for m, mo, st, cur in res[1:]:
+    assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo)
+    assert st.loss_sum == res[0][2].loss_sum
+comm.close()
+print("OK")
+'''
+    r = _py(code, {"DNN_FORCE_COLLECTIVES": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29633"})
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 _TWO_RANK = r'''
 import os, sys, numpy as np, torch
 from distributed_neural_network_amd.data import EpochSampler, synthetic
