@@ -17,6 +17,7 @@
 // products, fp32 accumulation: the layer engine's Linear math stays fp32 in both dtype modes)
 // with strided operand views; A may carry the ReLU mask of a saved activation.
 #include <algorithm>
+#include <cstdint>
 #include <stdexcept>
 
 #include "launchers.h"
@@ -94,8 +95,13 @@ __device__ __forceinline__ void xent_rows(const GemmArgs& g, const f32x4& sum, c
 // 16-32 serial memory latencies per batch).  MASK: A is multiplied by (am > 0).  XENT: the
 // tile holds whole rows of logits and wave 0 finishes the softmax cross-entropy (forward and
 // backward) of its 16 samples in the epilogue (see xent_rows).
-template <bool MASK, bool XENT = false>
-__device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4 (&red)[LIN_MAX_WAVES][64]) {
+//
+// VEC (forward: A = x rows and B = W rows both contiguous along k, K % 4 == 0, 16-B aligned): lane
+// (i, kq) takes the 16 CONSECUTIVE k = k0 + 16 kq + s of its rows instead of k = k0 + 4 s + kq, so
+// its operands are 4 + 4 dwordx4 loads (the strided mapping issued 32 scalar loads of 16 rows x
+// 16 B each); the k order inside an MFMA chain is a permutation of the same sum.
+template <bool MASK, bool XENT = false, bool VEC = false>
+__device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
   const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
@@ -116,6 +122,28 @@ __device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4 (&red)[
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int k0 = k_lo; k0 < k_hi; k0 += 64) {
     float av[16], bv[16], mk[16];
+    if constexpr (VEC) {
+      static_assert(!MASK, "VEC is the forward (unmasked) path");
+      const int kb = k0 + 16 * kq;
+      f32x4 ar[4], br[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {  // clamped group base: in bounds and 16-B aligned (K % 4 == 0)
+        const int kg = min(kb + 4 * t, g.K - 4);
+        ar[t] = *reinterpret_cast<const f32x4*>(g.a + ma + kg);
+        br[t] = *reinterpret_cast<const f32x4*>(g.b + nb + kg);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // all 8 loads in flight before the first use
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool kin = kb + 4 * t < k_hi;  // whole groups: K % 4 == 0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = (kin && mv) ? ar[t][e] : 0.f, b = (kin && nv) ? br[t][e] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const long kc = min(k0 + 4 * s + kq, g.K - 1);
@@ -135,11 +163,14 @@ __device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4 (&red)[
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
   }
-  red[wave][lane] = acc;
-  __syncthreads();
-  if (wave != 0) return;
-  f32x4 sum = red[0][lane];
-  for (int w = 1; w < nw; ++w) sum += red[w][lane];  // fixed order: deterministic
+  f32x4 sum = acc;
+  if (nw > 1) {  // waves' partial sums through LDS (dynamic: nw x 64 x 16 B)
+    red[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave != 0) return;
+    sum = red[lane];
+    for (int w = 1; w < nw; ++w) sum += red[w * 64 + lane];  // fixed order: deterministic
+  }
   // lane (i, kq) holds C[m0 + 4 kq + r][n0 + i], r = 0..3
   if constexpr (XENT) {
     xent_rows(g, sum, lab, bvalid, m0, i, kq, lane);
@@ -166,14 +197,29 @@ __device__ __forceinline__ void small_gemm_tile(const GemmArgs& g, f32x4 (&red)[
 // add exact zeros to the fixed-order sum.
 template <bool MASK>
 __global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_kernel(const GemmArgs g0, const GemmArgs g1) {
-  __shared__ f32x4 red[LIN_MAX_WAVES][64];
+  extern __shared__ f32x4 red[];
   if (blockIdx.z == 0) small_gemm_tile<MASK>(g0, red);
   else small_gemm_tile<MASK>(g1, red);
 }
 
+template <bool VEC>
 __global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_xent_kernel(const GemmArgs g) {
-  __shared__ f32x4 red[LIN_MAX_WAVES][64];
-  small_gemm_tile<false, true>(g, red);
+  extern __shared__ f32x4 red[];
+  small_gemm_tile<false, true, VEC>(g, red);
+}
+
+// forward GEMM with k-contiguous vector operand loads (see small_gemm_tile)
+__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_fwd_vec_kernel(const GemmArgs g) {
+  extern __shared__ f32x4 red[];
+  small_gemm_tile<false, false, true>(g, red);
+}
+
+// the forward operands qualify for the vector loads: rows contiguous along k, K a multiple of 4,
+// every row start 16-B aligned
+bool fwd_vec_ok(const GemmArgs& g) {
+  auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return g.a_k == 1 && g.b_k == 1 && g.K % 4 == 0 && g.K >= 4 && g.a_m % 4 == 0 && g.b_n % 4 == 0 && al(g.a) &&
+         al(g.b) && g.am == nullptr && g.ones_col < 0;
 }
 
 // waves per tile: one 64-deep batch each (all of a tile's loads in flight at once), at most
@@ -185,6 +231,9 @@ int prepare(GemmArgs& g) {
   g.kpw = ((g.K + nw - 1) / nw + 63) / 64 * 64;
   return (g.K + g.kpw - 1) / g.kpw;
 }
+
+// LDS of the waves' fixed-order reduction (none for a single wave)
+size_t lds_bytes(int waves) { return waves > 1 ? (size_t)waves * 64 * sizeof(f32x4) : 0; }
 
 // one launch for one GEMM, or for two (same MASK) in grid z = 0 / 1
 void launch(GemmArgs g0, const GemmArgs* g1p, hipStream_t s) {
@@ -200,8 +249,9 @@ void launch(GemmArgs g0, const GemmArgs* g1p, hipStream_t s) {
     gz = 2;
   }
   const dim3 grid(gx, gy, gz), block(64 * waves);
-  if (g0.am != nullptr) hipLaunchKernelGGL(small_gemm_kernel<true>, grid, block, 0, s, g0, g1);
-  else hipLaunchKernelGGL(small_gemm_kernel<false>, grid, block, 0, s, g0, g1);
+  const size_t lds = lds_bytes(waves);
+  if (g0.am != nullptr) hipLaunchKernelGGL(small_gemm_kernel<true>, grid, block, lds, s, g0, g1);
+  else hipLaunchKernelGGL(small_gemm_kernel<false>, grid, block, lds, s, g0, g1);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -234,6 +284,13 @@ void launch_linear_fwd(const float* x, const float* w, const float* b, float* y,
   g.c = y; g.c_m = N;
   g.bias = b;
   g.M = B; g.N = N; g.K = K; g.ones_col = -1; g.relu = relu;
+  if (fwd_vec_ok(g)) {
+    const int waves = prepare(g);
+    hipLaunchKernelGGL(small_gemm_fwd_vec_kernel, dim3((unsigned)((N + 15) / 16), (unsigned)((B + 15) / 16)),
+                       dim3(64 * waves), lds_bytes(waves), s, g);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   launch(g, nullptr, s);
 }
 
@@ -250,7 +307,9 @@ void launch_linear_fwd_xent(const float* x, const float* w, const float* b, floa
   g.M = B; g.N = N; g.K = K; g.ones_col = -1;
   g.labels = labels; g.state = state; g.loss = loss; g.correct = correct; g.dlogits = dlogits;
   const int waves = prepare(g);
-  hipLaunchKernelGGL(small_gemm_xent_kernel, dim3(1, (unsigned)((B + 15) / 16)), dim3(64 * waves), 0, s, g);
+  const dim3 grid(1, (unsigned)((B + 15) / 16));
+  if (fwd_vec_ok(g)) hipLaunchKernelGGL(small_gemm_xent_kernel<true>, grid, dim3(64 * waves), lds_bytes(waves), s, g);
+  else hipLaunchKernelGGL(small_gemm_xent_kernel<false>, grid, dim3(64 * waves), lds_bytes(waves), s, g);
   HIP_CHECK(hipGetLastError());
 }
 
