@@ -234,19 +234,26 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_layer_bookkeeping(book_args(loss, correct, batch, state, stats, order, order_len, batch_ids),
                                   S(stream));
   });
-  // SGD + packed conv-weight images + bookkeeping (loss == 0: no bookkeeping) in one launch
+  // SGD + packed conv-weight images + bookkeeping (loss == 0: no bookkeeping) in one launch;
+  // slices: (part, S, M, Kd, dw arena offset, db arena offset) of deferred conv wgrad slice sums
   m.def("sgd_tail", [book_args](u p, u g, u mom, long n, float lr, float momentum, float grad_scale,
                                 std::vector<std::tuple<u, u, int, int, int, int, int, int, int, int, int>> jobs,
-                                u arena, u loss, u correct, int batch, u state, u stats, u order, int order_len,
-                                u batch_ids, u stream) {
+                                u arena, std::vector<std::tuple<u, int, int, int, long, long>> slices, u loss,
+                                u correct, int batch, u state, u stats, u order, int order_len, u batch_ids,
+                                u stream) {
     std::vector<dnn::ConvPackJob> js;
     for (const auto& t : jobs)
       js.push_back(dnn::ConvPackJob{P<const float>(std::get<0>(t)), P<void>(std::get<1>(t)), std::get<2>(t),
                                     std::get<3>(t), std::get<4>(t), std::get<5>(t), std::get<6>(t), std::get<7>(t),
                                     std::get<8>(t), std::get<9>(t), std::get<10>(t)});
     const dnn::ReduceArgs a = book_args(loss, correct, batch, state, stats, order, order_len, batch_ids);
-    dnn::launch_sgd_tail(P<float>(p), P<const float>(g), P<float>(mom), n, lr, momentum, grad_scale, js.data(),
-                         (int)js.size(), P<const float>(arena), loss != 0 ? &a : nullptr, S(stream));
+    std::vector<dnn::SliceJob> sl;
+    for (const auto& t : slices)
+      sl.push_back(dnn::SliceJob{P<const float>(std::get<0>(t)), std::get<1>(t), std::get<2>(t), std::get<3>(t),
+                                 std::get<4>(t), std::get<5>(t)});
+    dnn::launch_sgd_tail(P<float>(p), P<float>(g), P<float>(mom), n, lr, momentum, grad_scale, js.data(),
+                         (int)js.size(), P<const float>(arena), sl.data(), (int)sl.size(), loss != 0 ? &a : nullptr,
+                         S(stream));
   });
   m.def("conv_fwd", [](u x, u w, u bias, u y, u ws, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
                        int flip, u stream) {

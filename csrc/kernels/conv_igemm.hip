@@ -723,7 +723,8 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
   *S = (int)((chunks + per - 1) / per);
 }
 
-// dw [M][C][K][K] and db [M] from one MFMA pass; part: S * M * (C K^2 + 1) floats
+// dw [M][C][K][K] and db [M] from one MFMA pass; part: S * M * (C K^2 + 1) floats.  dw == nullptr:
+// the slice partials only (the caller sums them later, e.g. inside the SGD tail launch)
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
                        int M, int K, int pad, int bf16_ops, hipStream_t s) {
   const Geom g = geom(B, C, H, W, K, pad);
@@ -731,6 +732,7 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   conv_wgrad_split(B, C, H, W, M, K, pad, &S, &cps);
   if (bf16_ops) wgrad_dispatch<true>(x, dy, part, g, M, S, cps, s);
   else wgrad_dispatch<false>(x, dy, part, g, M, S, cps, s);
+  if (dw == nullptr) return;
   const int Kd = C * K * K;
   const long n = (long)M * (Kd + 1);
   hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(SW * 64), 0, s, part, S, n, Kd, dw, db);

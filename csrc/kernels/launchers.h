@@ -122,10 +122,25 @@ struct PackScatter {
   } it[kMax];
   int n;
 };
+// deferred conv weight-gradient slice sums (launch_conv_wgrad with dw == nullptr): part rows are
+// [S][M][Kd + 1]; element e = m (Kd + 1) + j of their sum is dW[m][j] (j < Kd) or db[m] (j == Kd)
+struct SliceJob {
+  const float* part;
+  int S, M, Kd;
+  long dw_off, db_off;  // arena offsets of dW (M x Kd) and db (M)
+};
+struct SliceSet {
+  static constexpr int kMax = 8;
+  SliceJob it[kMax];
+  int start[kMax + 1];  // prefix sums of the jobs' 16-element groups
+  int n;
+};
 // SGD + packed conv-weight images (jobs: conv_pack_all's list; arena: the parameter arena the
-// jobs' weights live in) + the step bookkeeping (book != nullptr) in one launch
-void launch_sgd_tail(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
-                     const ConvPackJob* jobs, int njobs, const float* arena, const ReduceArgs* book, hipStream_t s);
+// jobs' weights live in) + the step bookkeeping (book != nullptr) in one launch; slices: conv
+// gradients still in slice partials - their elements are summed, stored to g and updated here
+void launch_sgd_tail(float* p, float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     const ConvPackJob* jobs, int njobs, const float* arena, const SliceJob* slices, int nslices,
+                     const ReduceArgs* book, hipStream_t s);
 // Linear layers on MFMA (linear.hip): y = act(x W^T + b); dx = dz W; dW = dz^T x, db = sum_b dz,
 // dz = dy masked by y > 0 when y != nullptr (fused ReLU)
 void launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int B, int K, int N, int relu,

@@ -468,24 +468,8 @@ __global__ void __launch_bounds__(LT) sgd_flat_kernel(float* __restrict__ p, con
   p[i] = pn;
 }
 
-// The step's tail in ONE launch: momentum SGD over the arena; every updated conv weight is also
-// stored into the layer's packed forward / dgrad images (the next step's conv kernels read
-// those: no pack launch at the next step's start); the last workgroup runs the step
-// bookkeeping (epoch loss / accuracy, cursor, next batch ids).
-template <bool BOOK>
-__global__ void __launch_bounds__(LT) sgd_tail_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                      float* __restrict__ m, long n, float lr, float momentum,
-                                                      float grad_scale, const PackScatter ps, const ReduceArgs book) {
-  if (BOOK && blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x < 64) bookkeeping<false>(book, threadIdx.x);
-    return;
-  }
-  const long i = (long)blockIdx.x * LT + threadIdx.x;
-  if (i >= n) return;
-  float pn, mn;
-  sgd_update(g[i] * grad_scale, p[i], m[i], lr, momentum, pn, mn);
-  m[i] = mn;
-  p[i] = pn;
+// packed-image stores of an updated conv weight (arena element i, new value pn)
+__device__ __forceinline__ void scatter_packed(const PackScatter& ps, long i, float pn) {
   for (int j = 0; j < ps.n; ++j) {
     const PackScatter::Item& it = ps.it[j];
     const long l = i - it.off;
@@ -493,13 +477,85 @@ __global__ void __launch_bounds__(LT) sgd_tail_kernel(float* __restrict__ p, con
     // layer weight [Cout][Cin][K][K]; the image holds (m, c, ky, kx) = (o, ci, y, x), or
     // (ci, o, K-1-y, K-1-x) for the flipped dgrad image (launch_conv_pack_all's element map)
     const int KK = it.K * it.K, cin = it.flip ? it.M : it.C;
-    const int x = (int)(l % it.K), y = (int)((l / it.K) % it.K), ci = (int)((l / KK) % cin), o = (int)(l / ((long)KK * cin));
+    const int x = (int)(l % it.K), y = (int)((l / it.K) % it.K), ci = (int)((l / KK) % cin);
+    const int o = (int)(l / ((long)KK * cin));
     const int mm = it.flip ? ci : o, cc = it.flip ? o : ci;
     const int tap = it.flip ? (it.K - 1 - y) * it.K + (it.K - 1 - x) : y * it.K + x;
     const long d = ((long)tap * it.Mp + mm) * it.Cp + cc;
     if (it.bf) reinterpret_cast<bf16*>(it.dst)[d] = (bf16)pn;
     else reinterpret_cast<float*>(it.dst)[d] = pn;
   }
+}
+
+// The step's tail in ONE launch of TT-thread workgroups, by workgroup role:
+//   [0, ss.start[ss.n])  deferred conv weight gradients, 64 elements per workgroup: wave w of 16
+//                        sums slices w, w + 16, ... (8 loads in flight per batch) and wave 0 adds
+//                        the 16 wave sums in w order - slice_sum_kernel's exact layout and order,
+//                        so the gradient is bit-identical to the two-launch path; then SGD;
+//   next ceil(n / TT)    momentum SGD over the rest of the arena;
+//   last (BOOK)          the step bookkeeping (epoch loss / accuracy, cursor, next batch ids).
+// Every updated conv weight is also stored into the layer's packed forward / dgrad images (the
+// next step's conv kernels read those: no pack launch at the next step's start).
+constexpr int TT = 1024;
+template <bool BOOK>
+__global__ void __launch_bounds__(TT) sgd_tail_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                      float* __restrict__ m, long n, float lr, float momentum,
+                                                      float grad_scale, const PackScatter ps, const SliceSet ss,
+                                                      const ReduceArgs book) {
+  const int nsg = ss.start[ss.n];
+  if (BOOK && blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < 64) bookkeeping<false>(book, threadIdx.x);
+    return;
+  }
+  if ((int)blockIdx.x < nsg) {
+    constexpr int SWV = TT / 64;  // waves over the slices
+    __shared__ float red[SWV][64];
+    int j = 0;
+    while (j + 1 < ss.n && (int)blockIdx.x >= ss.start[j + 1]) ++j;
+    const SliceJob& sj = ss.it[j];
+    const long ne = (long)sj.M * (sj.Kd + 1);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long e = (long)((int)blockIdx.x - ss.start[j]) * 64 + lane;
+    const bool ev = e < ne;
+    const float* src = sj.part + (ev ? e : 0);
+    float acc = 0.f;
+    for (int s0 = w; s0 < sj.S; s0 += 8 * SWV) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int sl = s0 + SWV * u;
+        v[u] = sl < sj.S ? src[(long)sl * ne] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w != 0 || !ev) return;
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < SWV; ++q) v += red[q][lane];
+    const int mr = (int)(e / (sj.Kd + 1)), jc = (int)(e - (long)mr * (sj.Kd + 1));
+    const long i = jc < sj.Kd ? sj.dw_off + (long)mr * sj.Kd + jc : sj.db_off + mr;
+    g[i] = v;
+    float pn, mn;
+    sgd_update(v * grad_scale, p[i], m[i], lr, momentum, pn, mn);
+    m[i] = mn;
+    p[i] = pn;
+    scatter_packed(ps, i, pn);
+    return;
+  }
+  const long i = (long)((int)blockIdx.x - nsg) * TT + threadIdx.x;
+  if (i >= n) return;
+  for (int q = 0; q < ss.n; ++q) {  // owned by a slice role
+    const SliceJob& sj = ss.it[q];
+    if ((i >= sj.dw_off && i < sj.dw_off + (long)sj.M * sj.Kd) || (i >= sj.db_off && i < sj.db_off + sj.M)) return;
+  }
+  float pn, mn;
+  sgd_update(g[i] * grad_scale, p[i], m[i], lr, momentum, pn, mn);
+  m[i] = mn;
+  p[i] = pn;
+  scatter_packed(ps, i, pn);
 }
 
 inline unsigned blocks(long n) { return (unsigned)((n + LT - 1) / LT); }
@@ -626,8 +682,9 @@ void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float
   if (n) hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks(n)), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale);
 }
 
-void launch_sgd_tail(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
-                     const ConvPackJob* jobs, int njobs, const float* arena, const ReduceArgs* book, hipStream_t s) {
+void launch_sgd_tail(float* p, float* g, float* m, long n, float lr, float momentum, float grad_scale,
+                     const ConvPackJob* jobs, int njobs, const float* arena, const SliceJob* slices, int nslices,
+                     const ReduceArgs* book, hipStream_t s) {
   PackScatter ps{};
   if (njobs > PackScatter::kMax) throw std::runtime_error("sgd_tail: too many packed conv images");
   for (int j = 0; j < njobs; ++j) {
@@ -641,13 +698,24 @@ void launch_sgd_tail(float* p, const float* g, float* m, long n, float lr, float
     it.flip = J.flip;
     it.bf = J.bf16_ops;
   }
-  const unsigned nb = blocks(n) + (book != nullptr ? 1u : 0u);
+  SliceSet ss{};
+  if (nslices > SliceSet::kMax) throw std::runtime_error("sgd_tail: too many deferred slice sums");
+  ss.start[0] = 0;
+  for (int j = 0; j < nslices; ++j) {
+    const SliceJob& sj = slices[j];
+    if (sj.S <= 0 || sj.M <= 0 || sj.Kd <= 0 || sj.dw_off < 0 || sj.dw_off + (long)sj.M * sj.Kd > n || sj.db_off < 0 ||
+        sj.db_off + sj.M > n)
+      throw std::runtime_error("sgd_tail: slice job outside the arena");
+    ss.it[ss.n++] = sj;
+    ss.start[j + 1] = ss.start[j] + (int)(((long)sj.M * (sj.Kd + 1) + 63) / 64);
+  }
+  const unsigned nb = (unsigned)(ss.start[ss.n] + (n + TT - 1) / TT) + (book != nullptr ? 1u : 0u);
   if (book != nullptr)
-    hipLaunchKernelGGL(sgd_tail_kernel<true>, dim3(nb), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
-                       *book);
+    hipLaunchKernelGGL(sgd_tail_kernel<true>, dim3(nb), dim3(TT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
+                       ss, *book);
   else
-    hipLaunchKernelGGL(sgd_tail_kernel<false>, dim3(nb), dim3(LT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
-                       ReduceArgs{});
+    hipLaunchKernelGGL(sgd_tail_kernel<false>, dim3(nb), dim3(TT), 0, s, p, g, m, n, lr, momentum, grad_scale, ps,
+                       ss, ReduceArgs{});
   HIP_CHECK(hipGetLastError());
 }
 

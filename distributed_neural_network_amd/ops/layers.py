@@ -78,10 +78,13 @@ class Conv2dFn(torch.autograd.Function):
     ``conv_pack_all`` launch (either may be None: packed per call).
     ``gw`` / ``gb``: when given, the weight / bias gradients are written straight into
     them (views of the engine's flat gradient arena) and autograd gets None for the
-    parameters - no per-parameter accumulation kernels, no arena zeroing."""
+    parameters - no per-parameter accumulation kernels, no arena zeroing.
+    ``slice_sink``: a list (GPU, with ``gw``): the backward leaves the weight gradient as split-K
+    slice partials and appends (partials, S, Cout, C K^2, gw, gb) for the engine's SGD tail
+    launch to sum (one launch fewer per layer); the list keeps the partials alive until then."""
 
     @staticmethod
-    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None):
+    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -103,6 +106,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.gemm_dtype = gemm_dtype
         ctx.gw, ctx.gb = gw, gb
         ctx.packed = packed
+        ctx.slice_sink = slice_sink if gw is not None else None
         return y
 
     @staticmethod
@@ -119,7 +123,11 @@ class Conv2dFn(torch.autograd.Function):
             ext, st = _ext(), _s(dy)
             S = ext.conv_wgrad_slices(B, C, H, W, Cout, K, pad)
             part = torch.empty(S * Cout * (C * K * K + 1), device=dy.device, dtype=torch.float32)
-            ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), _p(db), B, C, H, W, Cout, K, pad, bf, st)  # dW and db
+            if ctx.slice_sink is not None:  # partials only: summed by the engine's SGD tail
+                ext.conv_wgrad(_p(x), _p(dy), _p(part), 0, 0, B, C, H, W, Cout, K, pad, bf, st)
+                ctx.slice_sink.append((part, S, Cout, C * K * K, dw, db))
+            else:
+                ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), _p(db), B, C, H, W, Cout, K, pad, bf, st)  # dW, db
             if ctx.needs_input_grad[0]:
                 # dgrad: the forward kernel over dY with the flipped, transposed weights
                 # (flip=1: packed from w inside the launch), pad' = K - 1 - pad
@@ -139,8 +147,8 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 # ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------

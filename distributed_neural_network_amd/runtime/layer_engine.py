@@ -73,6 +73,7 @@ class LayerEngine(Engine):
         self._warm = False
         self._packed: dict[str, tuple] = {}
         self._pack_jobs: list[tuple] = []
+        self.defer_slice_sums = True  # conv wgrad slice sums inside the SGD tail (single GPU)
         if self.gpu:
             self._plan_weight_packing()
 
@@ -153,12 +154,13 @@ class LayerEngine(Engine):
 
     # -- model ------------------------------------------------------------------------------------
     def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None, pack: bool = True,
-                xent: L.XentFusion | None = None) -> torch.Tensor:
+                xent: L.XentFusion | None = None, slice_sink: list | None = None) -> torch.Tensor:
         """Layer stack.  Training: every op writes its parameter gradients straight into the
         flat gradient arena (views ``G``), so backward leaves ``grad`` complete with no
         accumulation or zeroing kernels.  ``pack``: refresh the packed conv-weight images
         from the arena first (False: the previous step's SGD tail already stored them).
-        ``xent``: offered to the last layer, which may fuse the loss (``xent.out``)."""
+        ``xent``: offered to the last layer, which may fuse the loss (``xent.out``).
+        ``slice_sink``: conv layers defer their weight-gradient slice sums to the SGD tail."""
         P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
         if pack and self._pack_jobs:
             self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
@@ -177,7 +179,8 @@ class LayerEngine(Engine):
                                            Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb)
                 skip = True
             elif isinstance(layer, zoo.Conv):
-                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, self._packed.get(n))
+                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, self._packed.get(n),
+                                     slice_sink)
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
                                           Bf[f"{n}.running_var"], state, training, layer.eps, layer.momentum, gw, gb)
@@ -240,7 +243,10 @@ class LayerEngine(Engine):
         self._ingest()
         tail = self.gpu and not self._fused_sgd()
         xent = L.XentFusion(self.labels, self.state) if self.gpu else None
-        logits = self.forward(self.x, True, self.state, pack=first or not tail, xent=xent)
+        # single GPU: the conv weight-gradient slice sums run inside the SGD tail launch (with a
+        # gradient all-reduce the gradients must be complete before it)
+        sink = [] if (tail and self.grad_sync is None and self.defer_slice_sums) else None
+        logits = self.forward(self.x, True, self.state, pack=first or not tail, xent=xent, slice_sink=sink)
         if xent is not None and xent.out is not None:
             loss, corr, dl = xent.out  # fused into the last Linear's launch
         else:
@@ -254,9 +260,12 @@ class LayerEngine(Engine):
         elif self.gpu:
             if self.grad_sync is not None:
                 self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
-            # SGD + the next step's packed conv weights + bookkeeping: one launch
-            self.ext.sgd_tail(self.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.play.total,
-                              self.lr, self.momentum, 1.0, self._pack_jobs, self.master.data_ptr(), loss.data_ptr(),
+            # conv slice sums + SGD + the next step's packed conv weights + bookkeeping: one launch
+            g0 = self.grad.data_ptr()
+            slices = [(part.data_ptr(), S, M, Kd, (dw.data_ptr() - g0) // 4, (db.data_ptr() - g0) // 4)
+                      for part, S, M, Kd, dw, db in (sink or [])]
+            self.ext.sgd_tail(self.master.data_ptr(), g0, self.mom.data_ptr(), self.play.total, self.lr,
+                              self.momentum, 1.0, self._pack_jobs, self.master.data_ptr(), slices, loss.data_ptr(),
                               corr.data_ptr(), self.batch, self.state.data_ptr(), self.stats.data_ptr(),
                               self.order.data_ptr(), self.order_len, self.batch_ids.data_ptr(),
                               torch.cuda.current_stream(self.device).cuda_stream)

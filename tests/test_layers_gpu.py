@@ -253,6 +253,24 @@ def test_sgd_tail_refreshes_packed_conv_images(model, dtype):
     assert st.batches == 7 and st.samples == 7 * 32
 
 
+@pytest.mark.parametrize("model,dtype", [("lenet", "fp32"), ("cifar-vgg", "bf16")])
+def test_deferred_slice_sums_bitwise(model, dtype):
+    """Conv weight-gradient slice sums inside the SGD tail launch == slice_sum_kernel + SGD, bit
+    for bit (same summation order), over several steps."""
+    data = synthetic(200, 6).to(DEV)
+    res = []
+    for defer in (True, False):
+        eng = LayerEngine(batch=32, model=model, device=DEV, gemm_dtype=dtype, graph_chunk=4, seed=8)
+        eng.defer_slice_sums = defer
+        eng.attach(data)
+        eng.begin_epoch(np.arange(200, dtype=np.int32))
+        eng.run_steps(6)
+        torch.cuda.synchronize()
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.grad.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_ingest_and_sgd_flat():
     data = synthetic(50, 5).to(DEV)
     eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)
