@@ -280,6 +280,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_conv_fwd_packed(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y), B, C, H, W, M,
                                 K, pad, bf16_ops, S(stream));
   });
+  m.def("conv_fwd_pool_ok", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+    return dnn::conv_fwd_pool_ok(B, C, H, W, M, K, pad, bf16_ops);
+  });
+  m.def("conv_fwd_packed_pool", [](u x, u wp, u bias, u y, u code, int B, int C, int H, int W, int M, int K, int pad,
+                                   int bf16_ops, u stream) {
+    dnn::launch_conv_fwd_packed_pool(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y),
+                                     P<uint8_t>(code), B, C, H, W, M, K, pad, bf16_ops, S(stream));
+  });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;
     dnn::conv_wgrad_split(B, C, H, W, M, K, pad, &s, &cps);

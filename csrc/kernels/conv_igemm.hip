@@ -328,6 +328,8 @@ struct PatchT {
 struct PGeom {
   int B, C, H, W, K, pad, OH, OW, M;
   int R, Wp, tiles, Cp, Mp;  // patch rows, padded width, tiles per image, padded C / M
+  int ppt;                   // output positions per tile (PNT; pooled: rpt whole rows x OW)
+  int rpt;                   // pooled: output rows per tile (even), else 0
 };
 
 // wp[(tap * Mp + m) * Cp + c] = w[m][c][ky][kx]            (forward)
@@ -347,11 +349,15 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
   }
 }
 
-template <bool BF16, int BM, int CCH, bool V4>
+// POOL: ReLU + 2x2 max-pool (first maximum wins, code 4 = max <= 0 - relu_pool_fwd_kernel's
+// exact rule) in the epilogue: tiles are rpt whole output rows, the tile's conv outputs go
+// through LDS, y is the pooled [B][M][OH/2][OW/2] output and code its argmax codes; the
+// full-resolution output is never written.
+template <bool BF16, int BM, int CCH, bool V4, bool POOL = false>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
                                                             const typename PatchT<BF16, CCH>::T* __restrict__ wp,
                                                             const float* __restrict__ bias, float* __restrict__ y,
-                                                            PGeom g) {
+                                                            PGeom g, uint8_t* __restrict__ code = nullptr) {
   static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
   using T = typename PatchT<BF16, CCH>::T;
   constexpr int CCP = PatchT<BF16, CCH>::CCP;
@@ -360,14 +366,17 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   T* As = reinterpret_cast<T*>(smem);  // [KK][BM][CCP]
   T* Ps = As + KK * BM * CCP;          // [R][Wp][CCP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, q = lane >> 4;
-  const int b = blockIdx.x / g.tiles, p0 = (blockIdx.x - b * g.tiles) * PNT;
+  const int tile = blockIdx.x;
+  const int b = tile / g.tiles, p0 = (tile - b * g.tiles) * g.ppt;
   const int m0 = blockIdx.y * BM;
   const int OHW = g.OH * g.OW;
   const int oy_lo = p0 / g.OW, iy0 = oy_lo - g.pad;
 
-  // this lane's output column (position) and its patch base
-  const int pn = p0 + wave * 16 + r16;
-  const int pc = min(pn, OHW - 1);
+  // this lane's output column (position) and its patch base (lanes past the tile's ppt
+  // positions compute a clamped copy and store nothing)
+  const int local = wave * 16 + r16;
+  const int pn = local < g.ppt ? p0 + local : OHW;
+  const int pc = min(p0 + min(local, g.ppt - 1), OHW - 1);
   const int oy = pc / g.OW, ox = pc - oy * g.OW;
   const int bbase = ((oy - oy_lo) * g.Wp + ox) * CCP + (BF16 ? 8 * q : q);
 
@@ -550,6 +559,37 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   }
 
   // epilogue: acc[i][j] = D[16 i + 4 q + j][16 wave + r16]
+  if constexpr (POOL) {
+    __syncthreads();  // every wave is done with As / Ps: the tile's outputs reuse the LDS
+    float* ot = reinterpret_cast<float*>(smem);  // [BM][PNT]
+#pragma unroll
+    for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = 16 * i + 4 * q + j, m = m0 + ml;
+        ot[ml * PNT + local] = acc[i][j] + ((bias != nullptr && m < g.M) ? bias[m] : 0.f);
+      }
+    }
+    __syncthreads();
+    const int OH2 = g.OH >> 1, OW2 = g.OW >> 1, pr_n = g.rpt >> 1, np = pr_n * OW2;
+    const int py0 = (p0 / g.OW) >> 1;
+    for (int e = tid; e < BM * np; e += CT) {
+      const int ml = e / np, pl = e - ml * np, pr = pl / OW2, px = pl - pr * OW2;
+      const int py = py0 + pr, m = m0 + ml;
+      if (py >= OH2 || m >= g.M) continue;
+      const float* t = ot + ml * PNT + 2 * pr * g.OW + 2 * px;
+      float best = t[0];
+      int arg = 0;
+      const float v1 = t[1], v2 = t[g.OW], v3 = t[g.OW + 1];
+      if (v1 > best) { best = v1; arg = 1; }
+      if (v2 > best) { best = v2; arg = 2; }
+      if (v3 > best) { best = v3; arg = 3; }
+      const long o = ((long)(b * g.M + m) * OH2 + py) * OW2 + px;
+      y[o] = fmaxf(best, 0.f);
+      code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+    }
+    return;
+  }
   if (pn < OHW) {
 #pragma unroll
     for (int i = 0; i < BM / 16; ++i) {
@@ -574,15 +614,26 @@ struct FastPlan {
   size_t lds = 0, ws_bytes = 0;
 };
 
-FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
+// pool_bm > 0: the plan of the pooled-epilogue variant, with the M tile of the plain plan (the
+// packed weight image's Mp must not change)
+FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf, int pool_bm = 0) {
   FastPlan f;
   const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
   if (OH <= 0 || OW <= 0) return f;
-  const int OHW = OH * OW, tiles = (OHW + PNT - 1) / PNT;
+  const int OHW = OH * OW;
+  int tiles = (OHW + PNT - 1) / PNT, ppt = PNT, rpt = 0;
   int span = 1;  // most output rows one 64-position tile touches
-  for (int t = 0; t < tiles; ++t) {
-    const int lo = t * PNT, hi = std::min(OHW, lo + PNT) - 1;
-    span = std::max(span, hi / OW - lo / OW + 1);
+  if (pool_bm > 0) {  // tiles of rpt whole rows (an even count, rpt * OW <= PNT)
+    rpt = 2 * (PNT / (2 * OW));
+    if (rpt < 2 || OH < 2) return f;
+    ppt = rpt * OW;
+    tiles = ((OH & ~1) + rpt - 1) / rpt;
+    span = rpt;
+  } else {
+    for (int t = 0; t < tiles; ++t) {
+      const int lo = t * PNT, hi = std::min(OHW, lo + PNT) - 1;
+      span = std::max(span, hi / OW - lo / OW + 1);
+    }
   }
   const int R = span + K - 1, Wp = W + 2 * pad;
   // M tile: <= 32 rows (enough workgroups on the small late layers), A fits the budget
@@ -591,33 +642,43 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
   const size_t es = bf ? 2 : 4, ccp = bf ? 40 : cch + 4;
   auto lds_of = [&](int bmv) { return ((size_t)K * K * bmv + (size_t)R * Wp + 4) * ccp * es; };  // + dummy pixels
   if (lds_of(bm) > kPatchLdsMax && bm == 32) bm = 16;
+  if (pool_bm > 0) bm = pool_bm;
   if (lds_of(bm) > kPatchLdsMax) return f;
   f.ok = true;
   f.bm = bm;
   f.cch = cch;
   f.gy = (M + bm - 1) / bm;
-  f.pg = PGeom{B, C, H, W, K, pad, OH, OW, M, R, Wp, tiles, (C + cch - 1) / cch * cch, f.gy * bm};
-  f.lds = lds_of(bm);
+  f.pg = PGeom{B, C, H, W, K, pad, OH, OW, M, R, Wp, tiles, (C + cch - 1) / cch * cch, f.gy * bm, ppt, rpt};
+  f.lds = std::max(lds_of(bm), pool_bm > 0 ? (size_t)bm * PNT * sizeof(float) : (size_t)0);  // + pooled out tile
+  if (f.lds > kPatchLdsMax) f.ok = false;
   f.ws_bytes = (size_t)K * K * f.pg.Mp * f.pg.Cp * es;
   return f;
 }
 
-template <bool BF16, int CCH, bool V4>
+template <bool BF16, int CCH, bool V4, bool POOL>
 void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
-                   float* y, hipStream_t s) {
+                   float* y, uint8_t* code, hipStream_t s) {
   dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
   if (f.bm == 16)
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, POOL>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
+                       code);
   else
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, POOL>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
+                       code);
   HIP_CHECK(hipGetLastError());
 }
-// float4 patch groups when image rows are whole 16-B vectors
+// float4 patch groups when image rows are whole 16-B vectors; code != nullptr: pooled epilogue
 template <bool BF16, int CCH>
 void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
-                 float* y, hipStream_t s) {
-  if (f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) fast_launch_v<BF16, CCH, true>(f, wp, x, bias, y, s);
-  else fast_launch_v<BF16, CCH, false>(f, wp, x, bias, y, s);
+                 float* y, hipStream_t s, uint8_t* code = nullptr) {
+  const bool v4 = f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
+  if (code != nullptr) {
+    if (v4) fast_launch_v<BF16, CCH, true, true>(f, wp, x, bias, y, code, s);
+    else fast_launch_v<BF16, CCH, false, true>(f, wp, x, bias, y, code, s);
+  } else {
+    if (v4) fast_launch_v<BF16, CCH, true, false>(f, wp, x, bias, y, nullptr, s);
+    else fast_launch_v<BF16, CCH, false, false>(f, wp, x, bias, y, nullptr, s);
+  }
 }
 
 template <bool BF16>
@@ -810,6 +871,33 @@ void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, f
     if (f.cch == 8) fast_launch<false, 8>(f, w, x, bias, y, s);
     else if (f.cch == 16) fast_launch<false, 16>(f, w, x, bias, y, s);
     else fast_launch<false, 32>(f, w, x, bias, y, s);
+  }
+}
+
+// the pooled plan of a layer whose plain plan packed the weight image (same M tile)
+FastPlan plan_pool(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
+  const FastPlan f0 = plan_fast(B, C, H, W, M, K, pad, bf);
+  if (!f0.ok) return f0;
+  return plan_fast(B, C, H, W, M, K, pad, bf, f0.bm);
+}
+
+int conv_fwd_pool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+  return plan_pool(B, C, H, W, M, K, pad, bf16_ops != 0).ok ? 1 : 0;
+}
+
+// y = maxpool2x2(relu(conv(x, w) + bias)) and its argmax codes, from the layer's packed image
+void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bias, float* y, uint8_t* code, int B,
+                                 int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  const FastPlan f = plan_pool(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (!f.ok) throw std::runtime_error("conv_fwd_packed_pool: layer has no pooled LDS-patch plan");
+  if (bf16_ops) {
+    fast_launch<true, 32>(f, reinterpret_cast<const bf16*>(wp), x, bias, y, s, code);
+  } else {
+    const float* w = reinterpret_cast<const float*>(wp);
+    if (f.cch == 8) fast_launch<false, 8>(f, w, x, bias, y, s, code);
+    else if (f.cch == 16) fast_launch<false, 16>(f, w, x, bias, y, s, code);
+    else fast_launch<false, 32>(f, w, x, bias, y, s, code);
   }
 }
 

@@ -108,6 +108,10 @@ struct ConvPackJob {
 void launch_conv_pack_all(const ConvPackJob* jobs, int n, hipStream_t s);
 void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, float* y, int B, int C, int H, int W,
                             int M, int K, int pad, int bf16_ops, hipStream_t s);
+// conv + bias + ReLU + 2x2 max-pool in one launch (pooled y, argmax codes as relu_pool_fwd)
+int conv_fwd_pool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
+void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bias, float* y, uint8_t* code, int B,
+                                 int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
 // element map of a packed conv-weight image (the LDS-patch plan of the job's layer)

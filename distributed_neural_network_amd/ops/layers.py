@@ -81,16 +81,26 @@ class Conv2dFn(torch.autograd.Function):
     parameters - no per-parameter accumulation kernels, no arena zeroing.
     ``slice_sink``: a list (GPU, with ``gw``): the backward leaves the weight gradient as split-K
     slice partials and appends (partials, S, Cout, C K^2, gw, gb) for the engine's SGD tail
-    launch to sum (one launch fewer per layer); the list keeps the partials alive until then."""
+    launch to sum (one launch fewer per layer); the list keeps the partials alive until then.
+    ``pool``: the following ReLU + 2x2 max-pool runs in the forward kernel's epilogue (GPU, packed
+    forward image): the op returns the pooled output, and its backward starts with the pool's."""
 
     @staticmethod
-    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None):
+    def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None,
+                pool: bool = False):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
         x = x.contiguous()
         bf = int(gemm_dtype == torch.bfloat16)
-        if _is_gpu(x):
+        ctx.code = None
+        if _is_gpu(x) and pool:
+            assert packed is not None and packed[0] is not None, "pooled conv needs the packed forward image"
+            y = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.float32)
+            ctx.code = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.uint8)
+            _ext().conv_fwd_packed_pool(_p(x), _p(packed[0]), _p(b), _p(y), _p(ctx.code), B, C, H, W, Cout, K, pad, bf,
+                                        _s(x))
+        elif _is_gpu(x):
             ext = _ext()
             y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
             if packed is not None and packed[0] is not None:  # image packed by the engine's conv_pack_all
@@ -115,6 +125,10 @@ class Conv2dFn(torch.autograd.Function):
         B, C, H, W, K, pad, OH, OW = ctx.shape
         Cout = w.shape[0]
         dy = dy.contiguous()
+        if ctx.code is not None:  # the fused pool's backward: scatter to the argmax positions
+            full = torch.empty(B, Cout, OH, OW, device=dy.device, dtype=torch.float32)
+            _ext().relu_pool_bwd(_p(dy), _p(ctx.code), B * Cout, OH, OW, _p(full), _s(dy))
+            dy = full
         bf = int(ctx.gemm_dtype == torch.bfloat16)
         dw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
         db = ctx.gb if ctx.gb is not None else torch.empty(Cout, device=dy.device, dtype=torch.float32)
@@ -147,8 +161,8 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 # ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------

@@ -73,6 +73,7 @@ class LayerEngine(Engine):
         self._warm = False
         self._packed: dict[str, tuple] = {}
         self._pack_jobs: list[tuple] = []
+        self._pool_ok: set[str] = set()  # conv layers with a pooled-epilogue plan
         self.defer_slice_sums = True  # conv wgrad slice sums inside the SGD tail (single GPU)
         if self.gpu:
             self._plan_weight_packing()
@@ -101,6 +102,8 @@ class LayerEngine(Engine):
                                       device=self.device, dtype=torch.uint8)
                     self._pack_jobs.append((w, dgr.data_ptr(), B, M, OH, OW, C, K, K - 1 - pad, bf, 1))
                 self._packed[n] = (fwd, dgr)
+                if fwd is not None and ext.conv_fwd_pool_ok(B, C, H, W, M, K, pad, bf):
+                    self._pool_ok.add(n)
                 first = False
                 H, W = OH, OW
             elif isinstance(layer, zoo.ReluPool):
@@ -179,8 +182,13 @@ class LayerEngine(Engine):
                                            Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb)
                 skip = True
             elif isinstance(layer, zoo.Conv):
-                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, self._packed.get(n),
-                                     slice_sink)
+                packed = self._packed.get(n)
+                # conv -> ReLU + max-pool: the pool in the conv kernel's epilogue (one launch)
+                pool = (self.gpu and isinstance(nxt, zoo.ReluPool) and packed is not None and packed[0] is not None
+                        and n in self._pool_ok)
+                x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, packed, slice_sink,
+                                     pool)
+                skip = pool
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
                                           Bf[f"{n}.running_var"], state, training, layer.eps, layer.momentum, gw, gb)

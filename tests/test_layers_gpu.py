@@ -271,6 +271,39 @@ def test_deferred_slice_sums_bitwise(model, dtype):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,C,H,M,K,pad,dtype", [(8, 3, 32, 6, 5, 0, torch.float32), (8, 6, 14, 16, 5, 0, torch.float32),
+                                                  (4, 32, 16, 64, 3, 1, torch.bfloat16), (3, 5, 11, 7, 3, 1, torch.float32)])
+def test_conv_pooled_epilogue_matches_conv_then_relu_pool(B, C, H, M, K, pad, dtype):
+    """conv_fwd_packed_pool (ReLU + 2x2 max-pool in the conv epilogue, row-aligned tiles) must equal
+    the plain conv kernel followed by relu_pool_fwd bit for bit (same MFMA order per output), codes
+    included; the backward through the fused op equals the two-op backward."""
+    ext = L._ext()
+    bf = int(dtype == torch.bfloat16)
+    OH = H + 2 * pad - K + 1
+    if not (ext.conv_fwd_fast(B, C, H, H, M, K, pad, bf) and ext.conv_fwd_pool_ok(B, C, H, H, M, K, pad, bf)):
+        pytest.skip("no pooled plan for this shape")
+    torch.manual_seed(B + C + H + M)
+    x = torch.randn(B, C, H, H, device=DEV)
+    w = (torch.randn(M, C, K, K) / (C * K * K) ** 0.5).to(DEV)
+    b = torch.randn(M, device=DEV)
+    img = torch.empty(ext.conv_fwd_workspace(B, C, H, H, M, K, pad, bf, 0), device=DEV, dtype=torch.uint8)
+    ext.conv_pack_all([(w.data_ptr(), img.data_ptr(), B, C, H, H, M, K, pad, bf, 0)], torch.cuda.current_stream().cuda_stream)
+    packed = (img, None)
+    outs = []
+    for fused in (True, False):
+        xx = x.clone().requires_grad_(True)
+        gw, gb = torch.zeros(M, C, K, K, device=DEV), torch.zeros(M, device=DEV)
+        y = L.Conv2dFn.apply(xx, w, b, pad, dtype, gw, gb, packed, None, fused)
+        if not fused:
+            y = L.ReluPoolFn.apply(y)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).to(DEV)
+        y.backward(dy)
+        outs.append((y.detach(), xx.grad, gw, gb))
+    assert outs[0][0].shape == (B, M, OH // 2, OH // 2)
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 def test_ingest_and_sgd_flat():
     data = synthetic(50, 5).to(DEV)
     eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)
