@@ -293,11 +293,16 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::conv_wgrad_split(B, C, H, W, M, K, pad, &s, &cps);
     return s;
   });
-  m.def("conv_wgrad", [](u x, u dy, u part, u dw, u db, int B, int C, int H, int W, int M, int K, int pad,
-                         int bf16_ops, u stream) {
-    dnn::launch_conv_wgrad(P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), P<float>(db), B, C, H,
-                           W, M, K, pad, bf16_ops, S(stream));
-  });
+  m.def(
+      "conv_wgrad",
+      [](u x, u dy, u part, u dw, u db, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, u stream,
+         u pool_code) {
+        dnn::launch_conv_wgrad(P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), P<float>(db), B, C,
+                               H, W, M, K, pad, bf16_ops, S(stream), P<const uint8_t>(pool_code));
+      },
+      py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("db"), py::arg("B"), py::arg("C"),
+      py::arg("H"), py::arg("W"), py::arg("M"), py::arg("K"), py::arg("pad"), py::arg("bf16_ops"), py::arg("stream"),
+      py::arg("pool_code") = 0);
   m.def("flip_weights", [](u w, int O, int C, int K, u wf, u stream) {
     dnn::launch_flip_weights(P<const float>(w), O, C, K, P<float>(wf), S(stream));
   });

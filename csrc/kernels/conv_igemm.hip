@@ -188,9 +188,13 @@ __global__ void __launch_bounds__(CT) conv_fwd_kernel(const float* __restrict__ 
 }
 
 // ---- wgrad: part[s][m][j] = sum_{r in slice s} dy[m][r] im2col(x)[j][r] -----------------------
-template <bool BF16, int BM>
+// UNPOOL: dy is the gradient of the 2x2 max-pool that followed this conv's ReLU ([B][M][OH/2][OW/2])
+// with its argmax codes; the full-resolution gradient is formed on the load (the value where the
+// code names the position, else 0) instead of by a relu_pool_bwd launch.
+template <bool BF16, int BM, bool UNPOOL = false>
 __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                        float* __restrict__ part, Geom g, int M, int chunks_per_slice) {
+                                                        float* __restrict__ part, Geom g, int M, int chunks_per_slice,
+                                                        const uint8_t* __restrict__ code = nullptr) {
   using T = typename Lds<BF16>::T;
   constexpr int LD = Lds<BF16>::LD;
   __shared__ __attribute__((aligned(16))) T As[BM * LD];
@@ -215,13 +219,35 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
     const bool rv = r < r_end;
     const long rc = rv ? r : r_end - 1;
     const int bb = (int)(rc / OHW), p = (int)(rc % OHW), oy = p / g.OW, ox = p % g.OW;
-    const float* dyb = dy + (long)bb * M * OHW + p;
+    if constexpr (UNPOOL) {
+      const int OH2 = g.OH >> 1, OW2 = g.OW >> 1, py = min(oy >> 1, OH2 - 1), px = min(ox >> 1, OW2 - 1);
+      const bool inb = (oy >> 1) < OH2 && (ox >> 1) < OW2;
+      const uint8_t sub = (uint8_t)(((oy & 1) << 1) | (ox & 1));
+      const long pp = (long)bb * M * OH2 * OW2 + py * OW2 + px;
+      float a[KPT];
+      uint8_t cd[KPT];
 #pragma unroll
-    for (int e = 0; e < KPT; ++e) {
-      const int m = m0 + rowg + e;
-      const bool mv = rowg + e < BM && m < M;
-      const float a = dyb[(long)(mv ? m : 0) * OHW];
-      av[e] = (mv && rv) ? a : 0.f;
+      for (int e = 0; e < KPT; ++e) {
+        const int m = m0 + rowg + e;
+        const long o = pp + (long)((rowg + e < BM && m < M) ? m : 0) * OH2 * OW2;
+        a[e] = dy[o];
+        cd[e] = code[o];
+      }
+#pragma unroll
+      for (int e = 0; e < KPT; ++e) {
+        const int m = m0 + rowg + e;
+        const bool mv = rowg + e < BM && m < M;
+        av[e] = (mv && rv && inb && cd[e] == sub) ? a[e] : 0.f;
+      }
+    } else {
+      const float* dyb = dy + (long)bb * M * OHW + p;
+#pragma unroll
+      for (int e = 0; e < KPT; ++e) {
+        const int m = m0 + rowg + e;
+        const bool mv = rowg + e < BM && m < M;
+        const float a = dyb[(long)(mv ? m : 0) * OHW];
+        av[e] = (mv && rv) ? a : 0.f;
+      }
     }
     gather_rows<true>(x, g, j0 + rowg, Kd, bb, oy, ox, rv, bv);
   };
@@ -711,15 +737,25 @@ void fwd_dispatch(const float* x, const float* w, const float* bias, float* y, c
   HIP_CHECK(hipGetLastError());
 }
 
-template <bool BF16>
-void wgrad_dispatch(const float* x, const float* dy, float* part, const Geom& g, int M, int S, int cps, hipStream_t s) {
+template <bool BF16, bool UNPOOL>
+void wgrad_dispatch_u(const float* x, const float* dy, float* part, const Geom& g, int M, int S, int cps,
+                      const uint8_t* code, hipStream_t s) {
   const int Kd = g.C * g.K * g.K;
   const int bm = pick_bm(M);
   dim3 grid((unsigned)((Kd + 1 + BN - 1) / BN), (unsigned)((M + bm - 1) / bm), (unsigned)S);  // + bias column
-  if (bm == 16) hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 16>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
-  else if (bm == 32) hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 32>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 64>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps);
+  if (bm == 16)
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 16, UNPOOL>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps, code);
+  else if (bm == 32)
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 32, UNPOOL>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps, code);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, 64, UNPOOL>), grid, dim3(CT), 0, s, x, dy, part, g, M, cps, code);
   HIP_CHECK(hipGetLastError());
+}
+template <bool BF16>
+void wgrad_dispatch(const float* x, const float* dy, float* part, const Geom& g, int M, int S, int cps,
+                    const uint8_t* code, hipStream_t s) {
+  if (code != nullptr) wgrad_dispatch_u<BF16, true>(x, dy, part, g, M, S, cps, code, s);
+  else wgrad_dispatch_u<BF16, false>(x, dy, part, g, M, S, cps, nullptr, s);
 }
 
 Geom geom(int B, int C, int H, int W, int K, int pad) {
@@ -785,14 +821,16 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
 }
 
 // dw [M][C][K][K] and db [M] from one MFMA pass; part: S * M * (C K^2 + 1) floats.  dw == nullptr:
-// the slice partials only (the caller sums them later, e.g. inside the SGD tail launch)
+// the slice partials only (the caller sums them later, e.g. inside the SGD tail launch).
+// pool_code != nullptr: dy is the pooled gradient of a fused conv + ReLU + max-pool (see UNPOOL)
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
-                       int M, int K, int pad, int bf16_ops, hipStream_t s) {
+                       int M, int K, int pad, int bf16_ops, hipStream_t s, const uint8_t* pool_code) {
   const Geom g = geom(B, C, H, W, K, pad);
   int S = 1, cps = 1;
   conv_wgrad_split(B, C, H, W, M, K, pad, &S, &cps);
-  if (bf16_ops) wgrad_dispatch<true>(x, dy, part, g, M, S, cps, s);
-  else wgrad_dispatch<false>(x, dy, part, g, M, S, cps, s);
+  if (pool_code != nullptr && (g.OH < 2 || g.OW < 2)) throw std::runtime_error("conv_wgrad: pooled dy of a < 2x2 map");
+  if (bf16_ops) wgrad_dispatch<true>(x, dy, part, g, M, S, cps, pool_code, s);
+  else wgrad_dispatch<false>(x, dy, part, g, M, S, cps, pool_code, s);
   if (dw == nullptr) return;
   const int Kd = C * K * K;
   const long n = (long)M * (Kd + 1);

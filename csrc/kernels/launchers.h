@@ -94,7 +94,8 @@ void launch_conv_fwd(const float* x, const float* w, const float* bias, float* y
                      int M, int K, int pad, int bf16_ops, int flip, hipStream_t s);
 void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S, int* cps);
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int C, int H, int W,
-                       int M, int K, int pad, int bf16_ops, hipStream_t s);
+                       int M, int K, int pad, int bf16_ops, hipStream_t s,
+                       const uint8_t* pool_code = nullptr);
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s);
 // Weight packing for the LDS-patch path, hoisted out of the convolutions: one launch packs
 // the forward (flip = 0) and dgrad (flip = 1) images of every fast-path layer of a step

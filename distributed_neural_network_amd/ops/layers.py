@@ -125,10 +125,14 @@ class Conv2dFn(torch.autograd.Function):
         B, C, H, W, K, pad, OH, OW = ctx.shape
         Cout = w.shape[0]
         dy = dy.contiguous()
-        if ctx.code is not None:  # the fused pool's backward: scatter to the argmax positions
+        pool_code = 0
+        if ctx.code is not None and ctx.needs_input_grad[0]:
+            # the fused pool's backward: scatter to the argmax positions (the dgrad reads full dy)
             full = torch.empty(B, Cout, OH, OW, device=dy.device, dtype=torch.float32)
             _ext().relu_pool_bwd(_p(dy), _p(ctx.code), B * Cout, OH, OW, _p(full), _s(dy))
             dy = full
+        elif ctx.code is not None:  # weight gradient only: it unpools dy on its loads
+            pool_code = _p(ctx.code)
         bf = int(ctx.gemm_dtype == torch.bfloat16)
         dw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
         db = ctx.gb if ctx.gb is not None else torch.empty(Cout, device=dy.device, dtype=torch.float32)
@@ -138,10 +142,10 @@ class Conv2dFn(torch.autograd.Function):
             S = ext.conv_wgrad_slices(B, C, H, W, Cout, K, pad)
             part = torch.empty(S * Cout * (C * K * K + 1), device=dy.device, dtype=torch.float32)
             if ctx.slice_sink is not None:  # partials only: summed by the engine's SGD tail
-                ext.conv_wgrad(_p(x), _p(dy), _p(part), 0, 0, B, C, H, W, Cout, K, pad, bf, st)
+                ext.conv_wgrad(_p(x), _p(dy), _p(part), 0, 0, B, C, H, W, Cout, K, pad, bf, st, pool_code)
                 ctx.slice_sink.append((part, S, Cout, C * K * K, dw, db))
-            else:
-                ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), _p(db), B, C, H, W, Cout, K, pad, bf, st)  # dW, db
+            else:  # dW, db
+                ext.conv_wgrad(_p(x), _p(dy), _p(part), _p(dw), _p(db), B, C, H, W, Cout, K, pad, bf, st, pool_code)
             if ctx.needs_input_grad[0]:
                 # dgrad: the forward kernel over dY with the flipped, transposed weights
                 # (flip=1: packed from w inside the launch), pad' = K - 1 - pad
