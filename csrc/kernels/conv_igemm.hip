@@ -29,6 +29,7 @@
 // The next chunk's global gathers are issued before the current chunk's MFMAs (register
 // prefetch), so their latency overlaps the math and the other resident workgroups.
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
@@ -802,6 +803,11 @@ int conv_fwd_fast(int B, int C, int H, int W, int M, int K, int pad, int bf16_op
   return plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0).ok ? 1 : 0;
 }
 
+long env_long(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  return (v != nullptr && *v != '\0') ? std::max(1L, std::atol(v)) : dflt;
+}
+
 // slices for the wgrad split: enough workgroups to fill the chip, >= 4 chunks per slice
 void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S, int* cps) {
   const Geom g = geom(B, C, H, W, K, pad);
@@ -809,12 +815,16 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
   const long chunks = (R + BK - 1) / BK;
   const int Kd = C * K * K, bm = pick_bm(M);
   const long tiles = (long)((Kd + 1 + BN - 1) / BN) * ((M + bm - 1) / bm);
-  // ~1024 workgroups (4 per CU: a slice's chunks run back to back, so the chip must be
-  // full), at most 256 slices (the slice sum reads S partials per element), at least 4
+  // ~2048 workgroups (8 per CU: a slice's chunks run back to back, so the chip must be
+  // full), at most 512 slices (the slice sum reads S partials per element), at least 2
   // chunks per slice.  (A 64-slice cap left conv1's single tile with 64 workgroups of
-  // 16 serial chunks each: 45 us.)
-  long want = std::max(1L, 1024 / std::max(1L, tiles));
-  want = std::min({want, 256L, std::max(1L, chunks / 4)});
+  // 16 serial chunks each: 45 us; 1024 / 256 / 4 -> 2048 / 512 / 2 took lenet 91.6 -> 84.7 us,
+  // cifar-vgg bf16 300.6 -> 296.3 us per step: profiles/r2/layer_fusion/wsplit/.)
+  // (DNN_WGRAD_WGS / _MAX_SLICES / _MIN_CHUNKS override the three numbers: tuning runs)
+  static const long wgs = env_long("DNN_WGRAD_WGS", 2048), max_s = env_long("DNN_WGRAD_MAX_SLICES", 512),
+                    min_c = env_long("DNN_WGRAD_MIN_CHUNKS", 2);
+  long want = std::max(1L, wgs / std::max(1L, tiles));
+  want = std::min({want, max_s, std::max(1L, chunks / min_c)});
   const long per = (chunks + want - 1) / want;
   *cps = (int)per;
   *S = (int)((chunks + per - 1) / per);
