@@ -18,6 +18,7 @@ New flags: --sync, --device, --data, --data-root, --seed, --save, --resume,
 from __future__ import annotations
 
 import argparse
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -67,6 +68,8 @@ class TrainConfig:
     engine: str = "auto"
     dtype: str = "bf16"
     check_sync: bool = False
+    debug_sync: bool = False
+    use_graphs: bool = True
     bucket_kb: int = 0
     extra: dict = field(default_factory=dict)
 
@@ -122,6 +125,9 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
     g.add_argument("--check-sync", action="store_true",
                    help="after every synchronisation assert that all ranks hold bit-identical parameters "
                         "(cross-rank checksum)")
+    g.add_argument("--debug-sync", action="store_true",
+                   help="race / fault hunting: serialised kernel launches (AMD_SERIALIZE_KERNEL=3, "
+                        "HIP_LAUNCH_BLOCKING=1), no hipGraphs, NCCL_DEBUG=INFO and --check-sync")
 
 
 def parser(mode: str) -> argparse.ArgumentParser:
@@ -146,4 +152,19 @@ def parse(mode: str, argv=None) -> TrainConfig:
     cfg = TrainConfig(mode=mode)
     for k, v in vars(ns).items():
         setattr(cfg, k, v)
+    if cfg.debug_sync:
+        apply_debug_sync(cfg)
     return cfg
+
+
+DEBUG_SYNC_ENV = {"AMD_SERIALIZE_KERNEL": "3", "HIP_LAUNCH_BLOCKING": "1", "NCCL_DEBUG": "INFO"}
+
+
+def apply_debug_sync(cfg: TrainConfig) -> None:
+    """--debug-sync: every kernel runs alone and the host waits for it, so a
+    faulting or racing kernel is reported at its own launch; replicas are checksummed after every
+    sync.  The HIP variables only act before the runtime initialises, which parse() precedes."""
+    for k, v in DEBUG_SYNC_ENV.items():
+        os.environ.setdefault(k, v)
+    cfg.check_sync = True
+    cfg.use_graphs = False

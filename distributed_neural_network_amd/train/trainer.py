@@ -157,7 +157,7 @@ class Trainer:
         c = self.cfg
         eng_kw = {}
         if self.device.type == "cuda":
-            eng_kw = dict(graph_chunk=c.graph_chunk, overlap=c.overlap)
+            eng_kw = dict(graph_chunk=c.graph_chunk, overlap=c.overlap, use_graphs=c.use_graphs)
         self.timers = PhaseTimers()
         with self.timers.phase(PhaseTimers.DATA, sync=False):
             self.train, self.test = get_splits(c.data, c.data_root, c.train_samples, c.test_samples, c.seed)

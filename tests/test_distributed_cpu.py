@@ -135,6 +135,20 @@ def test_typed_cli_overrides_work():
     assert (s.batch_size, s.epochs) == (4, 15)
 
 
+def test_debug_sync_flag(monkeypatch):
+    """--debug-sync: serialised launches via the HIP environment (set before the runtime starts),
+    eager steps, RCCL debug output and the cross-rank checksum after every sync."""
+    from distributed_neural_network_amd.train import parse
+    from distributed_neural_network_amd.train.config import DEBUG_SYNC_ENV
+    env = {k: v for k, v in os.environ.items() if k not in DEBUG_SYNC_ENV}
+    monkeypatch.setattr(os, "environ", env)  # restored after the test
+    c = parse("single", ["--debug-sync"])
+    assert c.check_sync and not c.use_graphs
+    for k, v in DEBUG_SYNC_ENV.items():
+        assert os.environ[k] == v
+    assert parse("single", []).use_graphs
+
+
 def test_straggler_prints(capsys):
     from distributed_neural_network_amd.parallel.fault import simulate_failure
     rng = np.random.default_rng(0)
