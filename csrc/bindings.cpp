@@ -196,13 +196,20 @@ PYBIND11_MODULE(_dnn_hip, m) {
                        P<const float>(smean), P<const float>(sinvstd), P<float>(dx), P<float>(dgamma),
                        P<float>(dbeta), P<double>(part), S(stream));
   });
-  m.def("bn_act_fwd_train", [](u x, int B, int C, int H, int W, u state, u gamma, u beta, float eps, float mom,
-                               u rmean, u rvar, u y, u code, u smean, u sinvstd, u part, int act, u stream) {
-    dnn::launch_bn_act_fwd_train(P<const float>(x), B, C, H, W, P<const int32_t>(state), P<const float>(gamma),
-                                 P<const float>(beta), eps, mom, P<float>(rmean), P<float>(rvar), P<float>(y),
-                                 P<uint8_t>(code), P<float>(smean), P<float>(sinvstd), P<double>(part), act,
-                                 S(stream));
-  });
+  // ext_parts > 0: part holds that many statistics partials per channel already (conv epilogue)
+  m.def(
+      "bn_act_fwd_train",
+      [](u x, int B, int C, int H, int W, u state, u gamma, u beta, float eps, float mom, u rmean, u rvar, u y, u code,
+         u smean, u sinvstd, u part, int act, u stream, int ext_parts) {
+        dnn::launch_bn_act_fwd_train(P<const float>(x), B, C, H, W, P<const int32_t>(state), P<const float>(gamma),
+                                     P<const float>(beta), eps, mom, P<float>(rmean), P<float>(rvar), P<float>(y),
+                                     P<uint8_t>(code), P<float>(smean), P<float>(sinvstd), P<double>(part), act,
+                                     S(stream), ext_parts);
+      },
+      py::arg("x"), py::arg("B"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("state"), py::arg("gamma"),
+      py::arg("beta"), py::arg("eps"), py::arg("mom"), py::arg("rmean"), py::arg("rvar"), py::arg("y"),
+      py::arg("code"), py::arg("smean"), py::arg("sinvstd"), py::arg("part"), py::arg("act"), py::arg("stream"),
+      py::arg("ext_parts") = 0);
   m.def("bn_act_bwd", [](u dy, u x, int B, int C, int H, int W, u state, u gamma, u beta, u smean, u sinvstd, u code,
                          u dx, u dgamma, u dbeta, u part, int act, u stream) {
     dnn::launch_bn_act_bwd(P<const float>(dy), P<const float>(x), B, C, H, W, P<const int32_t>(state),
@@ -287,6 +294,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                    int bf16_ops, u stream) {
     dnn::launch_conv_fwd_packed_pool(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y),
                                      P<uint8_t>(code), B, C, H, W, M, K, pad, bf16_ops, S(stream));
+  });
+  m.def("conv_fwd_stat_parts", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+    return dnn::conv_fwd_stat_parts(B, C, H, W, M, K, pad, bf16_ops);
+  });
+  m.def("conv_fwd_packed_stats", [](u x, u wp, u bias, u y, u stats, u state, int B, int C, int H, int W, int M, int K,
+                                    int pad, int bf16_ops, u stream) {
+    dnn::launch_conv_fwd_packed_stats(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y),
+                                      P<double>(stats), P<const int32_t>(state), B, C, H, W, M, K, pad, bf16_ops,
+                                      S(stream));
   });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;

@@ -376,15 +376,25 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
   }
 }
 
-// POOL: ReLU + 2x2 max-pool (first maximum wins, code 4 = max <= 0 - relu_pool_fwd_kernel's
-// exact rule) in the epilogue: tiles are rpt whole output rows, the tile's conv outputs go
-// through LDS, y is the pooled [B][M][OH/2][OW/2] output and code its argmax codes; the
-// full-resolution output is never written.
-template <bool BF16, int BM, int CCH, bool V4, bool POOL = false>
+// Epilogues (EPI):
+//   EPI_PLAIN  y = conv + bias.
+//   EPI_POOL   ReLU + 2x2 max-pool (first maximum wins, code 4 = max <= 0 - relu_pool_fwd_kernel's
+//              exact rule): tiles are rpt whole output rows, the tile's conv outputs go through
+//              LDS, y is the pooled [B][M][OH/2][OW/2] output and code its argmax codes; the
+//              full-resolution output is never written.
+//   EPI_STATS  y as EPI_PLAIN, plus the following BatchNorm's batch statistics: per channel the
+//              tile's (sum y, sum y^2) in fp64 over its positions (fixed order) into
+//              stats[(m * P + tile) * 2 + {0, 1}], P = B * tiles; images past the step state's
+//              valid count contribute 0 (the padded tail batch, as chan_partial_kernel).
+constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2;
+template <bool BF16, int BM, int CCH, bool V4, int EPI = EPI_PLAIN>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
                                                             const typename PatchT<BF16, CCH>::T* __restrict__ wp,
                                                             const float* __restrict__ bias, float* __restrict__ y,
-                                                            PGeom g, uint8_t* __restrict__ code = nullptr) {
+                                                            PGeom g, uint8_t* __restrict__ code = nullptr,
+                                                            double* __restrict__ stats = nullptr,
+                                                            const int32_t* __restrict__ state = nullptr) {
+  constexpr bool POOL = EPI == EPI_POOL;
   static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
   using T = typename PatchT<BF16, CCH>::T;
   constexpr int CCP = PatchT<BF16, CCH>::CCP;
@@ -627,6 +637,45 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       }
     }
   }
+  if constexpr (EPI == EPI_STATS) {
+    const int bvalid = state != nullptr ? min(state[ST_BVALID], g.B) : g.B;
+    __syncthreads();  // every wave is done with As / Ps: the tile's outputs reuse the LDS
+    float* ot = reinterpret_cast<float*>(smem);  // [BM][PNT]
+#pragma unroll
+    for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = 16 * i + 4 * q + j, m = m0 + ml;
+        ot[ml * PNT + local] =
+            (pn < OHW && m < g.M) ? acc[i][j] + (bias != nullptr ? bias[m] : 0.f) : 0.f;  // same value as y
+      }
+    }
+    __syncthreads();
+    // TPC consecutive threads per channel, PNT / TPC consecutive positions each, then a xor
+    // butterfly over the TPC lanes (fixed order; every lane ends with the same fp64 sums)
+    constexpr int TPC = CT / BM, PPT = PNT / TPC;
+    static_assert(TPC <= 64 && 64 % TPC == 0 && PNT % TPC == 0, "channel group inside one wave");
+    const int ml = tid / TPC, pi = tid - ml * TPC;
+    double s0 = 0.0, s1 = 0.0;
+    if (b < bvalid) {
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const double v = (double)ot[ml * PNT + pi * PPT + k];
+        s0 += v;
+        s1 += v * v;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < TPC; off <<= 1) {
+      s0 += __shfl_xor(s0, off);
+      s1 += __shfl_xor(s1, off);
+    }
+    if (pi == 0 && m0 + ml < g.M) {
+      const long P = (long)g.B * g.tiles, o = ((long)(m0 + ml) * P + tile) * 2;
+      stats[o] = s0;
+      stats[o + 1] = s1;
+    }
+  }
 }
 
 int pick_bm(int M) { return M <= 16 ? 16 : (M <= 32 ? 32 : 64); }
@@ -682,30 +731,37 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf, i
   return f;
 }
 
-template <bool BF16, int CCH, bool V4, bool POOL>
+struct EpiArgs {
+  uint8_t* code = nullptr;          // EPI_POOL
+  double* stats = nullptr;          // EPI_STATS
+  const int32_t* state = nullptr;   // EPI_STATS
+};
+template <bool BF16, int CCH, bool V4, int EPI>
 void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
-                   float* y, uint8_t* code, hipStream_t s) {
+                   float* y, const EpiArgs& e, hipStream_t s) {
   dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
   if (f.bm == 16)
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, POOL>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       code);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
+                       e.code, e.stats, e.state);
   else
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, POOL>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       code);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
+                       e.code, e.stats, e.state);
   HIP_CHECK(hipGetLastError());
 }
-// float4 patch groups when image rows are whole 16-B vectors; code != nullptr: pooled epilogue
+template <bool BF16, int CCH, int EPI>
+void fast_launch_e(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
+                   float* y, const EpiArgs& e, hipStream_t s) {
+  // float4 patch groups when image rows are whole 16-B vectors
+  if (f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) fast_launch_v<BF16, CCH, true, EPI>(f, wp, x, bias, y, e, s);
+  else fast_launch_v<BF16, CCH, false, EPI>(f, wp, x, bias, y, e, s);
+}
+// the epilogue follows from the arguments: code -> pooled, stats -> BatchNorm statistics
 template <bool BF16, int CCH>
 void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
-                 float* y, hipStream_t s, uint8_t* code = nullptr) {
-  const bool v4 = f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
-  if (code != nullptr) {
-    if (v4) fast_launch_v<BF16, CCH, true, true>(f, wp, x, bias, y, code, s);
-    else fast_launch_v<BF16, CCH, false, true>(f, wp, x, bias, y, code, s);
-  } else {
-    if (v4) fast_launch_v<BF16, CCH, true, false>(f, wp, x, bias, y, nullptr, s);
-    else fast_launch_v<BF16, CCH, false, false>(f, wp, x, bias, y, nullptr, s);
-  }
+                 float* y, hipStream_t s, const EpiArgs& e = EpiArgs{}) {
+  if (e.code != nullptr) fast_launch_e<BF16, CCH, EPI_POOL>(f, wp, x, bias, y, e, s);
+  else if (e.stats != nullptr) fast_launch_e<BF16, CCH, EPI_STATS>(f, wp, x, bias, y, e, s);
+  else fast_launch_e<BF16, CCH, EPI_PLAIN>(f, wp, x, bias, y, e, s);
 }
 
 template <bool BF16>
@@ -922,6 +978,18 @@ void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, f
   }
 }
 
+void fast_launch_packed(const FastPlan& f, const void* wp, const float* x, const float* bias, float* y, int bf16_ops,
+                        const EpiArgs& e, hipStream_t s) {
+  if (bf16_ops) {
+    fast_launch<true, 32>(f, reinterpret_cast<const bf16*>(wp), x, bias, y, s, e);
+  } else {
+    const float* w = reinterpret_cast<const float*>(wp);
+    if (f.cch == 8) fast_launch<false, 8>(f, w, x, bias, y, s, e);
+    else if (f.cch == 16) fast_launch<false, 16>(f, w, x, bias, y, s, e);
+    else fast_launch<false, 32>(f, w, x, bias, y, s, e);
+  }
+}
+
 // the pooled plan of a layer whose plain plan packed the weight image (same M tile)
 FastPlan plan_pool(int B, int C, int H, int W, int M, int K, int pad, bool bf) {
   const FastPlan f0 = plan_fast(B, C, H, W, M, K, pad, bf);
@@ -939,14 +1007,29 @@ void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bi
   geom(B, C, H, W, K, pad);
   const FastPlan f = plan_pool(B, C, H, W, M, K, pad, bf16_ops != 0);
   if (!f.ok) throw std::runtime_error("conv_fwd_packed_pool: layer has no pooled LDS-patch plan");
-  if (bf16_ops) {
-    fast_launch<true, 32>(f, reinterpret_cast<const bf16*>(wp), x, bias, y, s, code);
-  } else {
-    const float* w = reinterpret_cast<const float*>(wp);
-    if (f.cch == 8) fast_launch<false, 8>(f, w, x, bias, y, s, code);
-    else if (f.cch == 16) fast_launch<false, 16>(f, w, x, bias, y, s, code);
-    else fast_launch<false, 32>(f, w, x, bias, y, s, code);
-  }
+  EpiArgs e;
+  e.code = code;
+  fast_launch_packed(f, wp, x, bias, y, bf16_ops, e, s);
+}
+
+int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  return f.ok ? f.pg.B * f.pg.tiles : 0;
+}
+
+// y = conv(x, w) + bias from the packed image, plus the BatchNorm statistics partials of y
+// (stats: M * conv_fwd_stat_parts() * 2 doubles; see EPI_STATS)
+void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* bias, float* y, double* stats,
+                                  const int32_t* state, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                                  hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (!f.ok) throw std::runtime_error("conv_fwd_packed_stats: layer is not on the LDS-patch path");
+  if ((size_t)f.bm * PNT * sizeof(float) > f.lds) throw std::runtime_error("conv_fwd_packed_stats: LDS too small");
+  EpiArgs e;
+  e.stats = stats;
+  e.state = state;
+  fast_launch_packed(f, wp, x, bias, y, bf16_ops, e, s);
 }
 
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s) {

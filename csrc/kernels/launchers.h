@@ -78,7 +78,8 @@ void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const i
 // takes the gradient of the ACTIVATION output (pooled for act 2).
 void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const int32_t* state, const float* gamma,
                              const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
-                             float* smean, float* sinvstd, double* part, int act, hipStream_t s);
+                             float* smean, float* sinvstd, double* part, int act, hipStream_t s,
+                             int ext_parts = 0);
 void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
                        const float* gamma, const float* beta, const float* smean, const float* sinvstd,
                        const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
@@ -113,6 +114,11 @@ void launch_conv_fwd_packed(const float* x, const void* wp, const float* bias, f
 int conv_fwd_pool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
 void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bias, float* y, uint8_t* code, int B,
                                  int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
+// conv + bias with the following BatchNorm's batch-statistics partials in the epilogue
+int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
+void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* bias, float* y, double* stats,
+                                  const int32_t* state, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                                  hipStream_t s);
 void launch_sgd_flat(float* p, const float* g, float* m, long n, float lr, float momentum, float grad_scale,
                      hipStream_t s);
 // element map of a packed conv-weight image (the LDS-patch plan of the job's layer)

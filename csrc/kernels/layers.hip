@@ -284,13 +284,20 @@ __global__ void __launch_bounds__(LT) bn_apply_train_kernel(const float* __restr
                                                             float* __restrict__ save_mean,
                                                             float* __restrict__ save_invstd,
                                                             const double* __restrict__ part, int W,
-                                                            uint8_t* __restrict__ code) {
+                                                            uint8_t* __restrict__ code, int nparts) {
   __shared__ float st[2];
-  const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
+  __shared__ double red[2 * (LT / 64)];
+  const int c = blockIdx.y, p = blockIdx.x;
   const int bv = valid_count(state, B), ppb = chan_ppb(B, L);
+  // merge the channel's nparts partials (chan_partial_kernel's, or a conv epilogue's - one per
+  // output tile) across the block: strided fp64 sums, then the fixed-order block sum
+  double s0 = 0.0, s1 = 0.0;
+  for (int q = threadIdx.x; q < nparts; q += LT) {
+    s0 += part[((size_t)c * nparts + q) * 2];
+    s1 += part[((size_t)c * nparts + q) * 2 + 1];
+  }
+  block_sum2_d(s0, s1, red);
   if (threadIdx.x == 0) {
-    double s0, s1;
-    merge_parts(part, c, P, s0, s1);
     const double n = (double)bv * L;
     const double mean = n > 0 ? s0 / n : 0.0;
     const double var = n > 0 ? fmax(s1 / n - mean * mean, 0.0) : 0.0;
@@ -592,14 +599,17 @@ static bool vec4_ok(int L, int W, int act, std::initializer_list<const void*> pt
   return true;
 }
 template <int ACT, int VW>
+// ext_parts > 0: part already holds that many statistics partials per channel (the conv
+// forward epilogue wrote them) - only the normalise / activate kernel runs
 static void bn_fwd_launch(const float* x, int B, int C, int L, int W, const int32_t* state, const float* gamma,
                           const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
-                          float* smean, float* sinvstd, double* part, hipStream_t s) {
+                          float* smean, float* sinvstd, double* part, hipStream_t s, int ext_parts = 0) {
   const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL((chan_partial_kernel<0, 0, VW>), grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr,
-                     nullptr, part, nullptr, ActArgs{});
+  if (ext_parts <= 0)
+    hipLaunchKernelGGL((chan_partial_kernel<0, 0, VW>), grid, dim3(LT), 0, s, x, nullptr, B, C, L, state, nullptr,
+                       nullptr, part, nullptr, ActArgs{});
   hipLaunchKernelGGL((bn_apply_train_kernel<ACT, VW>), grid, dim3(LT), 0, s, x, B, C, L, state, gamma, beta, eps, m,
-                     rmean, rvar, y, smean, sinvstd, part, W, code);
+                     rmean, rvar, y, smean, sinvstd, part, W, code, ext_parts > 0 ? ext_parts : (int)grid.x);
 }
 void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                          const float* beta, float eps, float m, float* rmean, float* rvar, float* y, float* smean,
@@ -612,12 +622,12 @@ void launch_bn_fwd_train(const float* x, int B, int C, int L, const int32_t* sta
 }
 void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const int32_t* state, const float* gamma,
                              const float* beta, float eps, float m, float* rmean, float* rvar, float* y, uint8_t* code,
-                             float* smean, float* sinvstd, double* part, int act, hipStream_t s) {
+                             float* smean, float* sinvstd, double* part, int act, hipStream_t s, int ext_parts) {
   if (!C) return;
   const int L = H * W;
   const bool v4 = vec4_ok(L, W, act == 2 ? 0 : act, {x, act == 2 ? nullptr : y});  // (pooled output: scalar)
 #define BN_FWD(A, V) bn_fwd_launch<A, V>(x, B, C, L, W, state, gamma, beta, eps, m, rmean, rvar, y, code, smean, \
-                                          sinvstd, part, s)
+                                          sinvstd, part, s, ext_parts)
   if (act == 1) { if (v4) BN_FWD(1, 4); else BN_FWD(1, 1); }
   else if (act == 2) { if (v4) BN_FWD(2, 4); else BN_FWD(2, 1); }
   else { if (v4) BN_FWD(0, 4); else BN_FWD(0, 1); }

@@ -83,11 +83,14 @@ class Conv2dFn(torch.autograd.Function):
     slice partials and appends (partials, S, Cout, C K^2, gw, gb) for the engine's SGD tail
     launch to sum (one launch fewer per layer); the list keeps the partials alive until then.
     ``pool``: the following ReLU + 2x2 max-pool runs in the forward kernel's epilogue (GPU, packed
-    forward image): the op returns the pooled output, and its backward starts with the pool's."""
+    forward image): the op returns the pooled output, and its backward starts with the pool's.
+    ``stats``: a ``BnStats`` (GPU, packed forward image): the epilogue also writes the following
+    BatchNorm's batch-statistics partials, which ``BatchNormActFn`` then uses instead of its own
+    statistics pass."""
 
     @staticmethod
     def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None,
-                pool: bool = False):
+                pool: bool = False, stats: "BnStats | None" = None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -100,6 +103,15 @@ class Conv2dFn(torch.autograd.Function):
             ctx.code = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.uint8)
             _ext().conv_fwd_packed_pool(_p(x), _p(packed[0]), _p(b), _p(y), _p(ctx.code), B, C, H, W, Cout, K, pad, bf,
                                         _s(x))
+        elif _is_gpu(x) and stats is not None:
+            assert packed is not None and packed[0] is not None, "conv statistics epilogue needs the packed image"
+            y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
+            ext = _ext()
+            stats.nparts = ext.conv_fwd_stat_parts(B, C, H, W, Cout, K, pad, bf)
+            stats.part = torch.empty(Cout * stats.nparts * 2, device=x.device, dtype=torch.float64)
+            ext.conv_fwd_packed_stats(_p(x), _p(packed[0]), _p(b), _p(y), _p(stats.part),
+                                      _p(stats.state) if stats.state is not None else 0, B, C, H, W, Cout, K, pad, bf,
+                                      _s(x))
         elif _is_gpu(x):
             ext = _ext()
             y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
@@ -165,8 +177,18 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
+
+
+class BnStats:
+    """Hand-off of a BatchNorm's batch-statistics partials from the conv forward epilogue that
+    produced its input (``part``: fp64 [C][nparts][2], filled by the conv) to BatchNormActFn."""
+
+    def __init__(self, state: torch.Tensor | None) -> None:
+        self.state = state
+        self.part: torch.Tensor | None = None
+        self.nparts = 0
 
 
 # ---- fused ReLU + 2x2 max-pool ---------------------------------------------------------------
@@ -319,7 +341,10 @@ class LinearFn(torch.autograd.Function):
                 ext.linear_bwd(_p(dy), ym, _p(w), _p(x), _p(dx) if dx is not None else 0, _p(gw), _p(gb), B, K, N,
                                st)
             else:
-                dz = dy * (y > 0) if y is not None else dy
+                dz = dy
+                if y is not None:  # ReLU mask: one relu_bwd launch (not torch's compare + multiply)
+                    dz = torch.empty_like(dy)
+                    ext.relu_bwd(_p(dy), _p(y), dy.numel(), _p(dz), st)
                 if ctx.needs_input_grad[0]:
                     dx = torch.mm(dz, w)
                 torch.mm(dz.t(), x, out=gw)
@@ -433,7 +458,7 @@ class BatchNormActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, state, eps: float, momentum: float, act: int,
-                ggamma=None, gbeta=None):
+                ggamma=None, gbeta=None, stats: BnStats | None = None):
         B, C, H, W = x.shape
         x = x.contiguous()
         ext = _ext()
@@ -445,10 +470,13 @@ class BatchNormActFn(torch.autograd.Function):
         else:
             y = torch.empty_like(x)
             code = torch.zeros(0, device=x.device, dtype=torch.uint8)
-        part = _partials(x, B, C, H * W)
+        if stats is not None and stats.part is not None:  # partials from the conv epilogue
+            part, ext_parts = stats.part, stats.nparts
+        else:
+            part, ext_parts = _partials(x, B, C, H * W), 0
         ext.bn_act_fwd_train(_p(x), B, C, H, W, _p(state) if state is not None else 0, _p(gamma), _p(beta), eps,
                              momentum, _p(running_mean), _p(running_var), _p(y), _p(code) if act == 2 else 0,
-                             _p(mean), _p(invstd), _p(part), act, _s(x))
+                             _p(mean), _p(invstd), _p(part), act, _s(x), ext_parts)
         ctx.act = act
         ctx.gg, ctx.gb = ggamma, gbeta
         ctx.save_for_backward(x, gamma, beta, mean, invstd, code, state if state is not None else torch.zeros(0))
@@ -467,10 +495,10 @@ class BatchNormActFn(torch.autograd.Function):
         _ext().bn_act_bwd(_p(dy), _p(x), B, C, H, W, _p(state) if state is not None else 0, _p(gamma), _p(beta),
                           _p(mean), _p(invstd), _p(code) if ctx.act == 2 else 0, _p(dx), _p(dgamma), _p(dbeta),
                           _p(_partials(dy, B, C, H * W)), ctx.act, _s(dy))
-        none8 = (None,) * 8
+        none9 = (None,) * 9
         if inplace:
-            return (dx, None, None) + none8
-        return (dx, dgamma, dbeta) + none8
+            return (dx, None, None) + none9
+        return (dx, dgamma, dbeta) + none9
 
 
 # ---- softmax cross-entropy (mean over the valid batch) + accuracy ----------------------------

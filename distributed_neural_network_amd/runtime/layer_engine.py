@@ -169,6 +169,7 @@ class LayerEngine(Engine):
             self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
         fuse_act = training and self.gpu  # BN + following ReLU / ReLU-pool in one op (MI355X training)
         skip = False
+        bn_stats = None  # statistics partials a conv epilogue produced for the BatchNorm after it
         for i, layer in enumerate(self.spec):
             if skip:  # activation already applied by the fused BatchNorm
                 skip = False
@@ -179,15 +180,23 @@ class LayerEngine(Engine):
             if fuse_act and isinstance(layer, zoo.BN) and isinstance(nxt, (zoo.Relu, zoo.ReluPool)):
                 act = 2 if isinstance(nxt, zoo.ReluPool) else 1
                 x = L.BatchNormActFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
-                                           Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb)
+                                           Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb,
+                                           bn_stats)
+                bn_stats = None
                 skip = True
             elif isinstance(layer, zoo.Conv):
                 packed = self._packed.get(n)
                 # conv -> ReLU + max-pool: the pool in the conv kernel's epilogue (one launch)
                 pool = (self.gpu and isinstance(nxt, zoo.ReluPool) and packed is not None and packed[0] is not None
                         and n in self._pool_ok)
+                # conv -> BatchNorm (+ activation) in training: the conv epilogue computes the
+                # BatchNorm's batch statistics (no statistics pass over the conv output)
+                nn2 = self.spec[i + 2] if i + 2 < len(self.spec) else None
+                if (fuse_act and isinstance(nxt, zoo.BN) and isinstance(nn2, (zoo.Relu, zoo.ReluPool))
+                        and packed is not None and packed[0] is not None):
+                    bn_stats = L.BnStats(state)
                 x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, packed, slice_sink,
-                                     pool)
+                                     pool, bn_stats)
                 skip = pool
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],

@@ -307,6 +307,43 @@ def test_conv_pooled_epilogue_matches_conv_then_relu_pool(B, C, H, M, K, pad, dt
         assert (a is None and c is None) or torch.equal(a, c)
 
 
+@pytest.mark.parametrize("B,C,H,M,K,pad,dtype,act,bvalid", [(8, 3, 32, 16, 3, 1, torch.bfloat16, 1, 8),
+                                                          (8, 6, 14, 16, 5, 0, torch.float32, 2, 5),
+                                                          (6, 32, 16, 64, 3, 1, torch.bfloat16, 2, 6)])
+def test_conv_epilogue_batchnorm_statistics(B, C, H, M, K, pad, dtype, act, bvalid):
+    """BatchNorm statistics computed in the conv forward epilogue (fp64 per-tile partials, padded
+    tail masked) vs BatchNorm's own statistics pass: same normalised output, running stats and
+    backward (different fp64 summation order: close, not bitwise)."""
+    ext = L._ext()
+    bf = int(dtype == torch.bfloat16)
+    if not ext.conv_fwd_fast(B, C, H, H, M, K, pad, bf):
+        pytest.skip("not on the LDS-patch path")
+    torch.manual_seed(B * 3 + C + M)
+    x = torch.randn(B, C, H, H, device=DEV)
+    w = (torch.randn(M, C, K, K) / (C * K * K) ** 0.5).to(DEV)
+    b = torch.randn(M, device=DEV)
+    gamma, beta = torch.rand(M, device=DEV) + 0.5, torch.randn(M, device=DEV)
+    st = torch.tensor([0, bvalid, 0, 0], dtype=torch.int32, device=DEV)
+    img = torch.empty(ext.conv_fwd_workspace(B, C, H, H, M, K, pad, bf, 0), device=DEV, dtype=torch.uint8)
+    ext.conv_pack_all([(w.data_ptr(), img.data_ptr(), B, C, H, H, M, K, pad, bf, 0)], torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for fused in (True, False):
+        xx = x.clone().requires_grad_(True)
+        rm, rv = torch.zeros(M, device=DEV), torch.ones(M, device=DEV)
+        gw, gb = torch.zeros(M, C, K, K, device=DEV), torch.zeros(M, device=DEV)
+        gg, gbb = torch.zeros(M, device=DEV), torch.zeros(M, device=DEV)
+        stats = L.BnStats(st) if fused else None
+        y = L.Conv2dFn.apply(xx, w, b, pad, dtype, gw, gb, (img, None), None, False, stats)
+        if fused:
+            assert stats.part is not None and stats.nparts > 0
+        z = L.BatchNormActFn.apply(y, gamma, beta, rm, rv, st, 1e-5, 0.1, act, gg, gbb, stats)
+        dz = torch.randn(z.shape, generator=torch.Generator().manual_seed(9)).to(DEV)
+        z.backward(dz)
+        outs.append((z.detach(), rm, rv, xx.grad, gw, gb, gg, gbb))
+    for a, c in zip(*outs):
+        _close(a, c, 1e-5)
+
+
 def test_ingest_and_sgd_flat():
     data = synthetic(50, 5).to(DEV)
     eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)
