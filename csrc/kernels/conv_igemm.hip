@@ -214,12 +214,42 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
 #pragma unroll
   for (int i = 0; i < BM / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Every load is a raw buffer load whose offset is out of range (the hardware returns 0) when
+  // the element is: no exec-masked loads, no 64-bit address math.  The KPT im2col rows of this
+  // thread are chunk-invariant: their (c, ky, kx) decomposition is done once, as a row offset
+  // and the (ky - pad, kx - pad) shift; per chunk only the position (b, oy, ox) moves, walked
+  // incrementally (the per-chunk 64-bit division by OH*OW and the per-call (c, ky, kx)
+  // divisions were most of this kernel's VALU work).
+  constexpr unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x), 0, g.B * g.C * g.H * g.W * (int)sizeof(float), 0x00020000);
+  int rowoff[KPT];        // element offset of row k relative to the position's (b, 0, oy, ox)
+  unsigned shift[KPT];    // (ky - pad + 128) | (kx - pad + 128) << 8, or ~0 for k >= Kd (never in bounds)
+  unsigned ones = 0;      // bit e: row k == Kd (the bias column: value 1)
+  {
+    const int k0 = j0 + rowg, kc = min(k0, Kd - 1);
+    int c = kc / KK;
+    const int rr = kc - c * KK;
+    int ky = rr / g.K, kx = rr - ky * g.K;
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) {
+      const bool kin = k0 + e < Kd;
+      rowoff[e] = (c * g.H + ky - g.pad) * g.W + kx - g.pad;
+      shift[e] = kin ? (unsigned)(ky - g.pad + 128) | ((unsigned)(kx - g.pad + 128) << 8) : ~0u;
+      if (k0 + e == Kd) ones |= 1u << e;
+      if (++kx == g.K) { kx = 0; if (++ky == g.K) { ky = 0; ++c; } }
+    }
+  }
+  // this lane's position, walked by BK per chunk
+  const int rs = (int)min(r_begin + rl, R - 1);
+  int pb = rs / OHW, prem = rs - pb * OHW;
+  int poy = prem / g.OW, pox = prem - poy * g.OW;
+  const int dq = BK / g.OW, dr = BK - dq * g.OW;
+
   float av[KPT], bv[KPT];
   auto load = [&](long r0) {
-    const long r = r0 + rl;
-    const bool rv = r < r_end;
-    const long rc = rv ? r : r_end - 1;
-    const int bb = (int)(rc / OHW), p = (int)(rc % OHW), oy = p / g.OW, ox = p % g.OW;
+    const bool rv = r0 + rl < r_end;
+    const int bb = pb, oy = poy, ox = pox;
     if constexpr (UNPOOL) {
       const int OH2 = g.OH >> 1, OW2 = g.OW >> 1, py = min(oy >> 1, OH2 - 1), px = min(ox >> 1, OW2 - 1);
       const bool inb = (oy >> 1) < OH2 && (ox >> 1) < OW2;
@@ -241,16 +271,30 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
         av[e] = (mv && rv && inb && cd[e] == sub) ? a[e] : 0.f;
       }
     } else {
-      const float* dyb = dy + (long)bb * M * OHW + p;
+      const __amdgpu_buffer_rsrc_t dr_ = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(dy), 0, g.B * M * OHW * (int)sizeof(float), 0x00020000);
+      const int dbase = (bb * M + m0 + rowg) * OHW + oy * g.OW + ox;
 #pragma unroll
       for (int e = 0; e < KPT; ++e) {
-        const int m = m0 + rowg + e;
-        const bool mv = rowg + e < BM && m < M;
-        const float a = dyb[(long)(mv ? m : 0) * OHW];
-        av[e] = (mv && rv) ? a : 0.f;
+        const bool mv = rowg + e < BM && m0 + rowg + e < M && rv;
+        const unsigned off = mv ? (unsigned)(dbase + e * OHW) * 4u : OOB;
+        av[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dr_, (int)off, 0, 0));
       }
     }
-    gather_rows<true>(x, g, j0 + rowg, Kd, bb, oy, ox, rv, bv);
+    const int pbase = bb * g.C * g.H * g.W + oy * g.W + ox;
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) {
+      const int iy = oy + (int)(shift[e] & 0xffu) - 128, ix = ox + (int)((shift[e] >> 8) & 0xffu) - 128;
+      const bool in = rv && shift[e] != ~0u && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      const unsigned off = in ? (unsigned)(pbase + rowoff[e]) * 4u : OOB;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      bv[e] = ((ones >> e) & 1u) ? (rv ? 1.f : 0.f) : v;
+    }
+    // advance the position by BK for the next chunk
+    pox += dr; poy += dq;
+    if (pox >= g.OW) { pox -= g.OW; ++poy; }
+    while (poy >= g.OH) { poy -= g.OH; ++pb; }
+    if (pb >= g.B) { pb = g.B - 1; }  // past the end: every element of it is masked (rv false)
   };
   if (r_begin < r_end) load(r_begin);
   for (long r0 = r_begin; r0 < r_end; r0 += BK) {
@@ -895,6 +939,8 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   int S = 1, cps = 1;
   conv_wgrad_split(B, C, H, W, M, K, pad, &S, &cps);
   if (pool_code != nullptr && (g.OH < 2 || g.OW < 2)) throw std::runtime_error("conv_wgrad: pooled dy of a < 2x2 map");
+  if ((long)B * C * H * W * 4 >= (1L << 31) || (long)B * M * g.OH * g.OW * 4 >= (1L << 31))
+    throw std::runtime_error("conv_wgrad: tensor too large for 32-bit buffer offsets");
   if (bf16_ops) wgrad_dispatch<true>(x, dy, part, g, M, S, cps, pool_code, s);
   else wgrad_dispatch<false>(x, dy, part, g, M, S, cps, pool_code, s);
   if (dw == nullptr) return;
