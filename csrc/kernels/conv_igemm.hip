@@ -207,7 +207,9 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
   const long r_begin = (long)s * chunks_per_slice * BK;
   const long r_end = min(R, r_begin + (long)chunks_per_slice * BK);
 
-  // both tiles: lanes along BK consecutive r (contiguous positions), KPT rows per thread
+  // both tiles: lanes along BK consecutive r (contiguous positions), KPT rows per thread.  (A
+  // readfirstlane-uniform row group - scalar branches, row tables in SGPRs - measured slower:
+  // 100 SGPR spills; profiles/r2/layer_fusion/README.md.)
   const int rl = tid & 63, rowg = (tid >> 6) * KPT;
 
   f32x4 acc[BM / 16];
