@@ -4,8 +4,15 @@ Same interface as ``HipEngine`` (attach / begin_epoch / run_steps / epoch_stats 
 evaluate_samples / master / grad / mom / grad_sync), so the trainer, every sync policy,
 fault recovery and checkpointing work unchanged.  Where the fused engine is one
 hand-scheduled kernel for the reference LeNet in bf16, this engine runs a layer stack
-(csrc/kernels/layers.hip, conv_igemm.hip + library GEMMs for Linear) in fp32 - the
-reference's arithmetic class - or with bf16 convolution operands, and supports BatchNorm.
+(csrc/kernels/conv_igemm.hip, linear.hip, layers.hip; the library GEMM only for Linears
+above 16M multiply-adds) in fp32 - the reference's arithmetic class - or with bf16
+convolution operands, and supports BatchNorm.
+
+The step is launch-bound (a dependent kernel boundary costs ~1.65 us), so producers absorb
+their consumers where the data allows: ReLU + max-pool and BatchNorm statistics in the conv
+forward epilogue, the loss in the last Linear, both Linear gradients in one launch, and one
+tail launch for the conv slice sums, SGD, the next step's packed conv weights and the
+bookkeeping (profiles/r2/layer_fusion/).
 
 MI355X design points kept from the fused engine:
   * flat fp32 parameter / gradient / momentum arenas; every layer op writes its parameter
@@ -30,6 +37,10 @@ from ..models import zoo
 from ..ops import layers as L
 from ..ops import native
 from .engine import Engine, StepStats
+
+
+TAIL_MAX_PACKS = 16   # PackScatter::kMax
+TAIL_MAX_SLICES = 8   # SliceSet::kMax
 
 
 class LayerEngine(Engine):
@@ -75,8 +86,14 @@ class LayerEngine(Engine):
         self._pack_jobs: list[tuple] = []
         self._pool_ok: set[str] = set()  # conv layers with a pooled-epilogue plan
         self.defer_slice_sums = True  # conv wgrad slice sums inside the SGD tail (single GPU)
+        self._tail_packs = True       # the SGD tail refreshes the packed conv-weight images
         if self.gpu:
             self._plan_weight_packing()
+        # capacities of the one-launch step tail (csrc/kernels/launchers.h PackScatter / SliceSet):
+        # past them the tail leaves that part to the separate kernels
+        n_conv = sum(isinstance(layer, zoo.Conv) for layer in self.spec)
+        self._tail_packs = len(self._pack_jobs) <= TAIL_MAX_PACKS
+        self.defer_slice_sums = n_conv <= TAIL_MAX_SLICES
 
     def _plan_weight_packing(self) -> None:
         """Persistent packed weight images of every LDS-patch convolution (forward and, except
@@ -258,7 +275,7 @@ class LayerEngine(Engine):
         them refreshed by the previous step's SGD tail."""
         assert self.train is not None
         self._ingest()
-        tail = self.gpu and not self._fused_sgd()
+        tail = self.gpu and not self._fused_sgd() and self._tail_packs
         xent = L.XentFusion(self.labels, self.state) if self.gpu else None
         # single GPU: the conv weight-gradient slice sums run inside the SGD tail launch (with a
         # gradient all-reduce the gradients must be complete before it)
@@ -277,12 +294,13 @@ class LayerEngine(Engine):
         elif self.gpu:
             if self.grad_sync is not None:
                 self.grad_sync.allreduce_grads(self.grad, [(0, self.play.total)])
+            packs = self._pack_jobs if self._tail_packs else []
             # conv slice sums + SGD + the next step's packed conv weights + bookkeeping: one launch
             g0 = self.grad.data_ptr()
             slices = [(part.data_ptr(), S, M, Kd, (dw.data_ptr() - g0) // 4, (db.data_ptr() - g0) // 4)
                       for part, S, M, Kd, dw, db in (sink or [])]
             self.ext.sgd_tail(self.master.data_ptr(), g0, self.mom.data_ptr(), self.play.total, self.lr,
-                              self.momentum, 1.0, self._pack_jobs, self.master.data_ptr(), slices, loss.data_ptr(),
+                              self.momentum, 1.0, packs, self.master.data_ptr(), slices, loss.data_ptr(),
                               corr.data_ptr(), self.batch, self.state.data_ptr(), self.stats.data_ptr(),
                               self.order.data_ptr(), self.order_len, self.batch_ids.data_ptr(),
                               torch.cuda.current_stream(self.device).cuda_stream)
