@@ -344,6 +344,24 @@ def test_conv_epilogue_batchnorm_statistics(B, C, H, M, K, pad, dtype, act, bval
         _close(a, c, 1e-5)
 
 
+@pytest.mark.parametrize("model,dtype", [("lenet", "fp32"), ("cifar-vgg", "bf16")])
+def test_tail_capacity_fallback_bitwise(model, dtype):
+    """Past the tail launch's capacities the engine packs every step and keeps the slice-sum
+    kernels: same parameters bit for bit as the one-launch tail."""
+    data = synthetic(200, 7).to(DEV)
+    res = []
+    for fallback in (False, True):
+        eng = LayerEngine(batch=32, model=model, device=DEV, gemm_dtype=dtype, graph_chunk=4, seed=2)
+        if fallback:
+            eng._tail_packs = False
+        eng.attach(data)
+        eng.begin_epoch(np.arange(200, dtype=np.int32))
+        eng.run_steps(6)
+        torch.cuda.synchronize()
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats().samples))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
+
+
 def test_ingest_and_sgd_flat():
     data = synthetic(50, 5).to(DEV)
     eng = LayerEngine(batch=8, model="lenet", device=DEV, use_graphs=False)
