@@ -47,14 +47,15 @@ def _local(arena, data, idx, batch, epochs_orders, lr=0.05, momentum=0.9, reset=
     return eng
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_step_allreduce_equals_big_batch(tmp_path, world):
-    got = _run_worker(tmp_path, "step-allreduce", world, n=192, batch=16, epochs=1)
+    n = 48 * world  # 3 full batches of 16 per rank
+    got = _run_worker(tmp_path, "step-allreduce", world, n=n, batch=16, epochs=1)
     for r in range(1, world):
         assert torch.allclose(got[0], got[r], atol=0, rtol=0)  # replicas stay bitwise identical
-    data = synthetic(192, 3)
+    data = synthetic(n, 3)
     # single process, batch 16 * world: step t takes shard_r[16t:16t+16] of every rank r
-    shard = 192 // world
+    shard = n // world
     order = np.concatenate([np.concatenate([shard * r + np.arange(16 * t, 16 * t + 16) for r in range(world)])
                             for t in range(shard // 16)]).astype(np.int32)
     ref = _local(init_arena(seed=100), data, None, 16 * world, [order])
