@@ -47,17 +47,19 @@ def _local(arena, data, idx, batch, epochs_orders, lr=0.05, momentum=0.9, reset=
     return eng
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_step_allreduce_equals_big_batch(tmp_path, world):
-    n = 48 * world  # 3 full batches of 16 per rank
+@pytest.mark.parametrize("world,per_rank", [(2, 48), (4, 48), (8, 48), (4, 40)])
+def test_step_allreduce_equals_big_batch(tmp_path, world, per_rank):
+    n = per_rank * world  # 48: 3 full batches of 16 per rank; 40: 2 full + a tail of 8
     got = _run_worker(tmp_path, "step-allreduce", world, n=n, batch=16, epochs=1)
     for r in range(1, world):
         assert torch.allclose(got[0], got[r], atol=0, rtol=0)  # replicas stay bitwise identical
     data = synthetic(n, 3)
-    # single process, batch 16 * world: step t takes shard_r[16t:16t+16] of every rank r
+    # single process, batch 16 * world: step t takes shard_r[16t:16t+16] of every rank r (the
+    # tail step: the tails of every rank - the mean of per-rank means of equal tails)
     shard = n // world
-    order = np.concatenate([np.concatenate([shard * r + np.arange(16 * t, 16 * t + 16) for r in range(world)])
-                            for t in range(shard // 16)]).astype(np.int32)
+    order = np.concatenate([np.concatenate([shard * r + np.arange(16 * t, min(16 * t + 16, shard))
+                                            for r in range(world)])
+                            for t in range((shard + 15) // 16)]).astype(np.int32)
     ref = _local(init_arena(seed=100), data, None, 16 * world, [order])
     assert torch.allclose(got[0], ref.master, atol=2e-6), float((got[0] - ref.master).abs().max())
 
