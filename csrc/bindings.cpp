@@ -210,13 +210,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
       py::arg("beta"), py::arg("eps"), py::arg("mom"), py::arg("rmean"), py::arg("rvar"), py::arg("y"),
       py::arg("code"), py::arg("smean"), py::arg("sinvstd"), py::arg("part"), py::arg("act"), py::arg("stream"),
       py::arg("ext_parts") = 0);
-  m.def("bn_act_bwd", [](u dy, u x, int B, int C, int H, int W, u state, u gamma, u beta, u smean, u sinvstd, u code,
-                         u dx, u dgamma, u dbeta, u part, int act, u stream) {
-    dnn::launch_bn_act_bwd(P<const float>(dy), P<const float>(x), B, C, H, W, P<const int32_t>(state),
-                           P<const float>(gamma), P<const float>(beta), P<const float>(smean), P<const float>(sinvstd),
-                           P<const uint8_t>(code), P<float>(dx), P<float>(dgamma), P<float>(dbeta), P<double>(part),
-                           act, S(stream));
-  });
+  m.def(
+      "bn_act_bwd",
+      [](u dy, u x, int B, int C, int H, int W, u state, u gamma, u beta, u smean, u sinvstd, u code, u dx, u dgamma,
+         u dbeta, u part, int act, u stream, int ext_parts) {
+        dnn::launch_bn_act_bwd(P<const float>(dy), P<const float>(x), B, C, H, W, P<const int32_t>(state),
+                               P<const float>(gamma), P<const float>(beta), P<const float>(smean),
+                               P<const float>(sinvstd), P<const uint8_t>(code), P<float>(dx), P<float>(dgamma),
+                               P<float>(dbeta), P<double>(part), act, S(stream), ext_parts);
+      },
+      py::arg("dy"), py::arg("x"), py::arg("B"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("state"),
+      py::arg("gamma"), py::arg("beta"), py::arg("smean"), py::arg("sinvstd"), py::arg("code"), py::arg("dx"),
+      py::arg("dgamma"), py::arg("dbeta"), py::arg("part"), py::arg("act"), py::arg("stream"),
+      py::arg("ext_parts") = 0);
   m.def("chan_sum", [](u a, int B, int C, int L, u out, u part, u stream) {
     dnn::launch_chan_sum(P<const float>(a), B, C, L, P<float>(out), P<double>(part), S(stream));
   });
@@ -303,6 +309,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_conv_fwd_packed_stats(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y),
                                       P<double>(stats), P<const int32_t>(state), B, C, H, W, M, K, pad, bf16_ops,
                                       S(stream));
+  });
+  m.def("conv_fwd_packed_bnbwd", [](u x, u wp, u y, u stats, u state, u bn_z, u bn_mean, u bn_invstd, u bn_gamma,
+                                    u bn_beta, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                                    u stream) {
+    dnn::launch_conv_fwd_packed_bnbwd(P<const float>(x), P<const void>(wp), P<float>(y), P<double>(stats),
+                                      P<const int32_t>(state), P<const float>(bn_z), P<const float>(bn_mean),
+                                      P<const float>(bn_invstd), P<const float>(bn_gamma), P<const float>(bn_beta), B,
+                                      C, H, W, M, K, pad, bf16_ops, S(stream));
   });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;

@@ -432,14 +432,28 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
 //              tile's (sum y, sum y^2) in fp64 over its positions (fixed order) into
 //              stats[(m * P + tile) * 2 + {0, 1}], P = B * tiles; images past the step state's
 //              valid count contribute 0 (the padded tail batch, as chan_partial_kernel).
-constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2;
+//   EPI_BNBWD  (a data gradient whose output is the gradient of a BatchNorm + ReLU output) y as
+//              EPI_PLAIN, plus that BatchNorm's backward statistics: per channel the tile's
+//              (sum dz, sum dz * xhat) in fp64, dz = y where the BatchNorm output is > 0 (the
+//              bit-exact affine recompute of the backward kernels), xhat = (z - mean) * invstd
+//              from the BatchNorm input z - chan_partial_kernel<1, 1>'s terms, same layout as
+//              EPI_STATS.
+constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2, EPI_BNBWD = 3;
+struct BnTerms {  // EPI_BNBWD: the BatchNorm whose output gradient this kernel produces
+  const float* z;       // its input [B][M][OH][OW]
+  const float* mean;    // saved batch mean / inverse std, affine weight / bias [M]
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+};
 template <bool BF16, int BM, int CCH, bool V4, int EPI = EPI_PLAIN>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
                                                             const typename PatchT<BF16, CCH>::T* __restrict__ wp,
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             PGeom g, uint8_t* __restrict__ code = nullptr,
                                                             double* __restrict__ stats = nullptr,
-                                                            const int32_t* __restrict__ state = nullptr) {
+                                                            const int32_t* __restrict__ state = nullptr,
+                                                            const BnTerms bt = BnTerms{}) {
   constexpr bool POOL = EPI == EPI_POOL;
   static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
   using T = typename PatchT<BF16, CCH>::T;
@@ -722,6 +736,58 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       stats[o + 1] = s1;
     }
   }
+  if constexpr (EPI == EPI_BNBWD) {
+    const int bvalid = state != nullptr ? min(state[ST_BVALID], g.B) : g.B;
+    // the BatchNorm input under this lane's outputs: all loads in flight before the barrier
+    float zv[BM / 16][4];
+#pragma unroll
+    for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = min(m0 + 16 * i + 4 * q + j, g.M - 1);
+        zv[i][j] = bt.z[((long)b * g.M + m) * OHW + min(pn, OHW - 1)];
+      }
+    }
+    __syncthreads();  // every wave is done with As / Ps: the tile's terms reuse the LDS
+    float* od = reinterpret_cast<float*>(smem);   // [BM][PNT] dz
+    float* ox = od + BM * PNT;                    // [BM][PNT] xhat
+#pragma unroll
+    for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = 16 * i + 4 * q + j, m = min(m0 + ml, g.M - 1);
+        const float mu = bt.mean[m], is = bt.invstd[m];
+        const bool ok = pn < OHW && m0 + ml < g.M;
+        const float dyv = acc[i][j] + (bias != nullptr ? bias[m] : 0.f);
+        const bool on = __fmaf_rn(__fmul_rn(__fsub_rn(zv[i][j], mu), is), bt.gamma[m], bt.beta[m]) > 0.f;
+        od[ml * PNT + local] = (ok && on) ? dyv : 0.f;
+        ox[ml * PNT + local] = (zv[i][j] - mu) * is;
+      }
+    }
+    __syncthreads();
+    constexpr int TPC = CT / BM, PPT = PNT / TPC;
+    static_assert(TPC <= 64 && 64 % TPC == 0 && PNT % TPC == 0, "channel group inside one wave");
+    const int ml = tid / TPC, pi = tid - ml * TPC;
+    double s0 = 0.0, s1 = 0.0;
+    if (b < bvalid) {
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const double d = (double)od[ml * PNT + pi * PPT + k];
+        s0 += d;
+        s1 += d * (double)ox[ml * PNT + pi * PPT + k];
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < TPC; off <<= 1) {
+      s0 += __shfl_xor(s0, off);
+      s1 += __shfl_xor(s1, off);
+    }
+    if (pi == 0 && m0 + ml < g.M) {
+      const long P = (long)g.B * g.tiles, o = ((long)(m0 + ml) * P + tile) * 2;
+      stats[o] = s0;
+      stats[o + 1] = s1;
+    }
+  }
 }
 
 int pick_bm(int M) { return M <= 16 ? 16 : (M <= 32 ? 32 : 64); }
@@ -779,8 +845,9 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf, i
 
 struct EpiArgs {
   uint8_t* code = nullptr;          // EPI_POOL
-  double* stats = nullptr;          // EPI_STATS
-  const int32_t* state = nullptr;   // EPI_STATS
+  double* stats = nullptr;          // EPI_STATS / EPI_BNBWD
+  const int32_t* state = nullptr;   // EPI_STATS / EPI_BNBWD
+  BnTerms bn{};                     // EPI_BNBWD (bn.z != nullptr)
 };
 template <bool BF16, int CCH, bool V4, int EPI>
 void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
@@ -788,10 +855,10 @@ void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, c
   dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
   if (f.bm == 16)
     hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       e.code, e.stats, e.state);
+                       e.code, e.stats, e.state, e.bn);
   else
     hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       e.code, e.stats, e.state);
+                       e.code, e.stats, e.state, e.bn);
   HIP_CHECK(hipGetLastError());
 }
 template <bool BF16, int CCH, int EPI>
@@ -806,6 +873,7 @@ template <bool BF16, int CCH>
 void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                  float* y, hipStream_t s, const EpiArgs& e = EpiArgs{}) {
   if (e.code != nullptr) fast_launch_e<BF16, CCH, EPI_POOL>(f, wp, x, bias, y, e, s);
+  else if (e.stats != nullptr && e.bn.z != nullptr) fast_launch_e<BF16, CCH, EPI_BNBWD>(f, wp, x, bias, y, e, s);
   else if (e.stats != nullptr) fast_launch_e<BF16, CCH, EPI_STATS>(f, wp, x, bias, y, e, s);
   else fast_launch_e<BF16, CCH, EPI_PLAIN>(f, wp, x, bias, y, e, s);
 }
@@ -1078,6 +1146,23 @@ void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* b
   e.stats = stats;
   e.state = state;
   fast_launch_packed(f, wp, x, bias, y, bf16_ops, e, s);
+}
+
+// data gradient (packed flipped image of the next conv) whose output y is the gradient of a
+// BatchNorm + ReLU output, plus that BatchNorm's backward-statistics partials (EPI_BNBWD)
+void launch_conv_fwd_packed_bnbwd(const float* x, const void* wp, float* y, double* stats, const int32_t* state,
+                                  const float* bn_z, const float* bn_mean, const float* bn_invstd,
+                                  const float* bn_gamma, const float* bn_beta, int B, int C, int H, int W, int M, int K,
+                                  int pad, int bf16_ops, hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (!f.ok) throw std::runtime_error("conv_fwd_packed_bnbwd: layer is not on the LDS-patch path");
+  f.lds = std::max(f.lds, (size_t)2 * f.bm * PNT * sizeof(float));  // the epilogue's dz / xhat tiles
+  EpiArgs e;
+  e.stats = stats;
+  e.state = state;
+  e.bn = BnTerms{bn_z, bn_mean, bn_invstd, bn_gamma, bn_beta};
+  fast_launch_packed(f, wp, x, nullptr, y, bf16_ops, e, s);
 }
 
 void launch_flip_weights(const float* w, int O, int C, int K, float* wf, hipStream_t s) {

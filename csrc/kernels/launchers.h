@@ -83,7 +83,8 @@ void launch_bn_act_fwd_train(const float* x, int B, int C, int H, int W, const i
 void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
                        const float* gamma, const float* beta, const float* smean, const float* sinvstd,
                        const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
-                       hipStream_t s);
+                       hipStream_t s,
+                       int ext_parts = 0);
 void launch_chan_sum(const float* a, int B, int C, int L, float* out, double* part, hipStream_t s);
 void launch_xent(const float* logits, const int32_t* labels, int B, int NC, const int32_t* state, float* loss,
                  int32_t* correct, float* dlogits, hipStream_t s);
@@ -116,6 +117,10 @@ void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bi
                                  int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 // conv + bias with the following BatchNorm's batch-statistics partials in the epilogue
 int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
+void launch_conv_fwd_packed_bnbwd(const float* x, const void* wp, float* y, double* stats, const int32_t* state,
+                                  const float* bn_z, const float* bn_mean, const float* bn_invstd,
+                                  const float* bn_gamma, const float* bn_beta, int B, int C, int H, int W, int M, int K,
+                                  int pad, int bf16_ops, hipStream_t s);
 void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* bias, float* y, double* stats,
                                   const int32_t* state, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
                                   hipStream_t s);

@@ -379,13 +379,20 @@ __global__ void __launch_bounds__(LT) bn_bwd_apply_kernel(const float* __restric
                                                           const float* __restrict__ save_invstd,
                                                           float* __restrict__ dx, float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta,
-                                                          const double* __restrict__ part, ActArgs aa) {
+                                                          const double* __restrict__ part, ActArgs aa, int nparts) {
   __shared__ float st[2];
-  const int c = blockIdx.y, p = blockIdx.x, P = gridDim.x;
+  __shared__ double red[2 * (LT / 64)];
+  const int c = blockIdx.y, p = blockIdx.x;
   const int bv = valid_count(state, B), ppb = chan_ppb(B, L);
+  // the channel's nparts partials (chan_partial_kernel's, or a conv data-gradient epilogue's),
+  // merged across the block in a fixed order (as bn_apply_train_kernel)
+  double s0 = 0.0, s1 = 0.0;
+  for (int q = threadIdx.x; q < nparts; q += LT) {
+    s0 += part[((size_t)c * nparts + q) * 2];
+    s1 += part[((size_t)c * nparts + q) * 2 + 1];
+  }
+  block_sum2_d(s0, s1, red);
   if (threadIdx.x == 0) {
-    double s0, s1;
-    merge_parts(part, c, P, s0, s1);
     const double n = (double)bv * L;
     st[0] = n > 0 ? (float)(s0 / n) : 0.f;
     st[1] = n > 0 ? (float)(s1 / n) : 0.f;
@@ -640,14 +647,17 @@ void launch_bn_fwd_eval(const float* x, int B, int C, int L, const float* gamma,
                             rvar, y);
 }
 template <int ACT, int VW>
+// ext_parts > 0: part already holds that many backward-statistics partials per channel (the
+// producing conv data gradient's epilogue wrote them) - only the apply kernel runs
 static void bn_act_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                        const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
-                       ActArgs aa, hipStream_t s) {
+                       ActArgs aa, hipStream_t s, int ext_parts = 0) {
   const dim3 grid(chan_parts_of(B, L), C);
-  hipLaunchKernelGGL((chan_partial_kernel<1, ACT, VW>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd,
-                     part, gamma, aa);
+  if (ext_parts <= 0)
+    hipLaunchKernelGGL((chan_partial_kernel<1, ACT, VW>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, smean, sinvstd,
+                       part, gamma, aa);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, VW>), grid, dim3(LT), 0, s, dy, x, B, C, L, state, gamma, smean,
-                     sinvstd, dx, dgamma, dbeta, part, aa);
+                     sinvstd, dx, dgamma, dbeta, part, aa, ext_parts > 0 ? ext_parts : (int)grid.x);
 }
 void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const int32_t* state, const float* gamma,
                    const float* smean, const float* sinvstd, float* dx, float* dgamma, float* dbeta, double* part,
@@ -661,12 +671,13 @@ void launch_bn_bwd(const float* dy, const float* x, int B, int C, int L, const i
 void launch_bn_act_bwd(const float* dy, const float* x, int B, int C, int H, int W, const int32_t* state,
                        const float* gamma, const float* beta, const float* smean, const float* sinvstd,
                        const uint8_t* code, float* dx, float* dgamma, float* dbeta, double* part, int act,
-                       hipStream_t s) {
+                       hipStream_t s, int ext_parts) {
   if (!C) return;
   const int L = H * W;
   const ActArgs aa{beta, code, W, H / 2};
   const bool v4 = vec4_ok(L, W, act, {act == 2 ? nullptr : dy, x, dx});
-#define BN_BWD(A, V) bn_act_bwd<A, V>(dy, x, B, C, L, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s)
+#define BN_BWD(A, V) \
+  bn_act_bwd<A, V>(dy, x, B, C, L, state, gamma, smean, sinvstd, dx, dgamma, dbeta, part, aa, s, ext_parts)
   if (act == 1) { if (v4) BN_BWD(1, 4); else BN_BWD(1, 1); }
   else if (act == 2) { if (v4) BN_BWD(2, 4); else BN_BWD(2, 1); }
   else { if (v4) BN_BWD(0, 4); else BN_BWD(0, 1); }

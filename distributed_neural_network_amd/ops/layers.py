@@ -90,7 +90,7 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None,
-                pool: bool = False, stats: "BnStats | None" = None):
+                pool: bool = False, stats: "BnStats | None" = None, bnbwd: "BnBwdStats | None" = None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -129,6 +129,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.gw, ctx.gb = gw, gb
         ctx.packed = packed
         ctx.slice_sink = slice_sink if gw is not None else None
+        ctx.bnbwd = bnbwd
         return y
 
     @staticmethod
@@ -162,7 +163,16 @@ class Conv2dFn(torch.autograd.Function):
                 # dgrad: the forward kernel over dY with the flipped, transposed weights
                 # (flip=1: packed from w inside the launch), pad' = K - 1 - pad
                 dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
-                if ctx.packed is not None and ctx.packed[1] is not None:
+                h = ctx.bnbwd
+                if ctx.packed is not None and ctx.packed[1] is not None and h is not None and h.z is not None:
+                    # + the backward statistics of the BatchNorm + ReLU whose output this is
+                    h.nparts = ext.conv_fwd_stat_parts(B, Cout, OH, OW, C, K, K - 1 - pad, bf)
+                    h.part = torch.empty(C * h.nparts * 2, device=dy.device, dtype=torch.float64)
+                    ext.conv_fwd_packed_bnbwd(_p(dy), _p(ctx.packed[1]), _p(dx), _p(h.part),
+                                              _p(h.state) if h.state is not None else 0, _p(h.z), _p(h.mean),
+                                              _p(h.invstd), _p(h.gamma), _p(h.beta), B, Cout, OH, OW, C, K,
+                                              K - 1 - pad, bf, st)
+                elif ctx.packed is not None and ctx.packed[1] is not None:
                     ext.conv_fwd_packed(_p(dy), _p(ctx.packed[1]), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf,
                                         st)
                 else:
@@ -177,8 +187,21 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None
+
+
+class BnBwdStats:
+    """Hand-off of a BatchNorm (+ ReLU) layer's backward statistics (sum dz, sum dz * xhat) from the
+    data-gradient epilogue of the conv that consumed its output: ``BatchNormActFn`` fills the
+    forward tensors the epilogue needs, ``Conv2dFn.backward`` fills ``part`` / ``nparts``, and the
+    BatchNorm backward then skips its own statistics pass."""
+
+    def __init__(self, state: torch.Tensor | None) -> None:
+        self.state = state
+        self.z = self.mean = self.invstd = self.gamma = self.beta = None
+        self.part: torch.Tensor | None = None
+        self.nparts = 0
 
 
 class BnStats:
@@ -458,7 +481,7 @@ class BatchNormActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, state, eps: float, momentum: float, act: int,
-                ggamma=None, gbeta=None, stats: BnStats | None = None):
+                ggamma=None, gbeta=None, stats: BnStats | None = None, bwd: BnBwdStats | None = None):
         B, C, H, W = x.shape
         x = x.contiguous()
         ext = _ext()
@@ -479,6 +502,9 @@ class BatchNormActFn(torch.autograd.Function):
                              _p(mean), _p(invstd), _p(part), act, _s(x), ext_parts)
         ctx.act = act
         ctx.gg, ctx.gb = ggamma, gbeta
+        ctx.bwd = bwd if act == 1 else None
+        if ctx.bwd is not None:  # what the next conv's data-gradient epilogue needs
+            bwd.z, bwd.mean, bwd.invstd, bwd.gamma, bwd.beta = x, mean, invstd, gamma, beta
         ctx.save_for_backward(x, gamma, beta, mean, invstd, code, state if state is not None else torch.zeros(0))
         return y
 
@@ -492,13 +518,18 @@ class BatchNormActFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dgamma = ctx.gg if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
         dbeta = ctx.gb if inplace else torch.empty(C, device=x.device, dtype=torch.float32)
+        h = ctx.bwd
+        if h is not None and h.part is not None:  # statistics from the consuming conv's dgrad epilogue
+            part, ext_parts = h.part, h.nparts
+        else:
+            part, ext_parts = _partials(dy, B, C, H * W), 0
         _ext().bn_act_bwd(_p(dy), _p(x), B, C, H, W, _p(state) if state is not None else 0, _p(gamma), _p(beta),
                           _p(mean), _p(invstd), _p(code) if ctx.act == 2 else 0, _p(dx), _p(dgamma), _p(dbeta),
-                          _p(_partials(dy, B, C, H * W)), ctx.act, _s(dy))
-        none9 = (None,) * 9
+                          _p(part), ctx.act, _s(dy), ext_parts)
+        none10 = (None,) * 10
         if inplace:
-            return (dx, None, None) + none9
-        return (dx, dgamma, dbeta) + none9
+            return (dx, None, None) + none10
+        return (dx, dgamma, dbeta) + none10
 
 
 # ---- softmax cross-entropy (mean over the valid batch) + accuracy ----------------------------

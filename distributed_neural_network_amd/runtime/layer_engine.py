@@ -87,6 +87,7 @@ class LayerEngine(Engine):
         self._pool_ok: set[str] = set()  # conv layers with a pooled-epilogue plan
         self.defer_slice_sums = True  # conv wgrad slice sums inside the SGD tail (single GPU)
         self._tail_packs = True       # the SGD tail refreshes the packed conv-weight images
+        self.fuse_bn_bwd = True       # BatchNorm + ReLU backward statistics in the next conv's dgrad
         if self.gpu:
             self._plan_weight_packing()
         # capacities of the one-launch step tail (csrc/kernels/launchers.h PackScatter / SliceSet):
@@ -187,6 +188,7 @@ class LayerEngine(Engine):
         fuse_act = training and self.gpu  # BN + following ReLU / ReLU-pool in one op (MI355X training)
         skip = False
         bn_stats = None  # statistics partials a conv epilogue produced for the BatchNorm after it
+        bn_bwd = None    # a BatchNorm + ReLU whose backward statistics the next conv's dgrad computes
         for i, layer in enumerate(self.spec):
             if skip:  # activation already applied by the fused BatchNorm
                 skip = False
@@ -196,9 +198,15 @@ class LayerEngine(Engine):
             nxt = self.spec[i + 1] if i + 1 < len(self.spec) else None
             if fuse_act and isinstance(layer, zoo.BN) and isinstance(nxt, (zoo.Relu, zoo.ReluPool)):
                 act = 2 if isinstance(nxt, zoo.ReluPool) else 1
+                # BatchNorm + ReLU -> conv: that conv's data gradient also produces this layer's
+                # backward statistics (no statistics pass in the BatchNorm backward)
+                nn2 = self.spec[i + 2] if i + 2 < len(self.spec) else None
+                nxt_packed = self._packed.get(getattr(nn2, "name", "")) if isinstance(nn2, zoo.Conv) else None
+                if act == 1 and self.fuse_bn_bwd and nxt_packed is not None and nxt_packed[1] is not None:
+                    bn_bwd = L.BnBwdStats(state)
                 x = L.BatchNormActFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
                                            Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb,
-                                           bn_stats)
+                                           bn_stats, bn_bwd)
                 bn_stats = None
                 skip = True
             elif isinstance(layer, zoo.Conv):
@@ -213,7 +221,8 @@ class LayerEngine(Engine):
                         and packed is not None and packed[0] is not None):
                     bn_stats = L.BnStats(state)
                 x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, packed, slice_sink,
-                                     pool, bn_stats)
+                                     pool, bn_stats, bn_bwd)
+                bn_bwd = None
                 skip = pool
             elif isinstance(layer, zoo.BN):
                 x = L.BatchNorm2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
