@@ -311,12 +311,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                       S(stream));
   });
   m.def("conv_fwd_packed_bnbwd", [](u x, u wp, u y, u stats, u state, u bn_z, u bn_mean, u bn_invstd, u bn_gamma,
-                                    u bn_beta, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
-                                    u stream) {
+                                    u bn_beta, u bn_code, int zH, int zW, int B, int C, int H, int W, int M, int K,
+                                    int pad, int bf16_ops, u stream) {
     dnn::launch_conv_fwd_packed_bnbwd(P<const float>(x), P<const void>(wp), P<float>(y), P<double>(stats),
                                       P<const int32_t>(state), P<const float>(bn_z), P<const float>(bn_mean),
-                                      P<const float>(bn_invstd), P<const float>(bn_gamma), P<const float>(bn_beta), B,
-                                      C, H, W, M, K, pad, bf16_ops, S(stream));
+                                      P<const float>(bn_invstd), P<const float>(bn_gamma), P<const float>(bn_beta),
+                                      P<const uint8_t>(bn_code), zH, zW, B, C, H, W, M, K, pad, bf16_ops, S(stream));
   });
   m.def("conv_wgrad_slices", [](int B, int C, int H, int W, int M, int K, int pad) {
     int s = 1, cps = 1;

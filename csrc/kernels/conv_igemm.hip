@@ -432,19 +432,24 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
 //              tile's (sum y, sum y^2) in fp64 over its positions (fixed order) into
 //              stats[(m * P + tile) * 2 + {0, 1}], P = B * tiles; images past the step state's
 //              valid count contribute 0 (the padded tail batch, as chan_partial_kernel).
-//   EPI_BNBWD  (a data gradient whose output is the gradient of a BatchNorm + ReLU output) y as
-//              EPI_PLAIN, plus that BatchNorm's backward statistics: per channel the tile's
-//              (sum dz, sum dz * xhat) in fp64, dz = y where the BatchNorm output is > 0 (the
-//              bit-exact affine recompute of the backward kernels), xhat = (z - mean) * invstd
-//              from the BatchNorm input z - chan_partial_kernel<1, 1>'s terms, same layout as
-//              EPI_STATS.
+//   EPI_BNBWD  (a data gradient whose output is the gradient of a BatchNorm + ReLU (+ max-pool)
+//              output) y as EPI_PLAIN, plus that BatchNorm's backward statistics: per channel the
+//              tile's (sum dz, sum dz * xhat) in fp64 - chan_partial_kernel<1, ACT>'s terms, same
+//              layout as EPI_STATS.  ReLU: dz = y where the BatchNorm output is > 0 (the bit-exact
+//              affine recompute of the backward kernels), xhat = (z - mean) * invstd.  ReLU +
+//              pool: y is the pooled gradient; it lands on the window's argmax position (code
+//              < 4; code 4 = max <= 0: no gradient), so dz = y there and xhat is taken at that
+//              full-resolution position of z.
 constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2, EPI_BNBWD = 3;
 struct BnTerms {  // EPI_BNBWD: the BatchNorm whose output gradient this kernel produces
-  const float* z;       // its input [B][M][OH][OW]
+  const float* z;       // its input [B][M][zH][zW]
   const float* mean;    // saved batch mean / inverse std, affine weight / bias [M]
   const float* invstd;
   const float* gamma;
   const float* beta;
+  const uint8_t* code;  // ReLU + 2x2 max-pool after the BatchNorm: its argmax codes [B][M][OH][OW] (this
+                        // kernel's output grid), else nullptr (ReLU only: zH, zW = OH, OW)
+  int zH, zW;
 };
 template <bool BF16, int BM, int CCH, bool V4, int EPI = EPI_PLAIN>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
@@ -738,14 +743,36 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   }
   if constexpr (EPI == EPI_BNBWD) {
     const int bvalid = state != nullptr ? min(state[ST_BVALID], g.B) : g.B;
-    // the BatchNorm input under this lane's outputs: all loads in flight before the barrier
+    // the BatchNorm input under this lane's outputs (pooled: at the argmax position of each
+    // output's window, so the codes are loaded first)
+    const int pc_ = min(pn, OHW - 1);
     float zv[BM / 16][4];
+    bool onv[BM / 16][4];
+    if (bt.code != nullptr) {
+      uint8_t cd[BM / 16][4];
 #pragma unroll
-    for (int i = 0; i < BM / 16; ++i) {
+      for (int i = 0; i < BM / 16; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = min(m0 + 16 * i + 4 * q + j, g.M - 1);
-        zv[i][j] = bt.z[((long)b * g.M + m) * OHW + min(pn, OHW - 1)];
+        for (int j = 0; j < 4; ++j) cd[i][j] = bt.code[((long)b * g.M + min(m0 + 16 * i + 4 * q + j, g.M - 1)) * OHW + pc_];
+      const int py = pc_ / g.OW, px = pc_ - py * g.OW;
+#pragma unroll
+      for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = min(m0 + 16 * i + 4 * q + j, g.M - 1), c4 = cd[i][j] < 4 ? cd[i][j] : 0;
+          zv[i][j] = bt.z[(((long)b * g.M + m) * bt.zH + 2 * py + (c4 >> 1)) * bt.zW + 2 * px + (c4 & 1)];
+          onv[i][j] = cd[i][j] < 4;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BM / 16; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = min(m0 + 16 * i + 4 * q + j, g.M - 1);
+          zv[i][j] = bt.z[((long)b * g.M + m) * OHW + pc_];
+          onv[i][j] = __fmaf_rn(__fmul_rn(__fsub_rn(zv[i][j], bt.mean[m]), bt.invstd[m]), bt.gamma[m], bt.beta[m]) > 0.f;
+        }
       }
     }
     __syncthreads();  // every wave is done with As / Ps: the tile's terms reuse the LDS
@@ -759,8 +786,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
         const float mu = bt.mean[m], is = bt.invstd[m];
         const bool ok = pn < OHW && m0 + ml < g.M;
         const float dyv = acc[i][j] + (bias != nullptr ? bias[m] : 0.f);
-        const bool on = __fmaf_rn(__fmul_rn(__fsub_rn(zv[i][j], mu), is), bt.gamma[m], bt.beta[m]) > 0.f;
-        od[ml * PNT + local] = (ok && on) ? dyv : 0.f;
+        od[ml * PNT + local] = (ok && onv[i][j]) ? dyv : 0.f;
         ox[ml * PNT + local] = (zv[i][j] - mu) * is;
       }
     }
@@ -1152,16 +1178,18 @@ void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* b
 // BatchNorm + ReLU output, plus that BatchNorm's backward-statistics partials (EPI_BNBWD)
 void launch_conv_fwd_packed_bnbwd(const float* x, const void* wp, float* y, double* stats, const int32_t* state,
                                   const float* bn_z, const float* bn_mean, const float* bn_invstd,
-                                  const float* bn_gamma, const float* bn_beta, int B, int C, int H, int W, int M, int K,
-                                  int pad, int bf16_ops, hipStream_t s) {
-  geom(B, C, H, W, K, pad);
+                                  const float* bn_gamma, const float* bn_beta, const uint8_t* bn_code, int zH, int zW,
+                                  int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s) {
+  const Geom gg = geom(B, C, H, W, K, pad);
+  if (bn_code == nullptr ? (zH != gg.OH || zW != gg.OW) : (zH / 2 != gg.OH || zW / 2 != gg.OW))
+    throw std::runtime_error("conv_fwd_packed_bnbwd: BatchNorm map does not match the data-gradient grid");
   FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
   if (!f.ok) throw std::runtime_error("conv_fwd_packed_bnbwd: layer is not on the LDS-patch path");
   f.lds = std::max(f.lds, (size_t)2 * f.bm * PNT * sizeof(float));  // the epilogue's dz / xhat tiles
   EpiArgs e;
   e.stats = stats;
   e.state = state;
-  e.bn = BnTerms{bn_z, bn_mean, bn_invstd, bn_gamma, bn_beta};
+  e.bn = BnTerms{bn_z, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_code, zH, zW};
   fast_launch_packed(f, wp, x, nullptr, y, bf16_ops, e, s);
 }
 

@@ -119,8 +119,8 @@ void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bi
 int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
 void launch_conv_fwd_packed_bnbwd(const float* x, const void* wp, float* y, double* stats, const int32_t* state,
                                   const float* bn_z, const float* bn_mean, const float* bn_invstd,
-                                  const float* bn_gamma, const float* bn_beta, int B, int C, int H, int W, int M, int K,
-                                  int pad, int bf16_ops, hipStream_t s);
+                                  const float* bn_gamma, const float* bn_beta, const uint8_t* bn_code, int zH, int zW,
+                                  int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 void launch_conv_fwd_packed_stats(const float* x, const void* wp, const float* bias, float* y, double* stats,
                                   const int32_t* state, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
                                   hipStream_t s);

@@ -170,8 +170,9 @@ class Conv2dFn(torch.autograd.Function):
                     h.part = torch.empty(C * h.nparts * 2, device=dy.device, dtype=torch.float64)
                     ext.conv_fwd_packed_bnbwd(_p(dy), _p(ctx.packed[1]), _p(dx), _p(h.part),
                                               _p(h.state) if h.state is not None else 0, _p(h.z), _p(h.mean),
-                                              _p(h.invstd), _p(h.gamma), _p(h.beta), B, Cout, OH, OW, C, K,
-                                              K - 1 - pad, bf, st)
+                                              _p(h.invstd), _p(h.gamma), _p(h.beta),
+                                              _p(h.code) if h.code is not None else 0, h.z.shape[2], h.z.shape[3],
+                                              B, Cout, OH, OW, C, K, K - 1 - pad, bf, st)
                 elif ctx.packed is not None and ctx.packed[1] is not None:
                     ext.conv_fwd_packed(_p(dy), _p(ctx.packed[1]), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf,
                                         st)
@@ -200,6 +201,7 @@ class BnBwdStats:
     def __init__(self, state: torch.Tensor | None) -> None:
         self.state = state
         self.z = self.mean = self.invstd = self.gamma = self.beta = None
+        self.code: torch.Tensor | None = None  # ReLU + max-pool: the pool's argmax codes
         self.part: torch.Tensor | None = None
         self.nparts = 0
 
@@ -502,9 +504,10 @@ class BatchNormActFn(torch.autograd.Function):
                              _p(mean), _p(invstd), _p(part), act, _s(x), ext_parts)
         ctx.act = act
         ctx.gg, ctx.gb = ggamma, gbeta
-        ctx.bwd = bwd if act == 1 else None
+        ctx.bwd = bwd if act in (1, 2) else None
         if ctx.bwd is not None:  # what the next conv's data-gradient epilogue needs
             bwd.z, bwd.mean, bwd.invstd, bwd.gamma, bwd.beta = x, mean, invstd, gamma, beta
+            bwd.code = code if act == 2 else None
         ctx.save_for_backward(x, gamma, beta, mean, invstd, code, state if state is not None else torch.zeros(0))
         return y
 

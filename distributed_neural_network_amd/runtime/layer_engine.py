@@ -198,11 +198,11 @@ class LayerEngine(Engine):
             nxt = self.spec[i + 1] if i + 1 < len(self.spec) else None
             if fuse_act and isinstance(layer, zoo.BN) and isinstance(nxt, (zoo.Relu, zoo.ReluPool)):
                 act = 2 if isinstance(nxt, zoo.ReluPool) else 1
-                # BatchNorm + ReLU -> conv: that conv's data gradient also produces this layer's
-                # backward statistics (no statistics pass in the BatchNorm backward)
+                # BatchNorm + ReLU (+ pool) -> conv: that conv's data gradient also produces this
+                # layer's backward statistics (no statistics pass in the BatchNorm backward)
                 nn2 = self.spec[i + 2] if i + 2 < len(self.spec) else None
                 nxt_packed = self._packed.get(getattr(nn2, "name", "")) if isinstance(nn2, zoo.Conv) else None
-                if act == 1 and self.fuse_bn_bwd and nxt_packed is not None and nxt_packed[1] is not None:
+                if self.fuse_bn_bwd and nxt_packed is not None and nxt_packed[1] is not None:
                     bn_bwd = L.BnBwdStats(state)
                 x = L.BatchNormActFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], Bf[f"{n}.running_mean"],
                                            Bf[f"{n}.running_var"], state, layer.eps, layer.momentum, act, gw, gb,

@@ -362,13 +362,15 @@ def test_tail_capacity_fallback_bitwise(model, dtype):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
 
 
-@pytest.mark.parametrize("dtype,bvalid", [(torch.bfloat16, 6), (torch.float32, 4)])
-def test_conv_dgrad_epilogue_batchnorm_backward_statistics(dtype, bvalid):
+@pytest.mark.parametrize("dtype,bvalid,act", [(torch.bfloat16, 6, 1), (torch.float32, 4, 1), (torch.bfloat16, 5, 2),
+                                             (torch.float32, 6, 2)])
+def test_conv_dgrad_epilogue_batchnorm_backward_statistics(dtype, bvalid, act):
     """BatchNorm + ReLU -> conv: the conv's data-gradient epilogue computes the BatchNorm's backward
     statistics (sum dz, sum dz * xhat); the BatchNorm backward with them equals the one with its
     own statistics pass (close: another fp64 summation order)."""
     ext = L._ext()
-    B, C, H, M = 6, 32, 16, 64  # BN over C channels, then conv C -> M (3x3, pad 1)
+    B, C, H, M = 6, 32, 16, 64  # BN over C channels (+ ReLU, + 2x2 pool if act 2), then conv C -> M (3x3, pad 1)
+    Hc = H // 2 if act == 2 else H  # the conv's input size
     bf = int(dtype == torch.bfloat16)
     torch.manual_seed(11)
     z = torch.randn(B, C, H, H, device=DEV)
@@ -376,11 +378,11 @@ def test_conv_dgrad_epilogue_batchnorm_backward_statistics(dtype, bvalid):
     w = (torch.randn(M, C, 3, 3) / (9 * C) ** 0.5).to(DEV)
     b = torch.randn(M, device=DEV)
     st = torch.tensor([0, bvalid, 0, 0], dtype=torch.int32, device=DEV)
-    fwd = torch.empty(ext.conv_fwd_workspace(B, C, H, H, M, 3, 1, bf, 0), device=DEV, dtype=torch.uint8)
-    dgr = torch.empty(ext.conv_fwd_workspace(B, M, H, H, C, 3, 1, bf, 1), device=DEV, dtype=torch.uint8)
+    fwd = torch.empty(ext.conv_fwd_workspace(B, C, Hc, Hc, M, 3, 1, bf, 0), device=DEV, dtype=torch.uint8)
+    dgr = torch.empty(ext.conv_fwd_workspace(B, M, Hc, Hc, C, 3, 1, bf, 1), device=DEV, dtype=torch.uint8)
     s0 = torch.cuda.current_stream().cuda_stream
-    ext.conv_pack_all([(w.data_ptr(), fwd.data_ptr(), B, C, H, H, M, 3, 1, bf, 0),
-                       (w.data_ptr(), dgr.data_ptr(), B, M, H, H, C, 3, 1, bf, 1)], s0)
+    ext.conv_pack_all([(w.data_ptr(), fwd.data_ptr(), B, C, Hc, Hc, M, 3, 1, bf, 0),
+                       (w.data_ptr(), dgr.data_ptr(), B, M, Hc, Hc, C, 3, 1, bf, 1)], s0)
     outs = []
     for fused in (True, False):
         zz = z.clone().requires_grad_(True)
@@ -388,7 +390,7 @@ def test_conv_dgrad_epilogue_batchnorm_backward_statistics(dtype, bvalid):
         gg, gbb = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
         gw, gb = torch.zeros(M, C, 3, 3, device=DEV), torch.zeros(M, device=DEV)
         h = L.BnBwdStats(st) if fused else None
-        a = L.BatchNormActFn.apply(zz, gamma, beta, rm, rv, st, 1e-5, 0.1, 1, gg, gbb, None, h)
+        a = L.BatchNormActFn.apply(zz, gamma, beta, rm, rv, st, 1e-5, 0.1, act, gg, gbb, None, h)
         y = L.Conv2dFn.apply(a, w, b, 1, dtype, gw, gb, (fwd, dgr), None, False, None, h)
         y.backward(torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(DEV))
         if fused:
