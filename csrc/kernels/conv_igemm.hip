@@ -256,20 +256,24 @@ __global__ void __launch_bounds__(CT) conv_wgrad_kernel(const float* __restrict_
       const int OH2 = g.OH >> 1, OW2 = g.OW >> 1, py = min(oy >> 1, OH2 - 1), px = min(ox >> 1, OW2 - 1);
       const bool inb = (oy >> 1) < OH2 && (ox >> 1) < OW2;
       const uint8_t sub = (uint8_t)(((oy & 1) << 1) | (ox & 1));
-      const long pp = (long)bb * M * OH2 * OW2 + py * OW2 + px;
+      // raw buffer loads (out-of-range offsets read 0), 32-bit offsets: no masked loads
+      const int P2 = OH2 * OW2, pp = (bb * M + m0 + rowg) * P2 + py * OW2 + px;
+      const __amdgpu_buffer_rsrc_t dr2 = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(dy), 0, g.B * M * P2 * (int)sizeof(float), 0x00020000);
+      const __amdgpu_buffer_rsrc_t cr2 = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint8_t*>(code), 0, g.B * M * P2, 0x00020000);
       float a[KPT];
-      uint8_t cd[KPT];
+      unsigned cd[KPT];
 #pragma unroll
       for (int e = 0; e < KPT; ++e) {
-        const int m = m0 + rowg + e;
-        const long o = pp + (long)((rowg + e < BM && m < M) ? m : 0) * OH2 * OW2;
-        a[e] = dy[o];
-        cd[e] = code[o];
+        const bool mv = rowg + e < BM && m0 + rowg + e < M;
+        const int o = pp + e * P2;
+        a[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dr2, mv ? o * 4 : (int)OOB, 0, 0));
+        cd[e] = __builtin_amdgcn_raw_buffer_load_b8(cr2, mv ? o : (int)OOB, 0, 0);
       }
 #pragma unroll
       for (int e = 0; e < KPT; ++e) {
-        const int m = m0 + rowg + e;
-        const bool mv = rowg + e < BM && m < M;
+        const bool mv = rowg + e < BM && m0 + rowg + e < M;
         av[e] = (mv && rv && inb && cd[e] == sub) ? a[e] : 0.f;
       }
     } else {
