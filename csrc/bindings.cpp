@@ -293,6 +293,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_conv_fwd_packed(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y), B, C, H, W, M,
                                 K, pad, bf16_ops, S(stream));
   });
+  m.def("conv_fwd_unpool_ok", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+    return dnn::conv_fwd_unpool_ok(B, C, H, W, M, K, pad, bf16_ops);
+  });
+  // data gradient of a pooled conv straight from the pooled gradient + argmax codes
+  m.def("conv_fwd_packed_unpool", [](u x, u code, u wp, u y, int B, int C, int H, int W, int M, int K, int pad,
+                                     int bf16_ops, u stream) {
+    dnn::launch_conv_fwd_packed_unpool(P<const float>(x), P<const uint8_t>(code), P<const void>(wp), P<float>(y), B, C,
+                                       H, W, M, K, pad, bf16_ops, S(stream));
+  });
   m.def("conv_fwd_pool_ok", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
     return dnn::conv_fwd_pool_ok(B, C, H, W, M, K, pad, bf16_ops);
   });

@@ -444,7 +444,12 @@ __global__ void __launch_bounds__(CT) pack_weights_kernel(const float* __restric
 //              pool: y is the pooled gradient; it lands on the window's argmax position (code
 //              < 4; code 4 = max <= 0: no gradient), so dz = y there and xhat is taken at that
 //              full-resolution position of z.
-constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2, EPI_BNBWD = 3;
+//   EPI_UNPOOL (input side; epilogue as EPI_PLAIN) x is the gradient of the 2x2 max-pool that
+//              followed a ReLU ([B][C][H/2][W/2]) and `code` its argmax codes: the patch loads
+//              unpool on the fly, x(c, iy, ix) = code == ((iy & 1) << 1 | (ix & 1)) ? x_pooled : 0
+//              - the data gradient of a pooled conv without relu_pool_bwd's full-size round trip
+//              (scalar patch path, register batch only: conv_fwd_unpool_ok)
+constexpr int EPI_PLAIN = 0, EPI_POOL = 1, EPI_STATS = 2, EPI_BNBWD = 3, EPI_UNPOOL = 4;
 struct BnTerms {  // EPI_BNBWD: the BatchNorm whose output gradient this kernel produces
   const float* z;       // its input [B][M][zH][zW]
   const float* mean;    // saved batch mean / inverse std, affine weight / bias [M]
@@ -464,6 +469,8 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
                                                             const int32_t* __restrict__ state = nullptr,
                                                             const BnTerms bt = BnTerms{}) {
   constexpr bool POOL = EPI == EPI_POOL;
+  constexpr bool UNP = EPI == EPI_UNPOOL;
+  static_assert(!UNP || !V4, "the unpooling loads are on the scalar patch path");
   static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
   using T = typename PatchT<BF16, CCH>::T;
   constexpr int CCP = PatchT<BF16, CCH>::CCP;
@@ -510,10 +517,17 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   // a chunk adds c0.  Patch loads are raw buffer loads over image b: positions in the
   // zero padding, rows past R and channels past C get an offset >= num_records, which the
   // hardware returns as 0 - no per-element exec masks.
+  // UNP: x / code are the pooled [C][H/2][W/2] planes; a position's code sits at its float
+  // offset / 4, so one offset (and OOB / 4, still >= the code records) serves both loads
+  const int PH = g.H >> 1, PW = g.W >> 1;
+  const int plane = UNP ? PH * PW : g.H * g.W;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(x) + (long)b * g.C * g.H * g.W, 0, g.C * g.H * g.W * (int)sizeof(float), 0x00020000);
+      const_cast<float*>(x) + (long)b * g.C * plane, 0, g.C * plane * (int)sizeof(float), 0x00020000);
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+      UNP ? code + (long)b * g.C * plane : nullptr, 0, UNP ? g.C * plane : 0, 0x00020000);
   constexpr unsigned OOB = 0x80000000u;  // >= num_records for every chunk (C*H*W*4 < 2^31)
-  const unsigned cstep = (unsigned)(g.H * g.W * (int)sizeof(float));  // bytes per channel
+  const unsigned cstep = (unsigned)(plane * (int)sizeof(float));  // bytes per channel
+  unsigned long long psel = 0;  // UNP: 2-bit position (in its 2x2 window) of patch element i
   // LDS destinations are hoisted too; out-of-range entries go to a dummy slot past the
   // patch (Ps + R*Wp*CCP), so the stores need no exec masks either.
   const int dummy = (int)(Ps - As) + g.R * g.Wp * CCP;
@@ -532,8 +546,14 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
-      const bool ok = r < g.R && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-      poff[i] = ok ? (unsigned)(((c * g.H + iy) * g.W + ix) * (int)sizeof(float)) : OOB;
+      if constexpr (UNP) {
+        const bool ok = r < g.R && (unsigned)iy < (unsigned)(2 * PH) && (unsigned)ix < (unsigned)(2 * PW);
+        poff[i] = ok ? (unsigned)(((c * PH + (iy >> 1)) * PW + (ix >> 1)) * (int)sizeof(float)) : OOB;
+        psel |= (unsigned long long)(((iy & 1) << 1) | (ix & 1)) << (2 * i);
+      } else {
+        const bool ok = r < g.R && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+        poff[i] = ok ? (unsigned)(((c * g.H + iy) * g.W + ix) * (int)sizeof(float)) : OOB;
+      }
       pdst[i] = r < g.R ? (int)(Ps - As) + (r * g.Wp + xp) * CCP + c : dummy;
       xp += dr; row += dq;
       if (xp >= g.Wp) { xp -= g.Wp; ++row; }
@@ -573,6 +593,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   // scratch memory (112 B per lane) instead of living in registers
   u32x4 areg[AV];
   float preg[PV];
+  unsigned creg[UNP ? PV : 1];
   f32x4 greg[PG];
   auto p_val = [&](int row, int xp, int c0) {  // remainder path
     const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
@@ -593,8 +614,10 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
         greg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(goff[i] + cb), 0, 0));
     } else {
 #pragma unroll
-      for (int i = 0; i < PV; ++i)
+      for (int i = 0; i < PV; ++i) {
         preg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(poff[i] + cb), 0, 0));
+        if constexpr (UNP) creg[i] = __builtin_amdgcn_raw_buffer_load_b8(cr, (int)((poff[i] + cb) >> 2), 0, 0);
+      }
     }
   };
   auto store_batch = [&](int c0) {
@@ -618,7 +641,10 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < PV; ++i) As[pdst[i]] = (T)preg[i];
+      for (int i = 0; i < PV; ++i) {
+        if constexpr (UNP) As[pdst[i]] = (T)(creg[i] == (unsigned)((psel >> (2 * i)) & 3u) ? preg[i] : 0.f);
+        else As[pdst[i]] = (T)preg[i];
+      }
     }
     // remainder beyond the register batch (large kernels / wide images only)
     for (int v = tid + AV * CT; v < nv; v += CT) {
@@ -874,7 +900,8 @@ FastPlan plan_fast(int B, int C, int H, int W, int M, int K, int pad, bool bf, i
 }
 
 struct EpiArgs {
-  uint8_t* code = nullptr;          // EPI_POOL
+  uint8_t* code = nullptr;          // EPI_POOL (output) / EPI_UNPOOL (input, unpool = true)
+  bool unpool = false;
   double* stats = nullptr;          // EPI_STATS / EPI_BNBWD
   const int32_t* state = nullptr;   // EPI_STATS / EPI_BNBWD
   BnTerms bn{};                     // EPI_BNBWD (bn.z != nullptr)
@@ -895,14 +922,16 @@ template <bool BF16, int CCH, int EPI>
 void fast_launch_e(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                    float* y, const EpiArgs& e, hipStream_t s) {
   // float4 patch groups when image rows are whole 16-B vectors
-  if (f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) fast_launch_v<BF16, CCH, true, EPI>(f, wp, x, bias, y, e, s);
+  if (EPI != EPI_UNPOOL && f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0)
+    fast_launch_v<BF16, CCH, EPI != EPI_UNPOOL, EPI>(f, wp, x, bias, y, e, s);
   else fast_launch_v<BF16, CCH, false, EPI>(f, wp, x, bias, y, e, s);
 }
 // the epilogue follows from the arguments: code -> pooled, stats -> BatchNorm statistics
 template <bool BF16, int CCH>
 void fast_launch(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                  float* y, hipStream_t s, const EpiArgs& e = EpiArgs{}) {
-  if (e.code != nullptr) fast_launch_e<BF16, CCH, EPI_POOL>(f, wp, x, bias, y, e, s);
+  if (e.unpool) fast_launch_e<BF16, CCH, EPI_UNPOOL>(f, wp, x, bias, y, e, s);
+  else if (e.code != nullptr) fast_launch_e<BF16, CCH, EPI_POOL>(f, wp, x, bias, y, e, s);
   else if (e.stats != nullptr && e.bn.z != nullptr) fast_launch_e<BF16, CCH, EPI_BNBWD>(f, wp, x, bias, y, e, s);
   else if (e.stats != nullptr) fast_launch_e<BF16, CCH, EPI_STATS>(f, wp, x, bias, y, e, s);
   else fast_launch_e<BF16, CCH, EPI_PLAIN>(f, wp, x, bias, y, e, s);
@@ -1156,6 +1185,28 @@ void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bi
   EpiArgs e;
   e.code = code;
   fast_launch_packed(f, wp, x, bias, y, bf16_ops, e, s);
+}
+
+// EPI_UNPOOL: the scalar patch path with every element of a chunk in the register batch
+int conv_fwd_unpool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  if (!f.ok || H < 2 || W < 2) return 0;
+  const int pv = bf16_ops ? Batch<32>::PV : (f.cch == 8 ? Batch<8>::PV : (f.cch == 16 ? Batch<16>::PV : Batch<32>::PV));
+  return (long)f.pg.R * f.cch * f.pg.Wp <= (long)pv * CT ? 1 : 0;
+}
+
+// y = conv(unpool(x, code), w) + bias from the packed image: x [B][C][H/2][W/2] is the pooled
+// gradient of a ReLU + max-pool with argmax codes `code` (EPI_UNPOOL); H, W the unpooled size
+void launch_conv_fwd_packed_unpool(const float* x, const uint8_t* code, const void* wp, float* y, int B, int C, int H,
+                                   int W, int M, int K, int pad, int bf16_ops, hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  if (!conv_fwd_unpool_ok(B, C, H, W, M, K, pad, bf16_ops))
+    throw std::runtime_error("conv_fwd_packed_unpool: layer has no unpooling LDS-patch plan");
+  const FastPlan f = plan_fast(B, C, H, W, M, K, pad, bf16_ops != 0);
+  EpiArgs e;
+  e.code = const_cast<uint8_t*>(code);
+  e.unpool = true;
+  fast_launch_packed(f, wp, x, nullptr, y, bf16_ops, e, s);
 }
 
 int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {

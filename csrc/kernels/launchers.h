@@ -116,6 +116,9 @@ int conv_fwd_pool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16
 void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bias, float* y, uint8_t* code, int B,
                                  int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 // conv + bias with the following BatchNorm's batch-statistics partials in the epilogue
+int conv_fwd_unpool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
+void launch_conv_fwd_packed_unpool(const float* x, const uint8_t* code, const void* wp, float* y, int B, int C, int H,
+                                   int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
 void launch_conv_fwd_packed_bnbwd(const float* x, const void* wp, float* y, double* stats, const int32_t* state,
                                   const float* bn_z, const float* bn_mean, const float* bn_invstd,

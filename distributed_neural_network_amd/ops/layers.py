@@ -27,6 +27,9 @@ import torch.nn.functional as F
 from . import native
 
 ST_BVALID = 1
+# data gradient of a conv with a fused ReLU + max-pool straight from the pooled gradient
+# (conv_fwd_packed_unpool); DNN_UNPOOL_DGRAD=0 restores relu_pool_bwd + the plain dgrad
+_UNPOOL_DGRAD = os.environ.get("DNN_UNPOOL_DGRAD", "1") != "0"
 
 
 def _is_gpu(t: torch.Tensor) -> bool:
@@ -139,14 +142,20 @@ class Conv2dFn(torch.autograd.Function):
         Cout = w.shape[0]
         dy = dy.contiguous()
         pool_code = 0
-        if ctx.code is not None and ctx.needs_input_grad[0]:
-            # the fused pool's backward: scatter to the argmax positions (the dgrad reads full dy)
+        bf = int(ctx.gemm_dtype == torch.bfloat16)
+        # the fused pool's backward: both gradient kernels unpool dy on their loads when the
+        # data gradient runs on the packed LDS-patch path (EPI_UNPOOL); otherwise dy is
+        # scattered to the argmax positions once and the dgrad reads the full-size tensor
+        unpool_dgrad = (ctx.code is not None and ctx.needs_input_grad[0] and _is_gpu(dy) and _UNPOOL_DGRAD
+                        and ctx.packed is not None
+                        and ctx.packed[1] is not None and (ctx.bnbwd is None or ctx.bnbwd.z is None)
+                        and bool(_ext().conv_fwd_unpool_ok(B, Cout, OH, OW, C, K, K - 1 - pad, bf)))
+        if ctx.code is not None and ctx.needs_input_grad[0] and not unpool_dgrad:
             full = torch.empty(B, Cout, OH, OW, device=dy.device, dtype=torch.float32)
             _ext().relu_pool_bwd(_p(dy), _p(ctx.code), B * Cout, OH, OW, _p(full), _s(dy))
             dy = full
-        elif ctx.code is not None:  # weight gradient only: it unpools dy on its loads
+        elif ctx.code is not None:  # the weight gradient unpools dy on its loads
             pool_code = _p(ctx.code)
-        bf = int(ctx.gemm_dtype == torch.bfloat16)
         dw = ctx.gw if ctx.gw is not None else torch.empty_like(w)
         db = ctx.gb if ctx.gb is not None else torch.empty(Cout, device=dy.device, dtype=torch.float32)
         dx = None
@@ -173,6 +182,9 @@ class Conv2dFn(torch.autograd.Function):
                                               _p(h.invstd), _p(h.gamma), _p(h.beta),
                                               _p(h.code) if h.code is not None else 0, h.z.shape[2], h.z.shape[3],
                                               B, Cout, OH, OW, C, K, K - 1 - pad, bf, st)
+                elif unpool_dgrad:
+                    ext.conv_fwd_packed_unpool(_p(dy), _p(ctx.code), _p(ctx.packed[1]), _p(dx), B, Cout, OH, OW, C, K,
+                                               K - 1 - pad, bf, st)
                 elif ctx.packed is not None and ctx.packed[1] is not None:
                     ext.conv_fwd_packed(_p(dy), _p(ctx.packed[1]), 0, _p(dx), B, Cout, OH, OW, C, K, K - 1 - pad, bf,
                                         st)

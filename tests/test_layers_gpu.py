@@ -307,6 +307,71 @@ def test_conv_pooled_epilogue_matches_conv_then_relu_pool(B, C, H, M, K, pad, dt
         assert (a is None and c is None) or torch.equal(a, c)
 
 
+@pytest.mark.parametrize("B,Co,OH,Ci,K,pad,dtype", [(8, 16, 10, 6, 5, 0, torch.float32),
+                                                   (4, 7, 11, 5, 3, 1, torch.float32),
+                                                   (3, 6, 28, 3, 5, 0, torch.float32),
+                                                   (4, 16, 10, 6, 5, 0, torch.bfloat16)])
+def test_conv_unpool_dgrad_matches_relu_pool_bwd_then_dgrad(B, Co, OH, Ci, K, pad, dtype):
+    """The data gradient of a pooled conv read straight from the pooled gradient and its argmax
+    codes (EPI_UNPOOL: the patch loads unpool) must equal relu_pool_bwd followed by the plain
+    packed dgrad bit for bit - codes 0-3 and 4 (max <= 0), odd sizes (the last row / column of
+    an odd map gets no gradient)."""
+    ext = L._ext()
+    bf = int(dtype == torch.bfloat16)
+    pd = K - 1 - pad
+    if not ext.conv_fwd_unpool_ok(B, Co, OH, OH, Ci, K, pd, bf):
+        pytest.skip("no unpooling plan for this shape")
+    torch.manual_seed(B + Co + OH)
+    w = (torch.randn(Co, Ci, K, K) / (Ci * K * K) ** 0.5).to(DEV)  # the forward layer's weight
+    img = torch.empty(ext.conv_fwd_workspace(B, Co, OH, OH, Ci, K, pd, bf, 1), device=DEV, dtype=torch.uint8)
+    st = torch.cuda.current_stream().cuda_stream
+    ext.conv_pack_all([(w.data_ptr(), img.data_ptr(), B, Co, OH, OH, Ci, K, pd, bf, 1)], st)
+    P = OH // 2
+    dp = torch.randn(B, Co, P, P, device=DEV)
+    code = torch.randint(0, 5, (B, Co, P, P), device=DEV, dtype=torch.uint8)
+    full = torch.empty(B, Co, OH, OH, device=DEV)
+    ext.relu_pool_bwd(dp.data_ptr(), code.data_ptr(), B * Co, OH, OH, full.data_ptr(), st)
+    H = OH + 2 * pd - K + 1
+    ref = torch.full((B, Ci, H, H), float("nan"), device=DEV)
+    got = torch.full((B, Ci, H, H), float("nan"), device=DEV)
+    ext.conv_fwd_packed(full.data_ptr(), img.data_ptr(), 0, ref.data_ptr(), B, Co, OH, OH, Ci, K, pd, bf, st)
+    ext.conv_fwd_packed_unpool(dp.data_ptr(), code.data_ptr(), img.data_ptr(), got.data_ptr(), B, Co, OH, OH, Ci, K,
+                               pd, bf, st)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
+
+
+def test_pooled_conv_backward_with_unpool_dgrad():
+    """Conv2dFn with the fused pool and the packed flipped image (the layer engine's setup):
+    backward through the unpooling dgrad + unpooling wgrad equals conv -> ReluPoolFn -> backward
+    on the plain packed path, bitwise (dx, dW, db)."""
+    ext = L._ext()
+    B, C, H, M, K, pad = 8, 6, 14, 16, 5, 0
+    OH = H - K + 1
+    torch.manual_seed(3)
+    x = torch.randn(B, C, H, H, device=DEV)
+    w = (torch.randn(M, C, K, K) / (C * K * K) ** 0.5).to(DEV)
+    b = torch.randn(M, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    img = torch.empty(ext.conv_fwd_workspace(B, C, H, H, M, K, pad, 0, 0), device=DEV, dtype=torch.uint8)
+    imgf = torch.empty(ext.conv_fwd_workspace(B, M, OH, OH, C, K, K - 1 - pad, 0, 1), device=DEV, dtype=torch.uint8)
+    ext.conv_pack_all([(w.data_ptr(), img.data_ptr(), B, C, H, H, M, K, pad, 0, 0),
+                       (w.data_ptr(), imgf.data_ptr(), B, M, OH, OH, C, K, K - 1 - pad, 0, 1)], st)
+    assert ext.conv_fwd_unpool_ok(B, M, OH, OH, C, K, K - 1 - pad, 0)
+    outs = []
+    for fused in (True, False):
+        xx = x.clone().requires_grad_(True)
+        gw, gb = torch.zeros(M, C, K, K, device=DEV), torch.zeros(M, device=DEV)
+        y = L.Conv2dFn.apply(xx, w, b, pad, torch.float32, gw, gb, (img, imgf), None, fused)
+        if not fused:
+            y = L.ReluPoolFn.apply(y)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(7)).to(DEV)
+        y.backward(dy)
+        outs.append((y.detach(), xx.grad, gw, gb))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("B,C,H,M,K,pad,dtype,act,bvalid", [(8, 3, 32, 16, 3, 1, torch.bfloat16, 1, 8),
                                                           (8, 6, 14, 16, 5, 0, torch.float32, 2, 5),
                                                           (6, 32, 16, 64, 3, 1, torch.bfloat16, 2, 6)])
