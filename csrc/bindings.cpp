@@ -293,6 +293,18 @@ PYBIND11_MODULE(_dnn_hip, m) {
     dnn::launch_conv_fwd_packed(P<const float>(x), P<const void>(wp), P<const float>(bias), P<float>(y), B, C, H, W, M,
                                 K, pad, bf16_ops, S(stream));
   });
+  m.def("conv_fwd_ingest_ok", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int epi) {
+    return dnn::conv_fwd_ingest_ok(B, C, H, W, M, K, pad, bf16_ops, epi);
+  });
+  // first conv of a training step reading the u8 images of the batch ids (ingest folded in)
+  m.def("conv_fwd_packed_ingest", [](u images, u ids, u labels, u x_out, u lab_out, u wp, u bias, u y, u code, u stats,
+                                     u state, int B, int C, int H, int W, int M, int K, int pad, int bf16_ops,
+                                     u stream) {
+    dnn::launch_conv_fwd_packed_ingest(P<const uint8_t>(images), P<const int32_t>(ids), P<const int32_t>(labels),
+                                       P<float>(x_out), P<int32_t>(lab_out), P<const void>(wp), P<const float>(bias),
+                                       P<float>(y), P<uint8_t>(code), P<double>(stats), P<const int32_t>(state), B, C,
+                                       H, W, M, K, pad, bf16_ops, S(stream));
+  });
   m.def("conv_fwd_unpool_ok", [](int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {
     return dnn::conv_fwd_unpool_ok(B, C, H, W, M, K, pad, bf16_ops);
   });

@@ -460,16 +460,33 @@ struct BnTerms {  // EPI_BNBWD: the BatchNorm whose output gradient this kernel 
                         // kernel's output grid), else nullptr (ReLU only: zH, zW = OH, OW)
   int zH, zW;
 };
-template <bool BF16, int BM, int CCH, bool V4, int EPI = EPI_PLAIN>
+// U8 (float4 patch path): the layer's input is the training step's ingest - the patch loads
+// read the u8 dataset images of the batch's sample ids directly and normalise them as
+// ingest_kernel does (bit-identical), the workgroup that owns an input row (row-aligned
+// tiles: `own` rows each, the first / last tile also the rows above / below) stores the
+// normalised values to x_out for the weight gradient, and tile 0 copies the label - the
+// ingest launch of the step disappears.
+struct InArgs {
+  const uint8_t* images;  // [N][C][H][W] u8 dataset
+  const int32_t* ids;     // [B] sample id of each batch row
+  const int32_t* labels;  // [N]
+  float* x_out;           // [B][C][H][W] normalised input
+  int32_t* lab_out;       // [B]
+  int own;                // input rows owned per tile
+};
+
+template <bool BF16, int BM, int CCH, bool V4, int EPI = EPI_PLAIN, bool U8 = false>
 __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restrict__ x,
                                                             const typename PatchT<BF16, CCH>::T* __restrict__ wp,
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             PGeom g, uint8_t* __restrict__ code = nullptr,
                                                             double* __restrict__ stats = nullptr,
                                                             const int32_t* __restrict__ state = nullptr,
-                                                            const BnTerms bt = BnTerms{}) {
+                                                            const BnTerms bt = BnTerms{},
+                                                            const InArgs in = InArgs{}) {
   constexpr bool POOL = EPI == EPI_POOL;
   constexpr bool UNP = EPI == EPI_UNPOOL;
+  static_assert(!U8 || (V4 && !UNP), "ingest loads are on the float4 patch path");
   static_assert(!UNP || !V4, "the unpooling loads are on the scalar patch path");
   static_assert(!BF16 || CCH == 32, "bf16 chunks are one 32-deep MFMA K-step");
   using T = typename PatchT<BF16, CCH>::T;
@@ -521,8 +538,17 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   // offset / 4, so one offset (and OOB / 4, still >= the code records) serves both loads
   const int PH = g.H >> 1, PW = g.W >> 1;
   const int plane = UNP ? PH * PW : g.H * g.W;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(x) + (long)b * g.C * plane, 0, g.C * plane * (int)sizeof(float), 0x00020000);
+  const int sid = U8 ? in.ids[b] : 0;
+  const __amdgpu_buffer_rsrc_t xr =
+      U8 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(in.images) + (long)sid * g.C * plane, 0,
+                                             g.C * plane, 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x) + (long)b * g.C * plane, 0,
+                                             g.C * plane * (int)sizeof(float), 0x00020000);
+  if (U8 && tid == 0 && blockIdx.y == 0 && tile == b * g.tiles) in.lab_out[b] = in.labels[sid];
+  // U8: x_out of image b (no records for the other M-tiles: their stores are dropped)
+  const __amdgpu_buffer_rsrc_t xo = __builtin_amdgcn_make_buffer_rsrc(
+      U8 ? in.x_out + (long)b * g.C * plane : nullptr, 0,
+      (U8 && blockIdx.y == 0) ? g.C * plane * (int)sizeof(float) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
       UNP ? code + (long)b * g.C * plane : nullptr, 0, UNP ? g.C * plane : 0, 0x00020000);
   constexpr unsigned OOB = 0x80000000u;  // >= num_records for every chunk (C*H*W*4 < 2^31)
@@ -568,16 +594,21 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   const unsigned gq0 = V4 ? (unsigned)tid / (unsigned)G : 0u;
   const int gdq = V4 ? CT / G : 0, gdr = V4 ? CT - gdq * G : 0;
   unsigned goff[PG];
+  unsigned xoff[U8 ? PG : 1];  // U8: x_out byte offset of group i (OOB: another tile owns its row)
   int gdst[PG];
   if constexpr (V4) {
     unsigned row = gq0;
     int gx = tid - (int)gq0 * G;
+    const int t = tile - b * g.tiles;
+    const int own_lo = t == 0 ? -(1 << 30) : t * in.own - g.pad;
+    const int own_hi = t == g.tiles - 1 ? (1 << 30) : (t + 1) * in.own - g.pad;
 #pragma unroll
     for (int i = 0; i < PG; ++i) {
       const unsigned r = row / CCH, c = row & (CCH - 1);
       const int iy = iy0 + (int)r;
       const bool ok = r < (unsigned)g.R && (unsigned)iy < (unsigned)g.H;
       goff[i] = ok ? (unsigned)(((int)c * g.H + iy) * g.W + 4 * gx) * 4u : OOB;
+      if constexpr (U8) xoff[i] = (ok && iy >= own_lo && iy < own_hi) ? goff[i] : OOB;
       gdst[i] = r < (unsigned)g.R ? (int)(Ps - As) + ((int)r * g.Wp + 4 * gx + g.pad) * CCP + (int)c : dummy;
       gx += gdr; row += gdq;
       if (gx >= G) { gx -= G; ++row; }
@@ -594,6 +625,7 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   u32x4 areg[AV];
   float preg[PV];
   unsigned creg[UNP ? PV : 1];
+  unsigned ureg[U8 ? PG : 1];  // U8: 4 image bytes per group
   f32x4 greg[PG];
   auto p_val = [&](int row, int xp, int c0) {  // remainder path
     const int r = row / CCH, c = row - r * CCH, iy = iy0 + r, ix = xp - g.pad;
@@ -608,7 +640,10 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < AV; ++i) areg[i] = *reinterpret_cast<const u32x4*>(wp + aoff[i] + c0);
     const unsigned cb = (unsigned)c0 * cstep;
-    if constexpr (V4) {
+    if constexpr (U8) {  // byte offset = float offset / 4 (OOB / 4 is still past the records)
+#pragma unroll
+      for (int i = 0; i < PG; ++i) ureg[i] = __builtin_amdgcn_raw_buffer_load_b32(xr, (int)((goff[i] + cb) >> 2), 0, 0);
+    } else if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < PG; ++i)
         greg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(goff[i] + cb), 0, 0));
@@ -623,6 +658,19 @@ __global__ void __launch_bounds__(CT) conv_fwd_patch_kernel(const float* __restr
   auto store_batch = [&](int c0) {
 #pragma unroll
     for (int i = 0; i < AV; ++i) *reinterpret_cast<u32x4*>(As + adst[i]) = areg[i];
+    if constexpr (U8) {
+      const unsigned cb = (unsigned)c0 * cstep, lim = (unsigned)(g.C * plane * (int)sizeof(float));
+#pragma unroll
+      for (int i = 0; i < PG; ++i) {
+        // padding / rows past R / channels past C: 0 (not the normalised value of a 0 byte);
+        // torchvision op order with IEEE-rounded division, as ingest_kernel
+        const bool inr = goff[i] + cb < lim;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          greg[i][k] = inr ? __fdiv_rn(__fdiv_rn((float)((ureg[i] >> (8 * k)) & 0xffu), 255.0f) - 0.5f, 0.5f) : 0.f;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, greg[i]), xo, (int)(xoff[i] + cb), 0, 0);
+      }
+    }
     if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < PG; ++i) {
@@ -905,22 +953,30 @@ struct EpiArgs {
   double* stats = nullptr;          // EPI_STATS / EPI_BNBWD
   const int32_t* state = nullptr;   // EPI_STATS / EPI_BNBWD
   BnTerms bn{};                     // EPI_BNBWD (bn.z != nullptr)
+  const InArgs* in = nullptr;       // U8 ingest loads (float4 path)
 };
-template <bool BF16, int CCH, bool V4, int EPI>
+template <bool BF16, int CCH, bool V4, int EPI, bool U8 = false>
 void fast_launch_v(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                    float* y, const EpiArgs& e, hipStream_t s) {
   dim3 grid((unsigned)(f.pg.B * f.pg.tiles), (unsigned)f.gy);
+  const InArgs in = e.in ? *e.in : InArgs{};
   if (f.bm == 16)
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       e.code, e.stats, e.state, e.bn);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 16, CCH, V4, EPI, U8>), grid, dim3(CT), f.lds, s, x, wp, bias, y,
+                       f.pg, e.code, e.stats, e.state, e.bn, in);
   else
-    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, EPI>), grid, dim3(CT), f.lds, s, x, wp, bias, y, f.pg,
-                       e.code, e.stats, e.state, e.bn);
+    hipLaunchKernelGGL((conv_fwd_patch_kernel<BF16, 32, CCH, V4, EPI, U8>), grid, dim3(CT), f.lds, s, x, wp, bias, y,
+                       f.pg, e.code, e.stats, e.state, e.bn, in);
   HIP_CHECK(hipGetLastError());
 }
 template <bool BF16, int CCH, int EPI>
 void fast_launch_e(const FastPlan& f, const typename PatchT<BF16, CCH>::T* wp, const float* x, const float* bias,
                    float* y, const EpiArgs& e, hipStream_t s) {
+  if constexpr (EPI != EPI_UNPOOL && EPI != EPI_BNBWD) {
+    if (e.in != nullptr) {  // ingest loads (conv_fwd_ingest_ok checked the plan)
+      fast_launch_v<BF16, CCH, true, EPI, true>(f, wp, x, bias, y, e, s);
+      return;
+    }
+  }
   // float4 patch groups when image rows are whole 16-B vectors
   if (EPI != EPI_UNPOOL && f.pg.W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0)
     fast_launch_v<BF16, CCH, EPI != EPI_UNPOOL, EPI>(f, wp, x, bias, y, e, s);
@@ -1207,6 +1263,53 @@ void launch_conv_fwd_packed_unpool(const float* x, const uint8_t* code, const vo
   e.code = const_cast<uint8_t*>(code);
   e.unpool = true;
   fast_launch_packed(f, wp, x, nullptr, y, bf16_ops, e, s);
+}
+
+// U8 ingest loads: plan of the epilogue (epi 0 plain, 1 pooled, 2 BatchNorm statistics) with
+// float4 rows, every chunk in the register batch, row-aligned tiles and every input row inside
+// some tile's patch; returns the rows each tile owns (0: not possible)
+static int ingest_plan(int B, int C, int H, int W, int M, int K, int pad, bool bf, int epi, FastPlan* out) {
+  const FastPlan f = epi == 1 ? plan_pool(B, C, H, W, M, K, pad, bf) : plan_fast(B, C, H, W, M, K, pad, bf);
+  if (!f.ok || W % 4 != 0) return 0;
+  const PGeom& g = f.pg;
+  if ((long)g.R * f.cch * (W / 4) > 6L * CT) return 0;  // PG groups per thread
+  int own;
+  if (epi == 1) {
+    own = g.rpt;
+  } else {
+    if (g.ppt % g.OW != 0 || (g.OH * g.OW) % g.ppt != 0) return 0;
+    own = g.ppt / g.OW;
+  }
+  // the last tile's patch must reach the last input row
+  if ((g.tiles - 1) * own - pad + g.R < H) return 0;
+  if (out) *out = f;
+  return own;
+}
+
+int conv_fwd_ingest_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int epi) {
+  return ingest_plan(B, C, H, W, M, K, pad, bf16_ops != 0, epi, nullptr) > 0 ? 1 : 0;
+}
+
+// The first conv of a training step with the ingest folded in: y (+ pooled codes / BatchNorm
+// statistics partials) from the u8 images of the batch's sample ids; also stores the
+// normalised input x_out [B][C][H][W] and the labels (see InArgs)
+void launch_conv_fwd_packed_ingest(const uint8_t* images, const int32_t* ids, const int32_t* labels, float* x_out,
+                                   int32_t* lab_out, const void* wp, const float* bias, float* y, uint8_t* code,
+                                   double* stats, const int32_t* state, int B, int C, int H, int W, int M, int K,
+                                   int pad, int bf16_ops, hipStream_t s) {
+  geom(B, C, H, W, K, pad);
+  const int epi = code != nullptr ? 1 : (stats != nullptr ? 2 : 0);
+  FastPlan f;
+  const int own = ingest_plan(B, C, H, W, M, K, pad, bf16_ops != 0, epi, &f);
+  if (own == 0) throw std::runtime_error("conv_fwd_packed_ingest: layer has no ingest plan");
+  if (epi == 2) f.lds = std::max(f.lds, (size_t)f.bm * PNT * sizeof(float));  // the statistics' output tile
+  const InArgs in{images, ids, labels, x_out, lab_out, own};
+  EpiArgs e;
+  e.code = code;
+  e.stats = stats;
+  e.state = state;
+  e.in = &in;
+  fast_launch_packed(f, wp, nullptr, bias, y, bf16_ops, e, s);
 }
 
 int conv_fwd_stat_parts(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops) {

@@ -116,6 +116,11 @@ int conv_fwd_pool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16
 void launch_conv_fwd_packed_pool(const float* x, const void* wp, const float* bias, float* y, uint8_t* code, int B,
                                  int C, int H, int W, int M, int K, int pad, int bf16_ops, hipStream_t s);
 // conv + bias with the following BatchNorm's batch-statistics partials in the epilogue
+int conv_fwd_ingest_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops, int epi);
+void launch_conv_fwd_packed_ingest(const uint8_t* images, const int32_t* ids, const int32_t* labels, float* x_out,
+                                   int32_t* lab_out, const void* wp, const float* bias, float* y, uint8_t* code,
+                                   double* stats, const int32_t* state, int B, int C, int H, int W, int M, int K,
+                                   int pad, int bf16_ops, hipStream_t s);
 int conv_fwd_unpool_ok(int B, int C, int H, int W, int M, int K, int pad, int bf16_ops);
 void launch_conv_fwd_packed_unpool(const float* x, const uint8_t* code, const void* wp, float* y, int B, int C, int H,
                                    int W, int M, int K, int pad, int bf16_ops, hipStream_t s);

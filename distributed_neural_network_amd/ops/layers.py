@@ -93,14 +93,35 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, pad: int, gemm_dtype: torch.dtype, gw=None, gb=None, packed=None, slice_sink=None,
-                pool: bool = False, stats: "BnStats | None" = None, bnbwd: "BnBwdStats | None" = None):
+                pool: bool = False, stats: "BnStats | None" = None, bnbwd: "BnBwdStats | None" = None,
+                ingest: "IngestSrc | None" = None):
         B, C, H, W = x.shape
         Cout, _, K, _ = w.shape
         OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
         x = x.contiguous()
         bf = int(gemm_dtype == torch.bfloat16)
         ctx.code = None
-        if _is_gpu(x) and pool:
+        if _is_gpu(x) and ingest is not None:
+            # the step's ingest folded into this (first) conv: x is OUTPUT here - the kernel reads
+            # the u8 images of the batch ids, stores the normalised input into x and the labels
+            assert packed is not None and packed[0] is not None, "ingest conv needs the packed forward image"
+            ext = _ext()
+            code = part = 0
+            if pool:
+                y = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.float32)
+                ctx.code = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.uint8)
+                code = _p(ctx.code)
+            else:
+                y = torch.empty(B, Cout, OH, OW, device=x.device, dtype=torch.float32)
+                if stats is not None:
+                    stats.nparts = ext.conv_fwd_stat_parts(B, C, H, W, Cout, K, pad, bf)
+                    stats.part = torch.empty(Cout * stats.nparts * 2, device=x.device, dtype=torch.float64)
+                    part = _p(stats.part)
+            st = stats.state if stats is not None else None
+            ext.conv_fwd_packed_ingest(_p(ingest.images), _p(ingest.ids), _p(ingest.labels), _p(x), _p(ingest.lab_out),
+                                       _p(packed[0]), _p(b), _p(y), code, part, _p(st) if st is not None else 0,
+                                       B, C, H, W, Cout, K, pad, bf, _s(x))
+        elif _is_gpu(x) and pool:
             assert packed is not None and packed[0] is not None, "pooled conv needs the packed forward image"
             y = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.float32)
             ctx.code = torch.empty(B, Cout, OH // 2, OW // 2, device=x.device, dtype=torch.uint8)
@@ -200,8 +221,16 @@ class Conv2dFn(torch.autograd.Function):
                 dcols = _gemm(w.reshape(Cout, -1).t(), dy2, ctx.gemm_dtype).contiguous()  # [B, CKK, L]
                 dx = F.fold(dcols, (H, W), K, padding=pad)
         if ctx.gw is not None:
-            return dx, None, None, None, None, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None
+
+
+class IngestSrc:
+    """The training step's ingest for the first conv (``Conv2dFn(..., ingest=)``): u8 dataset
+    images / labels, the batch's sample ids, and where the labels go."""
+
+    def __init__(self, images: torch.Tensor, labels: torch.Tensor, ids: torch.Tensor, lab_out: torch.Tensor) -> None:
+        self.images, self.labels, self.ids, self.lab_out = images, labels, ids, lab_out
 
 
 class BnBwdStats:

@@ -29,6 +29,8 @@ MI355X design points kept from the fused engine:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -88,6 +90,8 @@ class LayerEngine(Engine):
         self.defer_slice_sums = True  # conv wgrad slice sums inside the SGD tail (single GPU)
         self._tail_packs = True       # the SGD tail refreshes the packed conv-weight images
         self.fuse_bn_bwd = True       # BatchNorm + ReLU backward statistics in the next conv's dgrad
+        # the step's ingest folded into the first conv's loads (DNN_FUSE_INGEST=0: ingest kernel)
+        self.fuse_ingest = False
         if self.gpu:
             self._plan_weight_packing()
         # capacities of the one-launch step tail (csrc/kernels/launchers.h PackScatter / SliceSet):
@@ -122,6 +126,15 @@ class LayerEngine(Engine):
                 self._packed[n] = (fwd, dgr)
                 if fwd is not None and ext.conv_fwd_pool_ok(B, C, H, W, M, K, pad, bf):
                     self._pool_ok.add(n)
+                if first and fwd is not None and self.spec[0] is layer:
+                    # the epilogue forward() will pick for this layer in training
+                    i = self.spec.index(layer)
+                    nxt = self.spec[i + 1] if i + 1 < len(self.spec) else None
+                    nn2 = self.spec[i + 2] if i + 2 < len(self.spec) else None
+                    epi = (1 if isinstance(nxt, zoo.ReluPool) and n in self._pool_ok else
+                           2 if isinstance(nxt, zoo.BN) and isinstance(nn2, (zoo.Relu, zoo.ReluPool)) else 0)
+                    self.fuse_ingest = (os.environ.get("DNN_FUSE_INGEST", "1") != "0" and C == 3 and H == W == 32
+                                        and bool(ext.conv_fwd_ingest_ok(B, C, H, W, M, K, pad, bf, epi)))
                 first = False
                 H, W = OH, OW
             elif isinstance(layer, zoo.ReluPool):
@@ -175,13 +188,15 @@ class LayerEngine(Engine):
 
     # -- model ------------------------------------------------------------------------------------
     def forward(self, x: torch.Tensor, training: bool, state: torch.Tensor | None, pack: bool = True,
-                xent: L.XentFusion | None = None, slice_sink: list | None = None) -> torch.Tensor:
+                xent: L.XentFusion | None = None, slice_sink: list | None = None,
+                ingest: L.IngestSrc | None = None) -> torch.Tensor:
         """Layer stack.  Training: every op writes its parameter gradients straight into the
         flat gradient arena (views ``G``), so backward leaves ``grad`` complete with no
         accumulation or zeroing kernels.  ``pack``: refresh the packed conv-weight images
         from the arena first (False: the previous step's SGD tail already stored them).
         ``xent``: offered to the last layer, which may fuse the loss (``xent.out``).
-        ``slice_sink``: conv layers defer their weight-gradient slice sums to the SGD tail."""
+        ``slice_sink``: conv layers defer their weight-gradient slice sums to the SGD tail.
+        ``ingest``: the first conv reads the batch's u8 images itself and fills ``x``."""
         P, G, Bf, dt = self.P, self.G, self.Bf, self.gemm_dtype
         if pack and self._pack_jobs:
             self.ext.conv_pack_all(self._pack_jobs, torch.cuda.current_stream(self.device).cuda_stream)
@@ -221,7 +236,7 @@ class LayerEngine(Engine):
                         and packed is not None and packed[0] is not None):
                     bn_stats = L.BnStats(state)
                 x = L.Conv2dFn.apply(x, P[f"{n}.weight"], P[f"{n}.bias"], layer.pad, dt, gw, gb, packed, slice_sink,
-                                     pool, bn_stats, bn_bwd)
+                                     pool, bn_stats, bn_bwd, ingest if i == 0 else None)
                 bn_bwd = None
                 skip = pool
             elif isinstance(layer, zoo.BN):
@@ -283,13 +298,18 @@ class LayerEngine(Engine):
         since the last step (epoch averaging, checkpoint load, recovery); later steps find
         them refreshed by the previous step's SGD tail."""
         assert self.train is not None
-        self._ingest()
+        ingest = None
+        if self.fuse_ingest:
+            ingest = L.IngestSrc(self.train.images, self.train.labels, self.batch_ids, self.labels)
+        else:
+            self._ingest()
         tail = self.gpu and not self._fused_sgd() and self._tail_packs
         xent = L.XentFusion(self.labels, self.state) if self.gpu else None
         # single GPU: the conv weight-gradient slice sums run inside the SGD tail launch (with a
         # gradient all-reduce the gradients must be complete before it)
         sink = [] if (tail and self.grad_sync is None and self.defer_slice_sums) else None
-        logits = self.forward(self.x, True, self.state, pack=first or not tail, xent=xent, slice_sink=sink)
+        logits = self.forward(self.x, True, self.state, pack=first or not tail, xent=xent, slice_sink=sink,
+                              ingest=ingest)
         if xent is not None and xent.out is not None:
             loss, corr, dl = xent.out  # fused into the last Linear's launch
         else:

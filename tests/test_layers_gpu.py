@@ -271,6 +271,31 @@ def test_deferred_slice_sums_bitwise(model, dtype):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("model,dtype", [("lenet", "fp32"), ("lenet", "bf16"), ("cifar-vgg", "bf16"),
+                                         ("cifar-vgg", "fp32")])
+def test_ingest_folded_into_first_conv_bitwise(model, dtype):
+    """The first conv reading the u8 images of the batch ids itself (normalising on the load,
+    storing the input for its weight gradient, copying the labels) == the ingest kernel + the
+    conv on its output, bit for bit over steps with a shuffled order and a tail batch.  (lenet-bn
+    has no plan: its 28-wide statistics tiles are not row-aligned.)"""
+    data = synthetic(150, 4).to(DEV)
+    order = np.random.default_rng(2).permutation(150).astype(np.int32)
+    res = []
+    for fuse in (True, False):
+        eng = LayerEngine(batch=32, model=model, device=DEV, gemm_dtype=dtype, graph_chunk=4, seed=9)
+        if fuse:
+            assert eng.fuse_ingest, "expected an ingest plan for the first conv"
+        eng.fuse_ingest = fuse
+        eng.attach(data)
+        eng.begin_epoch(order)
+        eng.run_steps(5)  # 4 full batches + a 22-sample tail
+        torch.cuda.synchronize()
+        st = eng.epoch_stats()
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.x.cpu(), eng.labels.cpu(), st.loss_sum, st.correct))
+    for a, b in zip(*res):
+        assert (a == b) if not isinstance(a, torch.Tensor) else torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,C,H,M,K,pad,dtype", [(8, 3, 32, 6, 5, 0, torch.float32), (8, 6, 14, 16, 5, 0, torch.float32),
                                                   (4, 32, 16, 64, 3, 1, torch.bfloat16), (3, 5, 11, 7, 3, 1, torch.float32)])
 @pytest.mark.parametrize("xgrad", [True, False])
