@@ -80,7 +80,7 @@ def _allreduce_kind(engine) -> str | None:
         return None
     kind = {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
     if kind == "xgmi":  # one launch: batch reduction + exchange + SGD in grad_reduce
-        kind = "xgmi-one-launch" if gs.group.one_launch else "xgmi-two-launch"
+        kind = ("xgmi-one-launch-" + ("push" if gs.group.push else "pull")) if gs.group.one_launch else "xgmi-two-launch"
     return kind
 
 

@@ -107,7 +107,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
-                          u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids) {
+                          u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -130,6 +130,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_scale = xp_scale;
       a.xp_gslot_off = dnn::xgmi_xp_off(xp_capacity);
       a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
+      if (xp_mode != 0 && xp_mode != 1) throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull) or 1 (push)");
+      a.xp_mode = xp_mode;
+      a.xp_rs_off = dnn::xgmi_rs_off(xp_capacity);
+      a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
     }
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
@@ -139,7 +143,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
-     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0);
+     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {

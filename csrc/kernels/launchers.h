@@ -35,6 +35,12 @@ struct ReduceArgs {
   long long xp_timeout_ticks = 0;      // s_memrealtime ticks (100 MHz)
   long long xp_gslot_off = 0, xp_gslot_bytes = 0;
   float xp_scale = 1.f;                // 1 / N
+  // xp_mode 0: pull one-shot (above).  xp_mode 1: push reduce-scatter + all-gather - block k's
+  // elements are owned by rank k % N; every other rank STORES its granules into the owner's
+  // rs inbox, the owner sums them in rank order and STORES {sum, step} into every peer's ag
+  // inbox; all waits poll local memory.  Per-link bytes drop from E to 2 E / N granules.
+  int xp_mode = 0;
+  long long xp_rs_off = 0, xp_ag_off = 0;
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

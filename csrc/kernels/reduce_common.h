@@ -54,7 +54,7 @@ struct DirectSink {
   }
 };
 struct XpSink {
-  unsigned long long* own;  // this rank's granule slot of the step
+  unsigned long long* own;  // where the granules go: this rank's slot (pull) / the owner's rs inbox (push)
   unsigned long long tag;   // step << 32
   int e[4] = {0, 0, 0, 0};
   float g[4] = {0.f, 0.f, 0.f, 0.f}, p[4], m[4];
@@ -62,7 +62,8 @@ struct XpSink {
   __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
     g_ *= a.grad_scale;
     e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
-    __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (own != nullptr)  // (push exchange: null on the owner of the block's elements)
+      __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 };
 

@@ -129,6 +129,117 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
   }
 }
 
+// The push form (xp_mode 1): reduce-scatter + all-gather with every wait on LOCAL memory.
+// Block k's elements belong to rank k % N.  A non-owner lane has already STORED its granules
+// into the owner's rs inbox [parity][its rank] (XpSink::put, one system-scope 64-bit store over
+// xGMI each); it now polls its own ag inbox for the owner's {sum, step}.  The owner lane polls
+// its rs inbox for the N - 1 peers' granules, sums the N values in RANK ORDER (the same fp32
+// additions as xp_exchange, so both forms give bit-identical parameters), stores {sum, step}
+// into every peer's ag inbox and applies SGD.  Per link and step this moves 2 E / N granules
+// instead of the one-shot's E, and nobody re-reads remote memory while waiting.
+// Slot reuse by parity is safe for the same reason as the pull form: a rank's step s + 2 store
+// into an inbox follows its own step s + 1, which needed the reader to be done with step s.
+template <int NR>
+__device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+  const int par = step & 1u;
+  const int owner = blockIdx.x % a.xp_nranks;
+  const long long t0 = wall_clock64();
+  float s[4];
+  if (owner == a.xp_rank) {
+    float v[NR][4];
+    unsigned pending = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[r][j] = sk.g[j];
+        if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
+      }
+    while (pending != 0u) {
+      unsigned long long x[NR][4];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(
+            a.xp_region[a.xp_rank] + a.xp_rs_off + (long long)(par * XG_MAX_RANKS + r) * a.xp_gslot_bytes);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src + sk.e[j]);
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if ((pending & (1u << (4 * r + j))) && (unsigned)(x[r][j] >> 32) == step) {
+            v[r][j] = __uint_as_float((unsigned)x[r][j]);
+            pending &= ~(1u << (4 * r + j));
+          }
+      if (pending == 0u || failed) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > a.xp_timeout_ticks ||
+          __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = v[0][j];
+#pragma unroll
+      for (int r = 1; r < NR; ++r)
+        if (r < a.xp_nranks) s[j] += v[r][j];
+    }
+    const unsigned long long tag = (unsigned long long)step << 32;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (r >= a.xp_nranks || r == a.xp_rank) continue;
+      unsigned long long* dst =
+          reinterpret_cast<unsigned long long*>(a.xp_region[r] + a.xp_ag_off + par * a.xp_gslot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (sk.v[j])
+          __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else {
+    const unsigned long long* src =
+        reinterpret_cast<const unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
+    unsigned pending = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = 0.f;
+      if (sk.v[j]) pending |= 1u << j;
+    }
+    while (pending != 0u) {
+      unsigned long long x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (pending & (1u << j)) x[j] = xp_ld(src + sk.e[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((pending & (1u << j)) && (unsigned)(x[j] >> 32) == step) {
+          s[j] = __uint_as_float((unsigned)x[j]);
+          pending &= ~(1u << j);
+        }
+      if (pending == 0u || failed) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > a.xp_timeout_ticks ||
+          __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!sk.v[j]) continue;
+    const float gr = s[j] * a.xp_scale;
+    float p, m;
+    sgd_update(gr, sk.p[j], sk.m[j], a.lr, a.momentum, p, m);
+    a.mom[sk.e[j]] = m;
+    a.master[sk.e[j]] = p;
+    write_shadow(a.shadow, sk.e[j], p);
+  }
+}
+
 // diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
 // end of the block's work (after its stores drained)
 __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
@@ -150,10 +261,20 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const unsigned step = a.xp_ctr[blockIdx.x] + 1u;
     const bool failed = *a.xp_err != 0u;
     XpSink sk;
-    sk.own = reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
-                                                   (step & 1u) * a.xp_gslot_bytes);
     sk.tag = (unsigned long long)step << 32;
-    if (grad_reduce_body(a, sk)) xp_exchange<NR>(a, sk, step, failed);
+    if (a.xp_mode == 0) {
+      sk.own = reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                     (step & 1u) * a.xp_gslot_bytes);
+      if (grad_reduce_body(a, sk)) xp_exchange<NR>(a, sk, step, failed);
+    } else {
+      const int owner = blockIdx.x % a.xp_nranks;
+      sk.own = owner == a.xp_rank
+                   ? nullptr
+                   : reinterpret_cast<unsigned long long*>(
+                         a.xp_region[owner] + a.xp_rs_off +
+                         (long long)((step & 1u) * XG_MAX_RANKS + a.xp_rank) * a.xp_gslot_bytes);
+      if (grad_reduce_body(a, sk)) xp_exchange_push<NR>(a, sk, step, failed);
+    }
     __syncthreads();  // every thread read this block's counter before it advances
     if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;
   } else {

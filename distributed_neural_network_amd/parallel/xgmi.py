@@ -77,6 +77,24 @@ def one_launch_wanted() -> bool:
     return v == "1"
 
 
+def push_wanted(grp: "XgmiGroup") -> bool:
+    """Collective: run the one-launch exchange in its push form (reduce-scatter + all-gather,
+    ``xp_mode`` 1 in csrc/kernels/reduce_sgd.hip)?  ``DNN_XGMI_EXCHANGE`` = auto | push | pull.
+
+    The pull one-shot moves every rank's whole gradient over every link (E granules per link
+    and step); the push form moves 2 E / N, at the price of a second one-way hop.  At N = 2 the
+    bytes are equal, so auto takes push from 4 ranks up.  Push polls the rank's OWN region for
+    stores that peers make over xGMI, so every region must be uncached memory (a cached
+    fallback region could serve a stale line); all ranks vote on that."""
+    choice = os.environ.get("DNN_XGMI_EXCHANGE", "auto")
+    if choice not in ("auto", "push", "pull"):
+        raise ValueError(f"DNN_XGMI_EXCHANGE must be auto, push or pull, not {choice!r}")
+    uncached = all(v == 1.0 for v in grp.comm.gather_scalars(1.0 if grp.kind == "uncached" else 0.0))
+    if choice == "pull" or not uncached:
+        return False
+    return choice == "push" or grp.world >= 4
+
+
 def wait_timeout(comm: Communicator) -> float:
     """Bound of one granule wait.  A live straggler (``--failure-duration`` sleeps before its
     epoch) must not be mistaken for a dead peer: the bound covers the longest injected
@@ -115,6 +133,7 @@ class XgmiGroup:
         # set once the exchange matched the two-launch path bit for bit on every rank
         # (HipEngine.selftest_exchange, run by the step-allreduce policy)
         self.one_launch = False
+        self.push = False  # one-launch exchange in its push form (push_wanted + self-test)
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
         # on a key that never comes
@@ -155,7 +174,7 @@ class XgmiGroup:
         err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
         return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
                     xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
-                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world)
+                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world, xp_mode=1 if self.push else 0)
 
     def clear_error(self) -> None:
         """Reset the sticky error word (only after every rank's kernels have drained)."""
@@ -312,4 +331,4 @@ class XgmiGradSync:
         return self.group.failed()
 
 
-__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "one_launch_wanted", "wanted"]
+__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "one_launch_wanted", "push_wanted", "wanted"]

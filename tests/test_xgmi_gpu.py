@@ -37,9 +37,11 @@ data = synthetic(1000, 5)
 a = init_arena(seed=9)
 res = []
 import os
-for sync_on, graphs, inl, one in [(False, True, False, "1"), (True, True, False, "1"), (True, False, False, "1"),
-                                  (True, True, True, "1"), (True, True, False, "0")]:
+for sync_on, graphs, inl, one, xch in [(False, True, False, "1", "auto"), (True, True, False, "1", "auto"),
+                                       (True, False, False, "1", "auto"), (True, True, True, "1", "auto"),
+                                       (True, True, False, "0", "auto"), (True, True, False, "1", "push")]:
     os.environ["DNN_XGMI_ONE_LAUNCH"] = one
+    os.environ["DNN_XGMI_EXCHANGE"] = xch
     eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, in_launch_reduce=inl)
     pol = make_policy("step-allreduce", comm)
     pol.attach(eng)
@@ -48,6 +50,7 @@ for sync_on, graphs, inl, one in [(False, True, False, "1"), (True, True, False,
     else:
         assert isinstance(eng.grad_sync, XgmiGradSync), type(eng.grad_sync)
         assert eng.grad_sync.group.one_launch == (one == "1"), "exchange self-test failed"
+        assert eng.grad_sync.group.push == (one == "1" and xch == "push"), "push self-test failed"
     eng.attach(data); eng.begin_epoch(np.arange(1000, dtype=np.int32)); eng.run_steps(16)
     torch.cuda.synchronize()
     if sync_on:
@@ -126,25 +129,26 @@ for ep in range(2):
     pol.epoch_end(eng, ep)
 kind = type(eng.grad_sync).__name__
 one = bool(getattr(getattr(eng.grad_sync, "group", None), "one_launch", False))
-torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one},
+push = bool(getattr(getattr(eng.grad_sync, "group", None), "push", False))
+torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "push": push},
            os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
 comm.close()
 '''
 
 
-def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1"):
-    out = tmp_path / f"{allreduce}{one_launch}"
+def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="auto"):
+    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
-               OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch)
+               OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch, DNN_XGMI_EXCHANGE=exchange)
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     import torch
-    return [torch.load(out / f"r{i}.pt", weights_only=True) for i in range(2)], r
+    return [torch.load(out / f"r{i}.pt", weights_only=True) for i in range(nproc)], r
 
 
 def test_xgmi_two_ranks_match_host_allreduce(tmp_path):
@@ -169,6 +173,22 @@ def test_xgmi_two_ranks_match_host_allreduce(tmp_path):
         float((xg[0]["master"] - host[0]["master"]).abs().max())
 
 
+def test_xgmi_push_exchange_four_ranks(tmp_path):
+    """4 ranks on the box's GPU: the push form of the one-launch exchange (reduce-scatter into
+    the owner's inbox, owner sums in rank order, all-gather into every peer's inbox; auto picks
+    it from 4 ranks up) passes its self-test and gives the pull form's parameters bit for bit,
+    identical on every rank."""
+    import torch
+
+    push, r = _two_ranks(tmp_path, "xgmi", "1", 29661, nproc=4, exchange="auto")
+    assert all(x["one_launch"] and x["push"] for x in push), r.stderr[-2000:]
+    pull, r2 = _two_ranks(tmp_path, "xgmi", "1", 29663, nproc=4, exchange="pull")
+    assert all(x["one_launch"] and not x["push"] for x in pull), r2.stderr[-2000:]
+    for i in range(4):
+        assert torch.equal(push[i]["master"], push[0]["master"])
+        assert torch.equal(push[i]["master"], pull[i]["master"])
+
+
 def test_bench_two_ranks_xgmi(tmp_path):
     """bench.py with 2 ranks sharing the GPU: graph-captured xGMI step all-reduce."""
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", OMP_NUM_THREADS="2")
@@ -178,4 +198,4 @@ def test_bench_two_ranks_xgmi(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
-    assert out["n_gpus"] == 2 and out["config"]["allreduce"] == "xgmi-one-launch", out
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] == "xgmi-one-launch-pull", out
