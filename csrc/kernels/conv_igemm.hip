@@ -1107,9 +1107,11 @@ void conv_wgrad_split(int B, int C, int H, int W, int M, int K, int pad, int* S,
   // cifar-vgg bf16 300.6 -> 296.3 us per step: profiles/r2/layer_fusion/wsplit/.)
   // (DNN_WGRAD_WGS / _MAX_SLICES / _MIN_CHUNKS override the three numbers: tuning runs)
   static const long wgs = env_long("DNN_WGRAD_WGS", 2048), max_s = env_long("DNN_WGRAD_MAX_SLICES", 512),
-                    min_c = env_long("DNN_WGRAD_MIN_CHUNKS", 2);
+                    min_c = env_long("DNN_WGRAD_MIN_CHUNKS", 2),
+                    max_kb = env_long("DNN_WGRAD_MAX_PART_KB", 1L << 30);  // partial bytes cap per layer
+  const long slice_kb = std::max(1L, (long)M * (Kd + 1) * 4 / 1024);
   long want = std::max(1L, wgs / std::max(1L, tiles));
-  want = std::min({want, max_s, std::max(1L, chunks / min_c)});
+  want = std::min({want, max_s, std::max(1L, chunks / min_c), std::max(1L, max_kb / slice_kb)});
   const long per = (chunks + want - 1) / want;
   *cps = (int)per;
   *S = (int)((chunks + per - 1) / per);
