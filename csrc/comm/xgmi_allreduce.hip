@@ -45,6 +45,10 @@ namespace dnn {
 constexpr int XG_THREADS = 256;
 constexpr int XG_PER_THREAD = XG_CHUNK / XG_THREADS;  // 4
 
+__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct XgmiArgs {
   unsigned char* region[XG_MAX_RANKS];  // every rank's shared region, mapped here (own included)
   int rank, nranks;
@@ -61,10 +65,135 @@ struct XgmiArgs {
   int max_blocks;
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  int push;                 // 1: push form (reduce-scatter + all-gather through the inboxes)
+  long long rs_off, ag_off; // inbox offsets in every region (xgmi_layout.h)
 };
 
-__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Push form (a.push): workgroup b's slice belongs to rank b % N.  Peers STORE their granules
+// into the owner's rs inbox [parity][source]; the owner polls its own inbox, sums in rank
+// order and STORES {sum, tag} into every peer's ag inbox, which they poll.  Same additions in
+// the same order as the pull form (bit-identical results), 2 n / N granules per link instead
+// of n, and no remote reads.  The inboxes are shared with grad_reduce's push exchange: this
+// kernel's tags carry bit 31 of the step word, so a granule of one path never matches a wait
+// of the other (each rank writes only its own source row of an inbox, and only after its
+// previous exchange completed, i.e. after every owner consumed that row).
+constexpr unsigned XG_PATH_BIT = 0x80000000u;
+template <int NR>
+__device__ __forceinline__ bool xg_poll(const unsigned long long* const* src, unsigned& pending, float (&v)[NR][XG_PER_THREAD],
+                                        const int (&e)[XG_PER_THREAD], unsigned want) {
+  unsigned long long x[NR][XG_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k)
+      if (pending & (1u << (4 * r + k))) x[r][k] = ld_sys64(src[r] + e[k]);
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k)
+      if ((pending & (1u << (4 * r + k))) && (unsigned)(x[r][k] >> 32) == want) {
+        v[r][k] = __uint_as_float((unsigned)x[r][k]);
+        pending &= ~(1u << (4 * r + k));
+      }
+  return pending == 0u;
+}
+
+template <int NR>
+__device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid, unsigned step, bool failed,
+                                               unsigned* err_w) {
+  const int par = step & 1u;
+  const int lo = b * XG_CHUNK;
+  const int owner = b % a.nranks;
+  const unsigned want = step | XG_PATH_BIT;
+  const unsigned long long tag = (unsigned long long)want << 32;
+  float v[NR][XG_PER_THREAD];
+  float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
+  int e[XG_PER_THREAD];
+  bool ok[XG_PER_THREAD];
+  unsigned long long* to_owner = reinterpret_cast<unsigned long long*>(
+      a.region[owner] + a.rs_off + (long long)(par * XG_MAX_RANKS + a.rank) * a.gslot_bytes);
+#pragma unroll
+  for (int k = 0; k < XG_PER_THREAD; ++k) {
+    ok[k] = lo + k * XG_THREADS + tid < a.n;
+    e[k] = min(lo + k * XG_THREADS + tid, a.n - 1);
+    const float g = a.grad[e[k]];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) v[r][k] = g;
+    if (a.mode != 0) {
+      p_old[k] = a.master[e[k]];
+      m_old[k] = a.mom[e[k]];
+    }
+    if (ok[k] && owner != a.rank)
+      __hip_atomic_store(to_owner + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // stores through a peer's mapping may be L2-cached here: publish them (system-scope release)
+  if (owner != a.rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // the owner waits for N - 1 inbox rows, everybody else for the one ag row
+  const unsigned long long* src[NR];
+  unsigned pending = 0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    if (owner == a.rank)
+      src[r] = reinterpret_cast<const unsigned long long*>(
+          a.region[a.rank] + a.rs_off + (long long)(par * XG_MAX_RANKS + r) * a.gslot_bytes);
+    else
+      src[r] = reinterpret_cast<const unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k) {
+      const bool need = owner == a.rank ? (r < a.nranks && r != a.rank) : r == 0;
+      if (need && ok[k]) pending |= 1u << (4 * r + k);
+    }
+  }
+  const long long t0 = wall_clock64();
+  while (pending != 0u) {
+    if (xg_poll<NR>(src, pending, v, e, want) || failed) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > a.timeout_ticks ||
+        __hip_atomic_load(a.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      __hip_atomic_store(err_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  float sum[XG_PER_THREAD];
+#pragma unroll
+  for (int k = 0; k < XG_PER_THREAD; ++k) {
+    if (owner == a.rank) {
+      sum[k] = v[0][k];
+#pragma unroll
+      for (int r = 1; r < NR; ++r)
+        if (r < a.nranks) sum[k] += v[r][k];
+    } else {
+      sum[k] = v[0][k];  // the owner's rank-order sum
+    }
+  }
+  if (owner == a.rank) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (r >= a.nranks || r == a.rank) continue;
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[r] + a.ag_off + par * a.gslot_bytes);
+#pragma unroll
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if (ok[k])
+          __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+#pragma unroll
+  for (int k = 0; k < XG_PER_THREAD; ++k) {
+    if (!ok[k]) continue;
+    const float gr = sum[k] * a.scale;
+    if (a.mode == 0) {
+      a.out[e[k]] = gr;
+    } else {
+      float p, m;
+      sgd_update(gr, p_old[k], m_old[k], a.lr, a.momentum, p, m);
+      a.mom[e[k]] = m;
+      a.master[e[k]] = p;
+      if (a.mode == 1) write_shadow(a.shadow, e[k], p);
+    }
+  }
+  __syncthreads();  // every thread read this workgroup's counter before it advances
+  if (tid == 0) a.ctr[b] = step;
 }
 
 // NR: group-size bucket (2, 4, 8 >= nranks; 1 for a 1-rank group) sizing the register arrays
@@ -86,6 +215,10 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   float v[NR][XG_PER_THREAD];
   float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
   int e[XG_PER_THREAD];
+  if (a.push) {
+    xgmi_push_body<NR>(a, b, tid, step, failed, err_w);
+    return;
+  }
   unsigned long long* mine = slot(a.rank);
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
@@ -242,7 +375,7 @@ void xgmi_free_abort_word(uintptr_t host_word) {
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, hipStream_t stream) {
+                           double timeout_s, hipStream_t stream, int push) {
   const int nranks = (int)regions.size();
   if (nranks < 1 || nranks > XG_MAX_RANKS) throw std::runtime_error("xgmi all-reduce: 1..8 ranks");
   if (rank < 0 || rank >= nranks) throw std::runtime_error("xgmi all-reduce: bad rank");
@@ -269,6 +402,9 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.max_blocks = xgmi_max_blocks(capacity);
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
+  a.push = push != 0 && nranks > 1;
+  a.rs_off = xgmi_rs_off(capacity);
+  a.ag_off = xgmi_ag_off(capacity);
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;
   auto* kern = nranks == 1 ? &xgmi_allreduce_kernel<1>
                            : (nranks <= 2 ? &xgmi_allreduce_kernel<2>

@@ -143,6 +143,11 @@ template <int NR>
 __device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
   const int par = step & 1u;
   const int owner = blockIdx.x % a.xp_nranks;
+  // The granules went through a PEER's mapping of its region, which (unlike the owner's own
+  // uncached mapping that the pull form writes) may be L2-cached here: a relaxed system-scope
+  // store can then sit in this GPU's L2 while the owner polls memory.  A system-scope release
+  // (L2 write-back) publishes them (profiles/r2/push: without it 4 ranks on one GPU stall).
+  if (owner != a.xp_rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   const long long t0 = wall_clock64();
   float s[4];
   if (owner == a.xp_rank) {
@@ -199,6 +204,7 @@ __device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSi
         if (sk.v[j])
           __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as above: the sums went through peer mappings)
   } else {
     const unsigned long long* src =
         reinterpret_cast<const unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);

@@ -78,28 +78,30 @@ def one_launch_wanted() -> bool:
 
 
 def push_wanted(grp: "XgmiGroup") -> bool:
-    """Collective: run the one-launch exchange in its push form (reduce-scatter + all-gather,
-    ``xp_mode`` 1 in csrc/kernels/reduce_sgd.hip)?  ``DNN_XGMI_EXCHANGE`` = auto | push | pull.
+    """Collective: run the exchange in its push form (reduce-scatter + all-gather, ``xp_mode``
+    1 in csrc/kernels/reduce_sgd.hip, ``push`` in xgmi_allreduce.hip)?
+    ``DNN_XGMI_EXCHANGE`` = pull (default) | push (experimental).
 
     The pull one-shot moves every rank's whole gradient over every link (E granules per link
-    and step); the push form moves 2 E / N, at the price of a second one-way hop.  At N = 2 the
-    bytes are equal, so auto takes push from 4 ranks up.  Push polls the rank's OWN region for
-    stores that peers make over xGMI, so every region must be uncached memory (a cached
-    fallback region could serve a stale line); all ranks vote on that."""
-    choice = os.environ.get("DNN_XGMI_EXCHANGE", "auto")
-    if choice not in ("auto", "push", "pull"):
-        raise ValueError(f"DNN_XGMI_EXCHANGE must be auto, push or pull, not {choice!r}")
+    and step); the push form moves 2 E / N, at the price of a second one-way hop.  It is NOT
+    the default: with 4 ranks sharing one GPU (the only multi-rank setup measured here) its
+    waits stall for seconds every few epochs even after a system-scope release on the writer
+    side, and then fail on the timeout (profiles/r2/push/), while the pull form never did.  On
+    distinct GPUs it is unmeasured.  Push polls the rank's OWN region for stores that peers
+    make, so every region must be uncached memory; all ranks vote on that."""
+    choice = os.environ.get("DNN_XGMI_EXCHANGE", "pull")
+    if choice not in ("push", "pull"):
+        raise ValueError(f"DNN_XGMI_EXCHANGE must be pull or push, not {choice!r}")
     uncached = all(v == 1.0 for v in grp.comm.gather_scalars(1.0 if grp.kind == "uncached" else 0.0))
-    if choice == "pull" or not uncached:
-        return False
-    return choice == "push" or grp.world >= 4
+    return choice == "push" and uncached
 
 
 def wait_timeout(comm: Communicator) -> float:
     """Bound of one granule wait.  A live straggler (``--failure-duration`` sleeps before its
     epoch) must not be mistaken for a dead peer: the bound covers the longest injected
     sleep twice over, plus the base minute."""
-    return 60.0 + 2.0 * float(getattr(comm, "straggler_s", 0.0) or 0.0)
+    base = float(os.environ.get("DNN_XGMI_TIMEOUT_S", "60"))
+    return base + 2.0 * float(getattr(comm, "straggler_s", 0.0) or 0.0)
 
 
 class XgmiGroup:
@@ -134,6 +136,7 @@ class XgmiGroup:
         # (HipEngine.selftest_exchange, run by the step-allreduce policy)
         self.one_launch = False
         self.push = False  # one-launch exchange in its push form (push_wanted + self-test)
+        self.ar_push = False  # the all-reduce kernel in its push form (build_group: push_wanted + self-test)
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
         # on a key that never comes
@@ -189,7 +192,7 @@ class XgmiGroup:
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, n, grad.data_ptr(), grad.data_ptr(),
                                 master.data_ptr(), mom.data_ptr(), shadow.data_ptr() if shadow is not None else 0,
                                 lr, momentum, 1.0 / self.world, mode, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s)
+                                self.timeout_s, s, int(self.ar_push))
 
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place average of a flat fp32 tensor."""
@@ -197,7 +200,7 @@ class XgmiGroup:
         s = torch.cuda.current_stream(t.device).cuda_stream
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, t.numel(), t.data_ptr(), t.data_ptr(),
                                 0, 0, 0, 0.0, 0.0, 1.0 / self.world, 0, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s)
+                                self.timeout_s, s, int(self.ar_push))
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
@@ -298,6 +301,17 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
               f"regions={[hex(r) for r in grp.regions] if grp is not None and ok else None} "
               f"kind={getattr(grp, 'kind', None)} devices={getattr(grp, 'devices', None)}", file=sys.stderr, flush=True)
     if all(v == 1.0 for v in votes):
+        # the push form of the all-reduce kernel where it is wanted, kept only if its own
+        # exact self-test passes on every rank
+        if push_wanted(grp) and os.environ.get("DNN_XGMI_AR_PUSH", "1") == "1":
+            grp.ar_push = True
+            try:
+                ok = grp.selftest()
+            except Exception:
+                ok = False
+            grp.ar_push = all(v == 1.0 for v in comm.gather_scalars(1.0 if ok else 0.0))
+            if not grp.ar_push and comm.rank == 0:
+                print("[xgmi] push all-reduce self-test failed: pull form", file=sys.stderr, flush=True)
         return grp
     if grp is not None:
         grp.close()
