@@ -80,7 +80,8 @@ def _allreduce_kind(engine) -> str | None:
         return None
     kind = {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
     if kind == "xgmi":  # one launch: batch reduction + exchange + SGD in grad_reduce
-        kind = ("xgmi-one-launch-" + ("push" if gs.group.push else "pull")) if gs.group.one_launch else "xgmi-two-launch"
+        form = {0: "pull", 1: "push", 2: "rsag"}[gs.group.xp_mode]
+        kind = f"xgmi-one-launch-{form}" if gs.group.one_launch else "xgmi-two-launch"
     return kind
 
 

@@ -130,7 +130,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_scale = xp_scale;
       a.xp_gslot_off = dnn::xgmi_xp_off(xp_capacity);
       a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
-      if (xp_mode != 0 && xp_mode != 1) throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull) or 1 (push)");
+      if (xp_mode < 0 || xp_mode > 2)
+        throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull), 1 (push) or 2 (two-hop pull)");
       a.xp_mode = xp_mode;
       a.xp_rs_off = dnn::xgmi_rs_off(xp_capacity);
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);

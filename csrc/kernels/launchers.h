@@ -39,6 +39,9 @@ struct ReduceArgs {
   // elements are owned by rank k % N; every other rank STORES its granules into the owner's
   // rs inbox, the owner sums them in rank order and STORES {sum, step} into every peer's ag
   // inbox; all waits poll local memory.  Per-link bytes drop from E to 2 E / N granules.
+  // xp_mode 2: the same reduce-scatter + all-gather with the pull form's access pattern (every
+  // rank writes only its own region: the owner reads the peers' pull slots and publishes the
+  // sum in its own ag slot, which the others read).
   int xp_mode = 0;
   long long xp_rs_off = 0, xp_ag_off = 0;
 };

@@ -139,15 +139,20 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
 // instead of the one-shot's E, and nobody re-reads remote memory while waiting.
 // Slot reuse by parity is safe for the same reason as the pull form: a rank's step s + 2 store
 // into an inbox follows its own step s + 1, which needed the reader to be done with step s.
-template <int NR>
-__device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+//
+// The two-hop pull form (xp_mode 2, PUSH = false) has the same ownership and sums but keeps the
+// pull form's access pattern - every rank writes only its OWN (uncached) region and reads its
+// peers': the owner reads its elements' granules from the peers' pull slots, stores {sum, step}
+// into its own ag slot, and the other ranks read that slot.  Also 2 E / N granules per link.
+template <int NR, bool PUSH>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
   const int par = step & 1u;
   const int owner = blockIdx.x % a.xp_nranks;
   // The granules went through a PEER's mapping of its region, which (unlike the owner's own
   // uncached mapping that the pull form writes) may be L2-cached here: a relaxed system-scope
   // store can then sit in this GPU's L2 while the owner polls memory.  A system-scope release
   // (L2 write-back) publishes them (profiles/r2/push: without it 4 ranks on one GPU stall).
-  if (owner != a.xp_rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (PUSH && owner != a.xp_rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   const long long t0 = wall_clock64();
   float s[4];
   if (owner == a.xp_rank) {
@@ -165,7 +170,8 @@ __device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSi
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(
-            a.xp_region[a.xp_rank] + a.xp_rs_off + (long long)(par * XG_MAX_RANKS + r) * a.xp_gslot_bytes);
+            PUSH ? a.xp_region[a.xp_rank] + a.xp_rs_off + (long long)(par * XG_MAX_RANKS + r) * a.xp_gslot_bytes
+                 : a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src + sk.e[j]);
@@ -194,20 +200,29 @@ __device__ __forceinline__ void xp_exchange_push(const ReduceArgs& a, const XpSi
         if (r < a.xp_nranks) s[j] += v[r][j];
     }
     const unsigned long long tag = (unsigned long long)step << 32;
+    if constexpr (PUSH) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (r >= a.xp_nranks || r == a.xp_rank) continue;
+      for (int r = 0; r < NR; ++r) {
+        if (r >= a.xp_nranks || r == a.xp_rank) continue;
+        unsigned long long* dst =
+            reinterpret_cast<unsigned long long*>(a.xp_region[r] + a.xp_ag_off + par * a.xp_gslot_bytes);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (sk.v[j])
+            __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as above: the sums went through peer mappings)
+    } else {
       unsigned long long* dst =
-          reinterpret_cast<unsigned long long*>(a.xp_region[r] + a.xp_ag_off + par * a.xp_gslot_bytes);
+          reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (sk.v[j])
           __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as above: the sums went through peer mappings)
   } else {
-    const unsigned long long* src =
-        reinterpret_cast<const unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(
+        a.xp_region[PUSH ? a.xp_rank : owner] + a.xp_ag_off + par * a.xp_gslot_bytes);
     unsigned pending = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -272,14 +287,20 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       sk.own = reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
                                                      (step & 1u) * a.xp_gslot_bytes);
       if (grad_reduce_body(a, sk)) xp_exchange<NR>(a, sk, step, failed);
-    } else {
+    } else if (a.xp_mode == 1) {
       const int owner = blockIdx.x % a.xp_nranks;
       sk.own = owner == a.xp_rank
                    ? nullptr
                    : reinterpret_cast<unsigned long long*>(
                          a.xp_region[owner] + a.xp_rs_off +
                          (long long)((step & 1u) * XG_MAX_RANKS + a.xp_rank) * a.xp_gslot_bytes);
-      if (grad_reduce_body(a, sk)) xp_exchange_push<NR>(a, sk, step, failed);
+      if (grad_reduce_body(a, sk)) xp_exchange_rsag<NR, true>(a, sk, step, failed);
+    } else {  // two-hop pull: granules into this rank's own pull slot (nobody reads the owner's)
+      const int owner = blockIdx.x % a.xp_nranks;
+      sk.own = owner == a.xp_rank ? nullptr
+                                  : reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                                          (step & 1u) * a.xp_gslot_bytes);
+      if (grad_reduce_body(a, sk)) xp_exchange_rsag<NR, false>(a, sk, step, failed);
     }
     __syncthreads();  // every thread read this block's counter before it advances
     if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;

@@ -129,22 +129,23 @@ class StepAllReduce(SyncPolicy):
             engine.grad_sync = None
         elif (xg := self._xgmi_group(engine)) is not None:
             # GPU hot path on one node: one-shot xGMI all-reduce fused with the optimizer
-            from .xgmi import XgmiGradSync, one_launch_wanted, push_wanted
+            from .xgmi import XgmiGradSync, exchange_mode, one_launch_wanted
 
             engine.grad_sync = XgmiGradSync(xg)
-            xg.one_launch = xg.push = False
+            xg.one_launch, xg.xp_mode = False, 0
             if one_launch_wanted() and hasattr(engine, "selftest_exchange"):
                 # batch reduction + all-reduce + SGD in ONE launch, once it has matched the
                 # two-launch path bit for bit on every rank (all ranks get the same vote);
-                # the push form first where it is wanted, the pull form if push fails
-                xg.push = push_wanted(xg)
+                # a requested push / rsag form first, the pull form if that fails
+                xg.xp_mode = exchange_mode(xg)
                 xg.one_launch = engine.selftest_exchange(xg, self.comm)
-                if xg.push and not xg.one_launch:
+                if xg.xp_mode != 0 and not xg.one_launch:
                     if self.comm.rank == 0:
                         import sys
 
-                        print("[xgmi] push exchange self-test failed: pull form", file=sys.stderr, flush=True)
-                    xg.push = False
+                        print(f"[xgmi] exchange form {xg.xp_mode} failed its self-test: pull form", file=sys.stderr,
+                              flush=True)
+                    xg.xp_mode = 0
                     xg.one_launch = engine.selftest_exchange(xg, self.comm)
                 if not xg.one_launch and self.comm.rank == 0:
                     import sys

@@ -89,11 +89,34 @@ def push_wanted(grp: "XgmiGroup") -> bool:
     side, and then fail on the timeout (profiles/r2/push/), while the pull form never did.  On
     distinct GPUs it is unmeasured.  Push polls the rank's OWN region for stores that peers
     make, so every region must be uncached memory; all ranks vote on that."""
-    choice = os.environ.get("DNN_XGMI_EXCHANGE", "pull")
-    if choice not in ("push", "pull"):
-        raise ValueError(f"DNN_XGMI_EXCHANGE must be pull or push, not {choice!r}")
+    return exchange_mode(grp) == 1
+
+
+EXCHANGE_MODES = {"pull": 0, "push": 1, "rsag": 2}
+
+
+def exchange_mode(grp: "XgmiGroup") -> int:
+    """Collective: ``xp_mode`` of the one-launch exchange from ``DNN_XGMI_EXCHANGE``:
+    pull (0: one hop, E granules per link), push (1, experimental, see ``push_wanted``),
+    rsag (2: two-hop pull - reduce-scatter + all-gather where every rank writes only its own
+    region, 2 E / N granules per link, one more dependent remote read) or auto (default).
+
+    auto = rsag when every rank has its own GPU and N >= 4, else pull.  Per link and step the
+    pull form moves the whole 496 KB granule slot (>= 6.5 us at ~77 GB/s per link direction);
+    rsag moves 2 / N of it and pays one more remote round trip, so it wins once the saved bytes
+    outweigh that trip (equal bytes at N = 2).  rsag uses exactly the pull form's memory
+    operations (own-region stores, remote loads).  With several ranks time-sharing ONE GPU
+    its two-level wait (the owner's sum needs every peer's block to have run first) stalls for
+    seconds when the GPU time-slices the processes (profiles/r2/push/), so auto keeps pull
+    there; on distinct GPUs nothing is time-sliced."""
+    choice = os.environ.get("DNN_XGMI_EXCHANGE", "auto")
+    if choice != "auto" and choice not in EXCHANGE_MODES:
+        raise ValueError(f"DNN_XGMI_EXCHANGE must be auto or one of {sorted(EXCHANGE_MODES)}, not {choice!r}")
     uncached = all(v == 1.0 for v in grp.comm.gather_scalars(1.0 if grp.kind == "uncached" else 0.0))
-    return choice == "push" and uncached
+    if choice == "auto":
+        return 2 if grp.devices == grp.world and grp.world >= 4 else 0
+    mode = EXCHANGE_MODES[choice]
+    return 0 if mode == 1 and not uncached else mode
 
 
 def wait_timeout(comm: Communicator) -> float:
@@ -135,7 +158,7 @@ class XgmiGroup:
         # set once the exchange matched the two-launch path bit for bit on every rank
         # (HipEngine.selftest_exchange, run by the step-allreduce policy)
         self.one_launch = False
-        self.push = False  # one-launch exchange in its push form (push_wanted + self-test)
+        self.xp_mode = 0  # one-launch exchange form (exchange_mode + self-test): 0 pull, 1 push, 2 rsag
         self.ar_push = False  # the all-reduce kernel in its push form (build_group: push_wanted + self-test)
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
@@ -168,6 +191,10 @@ class XgmiGroup:
         # step sees the value, so the hand-off needs no flag and no fence on any topology.
         self.devices = len(set(device_ids)) if device_ids else 1
 
+    @property
+    def push(self) -> bool:
+        return self.xp_mode == 1
+
     # -- launches --------------------------------------------------------------------------
     def exchange(self) -> dict:
         """grad_reduce kwargs of the one-launch all-reduce: every reduction lane publishes its
@@ -177,7 +204,7 @@ class XgmiGroup:
         err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
         return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
                     xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
-                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world, xp_mode=1 if self.push else 0)
+                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world, xp_mode=self.xp_mode)
 
     def clear_error(self) -> None:
         """Reset the sticky error word (only after every rank's kernels have drained)."""
@@ -345,4 +372,4 @@ class XgmiGradSync:
         return self.group.failed()
 
 
-__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "one_launch_wanted", "push_wanted", "wanted"]
+__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "exchange_mode", "one_launch_wanted", "push_wanted", "wanted"]

@@ -39,7 +39,8 @@ res = []
 import os
 for sync_on, graphs, inl, one, xch in [(False, True, False, "1", "pull"), (True, True, False, "1", "pull"),
                                        (True, False, False, "1", "pull"), (True, True, True, "1", "pull"),
-                                       (True, True, False, "0", "pull"), (True, True, False, "1", "push")]:
+                                       (True, True, False, "0", "pull"), (True, True, False, "1", "push"),
+                                       (True, True, False, "1", "rsag")]:
     os.environ["DNN_XGMI_ONE_LAUNCH"] = one
     os.environ["DNN_XGMI_EXCHANGE"] = xch
     eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, in_launch_reduce=inl)
@@ -136,13 +137,15 @@ kind = type(eng.grad_sync).__name__
 one = bool(getattr(getattr(eng.grad_sync, "group", None), "one_launch", False))
 push = bool(getattr(getattr(eng.grad_sync, "group", None), "push", False))
 ar_push = bool(getattr(getattr(eng.grad_sync, "group", None), "ar_push", False))
-torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "push": push, "ar_push": ar_push},
+xp_mode = int(getattr(getattr(eng.grad_sync, "group", None), "xp_mode", -1))
+torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "push": push, "ar_push": ar_push,
+            "xp_mode": xp_mode},
            os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
 comm.close()
 '''
 
 
-def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="pull", engine="fused"):
+def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="auto", engine="fused"):
     out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
@@ -177,6 +180,22 @@ def test_xgmi_two_ranks_match_host_allreduce(tmp_path):
     # same math up to fma contraction: sgd_apply rounds grad * grad_scale separately
     assert torch.allclose(xg[0]["master"], host[0]["master"], rtol=0, atol=1e-6), \
         float((xg[0]["master"] - host[0]["master"]).abs().max())
+
+
+def test_xgmi_rsag_exchange_two_ranks(tmp_path):
+    """2 ranks on the box's GPU: the two-hop pull exchange (owner reads its elements from the
+    peers' pull slots, publishes the rank-order sum in its own region, the others read it; the
+    default from 4 ranks on distinct GPUs) passes its self-test and gives the one-hop pull
+    form's parameters bit for bit, identical on both ranks."""
+    import torch
+
+    rs, r = _two_ranks(tmp_path, "xgmi", "1", 29671, exchange="rsag")
+    assert all(x["one_launch"] and x["xp_mode"] == 2 for x in rs), r.stderr[-2000:]
+    pull, r2 = _two_ranks(tmp_path, "xgmi", "1", 29673, exchange="pull")
+    assert all(x["one_launch"] and x["xp_mode"] == 0 for x in pull), r2.stderr[-2000:]
+    for i in range(2):
+        assert torch.equal(rs[i]["master"], rs[0]["master"])
+        assert torch.equal(rs[i]["master"], pull[i]["master"])
 
 
 _PUSH = pytest.mark.skipif(os.environ.get("DNN_TEST_PUSH") != "1",
