@@ -36,7 +36,7 @@ void xgmi_free_abort_word(uintptr_t host_word);
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, hipStream_t stream, int push);
+                           double timeout_s, hipStream_t stream, int form);
 // runtime/graph_exec.cpp
 void graph_upload(uintptr_t exec, uintptr_t stream);
 }  // namespace dnn
@@ -398,13 +398,13 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
-                             double timeout_s, u stream, int push) {
+                             double timeout_s, u stream, int form) {
     dnn::launch_xgmi_allreduce(regions, rank, capacity, n, P<const float>(grad), P<float>(out), P<float>(master),
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
-                               P<const unsigned>(abort_w), timeout_s, S(stream), push);
+                               P<const unsigned>(abort_w), timeout_s, S(stream), form);
   }, py::arg("regions"), py::arg("rank"), py::arg("capacity"), py::arg("n"), py::arg("grad"), py::arg("out"),
      py::arg("master"), py::arg("mom"), py::arg("shadow"), py::arg("lr"), py::arg("momentum"), py::arg("scale"),
-     py::arg("mode"), py::arg("ctr"), py::arg("abort_w"), py::arg("timeout_s"), py::arg("stream"), py::arg("push") = 0);
+     py::arg("mode"), py::arg("ctr"), py::arg("abort_w"), py::arg("timeout_s"), py::arg("stream"), py::arg("form") = 0);
   m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream, u images, u labels,
                           u next_ids, u stage) {
     dnn::launch_epoch_begin(P<const int32_t>(staged), P<int32_t>(order), n, P<int32_t>(state), P<int32_t>(batch_ids),

@@ -65,7 +65,7 @@ struct XgmiArgs {
   int max_blocks;
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  int push;                 // 1: push form (reduce-scatter + all-gather through the inboxes)
+  int form;                 // 0 one-hop pull, 1 push, 2 two-hop pull (reduce-scatter + all-gather)
   long long rs_off, ag_off; // inbox offsets in every region (xgmi_layout.h)
 };
 
@@ -98,8 +98,13 @@ __device__ __forceinline__ bool xg_poll(const unsigned long long* const* src, un
   return pending == 0u;
 }
 
-template <int NR>
-__device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid, unsigned step, bool failed,
+// The two-hop pull form (a.form 2, PUSH = false): the same ownership and sums with the pull
+// form's memory operations - every rank stores only into its OWN region (its pull slot, and as
+// owner its ag slot) and reads the peers'.  Its ag slot is shared with grad_reduce's: tags carry
+// the path bit, and an owner overwrites its ag slot only after every peer contributed to the
+// new exchange, i.e. finished reading the previous one.
+template <int NR, bool PUSH>
+__device__ __forceinline__ void xgmi_rsag_body(const XgmiArgs& a, int b, int tid, unsigned step, bool failed,
                                                unsigned* err_w) {
   const int par = step & 1u;
   const int lo = b * XG_CHUNK;
@@ -111,7 +116,8 @@ __device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid
   int e[XG_PER_THREAD];
   bool ok[XG_PER_THREAD];
   unsigned long long* to_owner = reinterpret_cast<unsigned long long*>(
-      a.region[owner] + a.rs_off + (long long)(par * XG_MAX_RANKS + a.rank) * a.gslot_bytes);
+      PUSH ? a.region[owner] + a.rs_off + (long long)(par * XG_MAX_RANKS + a.rank) * a.gslot_bytes
+           : a.region[a.rank] + par * a.gslot_bytes);  // (two-hop: this rank's own pull slot)
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
     ok[k] = lo + k * XG_THREADS + tid < a.n;
@@ -127,17 +133,20 @@ __device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid
       __hip_atomic_store(to_owner + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // stores through a peer's mapping may be L2-cached here: publish them (system-scope release)
-  if (owner != a.rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  // the owner waits for N - 1 inbox rows, everybody else for the one ag row
+  if (PUSH && owner != a.rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // the owner waits for N - 1 inbox rows (two-hop: the peers' pull slots), everybody else for
+  // the one ag row (two-hop: the owner's)
   const unsigned long long* src[NR];
   unsigned pending = 0;
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     if (owner == a.rank)
       src[r] = reinterpret_cast<const unsigned long long*>(
-          a.region[a.rank] + a.rs_off + (long long)(par * XG_MAX_RANKS + r) * a.gslot_bytes);
+          PUSH ? a.region[a.rank] + a.rs_off + (long long)(par * XG_MAX_RANKS + r) * a.gslot_bytes
+               : a.region[r] + par * a.gslot_bytes);
     else
-      src[r] = reinterpret_cast<const unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
+      src[r] = reinterpret_cast<const unsigned long long*>(a.region[PUSH ? a.rank : owner] + a.ag_off +
+                                                           par * a.gslot_bytes);
 #pragma unroll
     for (int k = 0; k < XG_PER_THREAD; ++k) {
       const bool need = owner == a.rank ? (r < a.nranks && r != a.rank) : r == 0;
@@ -166,7 +175,7 @@ __device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid
       sum[k] = v[0][k];  // the owner's rank-order sum
     }
   }
-  if (owner == a.rank) {
+  if (owner == a.rank && PUSH) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       if (r >= a.nranks || r == a.rank) continue;
@@ -177,6 +186,12 @@ __device__ __forceinline__ void xgmi_push_body(const XgmiArgs& a, int b, int tid
           __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  } else if (owner == a.rank) {  // two-hop: publish in this rank's own ag slot
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k)
+      if (ok[k])
+        __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
@@ -215,8 +230,12 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   float v[NR][XG_PER_THREAD];
   float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
   int e[XG_PER_THREAD];
-  if (a.push) {
-    xgmi_push_body<NR>(a, b, tid, step, failed, err_w);
+  if (a.form == 1) {
+    xgmi_rsag_body<NR, true>(a, b, tid, step, failed, err_w);
+    return;
+  }
+  if (a.form == 2) {
+    xgmi_rsag_body<NR, false>(a, b, tid, step, failed, err_w);
     return;
   }
   unsigned long long* mine = slot(a.rank);
@@ -375,7 +394,7 @@ void xgmi_free_abort_word(uintptr_t host_word) {
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, hipStream_t stream, int push) {
+                           double timeout_s, hipStream_t stream, int form) {
   const int nranks = (int)regions.size();
   if (nranks < 1 || nranks > XG_MAX_RANKS) throw std::runtime_error("xgmi all-reduce: 1..8 ranks");
   if (rank < 0 || rank >= nranks) throw std::runtime_error("xgmi all-reduce: bad rank");
@@ -402,7 +421,8 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.max_blocks = xgmi_max_blocks(capacity);
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
-  a.push = push != 0 && nranks > 1;
+  if (form < 0 || form > 2) throw std::runtime_error("xgmi all-reduce: form 0 (pull), 1 (push) or 2 (two-hop pull)");
+  a.form = nranks > 1 ? form : 0;
   a.rs_off = xgmi_rs_off(capacity);
   a.ag_off = xgmi_ag_off(capacity);
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;

@@ -159,7 +159,7 @@ class XgmiGroup:
         # (HipEngine.selftest_exchange, run by the step-allreduce policy)
         self.one_launch = False
         self.xp_mode = 0  # one-launch exchange form (exchange_mode + self-test): 0 pull, 1 push, 2 rsag
-        self.ar_push = False  # the all-reduce kernel in its push form (build_group: push_wanted + self-test)
+        self.ar_mode = 0  # form of the all-reduce kernel (build_group: exchange_mode + self-test)
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
         # on a key that never comes
@@ -195,6 +195,10 @@ class XgmiGroup:
     def push(self) -> bool:
         return self.xp_mode == 1
 
+    @property
+    def ar_push(self) -> bool:
+        return self.ar_mode == 1
+
     # -- launches --------------------------------------------------------------------------
     def exchange(self) -> dict:
         """grad_reduce kwargs of the one-launch all-reduce: every reduction lane publishes its
@@ -219,7 +223,7 @@ class XgmiGroup:
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, n, grad.data_ptr(), grad.data_ptr(),
                                 master.data_ptr(), mom.data_ptr(), shadow.data_ptr() if shadow is not None else 0,
                                 lr, momentum, 1.0 / self.world, mode, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s, int(self.ar_push))
+                                self.timeout_s, s, self.ar_mode)
 
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place average of a flat fp32 tensor."""
@@ -227,7 +231,7 @@ class XgmiGroup:
         s = torch.cuda.current_stream(t.device).cuda_stream
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, t.numel(), t.data_ptr(), t.data_ptr(),
                                 0, 0, 0, 0.0, 0.0, 1.0 / self.world, 0, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s, int(self.ar_push))
+                                self.timeout_s, s, self.ar_mode)
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
@@ -328,17 +332,19 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
               f"regions={[hex(r) for r in grp.regions] if grp is not None and ok else None} "
               f"kind={getattr(grp, 'kind', None)} devices={getattr(grp, 'devices', None)}", file=sys.stderr, flush=True)
     if all(v == 1.0 for v in votes):
-        # the push form of the all-reduce kernel where it is wanted, kept only if its own
+        # the all-reduce kernel's two-hop / push form where it is wanted, kept only if its own
         # exact self-test passes on every rank
-        if push_wanted(grp) and os.environ.get("DNN_XGMI_AR_PUSH", "1") == "1":
-            grp.ar_push = True
+        mode = exchange_mode(grp)
+        if mode != 0 and os.environ.get("DNN_XGMI_AR_PUSH", "1") == "1":
+            grp.ar_mode = mode
             try:
                 ok = grp.selftest()
             except Exception:
                 ok = False
-            grp.ar_push = all(v == 1.0 for v in comm.gather_scalars(1.0 if ok else 0.0))
-            if not grp.ar_push and comm.rank == 0:
-                print("[xgmi] push all-reduce self-test failed: pull form", file=sys.stderr, flush=True)
+            if not all(v == 1.0 for v in comm.gather_scalars(1.0 if ok else 0.0)):
+                grp.ar_mode = 0
+                if comm.rank == 0:
+                    print(f"[xgmi] all-reduce form {mode} failed its self-test: pull form", file=sys.stderr, flush=True)
         return grp
     if grp is not None:
         grp.close()

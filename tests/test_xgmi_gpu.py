@@ -138,8 +138,9 @@ one = bool(getattr(getattr(eng.grad_sync, "group", None), "one_launch", False))
 push = bool(getattr(getattr(eng.grad_sync, "group", None), "push", False))
 ar_push = bool(getattr(getattr(eng.grad_sync, "group", None), "ar_push", False))
 xp_mode = int(getattr(getattr(eng.grad_sync, "group", None), "xp_mode", -1))
+ar_mode = int(getattr(getattr(eng.grad_sync, "group", None), "ar_mode", -1))
 torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "push": push, "ar_push": ar_push,
-            "xp_mode": xp_mode},
+            "xp_mode": xp_mode, "ar_mode": ar_mode},
            os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
 comm.close()
 '''
@@ -190,9 +191,27 @@ def test_xgmi_rsag_exchange_two_ranks(tmp_path):
     import torch
 
     rs, r = _two_ranks(tmp_path, "xgmi", "1", 29671, exchange="rsag")
-    assert all(x["one_launch"] and x["xp_mode"] == 2 for x in rs), r.stderr[-2000:]
+    assert all(x["one_launch"] and x["xp_mode"] == 2 and x["ar_mode"] == 2 for x in rs), r.stderr[-2000:]
     pull, r2 = _two_ranks(tmp_path, "xgmi", "1", 29673, exchange="pull")
-    assert all(x["one_launch"] and x["xp_mode"] == 0 for x in pull), r2.stderr[-2000:]
+    assert all(x["one_launch"] and x["xp_mode"] == 0 and x["ar_mode"] == 0 for x in pull), r2.stderr[-2000:]
+    # the two-launch path with the all-reduce kernel in its two-hop form
+    two, r3 = _two_ranks(tmp_path, "xgmi", "1", 29675, one_launch="0", exchange="rsag")
+    assert all(not x["one_launch"] and x["ar_mode"] == 2 for x in two), r3.stderr[-2000:]
+    for i in range(2):
+        assert torch.equal(rs[i]["master"], rs[0]["master"])
+        assert torch.equal(rs[i]["master"], pull[i]["master"])
+        assert torch.equal(two[i]["master"], pull[i]["master"])
+
+
+def test_xgmi_rsag_allreduce_layer_engine_two_ranks(tmp_path):
+    """2 ranks of the layer engine (lenet-bn, fp32): the all-reduce kernel's two-hop form keeps
+    the replicas identical and equals its one-hop pull form bit for bit."""
+    import torch
+
+    rs, r = _two_ranks(tmp_path, "xgmi", "1", 29677, exchange="rsag", engine="layers")
+    assert all(x["kind"] == "XgmiGradSync" and x["ar_mode"] == 2 for x in rs), r.stderr[-2000:]
+    pull, r2 = _two_ranks(tmp_path, "xgmi", "1", 29679, exchange="pull", engine="layers")
+    assert all(x["ar_mode"] == 0 for x in pull), r2.stderr[-2000:]
     for i in range(2):
         assert torch.equal(rs[i]["master"], rs[0]["master"])
         assert torch.equal(rs[i]["master"], pull[i]["master"])

@@ -23,6 +23,6 @@ for ep in range(int(os.environ.get("EPOCHS", "4"))):
     eng.begin_epoch(samp.order(ep))
     eng.run_steps(samp.steps(64))
     eng.synchronize()
-    print(f"rank {comm.rank} ep {ep} mode={g.xp_mode} ar_push={g.ar_push} one={g.one_launch} "
+    print(f"rank {comm.rank} ep {ep} mode={g.xp_mode} ar_mode={g.ar_mode} one={g.one_launch} "
           f"{time.time() - t:.3f}s failed={g.failed()} ctr0={int(g.xp_ctr[0])}", file=sys.stderr, flush=True)
 comm.close()
