@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import os
+import threading
 import time
 from typing import Callable, Optional, Sequence
 
@@ -88,6 +89,14 @@ class Communicator:
     def _init_group(self) -> None:
         assert self.store is not None
         prefix = dist.PrefixStore(f"dnn/g{self.generation}", self.store)
+        # The default group's store keys carry torch's group counter, which only
+        # destroy_process_group resets - and only when it completes.  After a recovery whose
+        # teardown raised part-way, survivors could name the new group differently and wait
+        # for each other's gloo rendezvous keys until the group timeout: every generation
+        # starts from the same name.
+        dc = dist.distributed_c10d
+        if not dist.is_initialized() and hasattr(dc, "_world"):
+            dc._world.group_count = 0
         kwargs = {}
         if self.backend == "nccl":
             kwargs["device_id"] = self.device
@@ -259,6 +268,7 @@ class Communicator:
             self.aborted = True
             return
         self.aborted = True
+        pg = None
         try:
             pg = dist.distributed_c10d._get_default_group()
             if self.backend == "nccl":
@@ -273,6 +283,17 @@ class Communicator:
                 pg.abort()
         except Exception:
             pass
+        if self.backend != "nccl" and pg is not None:
+            # the aborted gloo group's destructor joins its work threads, and one of them can
+            # sit in a collective on the dead peer until the group timeout: it must not run on
+            # this thread (it did, when this frame released ``pg``: an intermittent hang of the
+            # rank-drop test).  Unregister it, then let a daemon thread drop the last reference.
+            box = [pg]
+            del pg
+            if _forget_default_group():
+                threading.Thread(target=box.clear, daemon=True, name="dnn-pg-reaper").start()
+                return
+            pg = box.pop()
         try:
             dist.destroy_process_group()
         except Exception:
@@ -294,6 +315,33 @@ class Communicator:
                 dist.destroy_process_group()
             except Exception:
                 pass
+
+
+def _forget_default_group() -> bool:
+    """Drop torch's registry of the (aborted) default gloo group without ``shutdown()``.
+
+    ``destroy_process_group`` shuts the group down, and a gloo shutdown waits for the work
+    threads - one of them can sit in a collective on the dead peer until the group timeout
+    (300 s), long after the other survivors wait in the next generation's rendezvous (seen
+    as an intermittent hang of the rank-drop test under load).  The aborted group's threads
+    end on their own; this clears what destroy_process_group clears, counter included.
+    Returns False (caller falls back to destroy_process_group) if torch's internals differ."""
+    dc = dist.distributed_c10d
+    w = getattr(dc, "_world", None)
+    need = ("pg_map", "pg_names", "pg_group_ranks", "pg_backend_config", "pg_to_tag", "tags_to_pg",
+            "pg_coalesce_state")
+    if w is None or not hasattr(dc, "_update_default_pg") or not all(hasattr(w, n) for n in need):
+        return False
+    try:
+        dc._update_default_pg(None)
+        for n in need:
+            getattr(w, n).clear()
+        if hasattr(dc, "_unregister_all_process_groups"):
+            dc._unregister_all_process_groups()
+        w.group_count = 0
+    except Exception:
+        return False
+    return not dist.is_initialized()
 
 
 class _Done:
