@@ -291,7 +291,9 @@ class Communicator:
             box = [pg]
             del pg
             if _forget_default_group():
-                threading.Thread(target=box.clear, daemon=True, name="dnn-pg-reaper").start()
+                t = threading.Thread(target=box.clear, daemon=True, name="dnn-pg-reaper")
+                t.start()
+                _REAPERS.append(t)
                 return
             pg = box.pop()
         try:
@@ -315,6 +317,24 @@ class Communicator:
                 dist.destroy_process_group()
             except Exception:
                 pass
+
+
+_REAPERS: list[threading.Thread] = []
+
+
+def exit_now_if_reaping(code: int = 0) -> None:
+    """End the process at once when an aborted gloo group is still being torn down.
+
+    A reaper thread (``Communicator.abort``) can still be inside the aborted group's
+    destructor, waiting for a work thread stuck on the dead peer; a normal interpreter exit
+    would then terminate in C++ teardown (SIGABRT) or wait out the group timeout.  The
+    entrypoints call this after a finished run: output is flushed, nothing else runs."""
+    if any(t.is_alive() for t in _REAPERS):
+        import sys
+
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(code)
 
 
 def _forget_default_group() -> bool:

@@ -12,7 +12,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from distributed_neural_network_amd.parallel.comm import exit_now_if_reaping  # noqa: E402
 from distributed_neural_network_amd.train import main  # noqa: E402
 
 if __name__ == "__main__":
     main("single")
+    exit_now_if_reaping()  # a recovered run may still be tearing an aborted group down
