@@ -101,20 +101,22 @@ def exchange_mode(grp: "XgmiGroup") -> int:
     rsag (2: two-hop pull - reduce-scatter + all-gather where every rank writes only its own
     region, 2 E / N granules per link, one more dependent remote read) or auto (default).
 
-    auto = rsag when every rank has its own GPU and N >= 4, else pull.  Per link and step the
+    auto = pull.  (rsag when every rank has its own GPU and N >= 4 is the byte model's choice,
+    kept opt-in until a real multi-GPU node has measured it - see below.)  Per link and step the
     pull form moves the whole 496 KB granule slot (>= 6.5 us at ~77 GB/s per link direction);
     rsag moves 2 / N of it and pays one more remote round trip, so it wins once the saved bytes
     outweigh that trip (equal bytes at N = 2).  rsag uses exactly the pull form's memory
     operations (own-region stores, remote loads).  With several ranks time-sharing ONE GPU
     its two-level wait (the owner's sum needs every peer's block to have run first) stalls for
-    seconds when the GPU time-slices the processes (profiles/r2/push/), so auto keeps pull
-    there; on distinct GPUs nothing is time-sliced."""
+    seconds when the GPU time-slices the processes (profiles/r2/push/).  On distinct GPUs
+    nothing is time-sliced, but that is unmeasured, and the pull form has no failure seen in
+    any setup: the default stays pull for the multi-GPU scaling run."""
     choice = os.environ.get("DNN_XGMI_EXCHANGE", "auto")
     if choice != "auto" and choice not in EXCHANGE_MODES:
         raise ValueError(f"DNN_XGMI_EXCHANGE must be auto or one of {sorted(EXCHANGE_MODES)}, not {choice!r}")
     uncached = all(v == 1.0 for v in grp.comm.gather_scalars(1.0 if grp.kind == "uncached" else 0.0))
     if choice == "auto":
-        return 2 if grp.devices == grp.world and grp.world >= 4 else 0
+        return 0
     mode = EXCHANGE_MODES[choice]
     return 0 if mode == 1 and not uncached else mode
 

@@ -1,8 +1,8 @@
 """CPU tests of the xGMI exchange-form choice (parallel/xgmi.py ``exchange_mode``).
 
 The kernels themselves are covered by tests/test_xgmi_gpu.py; this pins the policy: the
-two-hop pull form only when every rank has its own GPU and N >= 4, the experimental push form
-only on request and only over uncached regions, and every rank voting on the region kind."""
+one-hop pull form by default, the two-hop and push forms only on request (push only over
+uncached regions), and every rank voting on the region kind."""
 import types
 
 import pytest
@@ -21,7 +21,7 @@ def _grp(world, devices, kinds):
     return types.SimpleNamespace(comm=comm, world=world, devices=devices, kind=kinds[0]), calls
 
 
-@pytest.mark.parametrize("world,devices,want", [(1, 1, 0), (2, 2, 0), (4, 4, 2), (8, 8, 2), (4, 1, 0), (8, 1, 0)])
+@pytest.mark.parametrize("world,devices,want", [(1, 1, 0), (2, 2, 0), (4, 4, 0), (8, 8, 0), (4, 1, 0), (8, 1, 0)])
 def test_auto_mode(monkeypatch, world, devices, want):
     monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
     g, calls = _grp(world, devices, ["uncached"] * world)
