@@ -8,11 +8,16 @@ with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--sync step-allreduce|epoch-avg]
 
-Synchronisation defaults to a per-step gradient all-reduce inside the step hipGraph: on
-one node a one-hop exchange over the xGMI mesh inside the batch-reduction kernel, fused with
-the SGD update (every reduction block reads the same block of all peers' gradients;
-parallel/xgmi.py, kernels/reduce_sgd.hip), or native
-RCCL (DNN_ALLREDUCE=rccl, multi-node, or if the xGMI self-test fails).  --sync epoch-avg runs the reference algorithm
+Synchronisation defaults to a per-step gradient all-reduce inside the step hipGraph.  At N > 1
+the bench first MEASURES its transport (--allreduce ab, parallel/autotune.py): in the untimed
+set-up it times a few hundred real steps of every candidate - the one-launch xGMI exchange in
+its one-hop (xgmi-pull) and two-hop (xgmi-rsag) forms inside the batch-reduction kernel, native
+ncclAllReduce of one fused bucket (rccl) and of two buckets with the MLP bucket on a side stream
+(rccl-overlap) - plus the no-all-reduce step as the baseline, takes the max over ranks, and all
+ranks adopt the fastest path that passed its self-test.  The JSON line reports every
+candidate's us/step (allreduce_ab), the chosen path and the per-step exchange wait measured
+inside the kernel (s_memrealtime around the granule wait; median / p99 over the timed steps,
+max over ranks).  --sync epoch-avg runs the reference algorithm
 (data_parallelism_train.py:185-254): local SGD over the rank's shard with a fresh momentum
 buffer per epoch and an RCCL parameter all-reduce at every epoch end (epoch boundaries fall
 inside the timed window: 50,000 / N samples per rank and epoch).
@@ -36,53 +41,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
+from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
+from distributed_neural_network_amd.parallel.autotune import ORDER, allreduce_ab  # noqa: E402
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
+from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
 BASELINE_IMG_S = 1261.0  # BASELINE.md headline: bs64, "4 procs", training-phase whole-node img/s
 METRIC = "images/sec (whole node) + epoch time, CIFAR-10 CNN bs=64 at 1/2/4/8 MI355X"
-
-
-class EpochCursor:
-    """Feeds K steps to the engine, starting a new shuffled epoch whenever one ends."""
-
-    def __init__(self, engine, sampler, policy, batch):
-        self.engine, self.sampler, self.policy, self.batch = engine, sampler, policy, batch
-        self.epoch = -1
-        self.left = 0
-        self.steps_per_epoch = sampler.steps(batch)
-
-    def _next_epoch(self):
-        if self.epoch >= 0:
-            self.policy.epoch_end(self.engine, self.epoch)
-        self.epoch += 1
-        self.policy.epoch_start(self.engine, self.epoch)
-        self.engine.begin_epoch(self.sampler.order(self.epoch))
-        self.left = self.steps_per_epoch
-
-    def run(self, k):
-        while k > 0:
-            if self.left == 0:
-                self._next_epoch()
-            n = min(k, self.left)
-            self.engine.run_steps(n)
-            self.left -= n
-            k -= n
-
-
-def _allreduce_kind(engine) -> str | None:
-    """Which per-step gradient all-reduce ran: xgmi-one-launch (the batch-reduction kernel
-    exchanges its blocks over xGMI and applies SGD), xgmi-two-launch (reduction, then the
-    one-shot IPC all-reduce kernel fused with SGD), rccl (native ncclAllReduce), torch-pg
-    (host process group), or None (one rank)."""
-    gs = getattr(engine, "grad_sync", None)
-    if gs is None:
-        return None
-    kind = {"XgmiGradSync": "xgmi", "NativeGradAllReduce": "rccl"}.get(type(gs).__name__, "torch-pg")
-    if kind == "xgmi":  # one launch: batch reduction + exchange + SGD in grad_reduce
-        form = {0: "pull", 1: "push", 2: "rsag"}[gs.group.xp_mode]
-        kind = f"xgmi-one-launch-{form}" if gs.group.one_launch else "xgmi-two-launch"
-    return kind
 
 
 def _reserve_stdout() -> int:
@@ -110,9 +76,13 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
-    ap.add_argument("--in-launch-reduce", action="store_true",
-                    help="experimental: batch reduction + SGD in reducer workgroups inside the fused launch "
-                         "(counter hand-off) instead of a second kernel")
+    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + ("default",),
+                    help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
+                         "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
+    ap.add_argument("--ab-steps", type=int, default=300, help="timed steps per candidate and round of the A/B")
+    ap.add_argument("--noise", type=int, default=SYNTH_NOISE_HARD,
+                    help="synthetic data noise amplitude (255: the hard split of tools/convergence.py, so the "
+                         "epoch's val_acc / val_loss carry signal; 96: the easy template set)")
     ap.add_argument("--model", default="lenet", help="lenet (headline) | lenet-bn | cifar-vgg (layer engine)")
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "layers"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -137,12 +107,12 @@ def main():
     comm = Communicator(env, device)
     B = args.batch_size
 
-    train, test = synthetic(args.train_samples, args.seed, True), synthetic(10_000, args.seed, False)
+    train = synthetic(args.train_samples, args.seed, True, noise=args.noise)
+    test = synthetic(10_000, args.seed, False, noise=args.noise)
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
     if args.model == "lenet" and args.engine in ("auto", "fused") and args.dtype == "bf16":
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                           overlap=args.overlap, in_launch_reduce=args.in_launch_reduce,
-                           use_graphs=not args.no_graphs)
+                           overlap=args.overlap, use_graphs=not args.no_graphs)
     else:  # modular layer engine (other models / fp32)
         engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
                              dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16), use_graphs=not args.no_graphs)
@@ -150,9 +120,19 @@ def main():
     test_dev = test.to(device)
     policy = make_policy(args.sync, comm)
     policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
+    policy.record_waits = True  # per-step exchange wait stamps (one store per wave and step)
+    if args.allreduce in ORDER:
+        policy.path = args.allreduce
     policy.attach(engine)
     policy.initial_broadcast(engine)
     cur = EpochCursor(engine, sampler, policy, B)
+    ab = {}
+    if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
+        cur._next_epoch()
+        ab = allreduce_ab(policy, engine, cur.run, steps=args.ab_steps)
+        if comm.rank == 0:
+            print(f"[bench] all-reduce A/B (us/step, max over ranks): {ab}", file=sys.stderr, flush=True)
+        cur.left = 0  # the timed run starts on a fresh epoch
 
     # untimed set-up: capture every chunk graph, first-call costs of the eval path (kernel,
     # D2H, host ops), then the W warmup steps LAST, so the timed window starts on a busy,
@@ -170,6 +150,9 @@ def main():
         comm.allreduce_(wl2, "sum")
         eval_metrics(wl + wl2, wc.float() + wc2, B)
     cur.run(args.warmup)
+    xg = getattr(engine.grad_sync, "group", None)
+    if xg is not None:
+        xg.reset_wait_stats()
     comm.barrier()
     torch.cuda.synchronize(device)
 
@@ -188,10 +171,18 @@ def main():
     if diag:
         print(f"[bench] reported window: {1e6 * dt / args.steps:.2f} us/step wall, "
               f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
-    if getattr(engine, "sync_error", lambda: False)():
-        raise RuntimeError("in-launch reducer hand-off timed out (sync error flag set)")
     if hasattr(engine.grad_sync, "check"):
         engine.grad_sync.check()  # raises if any xGMI wait in the timed window timed out
+    # per-step exchange wait inside the kernel over the timed steps (xGMI paths): this rank's
+    # median / p99 / max, then the max over ranks
+    waits = xg.wait_stats() if xg is not None else None
+    if comm.distributed and args.sync == "step-allreduce":
+        have = comm.gather_scalars(1.0 if waits else 0.0)
+        if all(v == 1.0 for v in have):
+            waits = {k: comm.reduce_scalar(float(waits[k]), "max") for k in ("median", "p99", "max")}
+            waits = {k: round(v, 3) for k, v in waits.items()}
+        else:
+            waits = None
     for _ in range(args.diag_windows):  # diagnostic only: the reported window is the first one
         comm.barrier()
         torch.cuda.synchronize(device)
@@ -246,7 +237,8 @@ def main():
         out = {"metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": comm.world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 6),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
-               "dtype": args.dtype, "data": "synthetic (CIFAR-10-shaped 3x32x32 uint8, 50k train / 10k test), "
+               "dtype": args.dtype, "data": f"synthetic (CIFAR-10-shaped 3x32x32 uint8, template + noise "
+                                        f"{args.noise}, {args.train_samples // 1000}k train / 10k test), "
                                         "random-init weights",
                "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)"
                           if args.model == "lenet" else args.model,
@@ -254,9 +246,14 @@ def main():
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
-                          "reduce": "in-launch" if args.in_launch_reduce else "separate-kernel",
-                          "allreduce": _allreduce_kind(engine)},
+                          "allreduce": policy.installed(engine) if hasattr(policy, "installed") else None},
                **epoch}
+        if ab:
+            out["allreduce_ab"] = ab["allreduce_ab"]
+            out["allreduce_failed"] = ab["failed"]
+            out["local_step_us"] = ab["local_us_per_step"]  # same steps with no all-reduce (A/B baseline)
+        if comm.distributed and args.sync == "step-allreduce":
+            out["exchange_wait_us"] = waits
         os.write(out_fd, (json.dumps(out) + "\n").encode())
     comm.close()
 

@@ -36,9 +36,7 @@ void xgmi_free_abort_word(uintptr_t host_word);
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, hipStream_t stream, int form);
-// runtime/graph_exec.cpp
-void graph_upload(uintptr_t exec, uintptr_t stream);
+                           double timeout_s, hipStream_t stream, int form, unsigned long long* wait);
 }  // namespace dnn
 
 namespace py = pybind11;
@@ -69,34 +67,13 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
-                                  P<long long>(stamps), nullptr, nullptr, P<const int32_t>(next_ids),
-                                  P<unsigned char>(stage), S(stream));
+                                  P<long long>(stamps), P<const int32_t>(next_ids), P<unsigned char>(stage),
+                                  S(stream));
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0);
-  // fused training step WITH the in-launch reducer workgroups (batch reduction + SGD)
-  m.def("fused_train_reduce",
-        [](u images, u labels, u batch_ids, int batch, u state, u master, u shadow, u a0, u h1, u h2, u z1, u z2,
-           u z3, u slab, u loss, u correct, u grad, u mom, u stats, u order, int order_len, float lr,
-           float momentum, int fuse_sgd, u sync, u stream, u stamps) {
-          dnn::ReduceArgs r{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
-                            P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
-                            P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
-                            P<bf16>(shadow), P<int32_t>(state), P<double>(stats), P<const int32_t>(order),
-                            order_len, P<int32_t>(batch_ids), lr, momentum, 1.0f, fuse_sgd, 0, dnn::ARENA, 1};
-          dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(batch_ids),
-                                  order_len, batch, P<int32_t>(state), P<const float>(master),
-                                  P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
-                                  P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
-                                  P<long long>(stamps), &r, P<unsigned>(sync), nullptr, nullptr, S(stream));
-        },
-        py::arg("images"), py::arg("labels"), py::arg("batch_ids"), py::arg("batch"), py::arg("state"),
-        py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"),
-        py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("grad"),
-        py::arg("mom"), py::arg("stats"), py::arg("order"), py::arg("order_len"), py::arg("lr"),
-        py::arg("momentum"), py::arg("fuse_sgd"), py::arg("sync"), py::arg("stream"), py::arg("stamps") = 0);
   m.def("fused_eval", [](u images, u labels, u order, int n, int base, int count, u master, u shadow, u loss,
                          u correct, u stream) {
     dnn::launch_fused_eval(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), n, base,
@@ -107,7 +84,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           u grad, u mom, u shadow, u state, u stats, float lr, float momentum, float grad_scale,
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
-                          u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode) {
+                          u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode,
+                          u xp_wait) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -130,11 +108,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_scale = xp_scale;
       a.xp_gslot_off = dnn::xgmi_xp_off(xp_capacity);
       a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
-      if (xp_mode < 0 || xp_mode > 2)
-        throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull), 1 (push) or 2 (two-hop pull)");
+      if (xp_mode != 0 && xp_mode != 2)
+        throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull) or 2 (two-hop pull)");
       a.xp_mode = xp_mode;
-      a.xp_rs_off = dnn::xgmi_rs_off(xp_capacity);
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
+      a.xp_wait = P<unsigned long long>(xp_wait);
     }
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
@@ -144,7 +122,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
-     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0);
+     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0, py::arg("xp_wait") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {
@@ -386,7 +364,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_open", [](py::bytes h) { return dnn::xgmi_open(std::string(h)); });
   m.def("xgmi_close", &dnn::xgmi_close);
   m.def("xgmi_device_id", &dnn::xgmi_device_id);
-  m.def("graph_upload", &dnn::graph_upload, py::arg("exec"), py::arg("stream"));
   m.def("xgmi_free", &dnn::xgmi_free);
   m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
   m.def("xgmi_set_abort", &dnn::xgmi_set_abort);
@@ -395,16 +372,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_region_bytes", &dnn::xgmi_region_bytes);
   m.def("xgmi_gslot_bytes", &dnn::xgmi_gslot_bytes);
   m.def("xgmi_xp_max_blocks", []() { return dnn::XP_MAX_BLOCKS; });
+  m.def("xgmi_wait_ring", []() { return py::make_tuple(dnn::XP_WAIT_RING, dnn::XP_MAX_BLOCKS, 4); });
   m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
-                             double timeout_s, u stream, int form) {
+                             double timeout_s, u stream, int form, u wait) {
     dnn::launch_xgmi_allreduce(regions, rank, capacity, n, P<const float>(grad), P<float>(out), P<float>(master),
                                P<float>(mom), P<bf16>(shadow), lr, momentum, scale, mode, P<unsigned>(ctr),
-                               P<const unsigned>(abort_w), timeout_s, S(stream), form);
+                               P<const unsigned>(abort_w), timeout_s, S(stream), form,
+                               P<unsigned long long>(wait));
   }, py::arg("regions"), py::arg("rank"), py::arg("capacity"), py::arg("n"), py::arg("grad"), py::arg("out"),
      py::arg("master"), py::arg("mom"), py::arg("shadow"), py::arg("lr"), py::arg("momentum"), py::arg("scale"),
-     py::arg("mode"), py::arg("ctr"), py::arg("abort_w"), py::arg("timeout_s"), py::arg("stream"), py::arg("form") = 0);
+     py::arg("mode"), py::arg("ctr"), py::arg("abort_w"), py::arg("timeout_s"), py::arg("stream"), py::arg("form") = 0,
+     py::arg("wait") = 0);
   m.def("epoch_begin", [](u staged, u order, int n, u state, u batch_ids, int batch, u stream, u images, u labels,
                           u next_ids, u stage) {
     dnn::launch_epoch_begin(P<const int32_t>(staged), P<int32_t>(order), n, P<int32_t>(state), P<int32_t>(batch_ids),

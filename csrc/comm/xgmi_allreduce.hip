@@ -65,97 +65,39 @@ struct XgmiArgs {
   int max_blocks;
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  int form;                 // 0 one-hop pull, 1 push, 2 two-hop pull (reduce-scatter + all-gather)
-  long long rs_off, ag_off; // inbox offsets in every region (xgmi_layout.h)
+  int form;                 // 0 one-hop pull, 2 two-hop pull (reduce-scatter + all-gather)
+  long long ag_off;         // all-gather slot offset in every region (xgmi_layout.h)
+  unsigned long long* wait; // optional: per-step wait ring, as ReduceArgs::xp_wait
 };
 
-// Push form (a.push): workgroup b's slice belongs to rank b % N.  Peers STORE their granules
-// into the owner's rs inbox [parity][source]; the owner polls its own inbox, sums in rank
-// order and STORES {sum, tag} into every peer's ag inbox, which they poll.  Same additions in
-// the same order as the pull form (bit-identical results), 2 n / N granules per link instead
-// of n, and no remote reads.  The inboxes are shared with grad_reduce's push exchange: this
-// kernel's tags carry bit 31 of the step word, so a granule of one path never matches a wait
-// of the other (each rank writes only its own source row of an inbox, and only after its
-// previous exchange completed, i.e. after every owner consumed that row).
+// The two-hop form shares its ag slot with grad_reduce's: this kernel's tags carry bit 31 of
+// the step word, so a granule of one path never matches a wait of the other, and an owner
+// overwrites its ag slot only after every peer contributed to the new exchange, i.e. finished
+// reading the previous one.
 constexpr unsigned XG_PATH_BIT = 0x80000000u;
-template <int NR>
-__device__ __forceinline__ bool xg_poll(const unsigned long long* const* src, unsigned& pending, float (&v)[NR][XG_PER_THREAD],
-                                        const int (&e)[XG_PER_THREAD], unsigned want) {
-  unsigned long long x[NR][XG_PER_THREAD];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k)
-      if (pending & (1u << (4 * r + k))) x[r][k] = ld_sys64(src[r] + e[k]);
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k)
-      if ((pending & (1u << (4 * r + k))) && (unsigned)(x[r][k] >> 32) == want) {
-        v[r][k] = __uint_as_float((unsigned)x[r][k]);
-        pending &= ~(1u << (4 * r + k));
-      }
-  return pending == 0u;
-}
 
-// The two-hop pull form (a.form 2, PUSH = false): the same ownership and sums with the pull
-// form's memory operations - every rank stores only into its OWN region (its pull slot, and as
-// owner its ag slot) and reads the peers'.  Its ag slot is shared with grad_reduce's: tags carry
-// the path bit, and an owner overwrites its ag slot only after every peer contributed to the
-// new exchange, i.e. finished reading the previous one.
-template <int NR, bool PUSH>
-__device__ __forceinline__ void xgmi_rsag_body(const XgmiArgs& a, int b, int tid, unsigned step, bool failed,
-                                               unsigned* err_w) {
-  const int par = step & 1u;
-  const int lo = b * XG_CHUNK;
-  const int owner = b % a.nranks;
-  const unsigned want = step | XG_PATH_BIT;
-  const unsigned long long tag = (unsigned long long)want << 32;
-  float v[NR][XG_PER_THREAD];
-  float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
-  int e[XG_PER_THREAD];
-  bool ok[XG_PER_THREAD];
-  unsigned long long* to_owner = reinterpret_cast<unsigned long long*>(
-      PUSH ? a.region[owner] + a.rs_off + (long long)(par * XG_MAX_RANKS + a.rank) * a.gslot_bytes
-           : a.region[a.rank] + par * a.gslot_bytes);  // (two-hop: this rank's own pull slot)
-#pragma unroll
-  for (int k = 0; k < XG_PER_THREAD; ++k) {
-    ok[k] = lo + k * XG_THREADS + tid < a.n;
-    e[k] = min(lo + k * XG_THREADS + tid, a.n - 1);
-    const float g = a.grad[e[k]];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) v[r][k] = g;
-    if (a.mode != 0) {
-      p_old[k] = a.master[e[k]];
-      m_old[k] = a.mom[e[k]];
-    }
-    if (ok[k] && owner != a.rank)
-      __hip_atomic_store(to_owner + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // stores through a peer's mapping may be L2-cached here: publish them (system-scope release)
-  if (PUSH && owner != a.rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  // the owner waits for N - 1 inbox rows (two-hop: the peers' pull slots), everybody else for
-  // the one ag row (two-hop: the owner's)
-  const unsigned long long* src[NR];
-  unsigned pending = 0;
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    if (owner == a.rank)
-      src[r] = reinterpret_cast<const unsigned long long*>(
-          PUSH ? a.region[a.rank] + a.rs_off + (long long)(par * XG_MAX_RANKS + r) * a.gslot_bytes
-               : a.region[r] + par * a.gslot_bytes);
-    else
-      src[r] = reinterpret_cast<const unsigned long long*>(a.region[PUSH ? a.rank : owner] + a.ag_off +
-                                                           par * a.gslot_bytes);
-#pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k) {
-      const bool need = owner == a.rank ? (r < a.nranks && r != a.rank) : r == 0;
-      if (need && ok[k]) pending |= 1u << (4 * r + k);
-    }
-  }
+template <int NR>
+__device__ __forceinline__ long long xg_wait(const XgmiArgs& a, const unsigned long long* const (&src)[NR],
+                                             unsigned pending, float (&v)[NR][XG_PER_THREAD],
+                                             const int (&e)[XG_PER_THREAD], unsigned want, bool failed,
+                                             unsigned* err_w) {
   const long long t0 = wall_clock64();
   while (pending != 0u) {
-    if (xg_poll<NR>(src, pending, v, e, want) || failed) break;
+    unsigned long long x[NR][XG_PER_THREAD];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if (pending & (1u << (4 * r + k))) x[r][k] = ld_sys64(src[r] + e[k]);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if ((pending & (1u << (4 * r + k))) && (unsigned)(x[r][k] >> 32) == want) {
+          v[r][k] = __uint_as_float((unsigned)x[r][k]);
+          pending &= ~(1u << (4 * r + k));
+        }
+    if (pending == 0u || failed) break;
     __builtin_amdgcn_s_sleep(1);
     if (wall_clock64() - t0 > a.timeout_ticks ||
         __hip_atomic_load(a.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
@@ -163,52 +105,18 @@ __device__ __forceinline__ void xgmi_rsag_body(const XgmiArgs& a, int b, int tid
       break;
     }
   }
-  float sum[XG_PER_THREAD];
+  return wall_clock64() - t0;
+}
+
+// per-wave max wait of this step into the ring (see ReduceArgs::xp_wait)
+__device__ __forceinline__ void xg_record_wait(const XgmiArgs& a, unsigned step, long long ticks) {
+  if (a.wait == nullptr) return;
+  unsigned t = (unsigned)min(ticks, 0xffffffffll);
 #pragma unroll
-  for (int k = 0; k < XG_PER_THREAD; ++k) {
-    if (owner == a.rank) {
-      sum[k] = v[0][k];
-#pragma unroll
-      for (int r = 1; r < NR; ++r)
-        if (r < a.nranks) sum[k] += v[r][k];
-    } else {
-      sum[k] = v[0][k];  // the owner's rank-order sum
-    }
-  }
-  if (owner == a.rank && PUSH) {
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (r >= a.nranks || r == a.rank) continue;
-      unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[r] + a.ag_off + par * a.gslot_bytes);
-#pragma unroll
-      for (int k = 0; k < XG_PER_THREAD; ++k)
-        if (ok[k])
-          __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  } else if (owner == a.rank) {  // two-hop: publish in this rank's own ag slot
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
-#pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k)
-      if (ok[k])
-        __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-#pragma unroll
-  for (int k = 0; k < XG_PER_THREAD; ++k) {
-    if (!ok[k]) continue;
-    const float gr = sum[k] * a.scale;
-    if (a.mode == 0) {
-      a.out[e[k]] = gr;
-    } else {
-      float p, m;
-      sgd_update(gr, p_old[k], m_old[k], a.lr, a.momentum, p, m);
-      a.mom[e[k]] = m;
-      a.master[e[k]] = p;
-      if (a.mode == 1) write_shadow(a.shadow, e[k], p);
-    }
-  }
-  __syncthreads();  // every thread read this workgroup's counter before it advances
-  if (tid == 0) a.ctr[b] = step;
+  for (int off = 32; off > 0; off >>= 1) t = max(t, (unsigned)__shfl_xor((int)t, off));
+  if ((threadIdx.x & 63) == 0)
+    a.wait[((size_t)(step % XP_WAIT_RING) * XP_MAX_BLOCKS + blockIdx.x) * (XG_THREADS / 64) + (threadIdx.x >> 6)] =
+        ((unsigned long long)step << 32) | t;
 }
 
 // NR: group-size bucket (2, 4, 8 >= nranks; 1 for a 1-rank group) sizing the register arrays
@@ -220,27 +128,23 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   const bool failed = a.ctr[a.max_blocks] != 0u;
   const int par = step & 1u;
   const int lo = b * XG_CHUNK;
-  const unsigned long long tag = (unsigned long long)step << 32;
-  auto slot = [&](int r) {
-    return reinterpret_cast<unsigned long long*>(a.region[r] + par * a.gslot_bytes);
-  };
+  const bool two_hop = a.form == 2;
+  const int owner = two_hop ? b % a.nranks : a.rank;
+  // two-hop tags carry the path bit (its ag slot is shared with grad_reduce's)
+  const unsigned want = two_hop ? (step | XG_PATH_BIT) : step;
+  const unsigned long long tag = (unsigned long long)want << 32;
 
-  // 1. publish this slice as granules (the optimizer state is local and only this thread
-  //    touches it: prefetch it now, so the update after the gather costs no extra latency)
+  // 1. publish this slice as granules into this rank's own pull slot (two-hop: non-owners
+  //    only); the optimizer state is local and only this thread touches it: prefetch it now,
+  //    so the update after the gather costs no extra latency
   float v[NR][XG_PER_THREAD];
   float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
   int e[XG_PER_THREAD];
-  if (a.form == 1) {
-    xgmi_rsag_body<NR, true>(a, b, tid, step, failed, err_w);
-    return;
-  }
-  if (a.form == 2) {
-    xgmi_rsag_body<NR, false>(a, b, tid, step, failed, err_w);
-    return;
-  }
-  unsigned long long* mine = slot(a.rank);
+  bool ok[XG_PER_THREAD];
+  unsigned long long* mine = reinterpret_cast<unsigned long long*>(a.region[a.rank] + par * a.gslot_bytes);
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
+    ok[k] = lo + k * XG_THREADS + tid < a.n;
     e[k] = min(lo + k * XG_THREADS + tid, a.n - 1);
     const float g = a.grad[e[k]];
 #pragma unroll
@@ -249,53 +153,49 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
       p_old[k] = a.master[e[k]];
       m_old[k] = a.mom[e[k]];
     }
-    if (lo + k * XG_THREADS + tid < a.n)
+    if (ok[k] && (!two_hop || owner != a.rank))
       __hip_atomic_store(mine + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 
-  // 2. gather every peer's granules of these elements until their tags show this step
+  // 2. gather: the one-hop form (and the two-hop owner) reads every peer's pull slot, a two-hop
+  //    non-owner the owner's ag slot; all loads of a round in flight before the first check
+  const unsigned long long* src[NR];
   unsigned pending = 0;  // bit 4 r + k
+  const bool gather_all = !two_hop || owner == a.rank;
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
+  for (int r = 0; r < NR; ++r) {
+    src[r] = reinterpret_cast<const unsigned long long*>(
+        gather_all ? a.region[r] + par * a.gslot_bytes : a.region[owner] + a.ag_off + par * a.gslot_bytes);
 #pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k)
-      if (r < a.nranks && r != a.rank && lo + k * XG_THREADS + tid < a.n) pending |= 1u << (4 * r + k);
-  const long long t0 = wall_clock64();
-  while (pending != 0u) {
-    unsigned long long x[NR][XG_PER_THREAD];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const unsigned long long* src = slot(r);
-#pragma unroll
-      for (int k = 0; k < XG_PER_THREAD; ++k)
-        if (pending & (1u << (4 * r + k))) x[r][k] = ld_sys64(src + e[k]);
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int k = 0; k < XG_PER_THREAD; ++k)
-        if ((pending & (1u << (4 * r + k))) && (unsigned)(x[r][k] >> 32) == step) {
-          v[r][k] = __uint_as_float((unsigned)x[r][k]);
-          pending &= ~(1u << (4 * r + k));
-        }
-    if (pending == 0u || failed) break;
-    __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > a.timeout_ticks ||
-        __hip_atomic_load(a.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-      __hip_atomic_store(err_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
+    for (int k = 0; k < XG_PER_THREAD; ++k) {
+      const bool need = gather_all ? (r < a.nranks && r != a.rank) : r == 0;
+      if (need && ok[k]) pending |= 1u << (4 * r + k);
     }
   }
+  xg_record_wait(a, step, xg_wait<NR>(a, src, pending, v, e, want, failed, err_w));
 
-  // 3. rank-order sum, scale, optimizer
+  // 3. rank-order sum (two-hop non-owner: the owner's sum), publish (two-hop owner), scale,
+  //    optimizer
+  float sum[XG_PER_THREAD];
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
-    if (lo + k * XG_THREADS + tid >= a.n) continue;
-    float s = v[0][k];
+    sum[k] = v[0][k];
+    if (gather_all) {
 #pragma unroll
-    for (int r = 1; r < NR; ++r)
-      if (r < a.nranks) s += v[r][k];
-    const float gr = s * a.scale;
+      for (int r = 1; r < NR; ++r)
+        if (r < a.nranks) sum[k] += v[r][k];
+    }
+  }
+  if (two_hop && owner == a.rank) {
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k)
+      if (ok[k]) __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#pragma unroll
+  for (int k = 0; k < XG_PER_THREAD; ++k) {
+    if (!ok[k]) continue;
+    const float gr = sum[k] * a.scale;
     if (a.mode == 0) {
       a.out[e[k]] = gr;
     } else {
@@ -394,7 +294,7 @@ void xgmi_free_abort_word(uintptr_t host_word) {
 void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long long capacity, int n,
                            const float* grad, float* out, float* master, float* mom, bf16* shadow, float lr,
                            float momentum, float scale, int mode, unsigned* ctr, const unsigned* abort_w,
-                           double timeout_s, hipStream_t stream, int form) {
+                           double timeout_s, hipStream_t stream, int form, unsigned long long* wait) {
   const int nranks = (int)regions.size();
   if (nranks < 1 || nranks > XG_MAX_RANKS) throw std::runtime_error("xgmi all-reduce: 1..8 ranks");
   if (rank < 0 || rank >= nranks) throw std::runtime_error("xgmi all-reduce: bad rank");
@@ -421,11 +321,12 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.max_blocks = xgmi_max_blocks(capacity);
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
-  if (form < 0 || form > 2) throw std::runtime_error("xgmi all-reduce: form 0 (pull), 1 (push) or 2 (two-hop pull)");
+  if (form != 0 && form != 2) throw std::runtime_error("xgmi all-reduce: form 0 (pull) or 2 (two-hop pull)");
   a.form = nranks > 1 ? form : 0;
-  a.rs_off = xgmi_rs_off(capacity);
   a.ag_off = xgmi_ag_off(capacity);
+  a.wait = wait;
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;
+  if (wait != nullptr && nblk > XP_MAX_BLOCKS) throw std::runtime_error("xgmi all-reduce: wait ring holds 128 blocks");
   auto* kern = nranks == 1 ? &xgmi_allreduce_kernel<1>
                            : (nranks <= 2 ? &xgmi_allreduce_kernel<2>
                                           : (nranks <= 4 ? &xgmi_allreduce_kernel<4> : &xgmi_allreduce_kernel<8>));

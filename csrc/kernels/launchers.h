@@ -35,22 +35,22 @@ struct ReduceArgs {
   long long xp_timeout_ticks = 0;      // s_memrealtime ticks (100 MHz)
   long long xp_gslot_off = 0, xp_gslot_bytes = 0;
   float xp_scale = 1.f;                // 1 / N
-  // xp_mode 0: pull one-shot (above).  xp_mode 1: push reduce-scatter + all-gather - block k's
-  // elements are owned by rank k % N; every other rank STORES its granules into the owner's
-  // rs inbox, the owner sums them in rank order and STORES {sum, step} into every peer's ag
-  // inbox; all waits poll local memory.  Per-link bytes drop from E to 2 E / N granules.
-  // xp_mode 2: the same reduce-scatter + all-gather with the pull form's access pattern (every
-  // rank writes only its own region: the owner reads the peers' pull slots and publishes the
-  // sum in its own ag slot, which the others read).
+  // xp_mode 0: pull one-shot (above).  xp_mode 2: two-hop pull (reduce-scatter + all-gather):
+  // block k's elements are owned by rank k % N; the owner reads the peers' pull slots, sums in
+  // rank order and publishes {sum, step} in its own ag slot, which the others read (every rank
+  // writes only its own region).  Per-link bytes drop from E to 2 E / N granules.
   int xp_mode = 0;
-  long long xp_rs_off = 0, xp_ag_off = 0;
+  long long xp_ag_off = 0;
+  // diagnostic / accounting: per-step exchange wait (max over lanes, s_memrealtime ticks) as
+  // {step << 32 | ticks} words in a ring of XP_WAIT_RING entries (64-bit atomic max)
+  unsigned long long* xp_wait = nullptr;
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
-                        int32_t* correct, long long* stamps, const ReduceArgs* ra, unsigned* sync,
-                        const int32_t* next_ids, unsigned char* stage, hipStream_t stream);
+                        int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
+                        hipStream_t stream);
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);

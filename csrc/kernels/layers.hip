@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(LT) xent_kernel(const float* __restrict__ logi
 }
 
 // ---- step bookkeeping (epoch loss/accuracy, next batch ids) - shared with the fused path --
-__global__ void __launch_bounds__(64) layer_bookkeeping_kernel(ReduceArgs a) { bookkeeping<false>(a, threadIdx.x); }
+__global__ void __launch_bounds__(64) layer_bookkeeping_kernel(ReduceArgs a) { bookkeeping(a, threadIdx.x); }
 
 // ---- flat momentum SGD over an arena (no bf16 shadow: generic models) -------------------------
 // torch.optim.SGD (dampening 0, no nesterov) with the explicit fmas of sgd_update, so the
@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(TT) sgd_tail_kernel(float* __restrict__ p, flo
                                                       const ReduceArgs book) {
   const int nsg = ss.start[ss.n];
   if (BOOK && blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x < 64) bookkeeping<false>(book, threadIdx.x);
+    if (threadIdx.x < 64) bookkeeping(book, threadIdx.x);
     return;
   }
   if ((int)blockIdx.x < nsg) {

@@ -34,7 +34,7 @@
 //    barriers (s_waitcnt lgkmcnt(0); s_barrier) that leave vmcnt alone.
 //  * Every MFMA loop issues all of a tile's operand loads before its MFMA chain
 //    (sched_barrier), so LDS latency is paid once per batch, not once per K-step.
-#include "reduce_common.h"
+#include "launchers.h"
 
 namespace dnn {
 
@@ -226,110 +226,8 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
   }
 }
 
-// ---- in-launch reducer workgroups ------------------------------------------------------
-// The batch reduction of the weight gradients (+ SGD) runs in RED_BLOCKS extra
-// workgroups of the same launch, on CUs the sample workgroups leave idle.  The fc
-// reducers start as soon as every sample has published its MLP rows (end of phase D')
-// and overlap the conv backward (phases E-F); the conv reducers wait for the slabs.
-// Hand-off = MI355X_MICROARCH.md "valid forms", table row 1: the sample workgroups store
-// rows/slabs/loss WRITE-THROUGH (sc1), every storing wave drains (s_waitcnt vmcnt(0)),
-// workgroup barrier, ONE lane adds to an agent-scope counter; a reducer polls the counter
-// with relaxed (sc1) loads (bounded, s_sleep), barrier, then reads every handed-off byte
-// with sc1 buffer loads (reduce_common.h Src<true>).  No release fence (an L2 write-back
-// on the sample blocks' critical path) and no acquire.  Sample blocks never wait and
-// have the lowest block ids, so no residency / dispatch-order assumption is needed.
-// sync[0] rows-ready count, [1] slabs-ready count, [2] reducers-done count, [3] error.
-constexpr int RED_FC_BLOCKS = (FC_TILES + 7) / 8;          // 32 (8 wave-tiles per block)
-constexpr int RED_FCB_BLOCKS = (FCB_SLOTS + NT - 1) / NT;    // 2 (fc biases; the 2nd block's
-                                                             //    wave 7 runs the bookkeeping)
-constexpr int RED_CONV_BLOCKS = (CONV_SLOTS + NT - 1) / NT;  // 23
-constexpr int RED_BLOCKS = RED_FC_BLOCKS + RED_FCB_BLOCKS + RED_CONV_BLOCKS;
-static_assert(RED_FCB_BLOCKS * NT - FCB_SLOTS >= 64, "a free wave for the bookkeeping");
-
-// Write-through stores (sc1): the line leaves the XCD's L2 for memory at once.
-// Scalar values go through buffer-store builtins (cache policy 16 = sc1) so hipcc sees
-// the instruction and inserts the MFMA/VALU -> VMEM wait states itself (an inline-asm
-// store of an MFMA result would read the accumulator before it is written).  The
-// descriptor is built from the wave-uniform base; `i` is the element index.
-template <typename T>
-__device__ __forceinline__ void st_out(T* base, int i, T v, bool wt) {
-  if (wt) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, i * 4, 0, 16);
-  } else {
-    base[i] = v;
-  }
-}
-// 16-B row store from LDS-loaded registers (no pipeline hazard: the compiler's waitcnt
-// covers the ds_read; `s_nop 1` keeps hipcc from reusing the data VGPRs too early)
-__device__ __forceinline__ void st_wt4(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-__device__ __forceinline__ void signal_count(unsigned* cnt) {  // all threads of the producer block
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void wait_count(unsigned* cnt, unsigned target, unsigned* err) {
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins == (1u << 25)) {  // ~1 s: give up (error word) rather than hang the GPU
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below the poll
-}
-
-__device__ __forceinline__ void reducer_block(int r, const ReduceArgs ra, unsigned* sync, long long* stamps) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // diagnostic stamps: [12] fc reducer 0 released, [13] its tile done, [14] conv reducer 0
-  // released, [15] its columns done
-  const int si = r == 0 ? 12 : (r == RED_FC_BLOCKS + RED_FCB_BLOCKS ? 14 : -1);
-  const bool stamp = stamps != nullptr && si >= 0 && tid == 0;
-  if (r < RED_FC_BLOCKS + RED_FCB_BLOCKS) {
-    wait_count(&sync[0], (unsigned)ra.batch, &sync[3]);
-    if (stamp) stamps[si] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (r < RED_FC_BLOCKS) {
-      const int t = r * 8 + wave;
-      if (t < FC_T0) fc_tile<0, true>(t, ra);
-      else if (t < FC_T0 + FC_T1) fc_tile<1, true>(t - FC_T0, ra);
-      else if (t < FC_TILES) fc_tile<2, true>(t - FC_T0 - FC_T1, ra);
-    } else {
-      const int slot = (r - RED_FC_BLOCKS) * NT + tid;
-      if (slot < FCB_SLOTS) fcb_task<true>(slot, ra);
-      else if (r == RED_FC_BLOCKS + RED_FCB_BLOCKS - 1 && wave == 7 && ra.bookkeeping) bookkeeping<true>(ra, lane);
-    }
-  } else {
-    wait_count(&sync[1], (unsigned)ra.batch, &sync[3]);
-    if (stamp) stamps[si] = (long long)__builtin_amdgcn_s_memrealtime();
-    conv_task<true>((r - RED_FC_BLOCKS - RED_FCB_BLOCKS) * NT + tid, ra);
-  }
-  if (stamp) {
-    __builtin_amdgcn_s_waitcnt(0);
-    stamps[si + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-  }
-  // the last reducer to finish resets the counters for the next launch (every sample
-  // block has added to both counts before the conv reducers could pass their wait)
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == RED_BLOCKS - 1) {
-      __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// INL: in-launch reducer variant (extra reducer workgroups, write-through hand-off stores)
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
-template <bool TRAIN, bool INL, bool STAGED = false>
+template <bool TRAIN, bool STAGED = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -341,7 +239,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
     float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
-    long long* __restrict__ stamps, const ReduceArgs ra, unsigned* __restrict__ sync,
+    long long* __restrict__ stamps,
     const int32_t* __restrict__ next_ids,  // TRAIN + stage: sample ids of the NEXT step (-1: none)
     unsigned char* __restrict__ stage) {   // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
@@ -355,11 +253,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (btrace) {
     stamps[16 + 4 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
     stamps[16 + 4 * blockIdx.x + 3] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-  }
-  if (INL && (int)blockIdx.x >= batch) {
-    reducer_block((int)blockIdx.x - batch, ra, sync, stamps);
-    if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-    return;
   }
   // diagnostic phase timeline (block 0, thread 0): s_memrealtime ticks (100 MHz)
   const bool stamp = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
@@ -398,23 +291,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   }
   if (!valid) {
     if (TRAIN) {
-      constexpr bool wt = INL;
-      for (int i = tid; i < A0_LD; i += NT) st_out(a0_out + (size_t)b * A0_LD, i, 0.f, wt);
+      for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
       for (int i = tid; i < H1_LD; i += NT) {
-        st_out(h1_out + (size_t)b * H1_LD, i, 0.f, wt);
-        st_out(z1_out + (size_t)b * Z1_LD, i, 0.f, wt);
+        h1_out[(size_t)b * H1_LD + i] = 0.f;
+        z1_out[(size_t)b * Z1_LD + i] = 0.f;
       }
       for (int i = tid; i < H2_LD; i += NT) {
-        st_out(h2_out + (size_t)b * H2_LD, i, 0.f, wt);
-        st_out(z2_out + (size_t)b * Z2_LD, i, 0.f, wt);
+        h2_out[(size_t)b * H2_LD + i] = 0.f;
+        z2_out[(size_t)b * Z2_LD + i] = 0.f;
       }
-      for (int i = tid; i < Z3_LD; i += NT) st_out(z3_out + (size_t)b * Z3_LD, i, 0.f, wt);
-      for (int i = tid; i < SLAB; i += NT) st_out(slab_out + (size_t)b * SLAB, i, 0.f, wt);
-      if (tid == 0) { st_out(loss_out, b, 0.f, wt); st_out(correct_out, b, 0, wt); }
-      if constexpr (INL) {
-        signal_count(&sync[0]);
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      for (int i = tid; i < Z3_LD; i += NT) z3_out[(size_t)b * Z3_LD + i] = 0.f;
+      for (int i = tid; i < SLAB; i += NT) slab_out[(size_t)b * SLAB + i] = 0.f;
+      if (tid == 0) { loss_out[b] = 0.f; correct_out[b] = 0; }
     }
     return;
   }
@@ -690,8 +578,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
-      st_out(loss_out, b, lse - ll, INL);
-      st_out(correct_out, b, pred == label ? 1 : 0, INL);
+      loss_out[b] = lse - ll;
+      correct_out[b] = pred == label ? 1 : 0;
     }
     if (TRAIN && lane < 32) {
       const float dz = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
@@ -738,27 +626,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (fg == 0) DA0[16 * nt + fr] = acc[0];  // (the pool2/ReLU mask is applied via CODE2)
   }
   // per-sample rows for the batch-reduced fc weight gradients
-  if constexpr (INL) {
-    // rows as 16-B write-through stores (206 float4 over [A0 | H1 | DZ1 | H2 | DZ2 | DZ3])
-    if (tid < 206) {
-      const float* src;
-      float* dst;
-      int i;
-      if (tid < 100) { src = A0; dst = a0_out + (size_t)b * A0_LD; i = tid; }
-      else if (tid < 130) { src = H1; dst = h1_out + (size_t)b * H1_LD; i = tid - 100; }
-      else if (tid < 160) { src = DZ1; dst = z1_out + (size_t)b * Z1_LD; i = tid - 130; }
-      else if (tid < 181) { src = H2; dst = h2_out + (size_t)b * H2_LD; i = tid - 160; }
-      else if (tid < 202) { src = DZ2; dst = z2_out + (size_t)b * Z2_LD; i = tid - 181; }
-      else { src = DZ3; dst = z3_out + (size_t)b * Z3_LD; i = tid - 202; }
-      st_wt4(dst + 4 * i, *reinterpret_cast<const f32x4*>(src + 4 * i));
-    }
-    signal_count(&sync[0]);  // MLP rows (and loss/correct) published
-  } else {
-    for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
-    if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
-    if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
-    if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
-  }
+  for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
+  if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
+  if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
+  if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
   lds_barrier();
 
   STAMP(5);
@@ -771,7 +642,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
   //    flipped kernel WF - no col2im scratch, no gather pass.
   float* slab = slab_out + (size_t)b * SLAB;
-  constexpr bool wt = INL;  // in-launch reducers read the slab: write-through
   bf16x8* R3 = reinterpret_cast<bf16x8*>(smem + L_REGA + A_R3);
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
@@ -841,7 +711,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int k = 0; k < 3; ++k) t += (part + 4 * k < 10) ? RS[o * 10 + min(part + 4 * k, 9)] : 0.f;
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
-    if (part == 0) st_out(slab, SLAB_C2B + o, t, wt);
+    if (part == 0) slab[SLAB_C2B + o] = t;
   }
   // conv2 data gradient: 14 tiles (one output row each, lanes x >= 14 duplicate x = 13)
   // x 20 K-steps in two halves.  Waves 0-5 run rows w and w + 8 TOGETHER (one WF
@@ -918,7 +788,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       for (int u = 0; u < 2; ++u) {
         if ((u == 0 || two) && n[u] < 150) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) st_out(slab, SLAB_C2W + (4 * fg + i) * 150 + n[u], acc[u][i], wt);
+          for (int i = 0; i < 4; ++i) slab[SLAB_C2W + (4 * fg + i) * 150 + n[u]] = acc[u][i];
         }
       }
     }
@@ -986,7 +856,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
     t += __shfl_xor(t, 4);
-    if (part == 0 && lane < 48) st_out(slab, SLAB_C1B + c, t, wt);
+    if (part == 0 && lane < 48) slab[SLAB_C1B + c] = t;
   }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
     const int n = wave * 16 + fr, nc = min(n, 74);
@@ -1012,11 +882,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = 4 * fg + i;
-        if (o < 6) st_out(slab, SLAB_C1W + o * 75 + n, acc[i], wt);
+        if (o < 6) slab[SLAB_C1W + o * 75 + n] = acc[i];
       }
     }
   }
-  if constexpr (INL) signal_count(&sync[1]);  // conv slab published
   if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1033,13 +902,11 @@ namespace dnn {
 void init_kernels() {
   static bool done = false;
   if (done) return;
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<false, false>,
+  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, false, true>,
+  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<false, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   done = true;
 }
@@ -1047,19 +914,13 @@ void init_kernels() {
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
-                        int32_t* correct, long long* stamps, const ReduceArgs* ra, unsigned* sync,
-                        const int32_t* next_ids, unsigned char* stage, hipStream_t stream) {
+                        int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
+                        hipStream_t stream) {
   init_kernels();
-  if (stage != nullptr && (next_ids == nullptr || (ra && sync)))
-    throw std::runtime_error("fused_train: staging needs next_ids and separate reduce launches");
-  ReduceArgs r{};
-  if (ra) r = *ra;
-  const int grid = batch + (ra && sync ? RED_BLOCKS : 0);
-  auto* kern = (ra && sync) ? &lenet_fused_kernel<true, true>
-                            : (stage ? &lenet_fused_kernel<true, false, true> : &lenet_fused_kernel<true, false>);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_TOTAL, stream, images, labels,
-                     order, order_len, batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss,
-                     correct, stamps, r, ra ? sync : nullptr, next_ids, stage);
+  if (stage != nullptr && next_ids == nullptr) throw std::runtime_error("fused_train: staging needs next_ids");
+  auto* kern = stage ? &lenet_fused_kernel<true, true> : &lenet_fused_kernel<true, false>;
+  hipLaunchKernelGGL(kern, dim3(batch), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len, batch, 0,
+                     state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, next_ids, stage);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1070,7 +931,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct, nullptr, ReduceArgs{}, nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr);
   HIP_CHECK(hipGetLastError());
 }
 

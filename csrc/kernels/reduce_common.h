@@ -1,31 +1,10 @@
-// Device code of the batch gradient reduction + momentum SGD, shared by the standalone
-// grad_reduce kernel (reduce_sgd.hip) and the reducer workgroups that run inside the
-// fused training launch (lenet_fused.hip).  See reduce_sgd.hip for the parity notes.
+// Device code of the batch gradient reduction + momentum SGD of the grad_reduce kernel
+// (reduce_sgd.hip) and the step bookkeeping shared with the layer engine's kernels
+// (layers.hip).  See reduce_sgd.hip for the parity notes.
 #pragma once
 #include "launchers.h"
 
 namespace dnn {
-
-// Operand source of the reduction.  COH = the bytes were handed over INSIDE the launch by
-// other workgroups (in-launch reducers): every load is a buffer load with sc1 (aux 16),
-// which bypasses this CU's L1, so no agent acquire is needed; the producers store them
-// write-through (sc1) and drain before signalling (MI355X_MICROARCH.md, visibility, valid
-// forms row 1).  The descriptor is built from wave-uniform values only.
-template <bool COH, typename T = float>
-struct Src {
-  const T* p;
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ Src(const T* p_, int n) : p(p_) {
-    if constexpr (COH) r = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(p_), 0, n * (int)sizeof(T), 0x00020000);
-  }
-  __device__ __forceinline__ T operator[](int i) const {
-    if constexpr (COH) {
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, i * (int)sizeof(T), 0, 16));
-    } else {
-      return p[i];
-    }
-  }
-};
 
 // SGD epilogue with the master/momentum values already in registers (prefetched
 // together with the gradient operands, so the update costs no extra memory latency).
@@ -54,7 +33,7 @@ struct DirectSink {
   }
 };
 struct XpSink {
-  unsigned long long* own;  // where the granules go: this rank's slot (pull) / the owner's rs inbox (push)
+  unsigned long long* own;  // where the granules go: this rank's pull slot (null: not published)
   unsigned long long tag;   // step << 32
   int e[4] = {0, 0, 0, 0};
   float g[4] = {0.f, 0.f, 0.f, 0.f}, p[4], m[4];
@@ -62,7 +41,7 @@ struct XpSink {
   __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
     g_ *= a.grad_scale;
     e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
-    if (own != nullptr)  // (push exchange: null on the owner of the block's elements)
+    if (own != nullptr)  // (two-hop form: null on the owner of the block's elements)
       __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 };
@@ -77,11 +56,11 @@ constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
 constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
 constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
 
-template <int LAYER, bool COH, class Sink>
+template <int LAYER, class Sink>
 __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
   using L = Fc<LAYER>;
-  const Src<COH> z(LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3), a.batch * L::ZLD);
-  const Src<COH> x(LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2), a.batch * L::XLD);
+  const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
+  const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, kq = lane >> 4;
   const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
@@ -125,20 +104,14 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
     if (o < L::O && iv) sk.put(j, e[j], acc[j], pv[j], mv[j], a);
   }
 }
-template <int LAYER, bool COH>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a) {
-  DirectSink d;
-  fc_tile<LAYER, COH>(t, a, d);
-}
 
 // Column sums (fc biases: sum_b z[b][o]; conv slab columns: sum_b slab[b][j]) with SPLIT = 4
 // consecutive lanes per column: lane part q sums rows {64 c + 16 q + k}, then the 4
 // partials combine as (p0 + p1) + (p2 + p3) through lane shuffles - a fixed order (bitwise
-// reproducible, identical in the standalone and the in-launch reducers), 16-load chains
+// reproducible), 16-load chains
 // instead of 64, 4x the threads in flight.
 constexpr int SPLIT = 4;
-template <bool COH>
-__device__ __forceinline__ float column_sum_split(const Src<COH>& src, int ld, int col, int batch, int q) {
+__device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q) {
   float g = 0.f;
   for (int b0 = 0; b0 < batch; b0 += 64) {
     float v[16];
@@ -154,12 +127,12 @@ __device__ __forceinline__ float column_sum_split(const Src<COH>& src, int ld, i
 }
 
 // fc-bias slots: columns padded per source to multiples of 16 (one wave = 16 columns), so
-// each wave reads ONE source and its buffer descriptor stays in SGPRs (COH): fc1 [0,128)
+// each wave reads ONE source (wave-uniform base pointer): fc1 [0,128)
 // (120 used), fc2 [128,224) (84 used), fc3 [224,240) (10 used); slot = column * 4 + q.
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
-template <bool COH, class Sink>
+template <class Sink>
 __device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
@@ -169,17 +142,12 @@ __device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk) {
   if (grp < 8) { zp = a.z1; ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; }
   else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; }
   else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; }
-  const Src<COH> src(zp, a.batch * ld);
+  const float* src = zp;
   const int cc = min(col, n - 1);  // padding lanes recompute a real column (no divergence)
   const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
   const float g = column_sum_split(src, ld, cc, a.batch, q);  // every lane shuffles: no early exit
   if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
-}
-template <bool COH>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a) {
-  DirectSink d;
-  fcb_task<COH>(t, a, d);
 }
 
 constexpr int CONV_ELEMS = SLAB;
@@ -190,27 +158,21 @@ __device__ __forceinline__ int conv_dst(int e) {
   if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
   return OFF_C2B + (e - SLAB_C2B);
 }
-template <bool COH, class Sink>
+template <class Sink>
 __device__ __forceinline__ void conv_task(int t, const ReduceArgs a, Sink& sk) {
-  const Src<COH> src(a.slab, a.batch * SLAB);
+  const float* src = a.slab;
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
   const float g = column_sum_split(src, SLAB, e, a.batch, q);
   if (t < CONV_SLOTS && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
-template <bool COH>
-__device__ __forceinline__ void conv_task(int t, const ReduceArgs a) {
-  DirectSink d;
-  conv_task<COH>(t, a, d);
-}
 
 // Epoch statistics of the step that just ran + publication of the next step's cursor,
 // valid count and sample ids.  One wave (lanes 0..63), fixed summation order.
-template <bool COH>
 __device__ __forceinline__ void bookkeeping(const ReduceArgs a, int lane) {
-    const Src<COH> loss(a.loss, a.batch);
-    const Src<COH, int32_t> correct(a.correct, a.batch);
+    const float* loss = a.loss;
+    const int32_t* correct = a.correct;
     float ls = 0.f;
     int cs = 0;
     for (int b = lane; b < a.batch; b += 64) { ls += loss[b]; cs += correct[b]; }

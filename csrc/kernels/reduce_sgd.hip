@@ -31,25 +31,25 @@ __device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk) 
   if (mlp) {
     if (blk < TILE_BLOCKS) {
       const int t = blk * 4 + (threadIdx.x >> 6);
-      if (t < FC_T0) fc_tile<0, false>(t, a, sk);
-      else if (t < FC_T0 + FC_T1) fc_tile<1, false>(t - FC_T0, a, sk);
-      else if (t < FC_TILES) fc_tile<2, false>(t - FC_T0 - FC_T1, a, sk);
+      if (t < FC_T0) fc_tile<0>(t, a, sk);
+      else if (t < FC_T0 + FC_T1) fc_tile<1>(t - FC_T0, a, sk);
+      else if (t < FC_TILES) fc_tile<2>(t - FC_T0 - FC_T1, a, sk);
       return true;
     }
     blk -= TILE_BLOCKS;
     constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
     if (blk < FB) {
-      fcb_task<false>(blk * RT + threadIdx.x, a, sk);
+      fcb_task(blk * RT + threadIdx.x, a, sk);
       return true;
     }
     blk -= FB;
   }
   if (conv) {
     constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
-    if (blk < CB) { conv_task<false>(blk * RT + threadIdx.x, a, sk); return true; }
+    if (blk < CB) { conv_task(blk * RT + threadIdx.x, a, sk); return true; }
     blk -= CB;
   }
-  if (a.bookkeeping && blk == 0 && threadIdx.x < 64) bookkeeping<false>(a, threadIdx.x);
+  if (a.bookkeeping && blk == 0 && threadIdx.x < 64) bookkeeping(a, threadIdx.x);
   return false;
 }
 
@@ -62,41 +62,37 @@ __device__ __forceinline__ unsigned long long xp_ld(const unsigned long long* p)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The one-launch all-reduce exchange of ONE lane's (<= 4) reduced elements.  Each element
-// was stored as a granule {value, step} (XpSink::put); the lane reads the same element's
-// granule from every peer's slot over xGMI (7 links at once, every load in flight before the
-// first check) until each tag shows this step, sums the N values in RANK ORDER (bit-identical
-// replicas), scales by 1/N and applies momentum SGD + the bf16 images.  The value and its tag
-// are one 8-byte atomic word, so no flag, fence or barrier orders anything: a tag match IS
-// the data.  Waits are bounded (timeout / abort word -> sticky error word, never a hang).
-// Double buffering by step parity: the owner overwrites its element e of slot (s & 1) at step
-// s + 2 only after it read every peer's step s + 1 granule of e, which each peer wrote only
-// after it had read the owner's step s granule of e.
-// NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
-// group does not pay for 8 ranks' loads in flight.
+// Exchange-wait accounting (ReduceArgs::xp_wait, optional): every wave stores the longest wait
+// of its lanes for this step (s_memrealtime ticks, 100 MHz) into its own word of the ring entry
+// [step % XP_WAIT_RING][block][wave] as {step << 32 | ticks} - a plain store per wave, no
+// atomics; the host takes the max over blocks and waves (parallel/xgmi.py wait_stats).
+__device__ __forceinline__ void record_wait(const ReduceArgs& a, unsigned step, long long ticks) {
+  if (a.xp_wait == nullptr) return;
+  unsigned t = (unsigned)min(ticks, 0xffffffffll);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t = max(t, (unsigned)__shfl_xor((int)t, off));
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    a.xp_wait[((size_t)(step % XP_WAIT_RING) * XP_MAX_BLOCKS + blockIdx.x) * (RT / 64) + w] =
+        ((unsigned long long)step << 32) | t;
+  }
+}
+
+// Poll the granules in `pending` (bit 4 r + j: element j of source r) until each tag shows
+// `step`; the values land in v[r][j].  Every load of a round is in flight before the first
+// check.  Bounded: timeout / abort word -> sticky error word, never a hang.  Returns the wait.
 template <int NR>
-__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
-  const int par = step & 1u;
-  float v[NR][4];
-  unsigned pending = 0;  // bit 4 r + j: granule (r, j) still to read
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[r][j] = sk.g[j];
-      if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
-    }
+__device__ __forceinline__ long long poll_granules(const ReduceArgs& a, const unsigned long long* const (&src)[NR],
+                                                   const int (&e)[4], unsigned pending, unsigned step, bool failed,
+                                                   float (&v)[NR][4]) {
   const long long t0 = wall_clock64();
   while (pending != 0u) {
     unsigned long long x[NR][4];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const unsigned long long* src =
-          reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src + sk.e[j]);
-    }
+        if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src[r] + e[j]);
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -106,149 +102,17 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
           pending &= ~(1u << (4 * r + j));
         }
     if (pending == 0u || failed) break;
-    __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > a.xp_timeout_ticks || __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > a.xp_timeout_ticks ||
+        __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
       __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!sk.v[j]) continue;
-    float s = v[0][j];
-#pragma unroll
-    for (int r = 1; r < NR; ++r)
-      if (r < a.xp_nranks) s += v[r][j];
-    const float gr = s * a.xp_scale;
-    float p, m;
-    sgd_update(gr, sk.p[j], sk.m[j], a.lr, a.momentum, p, m);
-    a.mom[sk.e[j]] = m;
-    a.master[sk.e[j]] = p;
-    write_shadow(a.shadow, sk.e[j], p);
-  }
+  return wall_clock64() - t0;
 }
 
-// The push form (xp_mode 1): reduce-scatter + all-gather with every wait on LOCAL memory.
-// Block k's elements belong to rank k % N.  A non-owner lane has already STORED its granules
-// into the owner's rs inbox [parity][its rank] (XpSink::put, one system-scope 64-bit store over
-// xGMI each); it now polls its own ag inbox for the owner's {sum, step}.  The owner lane polls
-// its rs inbox for the N - 1 peers' granules, sums the N values in RANK ORDER (the same fp32
-// additions as xp_exchange, so both forms give bit-identical parameters), stores {sum, step}
-// into every peer's ag inbox and applies SGD.  Per link and step this moves 2 E / N granules
-// instead of the one-shot's E, and nobody re-reads remote memory while waiting.
-// Slot reuse by parity is safe for the same reason as the pull form: a rank's step s + 2 store
-// into an inbox follows its own step s + 1, which needed the reader to be done with step s.
-//
-// The two-hop pull form (xp_mode 2, PUSH = false) has the same ownership and sums but keeps the
-// pull form's access pattern - every rank writes only its OWN (uncached) region and reads its
-// peers': the owner reads its elements' granules from the peers' pull slots, stores {sum, step}
-// into its own ag slot, and the other ranks read that slot.  Also 2 E / N granules per link.
-template <int NR, bool PUSH>
-__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
-  const int par = step & 1u;
-  const int owner = blockIdx.x % a.xp_nranks;
-  // The granules went through a PEER's mapping of its region, which (unlike the owner's own
-  // uncached mapping that the pull form writes) may be L2-cached here: a relaxed system-scope
-  // store can then sit in this GPU's L2 while the owner polls memory.  A system-scope release
-  // (L2 write-back) publishes them (profiles/r2/push: without it 4 ranks on one GPU stall).
-  if (PUSH && owner != a.xp_rank) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  const long long t0 = wall_clock64();
-  float s[4];
-  if (owner == a.xp_rank) {
-    float v[NR][4];
-    unsigned pending = 0;
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[r][j] = sk.g[j];
-        if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
-      }
-    while (pending != 0u) {
-      unsigned long long x[NR][4];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(
-            PUSH ? a.xp_region[a.xp_rank] + a.xp_rs_off + (long long)(par * XG_MAX_RANKS + r) * a.xp_gslot_bytes
-                 : a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src + sk.e[j]);
-      }
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if ((pending & (1u << (4 * r + j))) && (unsigned)(x[r][j] >> 32) == step) {
-            v[r][j] = __uint_as_float((unsigned)x[r][j]);
-            pending &= ~(1u << (4 * r + j));
-          }
-      if (pending == 0u || failed) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > a.xp_timeout_ticks ||
-          __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-        __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[j] = v[0][j];
-#pragma unroll
-      for (int r = 1; r < NR; ++r)
-        if (r < a.xp_nranks) s[j] += v[r][j];
-    }
-    const unsigned long long tag = (unsigned long long)step << 32;
-    if constexpr (PUSH) {
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (r >= a.xp_nranks || r == a.xp_rank) continue;
-        unsigned long long* dst =
-            reinterpret_cast<unsigned long long*>(a.xp_region[r] + a.xp_ag_off + par * a.xp_gslot_bytes);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (sk.v[j])
-            __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as above: the sums went through peer mappings)
-    } else {
-      unsigned long long* dst =
-          reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (sk.v[j])
-          __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  } else {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(
-        a.xp_region[PUSH ? a.xp_rank : owner] + a.xp_ag_off + par * a.xp_gslot_bytes);
-    unsigned pending = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[j] = 0.f;
-      if (sk.v[j]) pending |= 1u << j;
-    }
-    while (pending != 0u) {
-      unsigned long long x[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (pending & (1u << j)) x[j] = xp_ld(src + sk.e[j]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if ((pending & (1u << j)) && (unsigned)(x[j] >> 32) == step) {
-          s[j] = __uint_as_float((unsigned)x[j]);
-          pending &= ~(1u << j);
-        }
-      if (pending == 0u || failed) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > a.xp_timeout_ticks ||
-          __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-        __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-  }
+__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSink& sk, const float (&s)[4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (!sk.v[j]) continue;
@@ -259,6 +123,103 @@ __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSi
     a.master[sk.e[j]] = p;
     write_shadow(a.shadow, sk.e[j], p);
   }
+}
+
+// The one-launch all-reduce exchange of ONE lane's (<= 4) reduced elements.  Each element
+// was stored as a granule {value, step} (XpSink::put); the lane reads the same element's
+// granule from every peer's slot over xGMI (7 links at once) until each tag shows this step,
+// sums the N values in RANK ORDER (bit-identical replicas), scales by 1/N and applies momentum
+// SGD + the bf16 images.  The value and its tag are one 8-byte atomic word, so no flag, fence or
+// barrier orders anything: a tag match IS the data.
+// Double buffering by step parity: the owner overwrites its element e of slot (s & 1) at step
+// s + 2 only after it read every peer's step s + 1 granule of e, which each peer wrote only
+// after it had read the owner's step s granule of e.
+// NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
+// group does not pay for 8 ranks' loads in flight.
+template <int NR>
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+  const int par = step & 1u;
+  float v[NR][4];
+  unsigned pending = 0;
+  const unsigned long long* src[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[r][j] = sk.g[j];
+      if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
+    }
+  }
+  record_wait(a, step, poll_granules<NR>(a, src, sk.e, pending, step, failed, v));
+  float s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[j] = v[0][j];
+#pragma unroll
+    for (int r = 1; r < NR; ++r)
+      if (r < a.xp_nranks) s[j] += v[r][j];
+  }
+  apply_update(a, sk, s);
+}
+
+// The two-hop pull form (xp_mode 2): reduce-scatter + all-gather where every rank writes only
+// its OWN region.  Block k's elements belong to rank k % N.  A non-owner lane has stored its
+// granules into its own pull slot (XpSink::put); the owner lane reads them from the N - 1 peers'
+// pull slots, sums the N values in RANK ORDER (the same fp32 additions as xp_exchange, so both
+// forms give bit-identical parameters), stores {sum, step} into its own ag slot and applies SGD;
+// the other ranks read that slot.  2 E / N granules per link instead of E, one more dependent
+// remote read.
+template <int NR>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+  const int par = step & 1u;
+  const int owner = blockIdx.x % a.xp_nranks;
+  float s[4];
+  long long waited;
+  if (owner == a.xp_rank) {
+    float v[NR][4];
+    unsigned pending = 0;
+    const unsigned long long* src[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[r][j] = sk.g[j];
+        if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
+      }
+    }
+    waited = poll_granules<NR>(a, src, sk.e, pending, step, failed, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = v[0][j];
+#pragma unroll
+      for (int r = 1; r < NR; ++r)
+        if (r < a.xp_nranks) s[j] += v[r][j];
+    }
+    const unsigned long long tag = (unsigned long long)step << 32;
+    unsigned long long* dst =
+        reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (sk.v[j])
+        __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    const unsigned long long* src[1] = {
+        reinterpret_cast<const unsigned long long*>(a.xp_region[owner] + a.xp_ag_off + par * a.xp_gslot_bytes)};
+    float v[1][4];
+    unsigned pending = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[0][j] = 0.f;
+      if (sk.v[j]) pending |= 1u << j;
+    }
+    waited = poll_granules<1>(a, src, sk.e, pending, step, failed, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = v[0][j];
+  }
+  record_wait(a, step, waited);
+  apply_update(a, sk, s);
 }
 
 // diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
@@ -277,30 +238,19 @@ template <int NR>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(const ReduceArgs a) {
   reduce_stamp(a, 0);
   if constexpr (NR > 1) {  // one-launch all-reduce: reduce -> exchange -> SGD, per lane
-    // (the arguments are only read on this path: the per-lane region index then reads the
-    //  kernel-argument segment directly instead of a private copy of the whole struct)
     const unsigned step = a.xp_ctr[blockIdx.x] + 1u;
     const bool failed = *a.xp_err != 0u;
     XpSink sk;
     sk.tag = (unsigned long long)step << 32;
-    if (a.xp_mode == 0) {
-      sk.own = reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
-                                                     (step & 1u) * a.xp_gslot_bytes);
-      if (grad_reduce_body(a, sk)) xp_exchange<NR>(a, sk, step, failed);
-    } else if (a.xp_mode == 1) {
-      const int owner = blockIdx.x % a.xp_nranks;
-      sk.own = owner == a.xp_rank
-                   ? nullptr
-                   : reinterpret_cast<unsigned long long*>(
-                         a.xp_region[owner] + a.xp_rs_off +
-                         (long long)((step & 1u) * XG_MAX_RANKS + a.xp_rank) * a.xp_gslot_bytes);
-      if (grad_reduce_body(a, sk)) xp_exchange_rsag<NR, true>(a, sk, step, failed);
-    } else {  // two-hop pull: granules into this rank's own pull slot (nobody reads the owner's)
-      const int owner = blockIdx.x % a.xp_nranks;
-      sk.own = owner == a.xp_rank ? nullptr
-                                  : reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
-                                                                          (step & 1u) * a.xp_gslot_bytes);
-      if (grad_reduce_body(a, sk)) xp_exchange_rsag<NR, false>(a, sk, step, failed);
+    // pull: every lane's granules go to this rank's slot; two-hop: only non-owners' (the owner
+    // publishes the SUM in its ag slot instead)
+    const bool publish = a.xp_mode == 0 || (int)(blockIdx.x % a.xp_nranks) != a.xp_rank;
+    sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                             (step & 1u) * a.xp_gslot_bytes)
+                     : nullptr;
+    if (grad_reduce_body(a, sk)) {
+      if (a.xp_mode == 0) xp_exchange<NR>(a, sk, step, failed);
+      else xp_exchange_rsag<NR>(a, sk, step, failed);
     }
     __syncthreads();  // every thread read this block's counter before it advances
     if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;

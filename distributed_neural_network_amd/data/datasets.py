@@ -57,9 +57,15 @@ def load_cifar10(root: str | os.PathLike, train: bool) -> Split:
     return Split(torch.from_numpy(images), torch.from_numpy(labels), "cifar10-" + ("train" if train else "test"))
 
 
-def synthetic(n: int, seed: int, train: bool = True) -> Split:
-    images, labels = native.io().synthetic(int(n), int(seed), split=0 if train else 1)
-    return Split(torch.from_numpy(images), torch.from_numpy(labels), "synthetic-" + ("train" if train else "test"))
+SYNTH_NOISE = 96       # default template + noise amplitude (learnable in about one epoch)
+SYNTH_NOISE_HARD = 255  # maximal noise: accuracy climbs over several epochs (tools/convergence.py)
+
+
+def synthetic(n: int, seed: int, train: bool = True, noise: int = SYNTH_NOISE) -> Split:
+    images, labels = native.io().synthetic(int(n), int(seed), noise=int(noise), split=0 if train else 1)
+    tag = "" if noise == SYNTH_NOISE else f"-noise{noise}"
+    return Split(torch.from_numpy(images), torch.from_numpy(labels),
+                 "synthetic" + tag + "-" + ("train" if train else "test"))
 
 
 def get_splits(kind: str, root: str = "./data", n_train: int | None = None, n_test: int | None = None,

@@ -35,7 +35,7 @@ HIP_SOURCES = [
     CSRC / "comm" / "xgmi_allreduce.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"
-HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "runtime" / "graph_exec.cpp"]
+HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp"]
 HIP_HEADERS = sorted((CSRC / "kernels").glob("*.h"))
 IO_SOURCES = [CSRC / "io" / "dataio.cpp"]
 

@@ -121,40 +121,80 @@ def _divergence_report(comm: Communicator, engine) -> str:
 
 
 class StepAllReduce(SyncPolicy):
+    """Per-step gradient all-reduce.  The transport is one of the PATHS below; ``path`` None
+    means the default choice (``default_path``), a name pins it (the multi-GPU bench sets the
+    winner of its start-up A/B, parallel/autotune.py).  ``attach`` re-installs the path after
+    every communicator re-form (rank-drop recovery)."""
+
     name = "step-allreduce"
+    # xgmi-pull / xgmi-rsag: the batch-reduction kernel exchanges its elements over xGMI
+    # (one-hop pull / two-hop reduce-scatter + all-gather) and applies SGD in ONE launch;
+    # rccl: ncclAllReduce of the fused gradient bucket + sgd_apply; rccl-overlap: the MLP bucket
+    # all-reduced on a side stream while the conv bucket is reduced; local: no all-reduce (A/B
+    # baseline only: replicas diverge)
+    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+    path: str | None = None
+    record_waits = False  # xGMI paths: record every step's exchange wait (XgmiGroup.wait_stats)
 
     def attach(self, engine) -> None:
         super().attach(engine)
         if not self.comm.distributed:
             engine.grad_sync = None
-        elif (xg := self._xgmi_group(engine)) is not None:
-            # GPU hot path on one node: one-shot xGMI all-reduce fused with the optimizer
-            from .xgmi import XgmiGradSync, exchange_mode, one_launch_wanted
-
-            engine.grad_sync = XgmiGradSync(xg)
-            xg.one_launch, xg.xp_mode = False, 0
-            if one_launch_wanted() and hasattr(engine, "selftest_exchange"):
-                # batch reduction + all-reduce + SGD in ONE launch, once it has matched the
-                # two-launch path bit for bit on every rank (all ranks get the same vote);
-                # a requested push / rsag form first, the pull form if that fails
-                xg.xp_mode = exchange_mode(xg)
-                xg.one_launch = engine.selftest_exchange(xg, self.comm)
-                if xg.xp_mode != 0 and not xg.one_launch:
-                    if self.comm.rank == 0:
-                        import sys
-
-                        print(f"[xgmi] exchange form {xg.xp_mode} failed its self-test: pull form", file=sys.stderr,
-                              flush=True)
-                    xg.xp_mode = 0
-                    xg.one_launch = engine.selftest_exchange(xg, self.comm)
-                if not xg.one_launch and self.comm.rank == 0:
+            return
+        name = self.path or self.default_path(engine)
+        chain = [name]
+        if name == "xgmi-rsag":
+            chain.append("xgmi-pull")
+        if name.startswith("xgmi"):
+            chain.append("rccl" if self.comm.backend == "nccl" else "torch-pg")
+        for i, n in enumerate(chain):
+            if self.install(engine, n):
+                if i and self.comm.rank == 0:
                     import sys
 
-                    print("[xgmi] one-launch exchange self-test failed: two-launch all-reduce", file=sys.stderr,
-                          flush=True)
-                engine.invalidate_graphs()
-        elif self.comm.backend == "nccl":
-            # GPU hot path: native RCCL communicator, all-reduce launched on the engine stream
+                    print(f"[allreduce] {name} unavailable: using {n}", file=sys.stderr, flush=True)
+                return
+        raise CommError(f"per-step all-reduce path {name!r} could not be installed")
+
+    def default_path(self, engine) -> str:
+        from . import xgmi
+
+        if getattr(engine, "overlap", False) or self.bucket_kb:
+            # --overlap / --bucket-kb ask for the bucketed collective path
+            return ("rccl-overlap" if getattr(engine, "overlap", False) else "rccl") \
+                if self.comm.backend == "nccl" else "torch-pg"
+        if xgmi.wanted(self.comm) and engine.grad.numel() <= self.XGMI_MAX_ELEMS:
+            return "xgmi-rsag" if xgmi.exchange_mode() == 2 else "xgmi-pull"
+        return "rccl" if self.comm.backend == "nccl" else "torch-pg"
+
+    def installed(self, engine) -> str | None:
+        """Name of the path the engine runs now (None: one rank, no all-reduce)."""
+        gs = engine.grad_sync
+        if gs is None:
+            return None if not self.comm.distributed else "local"
+        kind = type(gs).__name__
+        if kind == "XgmiGradSync":
+            form = {0: "pull", 2: "rsag"}[gs.group.xp_mode]
+            return f"xgmi-{form}" + ("" if gs.group.one_launch else "-two-launch")
+        if kind == "NativeGradAllReduce":
+            return "rccl-overlap" if gs.overlap else "rccl"
+        return "torch-pg"
+
+    def install(self, engine, name: str) -> bool:
+        """Collective: put path ``name`` on the engine.  Returns the agreed outcome (False on
+        every rank if it failed on any; the engine then has no all-reduce installed)."""
+        if hasattr(engine, "invalidate_graphs"):
+            engine.invalidate_graphs()
+        if hasattr(engine, "overlap"):
+            engine.overlap = name == "rccl-overlap"
+        engine.grad_sync = None
+        if name == "local":
+            return True
+        if name.startswith("xgmi"):
+            return self._install_xgmi(engine, 2 if name == "xgmi-rsag" else 0)
+        if name in ("rccl", "rccl-overlap"):
+            if self.comm.backend != "nccl":
+                return False
             from .rccl import NativeGradAllReduce, RcclComm
 
             rc = getattr(self.comm, "native", None)
@@ -162,25 +202,67 @@ class StepAllReduce(SyncPolicy):
                 rc = self.comm.native = RcclComm(self.comm)
             elif rc.generation != self.comm.generation:
                 rc.reinit()
-            engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=getattr(engine, "overlap", False),
+            engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=name == "rccl-overlap",
                                                    bucket_kb=self.bucket_kb)
-        else:
+            return True
+        if name == "torch-pg":
             engine.grad_sync = GradAllReduce(self.comm, bucket_kb=self.bucket_kb)
             if getattr(engine, "use_graphs", False):
                 # host-side (gloo) collectives cannot live inside a captured hipGraph
                 engine.use_graphs = False
-                if hasattr(engine, "invalidate_graphs"):
-                    engine.invalidate_graphs()
+            return True
+        raise ValueError(f"unknown all-reduce path {name!r}; expected one of {self.PATHS + ('local', 'torch-pg')}")
 
+    def _install_xgmi(self, engine, mode: int) -> bool:
+        from .xgmi import XgmiGradSync, one_launch_wanted
+
+        xg = self._xgmi_group(engine)
+        if xg is None:
+            return False
+        engine.grad_sync = XgmiGradSync(xg)
+        xg.one_launch, xg.xp_mode = False, mode
+        xg.enable_wait_stats(self.record_waits)
+        if one_launch_wanted() and hasattr(engine, "selftest_exchange"):
+            # batch reduction + all-reduce + SGD in ONE launch, once it has matched the
+            # two-launch path bit for bit on every rank (all ranks get the same vote); results
+            # are cached per form for this group
+            cache = xg.__dict__.setdefault("selftested", {})
+            if mode not in cache:
+                cache[mode] = engine.selftest_exchange(xg, self.comm)
+                if xg.broken:
+                    # a pass raised / timed out on some rank: the step counters may be out of
+                    # step across ranks - this group must not be used again
+                    self._drop_xgmi_group()
+                    engine.grad_sync = None
+                    return False
+            xg.one_launch = cache[mode]
+            if not xg.one_launch:
+                if mode != 0:
+                    engine.grad_sync = None
+                    return False  # the two-hop form exists only as the one-launch exchange
+                if self.comm.rank == 0:
+                    import sys
+
+                    print("[xgmi] one-launch exchange self-test failed: two-launch all-reduce", file=sys.stderr,
+                          flush=True)
+        if hasattr(engine, "invalidate_graphs"):
+            engine.invalidate_graphs()
+        return True
+
+    def _drop_xgmi_group(self) -> None:
+        grp = getattr(self.comm, "xgmi", None)
+        if grp is not None:
+            grp.close()
+        self.comm.xgmi = None
 
     XGMI_MAX_ELEMS = 4 << 20  # one-shot reads N x the gradient: beyond ~16 MB the RCCL ring wins
 
     def _xgmi_group(self, engine):
         """The one-shot xGMI group for this generation (built collectively, self-tested;
-        None -> RCCL).  ``--overlap`` / ``--bucket-kb`` ask for the bucketed RCCL path."""
+        None -> not available here)."""
         from . import xgmi
 
-        if getattr(engine, "overlap", False) or self.bucket_kb or not xgmi.wanted(self.comm):
+        if not xgmi.wanted(self.comm):
             return None
         n = engine.grad.numel()
         if n > self.XGMI_MAX_ELEMS:

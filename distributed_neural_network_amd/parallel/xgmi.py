@@ -77,48 +77,22 @@ def one_launch_wanted() -> bool:
     return v == "1"
 
 
-def push_wanted(grp: "XgmiGroup") -> bool:
-    """Collective: run the exchange in its push form (reduce-scatter + all-gather, ``xp_mode``
-    1 in csrc/kernels/reduce_sgd.hip, ``push`` in xgmi_allreduce.hip)?
-    ``DNN_XGMI_EXCHANGE`` = pull (default) | push (experimental).
-
-    The pull one-shot moves every rank's whole gradient over every link (E granules per link
-    and step); the push form moves 2 E / N, at the price of a second one-way hop.  It is NOT
-    the default: with 4 ranks sharing one GPU (the only multi-rank setup measured here) its
-    waits stall for seconds every few epochs even after a system-scope release on the writer
-    side, and then fail on the timeout (profiles/r2/push/), while the pull form never did.  On
-    distinct GPUs it is unmeasured.  Push polls the rank's OWN region for stores that peers
-    make, so every region must be uncached memory; all ranks vote on that."""
-    return exchange_mode(grp) == 1
+EXCHANGE_MODES = {"pull": 0, "rsag": 2}
 
 
-EXCHANGE_MODES = {"pull": 0, "push": 1, "rsag": 2}
-
-
-def exchange_mode(grp: "XgmiGroup") -> int:
-    """Collective: ``xp_mode`` of the one-launch exchange from ``DNN_XGMI_EXCHANGE``:
-    pull (0: one hop, E granules per link), push (1, experimental, see ``push_wanted``),
-    rsag (2: two-hop pull - reduce-scatter + all-gather where every rank writes only its own
-    region, 2 E / N granules per link, one more dependent remote read) or auto (default).
-
-    auto = pull.  (rsag when every rank has its own GPU and N >= 4 is the byte model's choice,
-    kept opt-in until a real multi-GPU node has measured it - see below.)  Per link and step the
-    pull form moves the whole 496 KB granule slot (>= 6.5 us at ~77 GB/s per link direction);
-    rsag moves 2 / N of it and pays one more remote round trip, so it wins once the saved bytes
-    outweigh that trip (equal bytes at N = 2).  rsag uses exactly the pull form's memory
-    operations (own-region stores, remote loads).  With several ranks time-sharing ONE GPU
-    its two-level wait (the owner's sum needs every peer's block to have run first) stalls for
-    seconds when the GPU time-slices the processes (profiles/r2/push/).  On distinct GPUs
-    nothing is time-sliced, but that is unmeasured, and the pull form has no failure seen in
-    any setup: the default stays pull for the multi-GPU scaling run."""
+def exchange_mode(grp: "XgmiGroup | None" = None) -> int:
+    """``xp_mode`` of the one-launch exchange from ``DNN_XGMI_EXCHANGE``: pull (0: one hop, E
+    granules per link) or rsag (2: two-hop pull - reduce-scatter + all-gather where every rank
+    writes only its own region, 2 E / N granules per link, one more dependent remote read).
+    auto (default) = pull; the multi-GPU bench measures both (parallel/autotune.py) and keeps
+    the faster.  With several ranks time-sharing ONE GPU the two-hop form's two-level wait (the
+    owner's sum needs every peer's block to have run first) stalls for seconds when the GPU
+    time-slices the processes (profiles/r2/push/); the pull form has no failure seen in any
+    setup."""
     choice = os.environ.get("DNN_XGMI_EXCHANGE", "auto")
     if choice != "auto" and choice not in EXCHANGE_MODES:
         raise ValueError(f"DNN_XGMI_EXCHANGE must be auto or one of {sorted(EXCHANGE_MODES)}, not {choice!r}")
-    uncached = all(v == 1.0 for v in grp.comm.gather_scalars(1.0 if grp.kind == "uncached" else 0.0))
-    if choice == "auto":
-        return 0
-    mode = EXCHANGE_MODES[choice]
-    return 0 if mode == 1 and not uncached else mode
+    return 0 if choice == "auto" else EXCHANGE_MODES[choice]
 
 
 def wait_timeout(comm: Communicator) -> float:
@@ -160,8 +134,14 @@ class XgmiGroup:
         # set once the exchange matched the two-launch path bit for bit on every rank
         # (HipEngine.selftest_exchange, run by the step-allreduce policy)
         self.one_launch = False
-        self.xp_mode = 0  # one-launch exchange form (exchange_mode + self-test): 0 pull, 1 push, 2 rsag
+        # set when a self-test pass raised or timed out on some rank: the per-block step counters
+        # may then be out of step across ranks, so the group must be rebuilt before any use
+        self.broken = False
+        self.xp_mode = 0  # one-launch exchange form (exchange_mode + self-test): 0 pull, 2 rsag
         self.ar_mode = 0  # form of the all-reduce kernel (build_group: exchange_mode + self-test)
+        # per-step exchange-wait records (ReduceArgs::xp_wait): [ring][block][wave] words of
+        # {step << 32 | ticks}; None = not recorded (enable_wait_stats)
+        self.wait: torch.Tensor | None = None
         key = f"dnn/xgmi/g{comm.generation}/i{next(_ids)}"
         # every rank publishes SOMETHING (an empty handle on failure), so no peer blocks
         # on a key that never comes
@@ -193,14 +173,6 @@ class XgmiGroup:
         # step sees the value, so the hand-off needs no flag and no fence on any topology.
         self.devices = len(set(device_ids)) if device_ids else 1
 
-    @property
-    def push(self) -> bool:
-        return self.xp_mode == 1
-
-    @property
-    def ar_push(self) -> bool:
-        return self.ar_mode == 1
-
     # -- launches --------------------------------------------------------------------------
     def exchange(self) -> dict:
         """grad_reduce kwargs of the one-launch all-reduce: every reduction lane publishes its
@@ -210,7 +182,46 @@ class XgmiGroup:
         err = self.ctr.data_ptr() + 4 * (self.ctr.numel() - 1)  # the same sticky error word
         return dict(xp_regions=list(self.regions), xp_rank=self.rank, xp_capacity=self.capacity,
                     xp_ctr=self.xp_ctr.data_ptr(), xp_err=err, xp_abort=self.abort_dev,
-                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world, xp_mode=self.xp_mode)
+                    xp_timeout_s=self.timeout_s, xp_scale=1.0 / self.world, xp_mode=self.xp_mode,
+                    xp_wait=self._wait_ptr())
+
+    # -- exchange-wait accounting ---------------------------------------------------------------
+    def _wait_ptr(self) -> int:
+        return 0 if self.wait is None else self.wait.data_ptr()
+
+    def enable_wait_stats(self, on: bool = True) -> None:
+        """Record every step's exchange wait (per wave: the longest lane wait, s_memrealtime
+        ticks) in a device ring.  One plain store per wave and step; launches captured into
+        graphs before this call do not record (re-capture after toggling)."""
+        if on and self.wait is None:
+            ring, blocks, waves = self.ext.xgmi_wait_ring()
+            self.wait = torch.zeros(ring * blocks * waves, device=self.comm.device, dtype=torch.int64)
+        elif not on:
+            self.wait = None
+
+    def reset_wait_stats(self) -> None:
+        if self.wait is not None:
+            self.wait.zero_()
+
+    def wait_stats(self) -> dict | None:
+        """Per-step exchange wait over the recorded steps (max over this rank's blocks and
+        waves), in microseconds: {steps, median, p99, max}.  None when nothing was recorded."""
+        if self.wait is None:
+            return None
+        ring, blocks, waves = self.ext.xgmi_wait_ring()
+        w = self.wait.view(ring, blocks * waves).cpu()
+        steps = (w >> 32) & 0xffffffff
+        ticks = (w & 0xffffffff).double()
+        valid = steps.max(dim=1).values > 0
+        if not bool(valid.any()):
+            return None
+        # per ring entry: the longest wait among the words of the entry's newest step
+        newest = steps.max(dim=1, keepdim=True).values
+        per_step = torch.where(steps == newest, ticks, torch.zeros_like(ticks)).max(dim=1).values[valid]
+        us = per_step / 100.0  # 100 MHz ticks -> us
+        q = torch.quantile(us, torch.tensor([0.5, 0.99], dtype=torch.float64))
+        return {"steps": int(us.numel()), "median": round(float(q[0]), 3), "p99": round(float(q[1]), 3),
+                "max": round(float(us.max()), 3)}
 
     def clear_error(self) -> None:
         """Reset the sticky error word (only after every rank's kernels have drained)."""
@@ -225,7 +236,7 @@ class XgmiGroup:
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, n, grad.data_ptr(), grad.data_ptr(),
                                 master.data_ptr(), mom.data_ptr(), shadow.data_ptr() if shadow is not None else 0,
                                 lr, momentum, 1.0 / self.world, mode, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s, self.ar_mode)
+                                self.timeout_s, s, self.ar_mode, self._wait_ptr())
 
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place average of a flat fp32 tensor."""
@@ -233,7 +244,7 @@ class XgmiGroup:
         s = torch.cuda.current_stream(t.device).cuda_stream
         self.ext.xgmi_allreduce(self.regions, self.rank, self.capacity, t.numel(), t.data_ptr(), t.data_ptr(),
                                 0, 0, 0, 0.0, 0.0, 1.0 / self.world, 0, self.ctr.data_ptr(), self.abort_dev,
-                                self.timeout_s, s, self.ar_mode)
+                                self.timeout_s, s, self.ar_mode, 0)
 
     # -- health ------------------------------------------------------------------------------
     def failed(self) -> bool:
@@ -334,10 +345,10 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
               f"regions={[hex(r) for r in grp.regions] if grp is not None and ok else None} "
               f"kind={getattr(grp, 'kind', None)} devices={getattr(grp, 'devices', None)}", file=sys.stderr, flush=True)
     if all(v == 1.0 for v in votes):
-        # the all-reduce kernel's two-hop / push form where it is wanted, kept only if its own
-        # exact self-test passes on every rank
+        # the all-reduce kernel's two-hop form where it is wanted, kept only if its own exact
+        # self-test passes on every rank
         mode = exchange_mode(grp)
-        if mode != 0 and os.environ.get("DNN_XGMI_AR_PUSH", "1") == "1":
+        if mode != 0:
             grp.ar_mode = mode
             try:
                 ok = grp.selftest()
@@ -380,4 +391,4 @@ class XgmiGradSync:
         return self.group.failed()
 
 
-__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "exchange_mode", "one_launch_wanted", "push_wanted", "wanted"]
+__all__ = ["XgmiGroup", "XgmiGradSync", "build_group", "exchange_mode", "one_launch_wanted", "wanted"]

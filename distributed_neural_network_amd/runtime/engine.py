@@ -189,8 +189,7 @@ class HipEngine(Engine):
 
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
-                 use_graphs: bool = True, overlap: bool = False, in_launch_reduce: bool = False,
-                 stage_images: bool | None = None) -> None:
+                 use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if not torch.cuda.is_available():
             raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -229,14 +228,9 @@ class HipEngine(Engine):
         # dependency on its sample ids (stage_images=False / DNN_STAGE_IMAGES=0 turns it off)
         if stage_images is None:
             stage_images = os.environ.get("DNN_STAGE_IMAGES", "1") != "0"
-        self.stage = (torch.zeros(B * (3072 + 4), device=dev, dtype=torch.uint8)
-                      if stage_images and not in_launch_reduce else None)
+        self.stage = torch.zeros(B * (3072 + 4), device=dev, dtype=torch.uint8) if stage_images else None
         self.next_ids = torch.full((B,), -1, device=dev, dtype=torch.int32)  # ids two steps ahead
         self._staged = False  # stage holds this epoch's step-0 batch (set by begin_epoch)
-        # in-launch reducer hand-off counters [rows, slabs, done, error] (lenet_fused.hip);
-        # zero between launches (the last reducer resets them)
-        self.sync = torch.zeros(4, device=dev, dtype=torch.int32)
-        self.in_launch_reduce = in_launch_reduce
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
@@ -316,35 +310,9 @@ class HipEngine(Engine):
                              self.order_len, self._p(self.batch_ids), s,
                              next_ids=self._p(self.next_ids) if self._staged else 0, **xg)
 
-    def _launch_fused_reduce(self, fuse_sgd: int, s: int) -> None:
-        """Fused step with the batch reduction (+ SGD when fuse_sgd) in the same launch."""
-        self.ext.fused_train_reduce(
-            self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids), self.batch,
-            self._p(self.state), self._p(self.master), self._p(self.shadow), self._p(self.a0), self._p(self.h1),
-            self._p(self.h2), self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
-            self._p(self.loss), self._p(self.correct), self._p(self.grad), self._p(self.mom), self._p(self.stats),
-            self._p(self.order), self.order_len, self.lr, self.momentum, fuse_sgd, self._p(self.sync), s)
-
-    def sync_error(self) -> bool:
-        """True if an in-launch reducer gave up waiting (hand-off protocol broken)."""
-        return bool(self.sync[3].item())
-
     def _launch_step(self) -> None:
         assert self.train is not None
         s = self._stream()
-        if self.in_launch_reduce and not self.overlap:
-            if self.grad_sync is None:
-                self._launch_fused_reduce(1, s)
-                return
-            self._launch_fused_reduce(0, s)
-            if getattr(self.grad_sync, "fuses_sgd", False):
-                self.grad_sync.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
-                                             self.momentum, LAYOUT.total)
-                return
-            self.grad_sync.allreduce_grads(self.grad, [(0, LAYOUT.total)])
-            self.ext.sgd_apply(self._p(self.master), self._p(self.grad), self._p(self.mom), self._p(self.shadow),
-                               LAYOUT.total, self.lr, self.momentum, 1.0, 0, self._stream())
-            return
         self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
                              self.order_len, self.batch, self._p(self.state), self._p(self.master),
                              self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
@@ -385,7 +353,10 @@ class HipEngine(Engine):
         """Collective: does the one-launch all-reduce (``grp.exchange()``) reproduce the
         two-launch path (batch reduce, then the xGMI all-reduce kernel) BIT FOR BIT on every
         rank?  Random per-rank reduction inputs, both parity slots; the engine's parameters,
-        optimizer state and buffers are restored afterwards.  Every rank returns the same vote."""
+        optimizer state and buffers are restored afterwards.  Every rank returns the same vote.
+        The ranks vote after EACH pass and stop together at the first failure; a pass that
+        raised or timed out anywhere marks the group ``broken`` (its step counters may differ
+        across ranks from then on)."""
         dev = self.device
         bufs = [self.a0, self.h1, self.h2, self.z1, self.z2, self.z3, self.slab]
         saved = [t.clone() for t in bufs + [self.master, self.mom, self.shadow]]
@@ -398,39 +369,45 @@ class HipEngine(Engine):
             real = LAYOUT.pad_mask().float()
             p0 = (torch.randn(self.master.shape, generator=torch.Generator().manual_seed(3)) * 0.1 * real).to(dev)
             m0 = (torch.randn(self.master.shape, generator=torch.Generator().manual_seed(4)) * 0.01 * real).to(dev)
-        results, err = [], False
+        results, why = [], ""
         timeout, grp.timeout_s = grp.timeout_s, min(grp.timeout_s, 10.0)
+        ok = True
         for one_launch in (False, True):
-            if not err:
-                try:
-                    with torch.cuda.device(dev):
-                        self.master.copy_(p0)
-                        self.mom.copy_(m0)
-                        self.params_changed()
-                        s = self._stream()
-                        for _ in range(steps):
-                            if one_launch:
-                                self._reduce(1, 0, LAYOUT.total, 0, s, **grp.exchange())
-                            else:
-                                self._reduce(0, 0, LAYOUT.total, 0, s)
-                                grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
-                                                  self.momentum, LAYOUT.total)
-                        torch.cuda.synchronize(dev)
-                        results.append((self.master.cpu(), self.mom.cpu(), self.shadow.cpu()))
-                except Exception as e:
-                    err = True
-                    why = f"{type(e).__name__}: {e}"
-            comm.gather_scalars(0.0)  # (every rank) done with these slots before they are reused
+            err = False
+            try:
+                with torch.cuda.device(dev):
+                    self.master.copy_(p0)
+                    self.mom.copy_(m0)
+                    self.params_changed()
+                    s = self._stream()
+                    for _ in range(steps):
+                        if one_launch:
+                            self._reduce(1, 0, LAYOUT.total, 0, s, **grp.exchange())
+                        else:
+                            self._reduce(0, 0, LAYOUT.total, 0, s)
+                            grp.allreduce_sgd(self.grad, self.master, self.mom, self.shadow, self.lr,
+                                              self.momentum, LAYOUT.total)
+                    torch.cuda.synchronize(dev)
+                    err = grp.failed()
+                    why = "wait failed" if err else why
+                    results.append((self.master.cpu(), self.mom.cpu(), self.shadow.cpu()))
+            except Exception as e:
+                err = True
+                why = f"{type(e).__name__}: {e}"
+            # (every rank) done with these slots before they are reused; stop together
+            if any(v != 0.0 for v in comm.gather_scalars(1.0 if err else 0.0)):
+                grp.broken = True
+                ok = False
+                break
         grp.timeout_s = timeout
-        ok = not err and not grp.failed() and all(torch.equal(x, y) for x, y in zip(*results))
+        if ok:
+            same = all(torch.equal(x, y) for x, y in zip(*results))
+            why = "" if same else "mismatch in " + str(
+                [name for name, (x, y) in zip(("master", "mom", "shadow"), zip(*results)) if not torch.equal(x, y)])
+            ok = same
         if not ok and os.environ.get("DNN_DEBUG_XGMI") == "1":
-            if not err:
-                why = "wait failed" if grp.failed() else "mismatch in " + str(
-                    [name for name, (x, y) in zip(("master", "mom", "shadow"), zip(*results)) if not torch.equal(x, y)])
             print(f"[xgmi] rank {comm.rank}: exchange self-test: {why}", file=sys.stderr, flush=True)
         votes = comm.gather_scalars(1.0 if ok else 0.0)
-        if not all(v == 1.0 for v in votes):
-            grp.clear_error()  # the two-launch path must not inherit a failed wait of this test
         with torch.no_grad():
             for t, v in zip(bufs + [self.master, self.mom, self.shadow], saved):
                 t.copy_(v)
@@ -438,8 +415,9 @@ class HipEngine(Engine):
         return all(v == 1.0 for v in votes)
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, self.grad_sync is not None, self.overlap, self.in_launch_reduce, self.order_len,
-               getattr(getattr(self.grad_sync, "group", None), "one_launch", None), self._staged)
+        key = (nsteps, id(self.grad_sync), self.overlap, self.order_len,
+               getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
+               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged)
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.

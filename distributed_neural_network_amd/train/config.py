@@ -13,7 +13,7 @@ argparse crashes on ``--lr 0.01`` / ``--batch-size 8`` from the CLI; quirk §2.7
 New flags: --sync, --device, --data, --data-root, --seed, --save, --resume,
 --drop-rank/--drop-at-epoch/--drop-at-step, --overlap, --compat, --profile,
 --metrics, --log-dir, --graph-chunk, --train-samples/--test-samples, --eval-sharded,
---model, --engine, --dtype, --check-sync.
+--model, --engine, --dtype, --check-sync, --allreduce.
 """
 from __future__ import annotations
 
@@ -71,6 +71,7 @@ class TrainConfig:
     debug_sync: bool = False
     use_graphs: bool = True
     bucket_kb: int = 0
+    allreduce: str = "default"           # step-allreduce transport: default | ab | a StepAllReduce.PATHS name
     extra: dict = field(default_factory=dict)
 
 
@@ -122,6 +123,11 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
     g.add_argument("--bucket-kb", type=int, default=0,
                    help="step-allreduce: split the flat gradient into all-reduce buckets of at most this many "
                         "KB (0 = one fused bucket, latency-optimal for the 248 KB reference gradient)")
+    g.add_argument("--allreduce", default="default",
+                   choices=("default", "ab", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"),
+                   help="step-allreduce transport: default (one-launch xGMI exchange on one node, else RCCL), "
+                        "ab (time every candidate at start-up and keep the fastest; parallel/autotune.py) or a "
+                        "path name")
     g.add_argument("--check-sync", action="store_true",
                    help="after every synchronisation assert that all ranks hold bit-identical parameters "
                         "(cross-rank checksum)")

@@ -173,8 +173,21 @@ class Trainer:
         if c.mode == "single":
             self.policy.reset_momentum_each_epoch = bool(c.momentum_reset)
         self.policy.bucket_kb = c.bucket_kb
+        if c.allreduce not in ("default", "ab") and hasattr(self.policy, "PATHS"):
+            self.policy.path = c.allreduce
         self.policy.attach(self.engine)
         self.sampler = self._sampler()
+        self.allreduce_ab = None
+        if c.allreduce == "ab" and self.comm.distributed and hasattr(self.policy, "PATHS"):
+            # start-up A/B of the per-step all-reduce on this node (parameters restored after)
+            from ..parallel.autotune import allreduce_ab
+            from ..runtime.cursor import EpochCursor
+
+            cur = EpochCursor(self.engine, self.sampler, self.policy, c.batch_size)
+            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur.run, steps=100, warmup=20)
+            self._say(f"[allreduce] start-up A/B (us/step, max over ranks): {self.allreduce_ab['allreduce_ab']}; "
+                      f"using {self.allreduce_ab['allreduce']}")
+            self.run_log.record(event="allreduce_ab", **self.allreduce_ab)
         if self.hb is not None:
             self.engine.poll = self.comm.check_alive  # between graph replays (main thread)
 

@@ -37,10 +37,56 @@ def failvote(out: str) -> None:
     comm.close()
 
 
+def ab(out: str) -> None:
+    """The all-reduce start-up A/B (parallel/autotune.py) over gloo with three test paths: the
+    real host all-reduce, a slower copy of it, and one that fails its install on rank 1 only.
+    Every rank must pick the same (fastest passing) path and get its start parameters back."""
+    import time
+
+    from distributed_neural_network_amd.parallel import StepAllReduce
+    from distributed_neural_network_amd.parallel.autotune import allreduce_ab
+    from distributed_neural_network_amd.parallel.comm import GradAllReduce
+    from distributed_neural_network_amd.runtime.cursor import EpochCursor
+
+    comm = Communicator(device="cpu")
+
+    class Slow(GradAllReduce):
+        def allreduce_grads(self, grad, buckets, before_last=None):
+            time.sleep(0.004)
+            super().allreduce_grads(grad, buckets, before_last)
+
+    class Policy(StepAllReduce):
+        def install(self, engine, name):
+            if name == "slow":
+                engine.grad_sync = Slow(self.comm)
+                return True
+            if name == "flaky":  # agreed outcome: fails everywhere because rank 1 failed
+                return all(v == 1.0 for v in self.comm.gather_scalars(0.0 if self.comm.rank == 1 else 1.0))
+            return super().install(engine, name)
+
+    data = synthetic(256, 3)
+    eng = CpuEngine(batch=16, lr=0.05, momentum=0.9, arena=init_arena(seed=comm.rank + 100))
+    eng.attach(data)
+    policy = Policy(comm)
+    policy.attach(eng)
+    policy.initial_broadcast(eng)
+    start = eng.master.clone()
+    samp = EpochSampler.for_rank(256, comm.rank, comm.world, seed=1, mode="shard")
+    cur = EpochCursor(eng, samp, policy, 16)
+    res = allreduce_ab(policy, eng, cur.run, steps=6, warmup=2, candidates=("torch-pg", "slow", "flaky"))
+    restored = bool(torch.equal(eng.master, start))
+    cur.run(3)  # the adopted path trains: replicas stay identical
+    torch.save({"master": eng.master, "res": res, "restored": restored, "path": policy.path},
+               os.path.join(out, f"ab{comm.rank}.pt"))
+    comm.close()
+
+
 def main(mode: str, out: str, n: int, batch: int, epochs: int) -> None:
     torch.set_num_threads(1)
     if mode == "failvote":
         return failvote(out)
+    if mode == "ab":
+        return ab(out)
     comm = Communicator(device="cpu")
     data = synthetic(n, 3)
     eng = CpuEngine(batch=batch, lr=0.05, momentum=0.9, arena=init_arena(seed=comm.rank + 100))  # differ on purpose

@@ -32,22 +32,6 @@ def test_graphs_are_bitwise_identical_to_eager():
     assert s1.samples == s2.samples == 1000 and s1.batches == 16
 
 
-def test_in_launch_reducers_match_separate_reduce_kernel():
-    """Reducer workgroups inside the fused launch (counter hand-off) must reproduce the
-    two-kernel step bitwise, incl. the tail batch, and leave the counters reset."""
-    data = synthetic(1000, 7)
-    a = init_arena(seed=5)
-    e1 = HipEngine(batch=64, arena=a, in_launch_reduce=False, graph_chunk=8)
-    e2 = HipEngine(batch=64, arena=a, in_launch_reduce=True, graph_chunk=8)
-    m1, s1 = _train(e1, data, 16)
-    m2, s2 = _train(e2, data, 16)
-    assert torch.equal(m1, m2)
-    assert torch.equal(e1.mom, e2.mom) and torch.equal(e1.shadow, e2.shadow)
-    assert s1.loss_sum == s2.loss_sum and s1.correct == s2.correct and s1.samples == s2.samples == 1000
-    assert not e2.sync_error()
-    assert int(e2.sync.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("graphs", [True, False])
 def test_staged_images_match_batch_id_path(graphs):
     """Image staging (the fused kernel of step c stores step c + 1's images; epoch_begin
@@ -102,8 +86,8 @@ assert comm.distributed
 data = synthetic(1000, 5)
 a = init_arena(seed=9)
 res = []
-for sync_on, overlap, inl in [(False, True, False), (True, True, False), (True, False, False), (True, False, True)]:
-    eng = HipEngine(batch=64, arena=a, graph_chunk=4, overlap=overlap, in_launch_reduce=inl)
+for sync_on, overlap in [(False, True), (True, True), (True, False)]:
+    eng = HipEngine(batch=64, arena=a, graph_chunk=4, overlap=overlap)
     pol = make_policy("step-allreduce", comm)
     pol.attach(eng)
     if not sync_on:

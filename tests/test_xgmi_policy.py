@@ -1,43 +1,70 @@
-"""CPU tests of the xGMI exchange-form choice (parallel/xgmi.py ``exchange_mode``).
-
-The kernels themselves are covered by tests/test_xgmi_gpu.py; this pins the policy: the
-one-hop pull form by default, the two-hop and push forms only on request (push only over
-uncached regions), and every rank voting on the region kind."""
-import types
+"""CPU tests of the per-step all-reduce choice: the xGMI exchange form (parallel/xgmi.py
+``exchange_mode``) and the start-up A/B that the multi-GPU bench runs (parallel/autotune.py):
+its selection rule and, over 2 gloo ranks, its collective behaviour (every rank adopts the same
+winner, a path that fails on one rank is excluded everywhere, parameters are restored)."""
+import math
+import os
+import subprocess
+import sys
 
 import pytest
+import torch
 
-from distributed_neural_network_amd.parallel import xgmi
+from distributed_neural_network_amd.parallel import autotune, xgmi
 
-
-def _grp(world, devices, kinds):
-    calls = []
-
-    def gather_scalars(v):
-        calls.append(v)
-        return [1.0 if k == "uncached" else 0.0 for k in kinds]
-
-    comm = types.SimpleNamespace(gather_scalars=gather_scalars)
-    return types.SimpleNamespace(comm=comm, world=world, devices=devices, kind=kinds[0]), calls
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,devices,want", [(1, 1, 0), (2, 2, 0), (4, 4, 0), (8, 8, 0), (4, 1, 0), (8, 1, 0)])
-def test_auto_mode(monkeypatch, world, devices, want):
+def test_auto_mode_is_pull(monkeypatch):
     monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
-    g, calls = _grp(world, devices, ["uncached"] * world)
-    assert xgmi.exchange_mode(g) == want
-    assert len(calls) == 1  # collective: every rank takes part in the vote
+    assert xgmi.exchange_mode() == 0
 
 
 def test_explicit_modes(monkeypatch):
-    for name, want in (("pull", 0), ("push", 1), ("rsag", 2)):
+    for name, want in (("pull", 0), ("rsag", 2)):
         monkeypatch.setenv("DNN_XGMI_EXCHANGE", name)
-        g, _ = _grp(8, 8, ["uncached"] * 8)
-        assert xgmi.exchange_mode(g) == want
-    # push needs uncached regions on EVERY rank
-    monkeypatch.setenv("DNN_XGMI_EXCHANGE", "push")
-    g, _ = _grp(4, 4, ["uncached", "device", "uncached", "uncached"])
-    assert xgmi.exchange_mode(g) == 0 and not xgmi.push_wanted(g)
-    monkeypatch.setenv("DNN_XGMI_EXCHANGE", "ring")
-    with pytest.raises(ValueError):
-        xgmi.exchange_mode(g)
+        assert xgmi.exchange_mode() == want
+    for bad in ("push", "ring"):
+        monkeypatch.setenv("DNN_XGMI_EXCHANGE", bad)
+        with pytest.raises(ValueError):
+            xgmi.exchange_mode()
+
+
+def _r(us, ok=True):
+    return {"us_per_step": us, "ok": ok}
+
+
+def test_choose_fastest_passing():
+    res = {"local": _r(10.0), "xgmi-pull": _r(30.0), "xgmi-rsag": _r(25.0), "rccl": _r(40.0),
+           "rccl-overlap": _r(None, False)}
+    assert autotune.choose(res) == "xgmi-rsag"
+
+
+def test_choose_never_local_and_skips_failed():
+    res = {"local": _r(1.0), "xgmi-pull": _r(5.0, False), "rccl": _r(50.0)}
+    assert autotune.choose(res) == "rccl"
+    assert autotune.choose({"local": _r(1.0)}) is None
+    assert autotune.choose({"rccl": _r(math.inf)}) is None
+
+
+def test_choose_tie_prefers_order():
+    res = {"rccl": _r(20.0), "xgmi-rsag": _r(20.0), "xgmi-pull": _r(20.0)}
+    assert autotune.choose(res) == "xgmi-pull"
+
+
+def test_ab_two_ranks_agree(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "distributed_neural_network_amd.parallel.launch", "-n", "2", "--cpu",
+           os.path.join(ROOT, "tests", "dist_worker.py"), "ab", str(tmp_path), "0", "0", "0"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = [torch.load(tmp_path / f"ab{i}.pt", weights_only=True) for i in range(2)]
+    for g in got:
+        res = g["res"]
+        assert res["allreduce"] == "torch-pg" and g["path"] == "torch-pg", res
+        assert res["failed"] == ["flaky"], res
+        assert res["allreduce_ab"]["slow"] > res["allreduce_ab"]["torch-pg"], res
+        assert res["local_us_per_step"] is not None
+        assert g["restored"], "parameters not restored after the A/B"
+    assert got[0]["res"] == got[1]["res"]  # one decision, from all-reduced numbers only
+    assert torch.equal(got[0]["master"], got[1]["master"])

@@ -22,7 +22,7 @@ PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' 
           "  A1 image landed", "  A2 R1 build + weights landed", "  A3 fc1 DMA issue + barrier"]
 
 
-def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
+def main(reps: int = 50, batch: int = 64):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False)
     eng.attach(tr)
@@ -30,37 +30,25 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
     stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
     blocks = []
     waves_e = []
-    red = []
     rows = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     walls = []
     for r in range(reps):
         eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
         ev0.record()
-        if in_launch:
-            e = eng
-            e.ext.fused_train_reduce(
-                e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.batch, e._p(e.state),
-                e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2), e._p(e.z1), e._p(e.z2),
-                e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct), e._p(e.grad), e._p(e.mom),
-                e._p(e.stats), e._p(e.order), e.order_len, e.lr, e.momentum, 1, e._p(e.sync), e._stream(),
-                stamps=stamps.data_ptr())
-        else:
-            e = eng
-            st = dict(next_ids=e._p(e.next_ids), stage=e._p(e.stage)) if e._staged else {}
-            e.ext.fused_train(e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.order_len, e.batch,
-                              e._p(e.state), e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2),
-                              e._p(e.z1), e._p(e.z2), e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct),
-                              e._stream(), stamps=stamps.data_ptr(), **st)
+        e = eng
+        st = dict(next_ids=e._p(e.next_ids), stage=e._p(e.stage)) if e._staged else {}
+        e.ext.fused_train(e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.order_len, e.batch,
+                          e._p(e.state), e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2),
+                          e._p(e.z1), e._p(e.z2), e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct),
+                          e._stream(), stamps=stamps.data_ptr(), **st)
         ev1.record()
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
         s = stamps.cpu().numpy()
         waves_e.append((s[3000:3008] - s[8]) * 0.01)
-        nb = batch + (39 if in_launch else 0)
+        nb = batch
         blocks.append(s[16:16 + 4 * nb].reshape(nb, 4).copy())
-        if in_launch:
-            red.append((s[12:16] - s[0]) * 0.01)
         rows.append(np.concatenate([np.diff(s[:8]), [s[8] - s[5], s[6] - s[8], s[10] - s[6],
                                                       s[7] - s[10], s[9] - s[0], s[11] - s[9],
                                                       s[1] - s[11]]]) * 0.01)  # 100 MHz ticks -> us
@@ -87,15 +75,7 @@ def main(reps: int = 50, batch: int = 64, in_launch: bool = False):
     slow = np.argsort(-smp[:, 2])[:6]
     print("  slowest blocks:", ", ".join(f"b{i}(xcc{xcc[i]}) start {smp[i, 0]:.2f} rows {smp[i, 1]:.2f} "
                                          f"end {smp[i, 2]:.2f}" for i in slow))
-    if in_launch:
-        red_b = med_b[batch:]
-        print("reducer blocks start min/max %.2f/%.2f  end min/med/max %.2f/%.2f/%.2f us" % (
-            red_b[:, 0].min(), red_b[:, 0].max(), red_b[:, 2].min(), np.median(red_b[:, 2]), red_b[:, 2].max()))
-        r = np.median(np.array(red[5:]), axis=0)
-        print(f"reducers (from block 0 start): fc released {r[0]:.2f} done {r[1]:.2f} | "
-              f"conv released {r[2]:.2f} done {r[3]:.2f} us")
-        assert not eng.sync_error()
 
 
 if __name__ == "__main__":
-    main(in_launch="--in-launch" in sys.argv)
+    main()
