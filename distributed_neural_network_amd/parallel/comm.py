@@ -52,6 +52,10 @@ class Communicator:
         self.store: dist.Store | None = None
         self.aborted = False
         self.watch: Optional[Callable[[], Sequence[int]]] = None  # liveness watch (fault.Heartbeat)
+        self.rccl_error = False  # set by the watchdog when ncclCommGetAsyncError reports an error
+        # set by the watchdog when other members started a recovery of this generation (their
+        # announce_alive): a rank blocked in a collective those peers have left learns it here
+        self.peer_recovery = -1
         # DNN_FORCE_COLLECTIVES=1: build a real process group and issue every collective
         # even at world size 1 (exercises the RCCL + hipGraph-capture path on one GPU)
         self.force = os.environ.get("DNN_FORCE_COLLECTIVES", "0") == "1"
@@ -79,6 +83,13 @@ class Communicator:
         if agent:
             # torchrun's agent (or parallel/launch.py) already serves a TCPStore on
             # MASTER_ADDR:MASTER_PORT; every rank is a client, so any rank may die.
+            self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
+                                       is_master=False, timeout=self.timeout)
+        elif self.env.world > 1 and os.environ.get("DNN_STORE_IN_RANK0", "0") != "1":
+            # no agent (mpiexec / plain env launch): rank 0 starts a stand-alone store process and
+            # every rank is a client, so the store survives rank 0 (parallel/store_server.py)
+            if self.env.rank == 0:
+                self._store_proc = _spawn_store_server(self.env.master_port, self.env.world)
             self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
                                        is_master=False, timeout=self.timeout)
         else:
@@ -121,7 +132,11 @@ class Communicator:
         replay or a collective the main thread is issuing."""
         lost = self.lost()
         if lost:
-            raise CommError(f"peer rank(s) {lost} lost (heartbeat stale)")
+            raise CommError(f"peer rank(s) {lost} lost (heartbeat stale / process exited)")
+        if self.rccl_error:
+            raise CommError("RCCL communicator reported an asynchronous error (ncclCommGetAsyncError)")
+        if self.peer_recovery == self.generation:
+            raise CommError(f"peers entered recovery of generation {self.generation}")
 
     def wait_device(self, poll_s: float = 50e-6) -> None:
         """Wait for this rank's queued GPU work without blocking uninterruptibly.
@@ -152,6 +167,15 @@ class Communicator:
                 xg.abort()
             except Exception:
                 pass
+        nat = getattr(self, "native", None)
+        if nat is not None and os.environ.get("HIP_LAUNCH_BLOCKING") == "1":
+            # --debug-sync: launches block the main thread until the kernel finishes, so an
+            # ncclAllReduce on a dead peer holds it INSIDE the launch, where no interruptible wait
+            # runs - only ncclCommAbort from this thread releases it (NCCL's watchdog pattern)
+            try:
+                nat.abort()
+            except Exception:
+                pass
 
     # -- collectives ---------------------------------------------------------------------
     def _avg_op(self):
@@ -173,6 +197,8 @@ class Communicator:
             lost = set(watch()) & members
             if lost:
                 raise CommError(f"peer rank(s) {sorted(lost)} lost during a collective")
+            if self.peer_recovery == self.generation:
+                raise CommError(f"peers entered recovery of generation {self.generation} during a collective")
             time.sleep(0.0005)
         w.wait()  # re-raises the collective's own error, if any
 
@@ -306,12 +332,18 @@ class Communicator:
         if self.orig_rank in dead:
             raise CommError("a dropped rank cannot join the re-formed group")
         self.abort()
+        self.rccl_error = False
         self.members = [r for r in self.members if r not in set(dead)]
         self.generation += 1
         if self.world > 1 or self.force:
             self._init_group()
 
     def close(self) -> None:
+        if self.store is not None:
+            try:
+                self.store.add("dnn/closed", 1)  # check out (the stand-alone store exits after the last)
+            except Exception:
+                pass
         if dist.is_initialized():
             try:
                 dist.destroy_process_group()
@@ -320,6 +352,20 @@ class Communicator:
 
 
 _REAPERS: list[threading.Thread] = []
+
+
+def _spawn_store_server(port: int, world: int):
+    """Start parallel/store_server.py as a child in its own session (a signal to this rank's
+    process group does not reach it) and return the Popen.  A child process, never an exec of
+    this one; it imports no GPU runtime."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    return subprocess.Popen([sys.executable, "-m", "distributed_neural_network_amd.parallel.store_server",
+                             "--port", str(port), "--world", str(world)], env=env, start_new_session=True,
+                            stdin=subprocess.DEVNULL, cwd=os.path.dirname(os.path.dirname(os.path.dirname(
+                                os.path.abspath(__file__)))))
 
 
 def exit_now_if_reaping(code: int = 0) -> None:

@@ -11,7 +11,11 @@ Capability parity:
       - ``DropInjector``: ``--drop-rank R --drop-at-epoch E [--drop-at-step S]`` makes
         rank R die hard (``os._exit``, no cleanup) at that point;
       - ``Heartbeat``: every rank stamps ``hb/<rank>`` in the rendezvous TCPStore from
-        a background thread; a watchdog marks a rank dead when its stamp goes stale.
+        a background thread every 0.1 s; a watchdog marks a rank dead when its stamp is
+        older than ``DNN_HEARTBEAT_TIMEOUT`` (1 s), when the launcher reports the rank's
+        process gone (``dead/<rank>``, parallel/launch.py - detection within ~0.1 s), or
+        when the native RCCL communicator reports an asynchronous error
+        (``ncclCommGetAsyncError``).
         The thread only flags it (and sets the xGMI abort word, which in-flight kernels
         poll); the main thread notices between graph replays and in its interruptible
         waits (``Communicator.check_alive`` / ``wait_device``), raises ``CommError`` and
@@ -64,23 +68,36 @@ class DropInjector:
             return self.at_step
         return None
 
-    def die(self, orig_rank: int, epoch: int, step: int) -> None:
-        print(f"[fault] injected drop: rank {orig_rank} exits at epoch {epoch} step {step}", flush=True)
+    def die(self, orig_rank: int, epoch: int, step: int, store=None) -> None:
+        t = time.time()
+        if store is not None:
+            try:  # the kill time, for the survivors' detection latency (tools/fault_bench.py)
+                store.set(f"dnn/drop_time/{orig_rank}", repr(t))
+            except Exception:
+                pass
+        print(f"[fault] injected drop: rank {orig_rank} exits at epoch {epoch} step {step} (t={t:.6f})", flush=True)
         os._exit(DROP_EXIT_CODE)
 
 
 class Heartbeat:
     """Background heartbeat + watchdog over the rendezvous TCPStore."""
 
-    def __init__(self, comm: Communicator, period_s: float = 0.2, timeout_s: float | None = None) -> None:
+    def __init__(self, comm: Communicator, period_s: float = 0.1, timeout_s: float | None = None) -> None:
         import torch.distributed as dist
 
         self.comm = comm
         self.period = period_s
-        # DNN_HEARTBEAT_TIMEOUT: seconds without a beat before a peer is declared dead (a
-        # loaded host can starve a live rank's beat thread for a few seconds)
-        self.timeout = float(os.environ.get("DNN_HEARTBEAT_TIMEOUT", "6.0")) if timeout_s is None else timeout_s
+        # DNN_HEARTBEAT_TIMEOUT: seconds without a beat before a peer is declared dead.  A live
+        # rank whose beat thread was starved past it (a loaded host) is flagged, but it still
+        # announces itself alive in the recovery agreement: the recovery is then an all-alive
+        # retry, and the agreement clears the flag (``clear``)
+        self.timeout = float(os.environ.get("DNN_HEARTBEAT_TIMEOUT", "1.0")) if timeout_s is None else timeout_s
         self.dead: set[int] = set()
+        self.detected_at: dict[int, float] = {}  # rank -> time.time() when the watchdog flagged it
+        # rank -> time its flag was cleared by a recovery agreement: staleness counts from here,
+        # so a rank that was only late gets a full timeout to beat again before a new flag
+        self.grace: dict[int, float] = {}
+        self.paused_until = 0.0  # fault injection (DNN_INJECT_BEAT_PAUSE): this rank's beats stop
         self._stop = threading.Event()
         env = comm.env
         # a private client connection for the thread
@@ -92,6 +109,8 @@ class Heartbeat:
         self._thread.start()
 
     def _beat(self) -> None:
+        if time.time() < self.paused_until:
+            return
         self.store.set(f"dnn/hb/{self.comm.orig_rank}", repr(time.time()))
 
     def last_seen(self, rank: int) -> float:
@@ -103,20 +122,57 @@ class Heartbeat:
             return 0.0
 
     def stale(self, rank: int) -> bool:
-        return time.time() - self.last_seen(rank) > self.timeout
+        return time.time() - max(self.last_seen(rank), self.grace.get(rank, 0.0)) > self.timeout
+
+    def reported_dead(self, rank: int) -> bool:
+        """The launcher saw this rank's process exit (parallel/launch.py publishes it)."""
+        try:
+            return bool(self.store.check([f"dnn/dead/{rank}"]))
+        except Exception:
+            return False
+
+    def _flag(self, r: int, why: str) -> None:
+        self.dead.add(r)
+        self.detected_at.setdefault(r, time.time())
+        print(f"[fault] watchdog: rank {r} {why}", flush=True)
+        # flag only: the main thread sees ``comm.lost()`` between graph replays / in its
+        # interruptible waits and does every teardown (ncclCommAbort, group destruction)
+        # itself in Trainer._recover
+        self.comm.signal_lost()
+
+    def clear(self, members) -> None:
+        """Members of the re-formed group are alive by agreement: drop their flags."""
+        now = time.time()
+        for r in members:
+            self.dead.discard(r)
+            self.detected_at.pop(r, None)
+            self.grace[r] = now
 
     def _run(self) -> None:
         while not self._stop.wait(self.period):
             try:
                 self._beat()
                 for r in list(self.comm.members):
-                    if r != self.comm.orig_rank and r not in self.dead and self.stale(r):
-                        self.dead.add(r)
-                        print(f"[fault] watchdog: rank {r} heartbeat stale > {self.timeout}s", flush=True)
-                        # flag only: the main thread sees ``comm.lost()`` between graph
-                        # replays / in its interruptible waits and does every teardown
-                        # (ncclCommAbort, group destruction) itself in Trainer._recover
-                        self.comm.signal_lost()
+                    if r == self.comm.orig_rank or r in self.dead:
+                        continue
+                    if self.reported_dead(r):
+                        self._flag(r, "process exited (reported by the launcher)")
+                    elif self.stale(r):
+                        self._flag(r, f"heartbeat stale > {self.timeout}s")
+                # peers started a recovery of this generation (a live rank they flagged, or a
+                # failed collective on their side): join it instead of waiting in a collective
+                # they have left
+                gen = self.comm.generation
+                if self.comm.peer_recovery != gen and self.store.check([f"dnn/recover/{gen}/begun"]):
+                    self.comm.peer_recovery = gen
+                    self.comm.signal_lost()
+                # native RCCL: an asynchronous error (e.g. ncclRemoteError after a peer died)
+                # flags the communicator itself; check_alive raises on the main thread
+                nat = getattr(self.comm, "native", None)
+                if nat is not None and not self.comm.rccl_error and not nat.healthy():
+                    self.comm.rccl_error = True
+                    print("[fault] watchdog: RCCL communicator reports an asynchronous error", flush=True)
+                    self.comm.signal_lost()
             except Exception:
                 pass
 
@@ -133,27 +189,37 @@ def announce_alive(comm: Communicator) -> None:
     miss the agreement deadline and get excluded."""
     assert comm.store is not None
     comm.store.set(f"dnn/recover/{comm.generation}/alive/{comm.orig_rank}", "1")
+    comm.store.set(f"dnn/recover/{comm.generation}/begun", str(comm.orig_rank))
 
 
-def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0) -> list[int]:
-    """Survivors of generation g agree on the member list of generation g+1."""
+def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0, grace_s: float | None = None) -> list[int]:
+    """Survivors of generation g agree on the member list of generation g+1.
+
+    A member is alive once it announced itself (``announce_alive``).  It is dead at once if the
+    launcher reported its process gone, and dead after ``grace_s`` (default: two heartbeat
+    timeouts) if its heartbeat is stale - a live rank whose beat was only late reaches its own
+    recovery (its next collective fails once the others tore their group down) and announces
+    itself within that grace, so it stays in the group: the recovery is an all-alive retry.
+    Ranks neither stale nor announced are waited for up to ``wait_s``."""
     assert comm.store is not None
     st = comm.store
     p = f"dnn/recover/{comm.generation}/"
     st.set(f"{p}alive/{comm.orig_rank}", "1")
-    deadline = time.time() + wait_s
+    grace = 2.0 * hb.timeout if grace_s is None else grace_s
+    t0 = time.time()
+    deadline = t0 + wait_s
     while True:
         alive, undecided = [], []
         for r in comm.members:
             if st.check([f"{p}alive/{r}"]):
                 alive.append(r)
-            elif hb.stale(r):
-                pass  # dead (a rank the watchdog flagged but that is beating again is waited for)
+            elif hb.reported_dead(r) or (hb.stale(r) and time.time() - t0 > grace):
+                pass  # dead
             else:
                 undecided.append(r)
         if not undecided or time.time() > deadline:
             break
-        time.sleep(0.05)
+        time.sleep(0.02)
     # first survivor to win the compare_set publishes the member list
     won = st.compare_set(f"{p}leader", "", str(comm.orig_rank)).decode() == str(comm.orig_rank)
     if won:
@@ -161,3 +227,14 @@ def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0) -> 
     st.wait([f"{p}members"])
     members = [int(x) for x in st.get(f"{p}members").decode().split(",") if x]
     return members
+
+
+def beat_pause_injection(orig_rank: int, epoch: int) -> float:
+    """Fault injection for tests (``DNN_INJECT_BEAT_PAUSE=rank:epoch:seconds``): this rank's
+    heartbeat thread stops beating for that long at the start of that epoch while the rank itself
+    keeps training - a live rank that LOOKS dead.  Returns the pause (0: none)."""
+    spec = os.environ.get("DNN_INJECT_BEAT_PAUSE", "")
+    if not spec:
+        return 0.0
+    r, e, d = spec.split(":")
+    return float(d) if int(r) == orig_rank and int(e) == epoch else 0.0

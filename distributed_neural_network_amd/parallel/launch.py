@@ -8,7 +8,10 @@ Capability parity: ``mpiexec -n N python data_parallelism_train.py --nb-proc N``
 The launcher hosts the rendezvous TCPStore itself (like torchrun's agent), so any
 rank - rank 0 included - may die and the survivors can still re-form.  Unlike
 torchrun it does NOT tear the job down when one rank exits: a rank that exits with
-the injected-drop code is reported as dropped and the rest keep running.
+the injected-drop code is reported as dropped and the rest keep running.  The moment a
+rank's process exits with a failure code the launcher publishes ``dnn/dead/<rank>`` in the
+store, which the survivors' fault watchdogs read within one beat period (~0.1 s) - far
+sooner than a heartbeat going stale.
 ``torchrun`` and ``mpiexec`` launches work too (parallel/env.py reads their env).
 """
 from __future__ import annotations
@@ -57,11 +60,16 @@ def main(argv=None) -> int:
         for r, p in enumerate(procs):
             if r not in codes and p.poll() is not None:
                 codes[r] = p.returncode
+                if p.returncode != 0:
+                    try:
+                        store.set(f"dnn/dead/{r}", repr(time.time()))
+                    except Exception:
+                        pass
                 if p.returncode == DROP_EXIT_CODE:
                     print(f"[launch] rank {r} dropped (injected failure)", flush=True)
                 elif p.returncode != 0:
                     print(f"[launch] rank {r} exited with code {p.returncode}", flush=True)
-        time.sleep(0.05)
+        time.sleep(0.02)
     del store
     bad = [c for c in codes.values() if c not in (0, DROP_EXIT_CODE)]
     return bad[0] if bad else 0

@@ -17,6 +17,7 @@ a side stream concurrently with the conv-bucket reduction kernel.
 from __future__ import annotations
 
 import os
+import threading
 from typing import Callable, Optional
 
 import torch
@@ -37,6 +38,9 @@ class RcclComm:
         self.ext = native.hip()
         self.version = self.ext.rccl_open(torch_rccl_path())
         self.handle = 0
+        # the watchdog thread polls ncclCommGetAsyncError; the main thread aborts / re-inits:
+        # the lock keeps the poll off a communicator being torn down
+        self._lock = threading.Lock()
         self._init()
 
     def _init(self) -> None:
@@ -64,14 +68,19 @@ class RcclComm:
             raise CommError(f"ncclAllReduce failed: {e}") from e
 
     def healthy(self) -> bool:
-        return self.handle != 0 and self.ext.rccl_async_error(self.handle) == 0
+        """False only if the live communicator reports an asynchronous error (ncclCommGetAsyncError;
+        polled by the fault watchdog, fault.Heartbeat).  An aborted communicator counts as healthy:
+        its failure was already handled."""
+        with self._lock:
+            return self.handle == 0 or self.ext.rccl_async_error(self.handle) == 0
 
     def abort(self) -> None:
         """ncclCommAbort: releases RCCL kernels spinning on a dead peer.  Main thread only
         (Communicator.abort from Trainer._recover); never concurrent with a replay."""
-        if self.handle:
-            self.ext.rccl_abort(self.handle)
-            self.handle = 0
+        with self._lock:
+            if self.handle:
+                h, self.handle = self.handle, 0
+                self.ext.rccl_abort(h)
 
     def reinit(self) -> None:
         """After Communicator.reform: new communicator over the survivors."""

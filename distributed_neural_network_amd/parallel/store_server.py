@@ -1,0 +1,63 @@
+"""Stand-alone rendezvous store for launches without an agent (mpiexec, a plain env launch).
+
+Under ``torchrun`` the agent serves the TCPStore and under ``parallel/launch.py`` the launcher
+does, so any rank may die and the survivors still rendezvous.  Under ``mpiexec -n N``
+(the reference launcher, README.md:28) nobody does: if rank 0 hosted the store, its death would
+take the store - and with it every survivor's recovery - down.  Rank 0 therefore starts THIS
+small process first (a child in its own session, so a signal to rank 0's process group does
+not reach it), every rank including rank 0 connects as a client, and the store outlives any
+single rank.
+
+It exits when every rank of the job has checked out (``dnn/closed`` counter, incremented by
+``Communicator.close``; a rank the recovery dropped counts through ``dnn/dropped``), or when
+nothing has changed for ``--idle`` seconds - no new key, no heartbeat (``dnn/hb/<rank>``) -
+i.e. every rank is gone without checking out.
+
+usage (started by Communicator; not by hand):
+    python -m distributed_neural_network_amd.parallel.store_server --port P --world N
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--idle", type=float, default=3600.0)
+    a = ap.parse_args(argv)
+
+    import torch.distributed as dist
+
+    store = dist.TCPStore(a.host, a.port, a.world + 1, is_master=True, wait_for_workers=False,
+                          timeout=__import__("datetime").timedelta(seconds=30))
+    store.set("dnn/store_server", "up")
+    last_change, last_sig = time.time(), None
+    while True:
+        time.sleep(0.2)
+        try:
+            closed = store.add("dnn/closed", 0)
+            dropped = store.add("dnn/dropped", 0)
+            beats = []
+            for r in range(a.world):
+                k = f"dnn/hb/{r}"
+                beats.append(store.get(k) if store.check([k]) else b"")
+            sig = (closed, dropped, store.num_keys(), tuple(beats))
+        except Exception:
+            return 1
+        if closed + dropped >= a.world:
+            time.sleep(1.0)  # let the last clients finish their final reads
+            return 0
+        if sig != last_sig:
+            last_sig, last_change = sig, time.time()
+        elif time.time() - last_change > a.idle:
+            print(f"[store] no activity for {a.idle:.0f} s: exiting", file=sys.stderr, flush=True)
+            return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import os
 import sys
+import time
 from dataclasses import dataclass
 from typing import Callable, Optional, Protocol
 
@@ -93,6 +94,11 @@ class Engine:
         # watchdog has flagged a dead peer, instead of queueing more work behind a
         # collective that can no longer complete
         self.poll: Optional[Callable[[], None]] = None
+        # interruptible device wait (Trainer installs Communicator.wait_device): every host wait
+        # on this rank's queued work - graph capture, buffer resizes - polls instead of blocking
+        # in torch.cuda.synchronize, which a collective spinning on a dead peer (native RCCL: no
+        # bounded wait) would never release
+        self.device_wait: Optional[Callable[[], None]] = None
 
     # -- parameters --------------------------------------------------------------------
     def state_dict(self):
@@ -116,6 +122,21 @@ class Engine:
 
     def synchronize(self) -> None:
         pass
+
+    def _wait(self) -> None:
+        """Wait for this rank's queued device work (interruptibly when a watch is installed)."""
+        if self.device_wait is not None:
+            self.device_wait()
+        else:
+            self.synchronize()
+
+    def _wait_event(self, ev) -> None:
+        if self.device_wait is None or self.poll is None:
+            ev.synchronize()
+            return
+        while not ev.query():
+            self.poll()
+            time.sleep(50e-6)
 
 
 class CpuEngine(Engine):
@@ -274,7 +295,7 @@ class HipEngine(Engine):
         order = np.ascontiguousarray(order, dtype=np.int32)
         n = int(order.shape[0])
         if self.order.numel() < n:
-            torch.cuda.synchronize(self.device)
+            self._wait()
             self.order = torch.zeros(n, device=self.device, dtype=torch.int32)
             self.staged = torch.zeros(n, device=self.device, dtype=torch.int32)
             self.invalidate_graphs()
@@ -286,7 +307,7 @@ class HipEngine(Engine):
             i = self._pin_i = self._pin_i ^ 1
             if self._pin[i].numel() < n:
                 self._pin[i] = torch.empty(n, dtype=torch.int32, pin_memory=True)
-            self._pin_ev[i].synchronize()  # this staging buffer's previous upload is done
+            self._wait_event(self._pin_ev[i])  # this staging buffer's previous upload is done
             self._pin[i][:n].numpy()[:] = order
             self.staged[:n].copy_(self._pin[i][:n], non_blocking=True)
             self._pin_ev[i].record(main)
@@ -420,8 +441,9 @@ class HipEngine(Engine):
                getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged)
         g = self._graphs.get(key)
         if g is None:
-            # Capture advances nothing: kernels are recorded, not run.
-            torch.cuda.synchronize(self.device)
+            # Capture advances nothing: kernels are recorded, not run.  The wait before it is
+            # interruptible: queued replays may hold collectives on a dead peer
+            self._wait()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
                 for _ in range(nsteps):

@@ -343,12 +343,12 @@ class LayerEngine(Engine):
         self._bookkeeping(loss, corr)
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, self.grad_sync is not None, self.order_len)
+        key = (nsteps, id(self.grad_sync), self.order_len)
         g = self._graphs.get(key)
         if g is None:
             if not self._warm:
                 self._warmup()
-            torch.cuda.synchronize(self.device)
+            self._wait()  # interruptible (queued replays may hold collectives on a dead peer)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for i in range(nsteps):

@@ -25,7 +25,8 @@ import torch
 
 from ..data import EpochSampler, get_splits
 from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
-from ..parallel.fault import DropInjector, Heartbeat, agree_survivors, announce_alive, simulate_failure
+from ..parallel.fault import (DropInjector, Heartbeat, agree_survivors, announce_alive, beat_pause_injection,
+                              simulate_failure)
 from ..runtime import eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
 from ..utils.metrics import Run
@@ -50,6 +51,12 @@ def resolve_device(spec: str, local_rank: int) -> torch.device:
 class Trainer:
     def __init__(self, cfg: TrainConfig) -> None:
         self.cfg = cfg
+        if os.environ.get("DNN_FAULTHANDLER_S"):
+            # hang forensics: every rank dumps all thread stacks to stderr every N seconds
+            import faulthandler
+            import sys
+
+            faulthandler.dump_traceback_later(float(os.environ["DNN_FAULTHANDLER_S"]), repeat=True, file=sys.stderr)
         self.env = detect()
         self.device = resolve_device(cfg.device, self.env.local_rank)
         if self.device.type == "cuda":
@@ -68,6 +75,8 @@ class Trainer:
         self.run_log = Run(cfg.metrics if self.rank0 else None)
         self.recoveries: list[dict] = []
         self.history: list[dict] = []
+        self._resume_pending: Optional[dict] = None  # recovery record awaiting its first step
+        self._paused: set[int] = set()
 
     # -- helpers --------------------------------------------------------------------------
     def _sampler(self) -> EpochSampler:
@@ -107,24 +116,65 @@ class Trainer:
         if lim is not None and lim <= n:
             self.engine.run_steps(lim)
             self.comm.wait_device()
-            self.drop.die(self.comm.orig_rank, epoch, lim)
+            self.drop.die(self.comm.orig_rank, epoch, lim, self.comm.store)
+        if self._resume_pending is not None and n > 0:
+            # first step on the re-formed group, timed on its own: the end of the recovery
+            self.engine.run_steps(1)
+            self.comm.wait_device()
+            rec = self._resume_pending
+            rec["t_resumed"] = time.time()
+            rec["time_to_resume_s"] = round(rec["t_resumed"] - rec["t_error"], 6)
+            rec["first_step_s"] = round(time.time() - rec["t_reformed"], 6)
+            self._resume_pending = None
+            self._say(f"[fault] first step on the re-formed group done {rec['time_to_resume_s']:.3f} s after the "
+                      f"failure was detected")
+            self.run_log.record(event="resumed", epoch=epoch, **{k: rec[k] for k in (
+                "t_resumed", "time_to_resume_s", "first_step_s", "generation")})
+            n -= 1
         self.engine.run_steps(n)
         self.comm.wait_device()  # interruptible: raises CommError if a peer is declared dead
 
     def _recover(self, epoch: int, snap: tuple[torch.Tensor, torch.Tensor], err: Exception) -> None:
+        """Survivor side of a failure: every stage is timed (wall clock, so the stamps compare
+        across the ranks of one host) and recorded: detect (the watchdog flagged a peer, or the
+        collective failed) -> abort -> agree -> reform -> restore/re-attach -> barrier, then the
+        first step on the new group (``_train_epoch``).  ``recovery_s`` is reform-side only
+        (error caught -> barrier passed); ``detect_s`` (tools/fault_bench.py) and
+        ``time_to_resume_s`` put the detection and the first useful step around it."""
+        t_err = time.time()
         t0 = time.perf_counter()
+        stages = {}
+
+        def stage(name: str) -> None:
+            stages[name] = round(time.perf_counter() - t0, 6)
+            if os.environ.get("DNN_FAULT_TRACE") == "1":
+                print(f"[fault] rank {self.comm.orig_rank} recovery stage {name} at +{stages[name]:.3f} s",
+                      flush=True)
+
         old = list(self.comm.members)
         assert self.hb is not None
+        detected = {r: t for r, t in self.hb.detected_at.items() if r in old}
         # tear our side of the broken group down FIRST: closing its sockets/communicator
         # fails the collectives peers may still be blocked in on us (a gloo ring peer would
         # otherwise sit in recv until our reform, past the agreement deadline)
         announce_alive(self.comm)
         self.comm.abort()
+        stage("abort")
         members = agree_survivors(self.comm, self.hb)
+        stage("agree")
         if self.comm.orig_rank not in members:
             raise RuntimeError("this rank was excluded from the re-formed group") from err
+        # the survivors are alive by agreement: a live rank whose beat was only late must not
+        # stay flagged (check_alive would raise on every later replay / collective)
+        self.hb.clear(members)
         dead = [r for r in old if r not in members]
         self.comm.reform(dead)
+        stage("reform")
+        if dead and self.comm.rank == 0:
+            try:  # the dropped ranks will never check out of the store (parallel/store_server.py)
+                self.comm.store.add("dnn/dropped", len(dead))
+            except Exception:
+                pass
         with torch.no_grad():
             self.engine.master.copy_(snap[0])
             self.engine.mom.copy_(snap[1])
@@ -134,10 +184,15 @@ class Trainer:
             self.engine.invalidate_graphs()  # captured collectives belong to the old communicator
         self.policy.attach(self.engine)
         self.sampler = self._sampler()
+        stage("reattach")
         self.comm.barrier()
+        stage("barrier")
         dt = time.perf_counter() - t0
         rec = {"epoch": epoch, "dead": dead, "survivors": members, "generation": self.comm.generation,
-               "recovery_s": dt, "error": str(err).splitlines()[0][:200] if str(err) else type(err).__name__}
+               "recovery_s": dt, "stages_s": stages, "t_error": t_err,
+               "t_detected": min(detected.values()) if detected else None,
+               "error": str(err).splitlines()[0][:200] if str(err) else type(err).__name__}
+        self._resume_pending = dict(rec, t_reformed=time.time())
         self.recoveries.append(rec)
         self.rank0 = self.comm.rank == 0
         if self.comm.rank == 0:
@@ -190,6 +245,7 @@ class Trainer:
             self.run_log.record(event="allreduce_ab", **self.allreduce_ab)
         if self.hb is not None:
             self.engine.poll = self.comm.check_alive  # between graph replays (main thread)
+            self.engine.device_wait = self.comm.wait_device  # graph capture, buffer resizes
 
         start_epoch = 0
         if c.resume:
@@ -221,6 +277,12 @@ class Trainer:
             if c.mode != "single":
                 self._say("Starting epoch ", epoch)
             simulate_failure(self.comm.orig_rank, c.failure_probability, c.failure_duration, self.rng)
+            pause = beat_pause_injection(self.comm.orig_rank, epoch)
+            if pause and self.hb is not None and epoch not in self._paused:
+                self._paused.add(epoch)
+                self.hb.paused_until = time.time() + pause
+                print(f"[fault] injected heartbeat pause: rank {self.comm.orig_rank} stops beating for {pause} s "
+                      f"(epoch {epoch}) while it keeps training", flush=True)
             snap = (self.engine.master.detach().clone(), self.engine.mom.detach().clone())
             try:
                 self.policy.epoch_start(self.engine, epoch)

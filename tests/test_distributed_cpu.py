@@ -29,6 +29,12 @@ def _launch(n, args, cwd, timeout=240):
     return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
 
 
+def _launch_env(n, args, cwd, env_extra, timeout=300):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", **env_extra)
+    cmd = [sys.executable, "-m", "distributed_neural_network_amd.parallel.launch", "-n", str(n), "--cpu"] + args
+    return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
 def _run_worker(tmp_path, mode, world, n=192, batch=16, epochs=2):
     r = _launch(world, [os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(tmp_path), str(n), str(batch),
                         str(epochs)], tmp_path)
@@ -189,9 +195,67 @@ def test_survivor_agreement_counts_early_announcements():
 
     store = dist.TCPStore("127.0.0.1", 0, 1, is_master=True, wait_for_workers=False)
     mk = lambda r: SimpleNamespace(store=store, generation=3, orig_rank=r, members=[0, 1, 2])
-    hb = SimpleNamespace(stale=lambda r: r == 2)
+    hb = SimpleNamespace(stale=lambda r: r == 2, reported_dead=lambda r: r == 2, timeout=1.0)
     announce_alive(mk(1))  # rank 1 is still blocked in its group teardown
     t0 = time.time()
     assert agree_survivors(mk(0), hb, wait_s=5.0) == [0, 1]
     assert time.time() - t0 < 2.0  # nobody undecided: no waiting for the deadline
     assert agree_survivors(mk(1), hb, wait_s=5.0) == [0, 1]  # the late survivor reads the same list
+
+
+def test_live_rank_with_stale_heartbeat_is_retried_not_dropped(tmp_path):
+    """A live rank whose heartbeat stops for longer than the timeout (DNN_INJECT_BEAT_PAUSE) is
+    flagged by its peers; the recovery agreement keeps it (it announces itself within the
+    grace), the flag is cleared, and the run finishes after ONE all-alive retry - no exclusion,
+    no endless retries (the flag used to stay set forever)."""
+    env_extra = {"DNN_INJECT_BEAT_PAUSE": "2:1:1.6", "DNN_HEARTBEAT_TIMEOUT": "1.0"}
+    r = _launch_env(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "12", "--batch-size", "32",
+                        "--sync", "step-allreduce", "--nb-proc", "3", "--train-samples", "3072", "--test-samples",
+                        "128", "--lr", "0.01", "--device", "cpu"], tmp_path, env_extra)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "injected heartbeat pause: rank 2" in r.stdout
+    assert r.stdout.count("with every rank alive; communicator re-created") == 1, r.stdout
+    assert "dropped in epoch" not in r.stdout
+    assert r.stdout.count("Validation loss of updated master model:") == 12
+
+
+def test_straggler_longer_than_heartbeat_timeout_is_not_excluded(tmp_path):
+    """Reference straggler injection (--failure-probability / --failure-duration) sleeps the
+    MAIN thread longer than the 1 s heartbeat timeout: the beat thread keeps beating, so nobody
+    is flagged, nothing is re-formed, every epoch completes."""
+    r = _launch_env(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2", "--batch-size", "32",
+                        "--nb-proc", "3", "--failure-probability", "1.0", "--failure-duration", "1.5"] + SMALL,
+                    tmp_path, {"DNN_HEARTBEAT_TIMEOUT": "1.0"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("failed! Sleeping for 1.5 seconds.") == 6
+    assert "[fault]" not in r.stdout, r.stdout
+    assert r.stdout.count("Validation loss of updated master model:") == 2
+
+
+def test_rank0_drop_under_env_launch(tmp_path):
+    """mpiexec-style launch (RANK / WORLD_SIZE / MASTER_* only, no launcher-hosted store): rank 0
+    starts the stand-alone store process, so when rank 0 itself dies the survivors still agree,
+    re-form and finish (the new rank 0 prints the parent lines)."""
+    import socket
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    procs = []
+    for rank in range(3):
+        env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", RANK=str(rank), WORLD_SIZE="3",
+                   LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="",
+                   HIP_VISIBLE_DEVICES="")
+        for k in ("DNN_STORE_EXTERNAL", "TORCHELASTIC_USE_AGENT_STORE", "LOCAL_WORLD_SIZE"):
+            env.pop(k, None)
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "3", "--batch-size", "32",
+             "--sync", "step-allreduce", "--drop-rank", "0", "--drop-at-epoch", "1", "--drop-at-step", "2",
+             "--nb-proc", "3"] + SMALL, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+            text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    codes = [p.returncode for p in procs]
+    assert codes[0] == 17 and codes[1] == 0 and codes[2] == 0, (codes, outs)
+    out1 = outs[1][0]
+    assert "[fault] rank(s) [0] dropped in epoch 1; communicator re-formed (generation 1, 2 ranks)" in out1, outs
+    assert out1.count("Validation loss of updated master model:") == 2  # epochs 1 and 2 as the new rank 0
