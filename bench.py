@@ -85,7 +85,9 @@ def main():
                          "epoch's val_acc / val_loss carry signal; 96: the easy template set)")
     ap.add_argument("--model", default="lenet", help="lenet (headline) | lenet-bn | cifar-vgg (layer engine)")
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "layers"])
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="bf16: bf16 MFMA operands, fp32 accumulation / master weights (lenet_fused.hip); fp32: "
+                         "fp32 operands throughout, the reference's arithmetic (lenet_f32.hip)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
@@ -110,9 +112,9 @@ def main():
     train = synthetic(args.train_samples, args.seed, True, noise=args.noise)
     test = synthetic(10_000, args.seed, False, noise=args.noise)
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
-    if args.model == "lenet" and args.engine in ("auto", "fused") and args.dtype == "bf16":
+    if args.model == "lenet" and args.engine in ("auto", "fused"):
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                           overlap=args.overlap, use_graphs=not args.no_graphs)
+                           overlap=args.overlap, use_graphs=not args.no_graphs, dtype=args.dtype)
     else:  # modular layer engine (other models / fp32)
         engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
                              dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16), use_graphs=not args.no_graphs)

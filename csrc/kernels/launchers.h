@@ -56,8 +56,18 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
                        hipStream_t stream);
 
 
+// fp32 fused kernel (lenet_f32.hip): same per-sample rows as launch_fused_train, fp32 weights
+// straight from the master arena, no bf16 shadow / image staging
+void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
+                            int batch, const int32_t* state, const float* master, float* a0, float* h1, float* h2,
+                            float* z1, float* z2, float* z3, float* slab, float* loss, int32_t* correct,
+                            hipStream_t stream);
+void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, int base, int count,
+                           const float* master, float* loss, int32_t* correct, hipStream_t stream);
+
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();
+void init_kernels_f32();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
 int grad_reduce_blocks();  // grid of a whole-arena grad_reduce launch (with bookkeeping)
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,

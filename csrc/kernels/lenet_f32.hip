@@ -1,0 +1,528 @@
+// Fused per-sample forward + data-backward + conv weight-gradient kernel, fp32 (gfx950).
+//
+// Capability parity: the reference trains in fp32 (models/model.py:13-18,
+// data_parallelism_train.py:187-199); this is the fp32 counterpart of lenet_fused.hip (bf16
+// MFMA operands).  One workgroup runs, for ONE CIFAR image, the ToTensor/Normalize ingest
+// (data_parallelism_train.py:24-27), conv/relu/maxpool/linear/CrossEntropy forward and every
+// backward op down to the conv weight gradients, writing the same
+// per-sample rows as the bf16 kernel (pooled conv2 output, MLP activations and deltas, the
+// conv weight/bias-gradient slab, loss, correct) - the batch reduction + SGD (grad_reduce,
+// reduce_sgd.hip) is shared and already fp32.
+//
+// Every multiply-add is an fp32 fma with fp32 operands: results differ from PyTorch's fp32 CPU
+// path only by summation order (~1e-6 relative; tests/test_kernels_gpu.py pins 1e-4).
+//
+// MI355X design (why VALU and not MFMA here): f32-input MFMA runs at the f32 VALU rate
+// (v_mfma_f32_16x16x4_f32: 32 MAC/clk/SIMD = v_pk_fma_f32, MI355X_MICROARCH.md), so MFMA only
+// pays where its 16-wide tiles are full.  This net's convolutions have 6 output channels
+// (conv1 fwd/wgrad, conv2 dgrad) - a 16-wide MFMA tile would waste 62 % - so every product is a
+// register-blocked packed fma (v_pk_fma_f32: two outputs per instruction) on the VALU:
+//  * one workgroup = one sample = 16 waves (1024 threads); everything lives in LDS (~137 KB),
+//    except fc1 (192 KB fp32 > LDS): each wave streams 8 of its rows ONCE from L2 into
+//    registers, uses them for the forward GEMV, keeps them through the loss, and reuses the
+//    same registers for the fc1 data gradient - no second pass over fc1;
+//  * ReLU + 2x2 maxpool fused into the conv epilogues with a 2-bit argmax code (4 = no
+//    gradient), exactly as lenet_fused.hip (first max wins, like torch.max_pool2d);
+//  * the conv weight gradients exploit the max-pool sparsity: dY = unpool(d pooled) has ONE
+//    nonzero per 2x2 window, so dW2 / dW1 sum over the 25 / 196 argmax pixels instead of the
+//    100 / 784 dense ones (4x fewer products; zeros add nothing in fp32);
+//  * fixed summation orders everywhere (no atomics): bitwise reproducible run to run.
+#include "launchers.h"
+
+namespace dnn {
+namespace f32k {
+
+constexpr int NT = 1024;
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ---- LDS map (bytes) ----------------------------------------------------------------
+constexpr int L_X = 0;                  // f32 [3][32][32] normalised image            12288
+constexpr int L_WT1 = L_X + 12288;      // f32 [75 (c,ky,kx)][6 o] conv1 weights        1808
+constexpr int L_WT2 = L_WT1 + 1808;     // f32 [150 (c,ky,kx)][16 o] conv2 weights      9600
+constexpr int L_W2N = L_WT2 + 9600;     // f32 [16][150] conv2 weights (dgrad order)   9600
+constexpr int L_P1 = L_W2N + 9600;      // f32 [6][14][14] pooled conv1 output          4704
+constexpr int L_C1 = L_P1 + 4704;       // u8  [6][196] conv1 pool codes                1184
+constexpr int L_A0 = L_C1 + 1184;       // f32 [400] pooled conv2 output (flatten order) 1600
+constexpr int L_C2 = L_A0 + 1600;       // u8  [400] conv2 pool codes                     400
+constexpr int L_BIAS = L_C2 + 400;      // f32 [c1 6 | c2 16 | f1 120 | f2 84 | f3 10]    960
+constexpr int L_H1 = L_BIAS + 960;      // f32 [128]                                      512
+constexpr int L_H2 = L_H1 + 512;        // f32 [96]                                       384
+constexpr int L_DZ3 = L_H2 + 384;       // f32 [16]                                        64
+constexpr int L_DZ2 = L_DZ3 + 64;       // f32 [96]                                       384
+constexpr int L_DZ1 = L_DZ2 + 384;      // f32 [128]                                      512
+constexpr int L_DA0 = L_DZ1 + 512;      // f32 [400]                                     1600
+constexpr int L_F2 = L_DA0 + 1600;      // f32 fc2 [84][120]                            40320
+constexpr int L_F3 = L_F2 + 40320;      // f32 fc3 [10][84]                              3360
+constexpr int L_PART = L_F3 + 3360;     // f32 partial sums: conv2 fwd / fc1 dgrad / dW1 25600
+constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][18] dY2 zero-padded by 4        20736
+constexpr int L_DP1 = L_DY2 + 20736;    // f32 [6][196] masked d(pooled conv1)           4704
+constexpr int LDS_TOTAL = L_DP1 + 4704;  // 140,320 B
+static_assert(LDS_TOTAL <= 163840, "LDS budget");
+constexpr int B_C1 = 0, B_C2 = 6, B_F1 = 22, B_F2 = 142, B_F3 = 226;  // bias offsets (floats)
+constexpr int DY2_LD = 18, DY2_CH = 18 * 18;
+constexpr int W1_PARTS = 11;  // conv1 weight gradient: q split in 11 slices of 18 windows
+static_assert(16 * 400 * 4 <= 25600 && W1_PARTS * 450 * 4 <= 25600 && 200 * 8 * 4 <= 25600, "partials");
+
+// ToTensor + Normalize((.5,.5,.5),(.5,.5,.5)) exactly as PyTorch's fp32 ops: u / 255 correctly
+// rounded (the double quotient of u / 255 is never within a double ulp of a float rounding
+// boundary - its bits repeat u with period 8 - so rounding it to float IS the correctly rounded
+// float quotient), then (t - 0.5) rounded, then / 0.5 (exact).
+__device__ __forceinline__ float u8norm(uint32_t u) {
+  const float t = (float)((double)u / 255.0);
+  return (t - 0.5f) * 2.0f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(NT) lenet_f32_kernel(
+    const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ order,  // TRAIN: this step's sample ids [batch]
+    int order_len, int batch, int base_index, const int32_t* __restrict__ state,
+    const float* __restrict__ master,  // fp32 parameter arena
+    float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
+    float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
+    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x;
+  int bvalid = 1, sample;
+  bool valid;
+  if (TRAIN) {
+    bvalid = state[ST_BVALID];
+    valid = b < bvalid;
+    sample = order[b];
+  } else {
+    const long g = (long)base_index + b;
+    valid = g < order_len;
+    sample = (int)g;
+  }
+  if (!valid) {  // tail of the last batch: zero rows, the reduction adds nothing
+    if (TRAIN) {
+      for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
+      if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = 0.f; z1_out[(size_t)b * Z1_LD + tid] = 0.f; }
+      if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = 0.f; z2_out[(size_t)b * Z2_LD + tid] = 0.f; }
+      if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = 0.f;
+      for (int i = tid; i < SLAB; i += NT) slab_out[(size_t)b * SLAB + i] = 0.f;
+      if (tid == 0) { loss_out[b] = 0.f; correct_out[b] = 0; }
+    }
+    return;
+  }
+  float* X = reinterpret_cast<float*>(smem + L_X);
+  float* WT1 = reinterpret_cast<float*>(smem + L_WT1);
+  float* WT2 = reinterpret_cast<float*>(smem + L_WT2);
+  float* W2N = reinterpret_cast<float*>(smem + L_W2N);
+  float* P1 = reinterpret_cast<float*>(smem + L_P1);
+  uint8_t* C1 = smem + L_C1;
+  float* A0 = reinterpret_cast<float*>(smem + L_A0);
+  uint8_t* C2 = smem + L_C2;
+  float* BIAS = reinterpret_cast<float*>(smem + L_BIAS);
+  float* H1 = reinterpret_cast<float*>(smem + L_H1);
+  float* H2 = reinterpret_cast<float*>(smem + L_H2);
+  float* DZ3 = reinterpret_cast<float*>(smem + L_DZ3);
+  float* DZ2 = reinterpret_cast<float*>(smem + L_DZ2);
+  float* DZ1 = reinterpret_cast<float*>(smem + L_DZ1);
+  float* DA0 = reinterpret_cast<float*>(smem + L_DA0);
+  float* F2 = reinterpret_cast<float*>(smem + L_F2);
+  float* F3 = reinterpret_cast<float*>(smem + L_F3);
+  float* PART = reinterpret_cast<float*>(smem + L_PART);
+  float* DY2 = reinterpret_cast<float*>(smem + L_DY2);
+  float* DP1 = reinterpret_cast<float*>(smem + L_DP1);
+
+  // ============ phase A: ingest + weight staging ========================================
+  {
+    const uint8_t* img = images + (size_t)sample * IMG;
+    if (tid < 192) {
+      const uint4 v = reinterpret_cast<const uint4*>(img)[tid];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = u8norm((w[k] >> (8 * j)) & 0xffu);
+        reinterpret_cast<f4*>(X)[4 * tid + k] = o;
+      }
+    }
+    for (int i = tid; i < 450; i += NT) {
+      const int o = i / 75, k = i - 75 * o;
+      WT1[k * 6 + o] = master[OFF_C1W + i];
+    }
+    for (int i = tid; i < 2400; i += NT) {
+      const float v = master[OFF_C2W + i];
+      const int o = i / 150, k = i - 150 * o;
+      WT2[k * 16 + o] = v;
+      W2N[i] = v;
+    }
+    const f4* f2src = reinterpret_cast<const f4*>(master + OFF_F2W);
+    for (int i = tid; i < 2520; i += NT) reinterpret_cast<f4*>(F2)[i] = f2src[i];
+    if (tid < 210) reinterpret_cast<f4*>(F3)[tid] = reinterpret_cast<const f4*>(master + OFF_F3W)[tid];
+    if (tid < 236) {
+      int src;
+      if (tid < B_C2) src = OFF_C1B + tid;
+      else if (tid < B_F1) src = OFF_C2B + tid - B_C2;
+      else if (tid < B_F2) src = OFF_F1B + tid - B_F1;
+      else if (tid < B_F3) src = OFF_F2B + tid - B_F2;
+      else src = OFF_F3B + tid - B_F3;
+      BIAS[tid] = master[src];
+    }
+    if (TRAIN)
+      for (int i = tid; i < 16 * DY2_CH; i += NT) DY2[i] = 0.f;  // dY2 padding (phase E fills the argmaxes)
+  }
+  __syncthreads();
+
+  // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + 2x2 maxpool ==================
+  // task = (channel pair p, pool window q): 4 pixels x 2 channels of packed accumulators
+  if (tid < 588) {
+    const int p = tid / 196, q = tid - 196 * p, qy = q / 14, qx = q - 14 * qy;
+    f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float xs[6][6];
+      const float* xr = X + c * 1024 + (2 * qy) * 32 + 2 * qx;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const f2 t = *reinterpret_cast<const f2*>(xr + r * 32 + 2 * j);
+          xs[r][2 * j] = t.x;
+          xs[r][2 * j + 1] = t.y;
+        }
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) {
+          const f2 w = *reinterpret_cast<const f2*>(WT1 + (c * 25 + ky * 5 + kx) * 6 + 2 * p);
+          acc[0] += w * xs[ky][kx];
+          acc[1] += w * xs[ky][kx + 1];
+          acc[2] += w * xs[ky + 1][kx];
+          acc[3] += w * xs[ky + 1][kx + 1];
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = 2 * p + h;
+      const float bias = BIAS[B_C1 + o];
+      float best = acc[0][h] + bias;
+      int arg = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        const float v = acc[i][h] + bias;
+        if (v > best) { best = v; arg = i; }
+      }
+      P1[o * 196 + q] = fmaxf(best, 0.f);
+      C1[o * 196 + q] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+    }
+  }
+  __syncthreads();
+
+  // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + 2x2 maxpool =================
+  // task = (input-channel half hh, channel pair pp, pool window w); the second half's partial
+  // sums meet the first half's through LDS (fixed order: c 0-2, then + c 3-5)
+  f2 cacc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  const int c_hh = tid / 200, c_r = tid - 200 * c_hh, c_pp = c_r / 25, c_w = c_r - 25 * c_pp;
+  if (tid < 400) {
+    const int wy = c_w / 5, wx = c_w - 5 * wy;
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      const int c = 3 * c_hh + cc;
+      float xs[6][6];
+      const float* xr = P1 + c * 196 + (2 * wy) * 14 + 2 * wx;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const f2 t = *reinterpret_cast<const f2*>(xr + r * 14 + 2 * j);
+          xs[r][2 * j] = t.x;
+          xs[r][2 * j + 1] = t.y;
+        }
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) {
+          const f2 w = *reinterpret_cast<const f2*>(WT2 + (c * 25 + ky * 5 + kx) * 16 + 2 * c_pp);
+          cacc[0] += w * xs[ky][kx];
+          cacc[1] += w * xs[ky][kx + 1];
+          cacc[2] += w * xs[ky + 1][kx];
+          cacc[3] += w * xs[ky + 1][kx + 1];
+        }
+    }
+    if (c_hh == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) reinterpret_cast<f2*>(PART)[c_r * 4 + i] = cacc[i];
+    }
+  }
+  __syncthreads();
+  if (tid < 200) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cacc[i] += reinterpret_cast<const f2*>(PART)[c_r * 4 + i];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = 2 * c_pp + h;
+      const float bias = BIAS[B_C2 + o];
+      float best = cacc[0][h] + bias;
+      int arg = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        const float v = cacc[i][h] + bias;
+        if (v > best) { best = v; arg = i; }
+      }
+      A0[o * 25 + c_w] = fmaxf(best, 0.f);  // torch.flatten order [16][5][5]
+      C2[o * 25 + c_w] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+    }
+  }
+  // fc1 rows of this wave (o = wave + 16 j): streamed from L2 ONCE, kept in registers through
+  // the loss for the data gradient.  Issued before the barrier: the loads fly while the
+  // conv2 epilogue finishes.
+  f4 r0[8], r1[8];
+  {
+    const f4* w1 = reinterpret_cast<const f4*>(master + OFF_F1W);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = min(wave + 16 * j, 119);
+      r0[j] = w1[o * 100 + lane];
+      r1[j] = w1[o * 100 + 64 + min(lane, 35)];
+    }
+  }
+  __syncthreads();
+
+  // ============ phase D: MLP forward + CrossEntropy =======================================
+  {
+    const f4 a0v = reinterpret_cast<const f4*>(A0)[lane];
+    const f4 a1v = lane < 36 ? reinterpret_cast<const f4*>(A0)[64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = wave + 16 * j;
+      float s = r0[j].x * a0v.x;
+      s = __builtin_fmaf(r0[j].y, a0v.y, s);
+      s = __builtin_fmaf(r0[j].z, a0v.z, s);
+      s = __builtin_fmaf(r0[j].w, a0v.w, s);
+      s = __builtin_fmaf(r1[j].x, a1v.x, s);
+      s = __builtin_fmaf(r1[j].y, a1v.y, s);
+      s = __builtin_fmaf(r1[j].z, a1v.z, s);
+      s = __builtin_fmaf(r1[j].w, a1v.w, s);
+      s = wave_sum(s);
+      if (lane == 0 && o < 120) H1[o] = fmaxf(s + BIAS[B_F1 + o], 0.f);
+    }
+  }
+  __syncthreads();
+  if (tid < 672) {  // fc2: 84 outputs x 8 lanes (15 inputs each)
+    const int o = tid >> 3, s = tid & 7;
+    const float* row = F2 + o * 120 + 15 * s;
+    const float* h = H1 + 15 * s;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) acc = __builtin_fmaf(row[i], h[i], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (s == 0) H2[o] = fmaxf(acc + BIAS[B_F2 + o], 0.f);
+  }
+  __syncthreads();
+  int label = 0;
+  if (wave == 0) {  // fc3 (10 x 84: 4 lanes per logit) + CrossEntropy + accuracy
+    label = labels[sample];
+    const int o = min(lane >> 2, 9), s = lane & 3;
+    const float* row = F3 + o * 84 + 21 * s;
+    const float* h = H2 + 21 * s;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 21; ++i) acc = __builtin_fmaf(row[i], h[i], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    const float logit = __shfl(acc, 4 * min(lane, 9)) + BIAS[B_F3 + min(lane, 9)];
+    const bool act = lane < 10;
+    const float lg = act ? logit : -INFINITY;
+    float mx = lg;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 16));
+    const float e = act ? expf(lg - mx) : 0.f;
+    float sum = e;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
+    int pred = (act && lg == mx) ? lane : 64;  // first max wins (torch.argmax)
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) pred = min(pred, __shfl_xor(pred, off, 16));
+    const float lse = mx + logf(sum);
+    const float ll = __shfl(lg, label & 15, 16);
+    if (lane == 0) {
+      loss_out[b] = lse - ll;
+      correct_out[b] = pred == label ? 1 : 0;
+    }
+    if (TRAIN && lane < 16) DZ3[lane] = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
+  }
+  if (!TRAIN) return;
+  __syncthreads();
+
+  // ============ phase D': MLP data gradient ==============================================
+  if (tid < 84) {  // dh2 = W3^T dz3, ReLU mask
+    float d = 0.f;
+#pragma unroll
+    for (int o = 0; o < 10; ++o) d = __builtin_fmaf(F3[o * 84 + tid], DZ3[o], d);
+    DZ2[tid] = H2[tid] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  if (tid < 480) {  // dh1 = W2^T dz2 (120 x 84: 4 lanes per input), ReLU mask
+    const int i = tid >> 2, s = tid & 3;
+    float d = 0.f;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) d = __builtin_fmaf(F2[(21 * s + k) * 120 + i], DZ2[21 * s + k], d);
+    d += __shfl_xor(d, 1);
+    d += __shfl_xor(d, 2);
+    if (s == 0) DZ1[i] = H1[i] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  {  // dA0 = W1^T dz1 from the fc1 rows still in registers: per-wave partials, then a fixed-order
+     // sum over the 16 waves
+    f4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = wave + 16 * j;
+      const float dz = o < 120 ? DZ1[o] : 0.f;
+      p0 += r0[j] * dz;
+      p1 += r1[j] * dz;
+    }
+    reinterpret_cast<f4*>(PART + wave * 400)[lane] = p0;
+    if (lane < 36) reinterpret_cast<f4*>(PART + wave * 400)[64 + lane] = p1;
+  }
+  __syncthreads();
+  if (tid < 400) {
+    float d = PART[tid];
+#pragma unroll
+    for (int w = 1; w < 16; ++w) d += PART[w * 400 + tid];
+    DA0[tid] = d;  // (the pool2 / ReLU2 mask is applied through C2)
+    a0_out[(size_t)b * A0_LD + tid] = A0[tid];
+  } else if (tid < 520) {
+    h1_out[(size_t)b * H1_LD + tid - 400] = H1[tid - 400];
+    z1_out[(size_t)b * Z1_LD + tid - 400] = DZ1[tid - 400];
+  } else if (tid < 604) {
+    h2_out[(size_t)b * H2_LD + tid - 520] = H2[tid - 520];
+    z2_out[(size_t)b * Z2_LD + tid - 520] = DZ2[tid - 520];
+  } else if (tid < 620) {
+    z3_out[(size_t)b * Z3_LD + tid - 604] = DZ3[tid - 604];
+  }
+  __syncthreads();
+
+  // ============ phase E: conv2 backward ===================================================
+  float* slab = slab_out + (size_t)b * SLAB;
+  if (tid < 400) {  // dY2 = unpool(dA0) at the argmax pixel (zero padding of 4 for the dgrad)
+    const int o = tid / 25, w = tid - 25 * o, wy = w / 5, wx = w - 5 * wy;
+    const int code = C2[tid];
+    if (code < 4) DY2[o * DY2_CH + (4 + 2 * wy + (code >> 1)) * DY2_LD + 4 + 2 * wx + (code & 1)] = DA0[tid];
+  } else if (tid < 416) {  // conv2 bias gradient
+    const int o = tid - 400;
+    float s = 0.f;
+    for (int w = 0; w < 25; ++w) s += C2[o * 25 + w] < 4 ? DA0[o * 25 + w] : 0.f;
+    slab[SLAB_C2B + o] = s;
+  }
+  if (tid >= 512 && tid < 992) {  // conv2 weight gradient over the 25 argmax pixels of channel o
+    const int t = tid - 512, o = t / 30, rem = t - 30 * o, c = rem / 5, ky = rem - 5 * c;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < 25; ++w) {
+      const int code = C2[o * 25 + w];
+      if (code < 4) {
+        const int wy = w / 5, wx = w - 5 * wy;
+        const float v = DA0[o * 25 + w];
+        const float* pr = P1 + c * 196 + (2 * wy + (code >> 1) + ky) * 14 + 2 * wx + (code & 1);
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, pr[kx], acc[kx]);
+      }
+    }
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) slab[SLAB_C2W + o * 150 + c * 25 + ky * 5 + kx] = acc[kx];
+  }
+  __syncthreads();
+  if (tid < 588) {  // conv2 data gradient (full correlation with the padded dY2), 2 pixels per lane
+    const int c = tid / 98, r = tid - 98 * c, py = r / 7, px0 = 2 * (r - 7 * (r / 7));
+    f2 acc = {0.f, 0.f};
+    for (int o = 0; o < 16; ++o) {
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky) {
+        const float* dr = DY2 + o * DY2_CH + (py - ky + 4) * DY2_LD + px0;
+        float d[6];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const f2 t = *reinterpret_cast<const f2*>(dr + 2 * j);
+          d[2 * j] = t.x;
+          d[2 * j + 1] = t.y;
+        }
+        const float* wr = W2N + o * 150 + c * 25 + ky * 5;
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) acc += wr[kx] * f2{d[4 - kx], d[5 - kx]};
+      }
+    }
+    const int q = py * 14 + px0;
+    DP1[c * 196 + q] = C1[c * 196 + q] < 4 ? acc.x : 0.f;          // ReLU1 mask (pool codes)
+    DP1[c * 196 + q + 1] = C1[c * 196 + q + 1] < 4 ? acc.y : 0.f;
+  }
+  __syncthreads();
+
+  // ============ phase F: conv1 weight + bias gradient =====================================
+  if (tid < 6) {
+    float s = 0.f;
+    for (int q = 0; q < 196; ++q) s += DP1[tid * 196 + q];
+    slab[SLAB_C1B + tid] = s;
+  }
+  if (tid >= 64 && tid < 64 + W1_PARTS * 90) {  // dW1 over the 196 argmax pixels, in 11 slices
+    const int t = tid - 64, part = t / 90, rem = t - 90 * part, o = rem / 15, c = (rem / 5) % 3, ky = rem % 5;
+    const int q0 = 18 * part, q1 = min(q0 + 18, 196);
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int q = q0; q < q1; ++q) {
+      const int code = C1[o * 196 + q];
+      if (code < 4) {
+        const int qy = q / 14, qx = q - 14 * qy;
+        const float v = DP1[o * 196 + q];
+        const float* xr = X + c * 1024 + (2 * qy + (code >> 1) + ky) * 32 + 2 * qx + (code & 1);
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, xr[kx], acc[kx]);
+      }
+    }
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) PART[part * 450 + o * 75 + c * 25 + ky * 5 + kx] = acc[kx];
+  }
+  __syncthreads();
+  if (tid < 450) {
+    float s = PART[tid];
+#pragma unroll
+    for (int p = 1; p < W1_PARTS; ++p) s += PART[p * 450 + tid];
+    slab[SLAB_C1W + tid] = s;
+  }
+}
+
+}  // namespace f32k
+
+void init_kernels_f32() {
+  static bool done = false;
+  if (done) return;
+  HIP_CHECK(hipFuncSetAttribute((const void*)f32k::lenet_f32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                f32k::LDS_TOTAL));
+  HIP_CHECK(hipFuncSetAttribute((const void*)f32k::lenet_f32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                f32k::LDS_TOTAL));
+  done = true;
+}
+
+void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
+                            int batch, const int32_t* state, const float* master, float* a0, float* h1, float* h2,
+                            float* z1, float* z2, float* z3, float* slab, float* loss, int32_t* correct,
+                            hipStream_t stream) {
+  init_kernels_f32();
+  hipLaunchKernelGGL(f32k::lenet_f32_kernel<true>, dim3(batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images, labels,
+                     order, order_len, batch, 0, state, master, a0, h1, h2, z1, z2, z3, slab, loss, correct);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, int base, int count,
+                           const float* master, float* loss, int32_t* correct, hipStream_t stream) {
+  init_kernels_f32();
+  if (count <= 0) return;
+  hipLaunchKernelGGL(f32k::lenet_f32_kernel<false>, dim3(count), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images,
+                     labels, nullptr, n, count, base, nullptr, master, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, loss, correct);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dnn

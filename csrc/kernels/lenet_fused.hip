@@ -908,6 +908,7 @@ void init_kernels() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<false, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
+  init_kernels_f32();
   done = true;
 }
 

@@ -77,10 +77,11 @@ def get_splits(kind: str, root: str = "./data", n_train: int | None = None, n_te
         if n_test is not None:
             te = Split(te.images[:n_test], te.labels[:n_test], te.name)
         return tr, te
-    if kind == "synthetic":
-        return (synthetic(CIFAR_TRAIN if n_train is None else n_train, seed, True),
-                synthetic(CIFAR_TEST if n_test is None else n_test, seed, False))
-    raise ValueError(f"unknown dataset kind {kind!r} (expected 'synthetic' or 'cifar10')")
+    if kind in ("synthetic", "synthetic-hard"):
+        noise = SYNTH_NOISE if kind == "synthetic" else SYNTH_NOISE_HARD
+        return (synthetic(CIFAR_TRAIN if n_train is None else n_train, seed, True, noise),
+                synthetic(CIFAR_TEST if n_test is None else n_test, seed, False, noise))
+    raise ValueError(f"unknown dataset kind {kind!r} (expected 'synthetic', 'synthetic-hard' or 'cifar10')")
 
 
 def write_cifar_bin(path: str | os.PathLike, images: np.ndarray, labels: np.ndarray) -> None:

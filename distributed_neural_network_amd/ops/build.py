@@ -28,6 +28,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = [
     CSRC / "kernels" / "lenet_fused.hip",
+    CSRC / "kernels" / "lenet_f32.hip",
     CSRC / "kernels" / "reduce_sgd.hip",
     CSRC / "kernels" / "layers.hip",
     CSRC / "kernels" / "conv_igemm.hip",

@@ -39,6 +39,7 @@ from ..ops import native
 from .comm import CommError, Communicator
 
 MAX_RANKS = 8
+MAX_SHARED = 2  # ranks that may time-share one GPU and still use the exchange (rehearsals / tests)
 _ids = itertools.count()
 
 
@@ -321,6 +322,17 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
     if not single_node:
         if comm.rank == 0:
             print("[xgmi] ranks span several hosts: per-step all-reduce over RCCL", file=sys.stderr, flush=True)
+        return None
+    per_dev = max(device_ids.count(d) for d in device_ids)
+    if per_dev > MAX_SHARED and os.environ.get("DNN_XGMI_SHARED_OK") != "1":
+        # The exchange's waits assume every rank's kernels make progress.  Ranks time-sharing
+        # one GPU compete for its CUs: with >2 of them, the blocks spinning in their exchange
+        # can hold enough CUs that a peer's fused kernel (1 workgroup per CU, whole register
+        # file) cannot be dispatched - a stall until the wait bound (profiles/r3/fault_bench/).
+        # One process per GPU (the product setup) never shares.
+        if comm.rank == 0:
+            print(f"[xgmi] {per_dev} ranks share one GPU: exchange progress is not guaranteed there; "
+                  f"per-step all-reduce over the process group", file=sys.stderr, flush=True)
         return None
     grp, ok, why = None, True, ""
     try:

@@ -210,8 +210,15 @@ class HipEngine(Engine):
 
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
-                 use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None) -> None:
+                 use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None,
+                 dtype: str = "bf16") -> None:
         super().__init__(batch, lr, momentum, arena, seed)
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError(f"HipEngine dtype must be bf16 or fp32, not {dtype!r}")
+        # bf16: lenet_fused.hip (bf16 MFMA operands from the optimizer-packed shadow, fp32
+        # accumulation); fp32: lenet_f32.hip (fp32 operands straight from the master arena -
+        # the reference's arithmetic).  Both write the same per-sample rows for grad_reduce.
+        self.dtype = dtype
         if not torch.cuda.is_available():
             raise RuntimeError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.ext = native.hip()
@@ -248,7 +255,9 @@ class HipEngine(Engine):
         # ([B][3072] u8 | [B] int32; lenet_fused.hip), so a step's image load has no
         # dependency on its sample ids (stage_images=False / DNN_STAGE_IMAGES=0 turns it off)
         if stage_images is None:
-            stage_images = os.environ.get("DNN_STAGE_IMAGES", "1") != "0"
+            stage_images = os.environ.get("DNN_STAGE_IMAGES", "1") != "0" and dtype == "bf16"
+        if stage_images and dtype != "bf16":
+            raise ValueError("image staging is a feature of the bf16 kernel")
         self.stage = torch.zeros(B * (3072 + 4), device=dev, dtype=torch.uint8) if stage_images else None
         self.next_ids = torch.full((B,), -1, device=dev, dtype=torch.int32)  # ids two steps ahead
         self._staged = False  # stage holds this epoch's step-0 batch (set by begin_epoch)
@@ -334,13 +343,20 @@ class HipEngine(Engine):
     def _launch_step(self) -> None:
         assert self.train is not None
         s = self._stream()
-        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
-                             self.order_len, self.batch, self._p(self.state), self._p(self.master),
-                             self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
-                             self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
-                             self._p(self.loss), self._p(self.correct), s,
-                             next_ids=self._p(self.next_ids) if self._staged else 0,
-                             stage=self._p(self.stage) if self._staged else 0)
+        if self.dtype == "fp32":
+            self.ext.fused_train_f32(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
+                                     self.order_len, self.batch, self._p(self.state), self._p(self.master),
+                                     self._p(self.a0), self._p(self.h1), self._p(self.h2), self._p(self.z1),
+                                     self._p(self.z2), self._p(self.z3), self._p(self.slab), self._p(self.loss),
+                                     self._p(self.correct), s)
+        else:
+            self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
+                                 self.order_len, self.batch, self._p(self.state), self._p(self.master),
+                                 self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
+                                 self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
+                                 self._p(self.loss), self._p(self.correct), s,
+                                 next_ids=self._p(self.next_ids) if self._staged else 0,
+                                 stage=self._p(self.stage) if self._staged else 0)
         if self.grad_sync is None:
             self._reduce(1, 0, LAYOUT.total, 1, s)
             return
@@ -513,9 +529,13 @@ class HipEngine(Engine):
         corr = torch.zeros(n, device=self.device, dtype=torch.int32)
         if n:
             with torch.cuda.device(self.device):
-                self.ext.fused_eval(self._p(split.images), self._p(split.labels), 0, hi, lo, n,
-                                    self._p(self.master), self._p(self.shadow), self._p(loss), self._p(corr),
-                                    self._stream())
+                if self.dtype == "fp32":
+                    self.ext.fused_eval_f32(self._p(split.images), self._p(split.labels), hi, lo, n,
+                                            self._p(self.master), self._p(loss), self._p(corr), self._stream())
+                else:
+                    self.ext.fused_eval(self._p(split.images), self._p(split.labels), 0, hi, lo, n,
+                                        self._p(self.master), self._p(self.shadow), self._p(loss), self._p(corr),
+                                        self._stream())
         return loss, corr
 
 
@@ -527,25 +547,26 @@ def make_engine(device: str, batch: int, lr: float, momentum: float, arena: torc
                 **kw) -> Engine:
     """Pick the engine for (model, device, dtype).
 
-    * ``fused``  - the reference LeNet as ONE hand-scheduled gfx950 kernel per step, bf16
-      MFMA operands / fp32 accumulation (the performance path; GPU only).
+    * ``fused``  - the reference LeNet as ONE hand-scheduled gfx950 kernel per step (+ the
+      batch reduction): bf16 MFMA operands / fp32 accumulation (lenet_fused.hip, the
+      performance path) or fp32 throughout (lenet_f32.hip, the reference's arithmetic); GPU only.
     * ``layers`` - any zoo model on the generic layer kernels (runtime/layer_engine.py),
       fp32 or bf16 GEMM operands, BatchNorm support; CPU or GPU.
-    * ``auto``   - fused for lenet/bf16 on a GPU, the CPU oracle engine for lenet on the
-      CPU, layers otherwise.
+    * ``auto``   - fused for lenet on a GPU, the CPU oracle engine for lenet on the CPU,
+      layers otherwise.
     """
     if engine not in ENGINES:
         raise ValueError(f"unknown engine {engine!r}; expected one of {ENGINES}")
     if engine == "auto":
         if model == "lenet" and device == "cpu":
             return CpuEngine(batch, lr, momentum, arena, seed)
-        engine = "fused" if (model == "lenet" and dtype == "bf16") else "layers"
+        engine = "fused" if model == "lenet" else "layers"
     if engine == "fused":
         if model != "lenet":
             raise ValueError(f"the fused engine implements the reference lenet only, not {model!r}")
         if device == "cpu":
             return CpuEngine(batch, lr, momentum, arena, seed)
-        return HipEngine(batch, lr, momentum, arena, seed, device=device, **kw)
+        return HipEngine(batch, lr, momentum, arena, seed, device=device, dtype=dtype, **kw)
     from .layer_engine import LayerEngine
     lkw = {k: v for k, v in kw.items() if k in ("use_graphs", "graph_chunk")}
     return LayerEngine(batch, lr, momentum, model=model, arena=arena, seed=seed, device=device,

@@ -87,7 +87,9 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
                         "reference topology (rank 0 = non-training parameter server); step-allreduce: "
                         "per-step bucketed gradient all-reduce")
     g.add_argument("--device", default="auto", help="auto | cpu | cuda | cuda:N (auto: this rank's GPU if any)")
-    g.add_argument("--data", choices=["synthetic", "cifar10"], default="synthetic")
+    g.add_argument("--data", choices=["synthetic", "synthetic-hard", "cifar10"], default="synthetic",
+                   help="synthetic: learnable template + noise CIFAR-shaped set; synthetic-hard: maximal noise "
+                        "(accuracy climbs over several epochs); cifar10: the binary batches under --data-root")
     g.add_argument("--data-root", default="./data", help="directory holding cifar-10-batches-bin/")
     g.add_argument("--train-samples", type=int, default=None, help="use only the first N training samples")
     g.add_argument("--test-samples", type=int, default=None, help="use only the first N test samples")
@@ -118,8 +120,8 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
                    help="fused: one gfx950 kernel per step (lenet, bf16); layers: generic layer kernels "
                         "(any model, fp32 or bf16); auto picks")
     g.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                   help="MFMA/GEMM operand precision (fp32 accumulation always); fp32 = the reference's "
-                        "arithmetic, via the layer engine")
+                   help="operand precision (fp32 accumulation always): bf16 MFMA operands, or fp32 throughout = "
+                        "the reference's arithmetic (fused fp32 kernel for lenet, fp32 GEMMs in the layer engine)")
     g.add_argument("--bucket-kb", type=int, default=0,
                    help="step-allreduce: split the flat gradient into all-reduce buckets of at most this many "
                         "KB (0 = one fused bucket, latency-optimal for the 248 KB reference gradient)")

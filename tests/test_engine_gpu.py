@@ -126,7 +126,7 @@ def test_trainer_layer_engine_on_gpu(tmp_path, model, dtype):
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2",
                         "--batch-size", "32", "--train-samples", "1024", "--test-samples", "256", "--lr", "0.01",
-                        "--model", model, "--dtype", dtype, "--save", "ck.pt", "--device", "cuda"],
+                        "--model", model, "--dtype", dtype, "--engine", "layers", "--save", "ck.pt", "--device", "cuda"],
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("Validation loss of updated master model:") == 2

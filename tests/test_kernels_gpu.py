@@ -137,3 +137,76 @@ def test_eval_matches_oracle():
     assert _rel(loss, ref_loss) < 2e-2
     agree = (corr.cpu() == (logits.argmax(1) == split.labels.long()).int()).float().mean()
     assert agree > 0.98
+
+
+# ---- fp32 fused kernel (lenet_f32.hip): the reference's arithmetic ---------------------------
+
+def _row_rel(got: torch.Tensor, ref: torch.Tensor) -> float:
+    """Largest per-sample-row relative error (rows whose reference is all zero must be zero)."""
+    g, r = got.double().cpu(), ref.double().cpu()
+    num = (g - r).norm(dim=1)
+    den = r.norm(dim=1)
+    zero = den == 0
+    if bool(zero.any()) and float(num[zero].max()) > 0:
+        return float("inf")
+    return float((num[~zero] / den[~zero]).max()) if bool((~zero).any()) else 0.0
+
+
+@pytest.mark.parametrize("B,n", [(1, 1), (3, 2), (16, 13), (64, 64), (257, 200)])
+def test_fused_f32_rows_match_oracle(B, n):
+    """Every per-sample row of the fp32 kernel against the fp32 PyTorch oracle at 1e-4 relative
+    (row by row: activations, deltas, the four conv-gradient segments, loss)."""
+    split = synthetic(300, seed=3)
+    eng = HipEngine(batch=B, seed=1, use_graphs=False, dtype="fp32")
+    eng.attach(split)
+    order = np.arange(5, 5 + n, dtype=np.int32)
+    eng.begin_epoch(order)
+    with torch.cuda.device(eng.device):
+        eng.ext.fused_train_f32(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids),
+                                eng.order_len, eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.a0),
+                                eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
+                                eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), eng._stream())
+    torch.cuda.synchronize()
+    bvalid = min(B, n)
+    idx = torch.from_numpy(order[:bvalid].astype(np.int64))
+    ref = reference.per_sample_outputs(eng.master.cpu(), split.images[idx], split.labels[idx], bvalid)
+    got = {k: getattr(eng, k)[:bvalid].float().cpu() for k in ["a0", "h1", "h2", "z1", "z2", "z3", "slab"]}
+    errs = {k: _row_rel(got[k], ref[k]) for k in got if k != "slab"}
+    for lo, hi, name in [(0, 450, "dW1"), (450, 456, "db1"), (456, 2856, "dW2"), (2856, 2872, "db2")]:
+        errs[name] = _row_rel(got["slab"][:, lo:hi], ref["slab"][:, lo:hi])
+    errs["loss"] = _row_rel(eng.loss[:bvalid, None].cpu(), ref["loss"][:, None])
+    print("fp32 kernel vs fp32 oracle (max row rel err):", {k: f"{v:.2e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < 1e-4, f"{k}: max per-row rel err {v:.3e}"
+    assert torch.equal(eng.correct[:bvalid].cpu(), ref["correct"])
+    if B > n:
+        assert float(eng.a0[bvalid:].abs().sum()) == 0.0 and float(eng.slab[bvalid:].abs().sum()) == 0.0
+
+
+def test_fused_f32_train_steps_track_cpu_oracle():
+    """10 fp32 steps (fused kernel + batch reduction + SGD, graphs) against the plain-PyTorch fp32
+    CPU engine from the same initial weights: parameter updates agree to 1e-4 relative."""
+    split = synthetic(640, seed=5)
+    arena = init_arena(seed=7)
+    hip = HipEngine(batch=64, arena=arena, use_graphs=True, graph_chunk=4, dtype="fp32")
+    cpu = CpuEngine(batch=64, arena=arena)
+    for e in (hip, cpu):
+        e.attach(split)
+        e.begin_epoch(np.arange(640, dtype=np.int32))
+    hip.run_steps(10)
+    cpu.run_steps(10)
+    hs, cs = hip.epoch_stats(), cpu.epoch_stats()
+    assert hs.batches == cs.batches == 10 and hs.samples == cs.samples == 640 and hs.correct == cs.correct
+    assert abs(hs.mean_loss - cs.mean_loss) < 1e-5 * abs(cs.mean_loss)
+    r = _rel(hip.master.cpu() - arena, cpu.master - arena)
+    assert r < 1e-4, f"parameter update rel err {r:.3e}"
+
+
+def test_fused_f32_eval_matches_oracle():
+    split = synthetic(1000, seed=9, train=False)
+    eng = HipEngine(batch=64, seed=2, dtype="fp32")
+    loss, corr = eng.evaluate_samples(split, 0, 1000)
+    logits = reference.forward(eng.master.cpu(), reference.normalize_u8(split.images))
+    ref_loss = torch.nn.functional.cross_entropy(logits, split.labels.long(), reduction="none")
+    assert _rel(loss, ref_loss) < 1e-5
+    assert torch.equal(corr.cpu(), (logits.argmax(1) == split.labels.long()).int())
