@@ -462,13 +462,15 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   __syncthreads();
 
   // ============ phase F: conv1 weight + bias gradient =====================================
-  if (tid < 6) {
+  static_assert(W1_PARTS * 90 + 6 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
+  if (tid >= W1_PARTS * 90 && tid < W1_PARTS * 90 + 6) {
+    const int c = tid - W1_PARTS * 90;
     float s = 0.f;
-    for (int q = 0; q < 196; ++q) s += DP1[tid * 196 + q];
-    slab[SLAB_C1B + tid] = s;
+    for (int q = 0; q < 196; ++q) s += DP1[c * 196 + q];
+    slab[SLAB_C1B + c] = s;
   }
-  if (tid >= 64 && tid < 64 + W1_PARTS * 90) {  // dW1 over the 196 argmax pixels, in 11 slices
-    const int t = tid - 64, part = t / 90, rem = t - 90 * part, o = rem / 15, c = (rem / 5) % 3, ky = rem % 5;
+  if (tid < W1_PARTS * 90) {  // dW1 over the 196 argmax pixels, in 11 slices
+    const int t = tid, part = t / 90, rem = t - 90 * part, o = rem / 15, c = (rem / 5) % 3, ky = rem % 5;
     const int q0 = 18 * part, q1 = min(q0 + 18, 196);
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     for (int q = q0; q < q1; ++q) {
