@@ -75,12 +75,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0);
   m.def("fused_train_f32", [](u images, u labels, u order, int order_len, int batch, u state, u master, u a0, u h1,
-                              u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream) {
+                              u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
     dnn::launch_fused_train_f32(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), order_len,
                                 batch, P<const int32_t>(state), P<const float>(master), P<float>(a0), P<float>(h1),
                                 P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss),
-                                P<int32_t>(correct), S(stream));
-  });
+                                P<int32_t>(correct), S(stream), P<long long>(stamps));
+  }, py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"), py::arg("state"),
+     py::arg("master"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
+     py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("stream"), py::arg("stamps") = 0);
   m.def("fused_eval_f32", [](u images, u labels, int n, int base, int count, u master, u loss, u correct, u stream) {
     dnn::launch_fused_eval_f32(P<const uint8_t>(images), P<const int32_t>(labels), n, base, count,
                                P<const float>(master), P<float>(loss), P<int32_t>(correct), S(stream));

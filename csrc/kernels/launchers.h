@@ -61,7 +61,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
 void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                             int batch, const int32_t* state, const float* master, float* a0, float* h1, float* h2,
                             float* z1, float* z2, float* z3, float* slab, float* loss, int32_t* correct,
-                            hipStream_t stream);
+                            hipStream_t stream, long long* stamps = nullptr);
 void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, int base, int count,
                            const float* master, float* loss, int32_t* correct, hipStream_t stream);
 

@@ -37,12 +37,25 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // ---- LDS map (bytes) ----------------------------------------------------------------
-constexpr int L_X = 0;                  // f32 [3][32][32] normalised image            12288
-constexpr int L_WT1 = L_X + 12288;      // f32 [75 (c,ky,kx)][6 o] conv1 weights        1808
-constexpr int L_WT2 = L_WT1 + 1808;     // f32 [150 (c,ky,kx)][16 o] conv2 weights      9600
-constexpr int L_W2N = L_WT2 + 9600;     // f32 [16][150] conv2 weights (dgrad order)   9600
-constexpr int L_P1 = L_W2N + 9600;      // f32 [6][14][14] pooled conv1 output          4704
-constexpr int L_C1 = L_P1 + 4704;       // u8  [6][196] conv1 pool codes                1184
+// Strides chosen against the 64 x 4 B LDS banks (MI355X_MICROARCH.md §LDS; searched with a bank
+// model for each access pattern): X rows of 46 floats make conv1's 8-byte patch reads
+// conflict-free; P1 channels of 198 floats keep conv2's weight-gradient reads <= 2-way; the conv1
+// weight gradient reads a re-strided copy XW (rows 33, channels 1061: conflict-free) that phase E
+// builds in the dead fc2 region.
+constexpr int X_RS = 46, X_CH = 32 * X_RS;        // normalised image [3][32][46]
+constexpr int XW_RS = 33, XW_CH = 1061;           // its copy for the conv1 weight gradient
+constexpr int P1_CH = 198;                        // pooled conv1 output [6][198] (14 x 14 used)
+constexpr int WD_LD = 28;                         // conv2 dgrad weights [6 c][16 o][28] (25 used)
+constexpr int L_X = 0;                  // f32 [3][X_CH] normalised image                17664
+// forward weights by output-channel PAIR p: [p][c][ky][6 (kx, padded)][2 (o = 2p, 2p + 1)], so
+// one 16-B read delivers two taps of both channels (the packed-fma operand pairs), a kernel row
+// in three reads
+constexpr int WP_R = 12, WP_C = 5 * WP_R;  // floats per (pair, c, ky) / per (pair, c)
+constexpr int L_WT1 = L_X + 17664;      // f32 [3 p][3 c][WP_C] conv1 weights             2160
+constexpr int L_WT2 = L_WT1 + 2160;     // f32 [8 p][6 c][WP_C] conv2 weights            11520
+constexpr int L_WD = L_WT2 + 11520;     // f32 [6][16][WD_LD] conv2 dgrad weights      10752
+constexpr int L_P1 = L_WD + 10752;      // f32 [6][P1_CH] pooled conv1 output          4752
+constexpr int L_C1 = L_P1 + 4752;       // u8  [6][196] conv1 pool codes                1184
 constexpr int L_A0 = L_C1 + 1184;       // f32 [400] pooled conv2 output (flatten order) 1600
 constexpr int L_C2 = L_A0 + 1600;       // u8  [400] conv2 pool codes                     400
 constexpr int L_BIAS = L_C2 + 400;      // f32 [c1 6 | c2 16 | f1 120 | f2 84 | f3 10]    960
@@ -55,12 +68,15 @@ constexpr int L_DA0 = L_DZ1 + 512;      // f32 [400]                            
 constexpr int L_F2 = L_DA0 + 1600;      // f32 fc2 [84][120]                            40320
 constexpr int L_F3 = L_F2 + 40320;      // f32 fc3 [10][84]                              3360
 constexpr int L_PART = L_F3 + 3360;     // f32 partial sums: conv2 fwd / fc1 dgrad / dW1 25600
-constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][18] dY2 zero-padded by 4        20736
-constexpr int L_DP1 = L_DY2 + 20736;    // f32 [6][196] masked d(pooled conv1)           4704
-constexpr int LDS_TOTAL = L_DP1 + 4704;  // 140,320 B
+constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][20] dY2 zero-padded (4 left/top)  23040
+constexpr int L_DP1 = L_DY2 + 23040;    // f32 [6][196] masked d(pooled conv1)           4704
+constexpr int LDS_TOTAL = L_DP1 + 4704;  // 151,472 B
+static_assert(L_WT1 % 16 == 0 && L_WT2 % 16 == 0 && L_WD % 16 == 0 && L_F2 % 16 == 0 && L_DY2 % 16 == 0,
+              "16-B aligned b128 regions");
+static_assert(3 * XW_CH * 4 <= 40320, "XW fits the dead fc2 region");
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 constexpr int B_C1 = 0, B_C2 = 6, B_F1 = 22, B_F2 = 142, B_F3 = 226;  // bias offsets (floats)
-constexpr int DY2_LD = 18, DY2_CH = 18 * 18;
+constexpr int DY2_LD = 20, DY2_CH = 18 * DY2_LD;  // rows of 20: 16-B aligned 8-wide windows
 constexpr int W1_PARTS = 11;  // conv1 weight gradient: q split in 11 slices of 18 windows
 static_assert(16 * 400 * 4 <= 25600 && W1_PARTS * 450 * 4 <= 25600 && 200 * 8 * 4 <= 25600, "partials");
 
@@ -72,6 +88,12 @@ __device__ __forceinline__ float u8norm(uint32_t u) {
   const float t = (float)((double)u / 255.0);
   return (t - 0.5f) * 2.0f;
 }
+
+// Barrier for LDS hand-offs only: s_waitcnt lgkmcnt(0) + s_barrier.  __syncthreads() would also
+// wait for vmcnt(0) - every outstanding global load AND store of the wave (gfx9 counts stores in
+// vmcnt) - so a row store or the in-flight fc1 stream would stall every barrier behind it.  The
+// compiler still waits for each global load before the first use of its register.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -87,10 +109,14 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     const float* __restrict__ master,  // fp32 parameter arena
     float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
-    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out) {
+    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
+    long long* __restrict__ stamps) {  // diagnostic: block 0's phase timeline (s_memrealtime, 100 MHz)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
+  const bool stamp = stamps != nullptr && b == 0 && tid == 0;
+#define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+  STAMP(0);
   int bvalid = 1, sample;
   bool valid;
   if (TRAIN) {
@@ -116,7 +142,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   float* X = reinterpret_cast<float*>(smem + L_X);
   float* WT1 = reinterpret_cast<float*>(smem + L_WT1);
   float* WT2 = reinterpret_cast<float*>(smem + L_WT2);
-  float* W2N = reinterpret_cast<float*>(smem + L_W2N);
+  float* WD = reinterpret_cast<float*>(smem + L_WD);
   float* P1 = reinterpret_cast<float*>(smem + L_P1);
   uint8_t* C1 = smem + L_C1;
   float* A0 = reinterpret_cast<float*>(smem + L_A0);
@@ -137,26 +163,27 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   // ============ phase A: ingest + weight staging ========================================
   {
     const uint8_t* img = images + (size_t)sample * IMG;
-    if (tid < 192) {
+    if (tid < 192) {  // 16 pixels of row (c, y) = tid / 2, columns 16 (tid & 1) ..
       const uint4 v = reinterpret_cast<const uint4*>(img)[tid];
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const int row = tid >> 1, c = row >> 5, y = row & 31;
+      float* dst = X + c * X_CH + y * X_RS + 16 * (tid & 1);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        f4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = u8norm((w[k] >> (8 * j)) & 0xffu);
-        reinterpret_cast<f4*>(X)[4 * tid + k] = o;
-      }
+      for (int k = 0; k < 8; ++k)
+        reinterpret_cast<f2*>(dst)[k] = f2{u8norm((w[k >> 1] >> (16 * (k & 1))) & 0xffu),
+                                           u8norm((w[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu)};
     }
     for (int i = tid; i < 450; i += NT) {
-      const int o = i / 75, k = i - 75 * o;
-      WT1[k * 6 + o] = master[OFF_C1W + i];
+      const int o = i / 75, k = i - 75 * o, c = k / 25;
+      const int t = k - 25 * c, ky = t / 5;
+      WT1[((o >> 1) * 3 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = master[OFF_C1W + i];
     }
     for (int i = tid; i < 2400; i += NT) {
       const float v = master[OFF_C2W + i];
-      const int o = i / 150, k = i - 150 * o;
-      WT2[k * 16 + o] = v;
-      W2N[i] = v;
+      const int o = i / 150, k = i - 150 * o, c = k / 25;
+      const int t = k - 25 * c, ky = t / 5;
+      WT2[((o >> 1) * 6 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = v;
+      WD[(c * 16 + o) * WD_LD + k - 25 * c] = v;
     }
     const f4* f2src = reinterpret_cast<const f4*>(master + OFF_F2W);
     for (int i = tid; i < 2520; i += NT) reinterpret_cast<f4*>(F2)[i] = f2src[i];
@@ -173,7 +200,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     if (TRAIN)
       for (int i = tid; i < 16 * DY2_CH; i += NT) DY2[i] = 0.f;  // dY2 padding (phase E fills the argmaxes)
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + 2x2 maxpool ==================
   // task = (channel pair p, pool window q): 4 pixels x 2 channels of packed accumulators
@@ -183,25 +211,34 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       float xs[6][6];
-      const float* xr = X + c * 1024 + (2 * qy) * 32 + 2 * qx;
+      const float* xr = X + c * X_CH + (2 * qy) * X_RS + 2 * qx;
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const f2 t = *reinterpret_cast<const f2*>(xr + r * 32 + 2 * j);
+          const f2 t = *reinterpret_cast<const f2*>(xr + r * X_RS + 2 * j);
           xs[r][2 * j] = t.x;
           xs[r][2 * j + 1] = t.y;
         }
 #pragma unroll
-      for (int ky = 0; ky < 5; ++ky)
+      for (int ky = 0; ky < 5; ++ky) {
+        f2 wv[6];
+        const f4* wr = reinterpret_cast<const f4*>(WT1 + (p * 3 + c) * WP_C + ky * WP_R);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const f4 t = wr[j];
+          wv[2 * j] = f2{t.x, t.y};
+          wv[2 * j + 1] = f2{t.z, t.w};
+        }
 #pragma unroll
         for (int kx = 0; kx < 5; ++kx) {
-          const f2 w = *reinterpret_cast<const f2*>(WT1 + (c * 25 + ky * 5 + kx) * 6 + 2 * p);
+          const f2 w = wv[kx];
           acc[0] += w * xs[ky][kx];
           acc[1] += w * xs[ky][kx + 1];
           acc[2] += w * xs[ky + 1][kx];
           acc[3] += w * xs[ky + 1][kx + 1];
         }
+      }
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -214,15 +251,23 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
         const float v = acc[i][h] + bias;
         if (v > best) { best = v; arg = i; }
       }
-      P1[o * 196 + q] = fmaxf(best, 0.f);
+      P1[o * P1_CH + qy * 14 + qx] = fmaxf(best, 0.f);
       C1[o * 196 + q] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(2);
 
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + 2x2 maxpool =================
   // task = (input-channel half hh, channel pair pp, pool window w); the second half's partial
   // sums meet the first half's through LDS (fixed order: c 0-2, then + c 3-5)
+  // fc1 rows of this wave (o = wave + 16 j): streamed from L2 ONCE, kept in registers through
+  // the loss for the data gradient.  Issued now: the loads fly under conv2.
+  // (the first 64 columns of the rows now, the remaining 36 after conv2: register budget)
+  f4 r0[8], r1[8];
+  const f4* w1 = reinterpret_cast<const f4*>(master + OFF_F1W);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r0[j] = w1[min(wave + 16 * j, 119) * 100 + lane];
   f2 cacc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
   const int c_hh = tid / 200, c_r = tid - 200 * c_hh, c_pp = c_r / 25, c_w = c_r - 25 * c_pp;
   if (tid < 400) {
@@ -231,7 +276,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     for (int cc = 0; cc < 3; ++cc) {
       const int c = 3 * c_hh + cc;
       float xs[6][6];
-      const float* xr = P1 + c * 196 + (2 * wy) * 14 + 2 * wx;
+      const float* xr = P1 + c * P1_CH + (2 * wy) * 14 + 2 * wx;
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -241,22 +286,32 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
           xs[r][2 * j + 1] = t.y;
         }
 #pragma unroll
-      for (int ky = 0; ky < 5; ++ky)
+      for (int ky = 0; ky < 5; ++ky) {
+        f2 wv[6];
+        const f4* wr = reinterpret_cast<const f4*>(WT2 + (c_pp * 6 + c) * WP_C + ky * WP_R);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const f4 t = wr[j];
+          wv[2 * j] = f2{t.x, t.y};
+          wv[2 * j + 1] = f2{t.z, t.w};
+        }
 #pragma unroll
         for (int kx = 0; kx < 5; ++kx) {
-          const f2 w = *reinterpret_cast<const f2*>(WT2 + (c * 25 + ky * 5 + kx) * 16 + 2 * c_pp);
+          const f2 w = wv[kx];
           cacc[0] += w * xs[ky][kx];
           cacc[1] += w * xs[ky][kx + 1];
           cacc[2] += w * xs[ky + 1][kx];
           cacc[3] += w * xs[ky + 1][kx + 1];
         }
+      }
     }
     if (c_hh == 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) reinterpret_cast<f2*>(PART)[c_r * 4 + i] = cacc[i];
     }
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(3);
   if (tid < 200) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) cacc[i] += reinterpret_cast<const f2*>(PART)[c_r * 4 + i];
@@ -275,20 +330,10 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       C2[o * 25 + c_w] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
-  // fc1 rows of this wave (o = wave + 16 j): streamed from L2 ONCE, kept in registers through
-  // the loss for the data gradient.  Issued before the barrier: the loads fly while the
-  // conv2 epilogue finishes.
-  f4 r0[8], r1[8];
-  {
-    const f4* w1 = reinterpret_cast<const f4*>(master + OFF_F1W);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int o = min(wave + 16 * j, 119);
-      r0[j] = w1[o * 100 + lane];
-      r1[j] = w1[o * 100 + 64 + min(lane, 35)];
-    }
-  }
-  __syncthreads();
+  for (int j = 0; j < 8; ++j) r1[j] = w1[min(wave + 16 * j, 119) * 100 + 64 + min(lane, 35)];
+  lds_barrier();
+  STAMP(4);
 
   // ============ phase D: MLP forward + CrossEntropy =======================================
   {
@@ -309,7 +354,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       if (lane == 0 && o < 120) H1[o] = fmaxf(s + BIAS[B_F1 + o], 0.f);
     }
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(5);
   if (tid < 672) {  // fc2: 84 outputs x 8 lanes (15 inputs each)
     const int o = tid >> 3, s = tid & 7;
     const float* row = F2 + o * 120 + 15 * s;
@@ -322,7 +368,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     acc += __shfl_xor(acc, 4);
     if (s == 0) H2[o] = fmaxf(acc + BIAS[B_F2 + o], 0.f);
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(6);
   int label = 0;
   if (wave == 0) {  // fc3 (10 x 84: 4 lanes per logit) + CrossEntropy + accuracy
     label = labels[sample];
@@ -356,7 +403,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     if (TRAIN && lane < 16) DZ3[lane] = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
   }
   if (!TRAIN) return;
-  __syncthreads();
+  lds_barrier();
+  STAMP(7);
 
   // ============ phase D': MLP data gradient ==============================================
   if (tid < 84) {  // dh2 = W3^T dz3, ReLU mask
@@ -365,7 +413,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     for (int o = 0; o < 10; ++o) d = __builtin_fmaf(F3[o * 84 + tid], DZ3[o], d);
     DZ2[tid] = H2[tid] > 0.f ? d : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(8);
   if (tid < 480) {  // dh1 = W2^T dz2 (120 x 84: 4 lanes per input), ReLU mask
     const int i = tid >> 2, s = tid & 3;
     float d = 0.f;
@@ -375,7 +424,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     d += __shfl_xor(d, 2);
     if (s == 0) DZ1[i] = H1[i] > 0.f ? d : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(9);
   {  // dA0 = W1^T dz1 from the fc1 rows still in registers: per-wave partials, then a fixed-order
      // sum over the 16 waves
     f4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
@@ -389,7 +439,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     reinterpret_cast<f4*>(PART + wave * 400)[lane] = p0;
     if (lane < 36) reinterpret_cast<f4*>(PART + wave * 400)[64 + lane] = p1;
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(10);
   if (tid < 400) {
     float d = PART[tid];
 #pragma unroll
@@ -405,7 +456,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   } else if (tid < 620) {
     z3_out[(size_t)b * Z3_LD + tid - 604] = DZ3[tid - 604];
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(11);
 
   // ============ phase E: conv2 backward ===================================================
   float* slab = slab_out + (size_t)b * SLAB;
@@ -427,7 +479,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       if (code < 4) {
         const int wy = w / 5, wx = w - 5 * wy;
         const float v = DA0[o * 25 + w];
-        const float* pr = P1 + c * 196 + (2 * wy + (code >> 1) + ky) * 14 + 2 * wx + (code & 1);
+        const float* pr = P1 + c * P1_CH + (2 * wy + (code >> 1) + ky) * 14 + 2 * wx + (code & 1);
 #pragma unroll
         for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, pr[kx], acc[kx]);
       }
@@ -435,31 +487,80 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
     for (int kx = 0; kx < 5; ++kx) slab[SLAB_C2W + o * 150 + c * 25 + ky * 5 + kx] = acc[kx];
   }
-  __syncthreads();
-  if (tid < 588) {  // conv2 data gradient (full correlation with the padded dY2), 2 pixels per lane
-    const int c = tid / 98, r = tid - 98 * c, py = r / 7, px0 = 2 * (r - 7 * (r / 7));
-    f2 acc = {0.f, 0.f};
-    for (int o = 0; o < 16; ++o) {
+  lds_barrier();
+  STAMP(12);
+  // conv2 data gradient: full correlation of the padded dY2 with the kernel.  A lane owns a
+  // 2 x 4 pixel block of one input channel for a quarter of the output channels: per channel o
+  // one 6 x 8 dY2 window (12 aligned 16-B reads) and 25 weights (7 16-B reads, broadcast over the
+  // lanes of the same c and o) feed 8 outputs; the quarters' partial sums meet through LDS in a
+  // fixed order
+  f2 dacc[2][2] = {{{0.f, 0.f}, {0.f, 0.f}}, {{0.f, 0.f}, {0.f, 0.f}}};
+  const int d_q = tid / 168, d_r = tid - 168 * d_q, d_c = d_r / 28, d_yx = d_r - 28 * d_c;
+  const int d_y0 = 2 * (d_yx >> 2), d_x0 = 4 * (d_yx & 3);
+  if (tid < 672) {
 #pragma unroll
-      for (int ky = 0; ky < 5; ++ky) {
-        const float* dr = DY2 + o * DY2_CH + (py - ky + 4) * DY2_LD + px0;
-        float d[6];
+    for (int i = 0; i < 4; ++i) {
+      const int o = 4 * d_q + i;
+      float D[6][8];
+      const f4* dr = reinterpret_cast<const f4*>(DY2 + o * DY2_CH + d_y0 * DY2_LD + d_x0);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const f2 t = *reinterpret_cast<const f2*>(dr + 2 * j);
-          d[2 * j] = t.x;
-          d[2 * j + 1] = t.y;
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f4 t = dr[r * (DY2_LD / 4) + j];
+          D[r][4 * j] = t.x; D[r][4 * j + 1] = t.y; D[r][4 * j + 2] = t.z; D[r][4 * j + 3] = t.w;
         }
-        const float* wr = W2N + o * 150 + c * 25 + ky * 5;
+      float w[28];
+      const f4* wr = reinterpret_cast<const f4*>(WD + (d_c * 16 + o) * WD_LD);
 #pragma unroll
-        for (int kx = 0; kx < 5; ++kx) acc += wr[kx] * f2{d[4 - kx], d[5 - kx]};
+      for (int j = 0; j < 7; ++j) {
+        const f4 t = wr[j];
+        w[4 * j] = t.x; w[4 * j + 1] = t.y; w[4 * j + 2] = t.z; w[4 * j + 3] = t.w;
       }
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx)
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp)
+              dacc[dy][pp] += w[ky * 5 + kx] * f2{D[dy - ky + 4][2 * pp + 4 - kx], D[dy - ky + 4][2 * pp + 5 - kx]};
     }
-    const int q = py * 14 + px0;
-    DP1[c * 196 + q] = C1[c * 196 + q] < 4 ? acc.x : 0.f;          // ReLU1 mask (pool codes)
-    DP1[c * 196 + q + 1] = C1[c * 196 + q + 1] < 4 ? acc.y : 0.f;
+    if (d_q > 0) {
+      f2* part = reinterpret_cast<f2*>(PART) + ((d_q - 1) * 168 + d_r) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part[k] = dacc[k >> 1][k & 1];
+    }
+  } else {  // idle lanes: the re-strided image copy for the conv1 weight gradient (fc2 is dead)
+    float* XW = reinterpret_cast<float*>(smem + L_F2);
+    for (int i = tid - 672; i < 3072; i += NT - 672) {
+      const int c = i >> 10, y = (i >> 5) & 31, x = i & 31;
+      XW[c * XW_CH + y * XW_RS + x] = X[c * X_CH + y * X_RS + x];
+    }
   }
-  __syncthreads();
+  lds_barrier();
+  if (tid < 168) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const f2* part = reinterpret_cast<const f2*>(PART) + (q * 168 + d_r) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dacc[k >> 1][k & 1] += part[k];
+    }
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int x = d_x0 + 2 * pp;
+        if (x < 14) {
+          const int q = (d_y0 + dy) * 14 + x;
+          DP1[d_c * 196 + q] = C1[d_c * 196 + q] < 4 ? dacc[dy][pp].x : 0.f;  // ReLU1 mask (pool codes)
+          DP1[d_c * 196 + q + 1] = C1[d_c * 196 + q + 1] < 4 ? dacc[dy][pp].y : 0.f;
+        }
+      }
+  }
+  lds_barrier();
+  STAMP(13);
 
   // ============ phase F: conv1 weight + bias gradient =====================================
   static_assert(W1_PARTS * 90 + 6 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
@@ -469,6 +570,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     for (int q = 0; q < 196; ++q) s += DP1[c * 196 + q];
     slab[SLAB_C1B + c] = s;
   }
+  const float* XW = reinterpret_cast<const float*>(smem + L_F2);
   if (tid < W1_PARTS * 90) {  // dW1 over the 196 argmax pixels, in 11 slices
     const int t = tid, part = t / 90, rem = t - 90 * part, o = rem / 15, c = (rem / 5) % 3, ky = rem % 5;
     const int q0 = 18 * part, q1 = min(q0 + 18, 196);
@@ -478,7 +580,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       if (code < 4) {
         const int qy = q / 14, qx = q - 14 * qy;
         const float v = DP1[o * 196 + q];
-        const float* xr = X + c * 1024 + (2 * qy + (code >> 1) + ky) * 32 + 2 * qx + (code & 1);
+        const float* xr = XW + c * XW_CH + (2 * qy + (code >> 1) + ky) * XW_RS + 2 * qx + (code & 1);
 #pragma unroll
         for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, xr[kx], acc[kx]);
       }
@@ -486,13 +588,19 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
     for (int kx = 0; kx < 5; ++kx) PART[part * 450 + o * 75 + c * 25 + ky * 5 + kx] = acc[kx];
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(14);
   if (tid < 450) {
     float s = PART[tid];
 #pragma unroll
     for (int p = 1; p < W1_PARTS; ++p) s += PART[p * 450 + tid];
     slab[SLAB_C1W + tid] = s;
   }
+  if (stamp) {
+    __builtin_amdgcn_s_waitcnt(0);
+    STAMP(15);
+  }
+#undef STAMP
 }
 
 }  // namespace f32k
@@ -510,10 +618,10 @@ void init_kernels_f32() {
 void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                             int batch, const int32_t* state, const float* master, float* a0, float* h1, float* h2,
                             float* z1, float* z2, float* z3, float* slab, float* loss, int32_t* correct,
-                            hipStream_t stream) {
+                            hipStream_t stream, long long* stamps) {
   init_kernels_f32();
   hipLaunchKernelGGL(f32k::lenet_f32_kernel<true>, dim3(batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images, labels,
-                     order, order_len, batch, 0, state, master, a0, h1, h2, z1, z2, z3, slab, loss, correct);
+                     order, order_len, batch, 0, state, master, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -523,7 +631,7 @@ void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, 
   if (count <= 0) return;
   hipLaunchKernelGGL(f32k::lenet_f32_kernel<false>, dim3(count), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images,
                      labels, nullptr, n, count, base, nullptr, master, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, loss, correct);
+                     nullptr, nullptr, loss, correct, nullptr);
   HIP_CHECK(hipGetLastError());
 }
 
