@@ -43,7 +43,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
-from distributed_neural_network_amd.parallel.autotune import ORDER, allreduce_ab  # noqa: E402
+from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, allreduce_ab  # noqa: E402
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
@@ -76,9 +76,12 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
-    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + ("default",),
+    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + BF16_PATHS + ("default",),
                     help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
                          "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
+    ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
+                    help="bf16: the A/B also times the xGMI exchanges with bf16 gradient granules (opt-in "
+                         "lower-precision gradient communication; the default path becomes its -bf16 form)")
     ap.add_argument("--ab-steps", type=int, default=300, help="timed steps per candidate and round of the A/B")
     ap.add_argument("--noise", type=int, default=SYNTH_NOISE_HARD,
                     help="synthetic data noise amplitude (255: the hard split of tools/convergence.py, so the "
@@ -123,7 +126,8 @@ def main():
     policy = make_policy(args.sync, comm)
     policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
     policy.record_waits = True  # per-step exchange wait stamps (one store per wave and step)
-    if args.allreduce in ORDER:
+    policy.grad_comm = args.grad_comm
+    if args.allreduce in ORDER + BF16_PATHS:
         policy.path = args.allreduce
     policy.attach(engine)
     policy.initial_broadcast(engine)
@@ -131,7 +135,8 @@ def main():
     ab = {}
     if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
         cur._next_epoch()
-        ab = allreduce_ab(policy, engine, cur.run, steps=args.ab_steps)
+        ab = allreduce_ab(policy, engine, cur.run, steps=args.ab_steps,
+                          candidates=ORDER + (BF16_PATHS if args.grad_comm == "bf16" else ()))
         if comm.rank == 0:
             print(f"[bench] all-reduce A/B (us/step, max over ranks): {ab}", file=sys.stderr, flush=True)
         cur.left = 0  # the timed run starts on a fresh epoch

@@ -121,8 +121,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_scale = xp_scale;
       a.xp_gslot_off = dnn::xgmi_xp_off(xp_capacity);
       a.xp_gslot_bytes = dnn::xgmi_gslot_bytes(xp_capacity);
-      if (xp_mode != 0 && xp_mode != 2)
-        throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull) or 2 (two-hop pull)");
+      if (xp_mode < 0 || xp_mode > 6 || (xp_mode & 1))
+        throw std::runtime_error("grad_reduce exchange: xp_mode 0 (pull) or 2 (two-hop pull), + 4 for bf16 granules");
       a.xp_mode = xp_mode;
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
       a.xp_wait = P<unsigned long long>(xp_wait);

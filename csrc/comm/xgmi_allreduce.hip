@@ -65,7 +65,7 @@ struct XgmiArgs {
   int max_blocks;
   const unsigned* abort_w;  // host-mapped abort word (fault watchdog)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  int form;                 // 0 one-hop pull, 2 two-hop pull (reduce-scatter + all-gather)
+  int form;                 // 0 one-hop pull, 2 two-hop pull (reduce-scatter + all-gather); + 4: bf16 granules
   long long ag_off;         // all-gather slot offset in every region (xgmi_layout.h)
   unsigned long long* wait; // optional: per-step wait ring, as ReduceArgs::xp_wait
 };
@@ -119,8 +119,41 @@ __device__ __forceinline__ void xg_record_wait(const XgmiArgs& a, unsigned step,
         ((unsigned long long)step << 32) | t;
 }
 
+// bf16 granules (PK, form bit 4): a thread's elements k = (0, 1) and (2, 3) travel as ONE word
+// {bf16 | bf16 << 16, step} at the index of the pair's first element, exactly as the one-launch
+// exchange's pairs (kernels/reduce_sgd.hip pack_pairs): every rank sums the same bf16-rounded
+// values in fp32, rank order; the two-hop owner all-gathers its sum as bf16 too.
+template <bool PK>
+__device__ __forceinline__ void xg_pack(float (&x)[XG_PER_THREAD], const bool (&ok)[XG_PER_THREAD],
+                                        const int (&e)[XG_PER_THREAD], unsigned long long* dst,
+                                        unsigned long long tag) {
+#pragma unroll
+  for (int k = 0; k < XG_PER_THREAD; k += 2) {
+    if (!ok[k]) continue;
+    const unsigned lo = bf16_bits(x[k]), hi = ok[k + 1] ? bf16_bits(x[k + 1]) : 0u;
+    x[k] = bf16_lo(lo);
+    x[k + 1] = bf16_lo(hi);
+    if (dst != nullptr)
+      __hip_atomic_store(dst + e[k], tag | (unsigned long long)(lo | (hi << 16)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <bool PK>
+__device__ __forceinline__ void xg_unpack(float (&x)[XG_PER_THREAD], const bool (&ok)[XG_PER_THREAD]) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; k += 2)
+      if (ok[k]) {
+        const unsigned w = __float_as_uint(x[k]);
+        x[k] = bf16_lo(w);
+        x[k + 1] = bf16_hi(w);
+      }
+  }
+}
+
 // NR: group-size bucket (2, 4, 8 >= nranks; 1 for a 1-rank group) sizing the register arrays
-template <int NR>
+template <int NR, bool PK = false>
 __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   unsigned* err_w = a.ctr + a.max_blocks;
@@ -128,7 +161,7 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   const bool failed = a.ctr[a.max_blocks] != 0u;
   const int par = step & 1u;
   const int lo = b * XG_CHUNK;
-  const bool two_hop = a.form == 2;
+  const bool two_hop = (a.form & 2) != 0;
   const int owner = two_hop ? b % a.nranks : a.rank;
   // two-hop tags carry the path bit (its ag slot is shared with grad_reduce's)
   const unsigned want = two_hop ? (step | XG_PATH_BIT) : step;
@@ -138,24 +171,28 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   //    only); the optimizer state is local and only this thread touches it: prefetch it now,
   //    so the update after the gather costs no extra latency
   float v[NR][XG_PER_THREAD];
-  float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD];
+  float p_old[XG_PER_THREAD], m_old[XG_PER_THREAD], g[XG_PER_THREAD];
   int e[XG_PER_THREAD];
   bool ok[XG_PER_THREAD];
   unsigned long long* mine = reinterpret_cast<unsigned long long*>(a.region[a.rank] + par * a.gslot_bytes);
+  const bool publish = !two_hop || owner != a.rank;
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
     ok[k] = lo + k * XG_THREADS + tid < a.n;
     e[k] = min(lo + k * XG_THREADS + tid, a.n - 1);
-    const float g = a.grad[e[k]];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) v[r][k] = g;
+    g[k] = a.grad[e[k]];
     if (a.mode != 0) {
       p_old[k] = a.master[e[k]];
       m_old[k] = a.mom[e[k]];
     }
-    if (ok[k] && (!two_hop || owner != a.rank))
-      __hip_atomic_store(mine + e[k], tag | __float_as_uint(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!PK && ok[k] && publish)
+      __hip_atomic_store(mine + e[k], tag | __float_as_uint(g[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if constexpr (PK) xg_pack<PK>(g, ok, e, publish ? mine : nullptr, tag);
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int k = 0; k < XG_PER_THREAD; ++k) v[r][k] = g[k];
 
   // 2. gather: the one-hop form (and the two-hop owner) reads every peer's pull slot, a two-hop
   //    non-owner the owner's ag slot; all loads of a round in flight before the first check
@@ -169,10 +206,13 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
 #pragma unroll
     for (int k = 0; k < XG_PER_THREAD; ++k) {
       const bool need = gather_all ? (r < a.nranks && r != a.rank) : r == 0;
-      if (need && ok[k]) pending |= 1u << (4 * r + k);
+      if (need && ok[k] && (!PK || (k & 1) == 0)) pending |= 1u << (4 * r + k);
     }
   }
   xg_record_wait(a, step, xg_wait<NR>(a, src, pending, v, e, want, failed, err_w));
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (gather_all ? (r < a.nranks && r != a.rank) : r == 0) xg_unpack<PK>(v[r], ok);
 
   // 3. rank-order sum (two-hop non-owner: the owner's sum), publish (two-hop owner), scale,
   //    optimizer
@@ -188,9 +228,13 @@ __global__ void __launch_bounds__(XG_THREADS) xgmi_allreduce_kernel(XgmiArgs a) 
   }
   if (two_hop && owner == a.rank) {
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.region[a.rank] + a.ag_off + par * a.gslot_bytes);
+    if constexpr (PK) {
+      xg_pack<PK>(sum, ok, e, dst, tag);
+    } else {
 #pragma unroll
-    for (int k = 0; k < XG_PER_THREAD; ++k)
-      if (ok[k]) __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int k = 0; k < XG_PER_THREAD; ++k)
+        if (ok[k]) __hip_atomic_store(dst + e[k], tag | __float_as_uint(sum[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 #pragma unroll
   for (int k = 0; k < XG_PER_THREAD; ++k) {
@@ -321,15 +365,19 @@ void launch_xgmi_allreduce(const std::vector<uintptr_t>& regions, int rank, long
   a.max_blocks = xgmi_max_blocks(capacity);
   a.abort_w = abort_w;
   a.timeout_ticks = (long long)(timeout_s * 1.0e8);
-  if (form != 0 && form != 2) throw std::runtime_error("xgmi all-reduce: form 0 (pull) or 2 (two-hop pull)");
-  a.form = nranks > 1 ? form : 0;
+  if (form < 0 || form > 6 || (form & 1))
+    throw std::runtime_error("xgmi all-reduce: form 0 (pull) or 2 (two-hop pull), + 4 for bf16 granules");
+  a.form = nranks > 1 ? form : (form & 4);  // (one rank: no two-hop; bf16 rounding as the exchange does)
   a.ag_off = xgmi_ag_off(capacity);
   a.wait = wait;
   const int nblk = (n + XG_CHUNK - 1) / XG_CHUNK;
   if (wait != nullptr && nblk > XP_MAX_BLOCKS) throw std::runtime_error("xgmi all-reduce: wait ring holds 128 blocks");
-  auto* kern = nranks == 1 ? &xgmi_allreduce_kernel<1>
-                           : (nranks <= 2 ? &xgmi_allreduce_kernel<2>
-                                          : (nranks <= 4 ? &xgmi_allreduce_kernel<4> : &xgmi_allreduce_kernel<8>));
+  const bool pk = (a.form & 4) != 0;
+  auto* kern = nranks == 1 ? (pk ? &xgmi_allreduce_kernel<1, true> : &xgmi_allreduce_kernel<1>)
+               : pk ? (nranks <= 2 ? &xgmi_allreduce_kernel<2, true>
+                                   : (nranks <= 4 ? &xgmi_allreduce_kernel<4, true> : &xgmi_allreduce_kernel<8, true>))
+                    : (nranks <= 2 ? &xgmi_allreduce_kernel<2>
+                                   : (nranks <= 4 ? &xgmi_allreduce_kernel<4> : &xgmi_allreduce_kernel<8>));
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(XG_THREADS), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }

@@ -61,6 +61,15 @@ constexpr int SH_W2T = SH_WF + 80 * 16 * 8;   // fc2 transposed [120 i][96 o]
 constexpr int SH_W3T = SH_W2T + 120 * 96;     // fc3 transposed [84 i][16 o]
 constexpr int SH_TOTAL = SH_W3T + 84 * 16 + 64;  // + slack so padded fragment reads stay in bounds
 
+// bf16 gradient granules (the xGMI exchanges' bf16 option): round-to-nearest-even bits, and
+// a pair {lo | hi << 16} back to the two floats
+__device__ __forceinline__ unsigned bf16_bits(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+
 __device__ __forceinline__ void write_shadow(bf16* __restrict__ sh, int e, float p) {
   const bf16 v = (bf16)p;
   sh[e] = v;

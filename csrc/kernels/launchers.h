@@ -39,10 +39,12 @@ struct ReduceArgs {
   // block k's elements are owned by rank k % N; the owner reads the peers' pull slots, sums in
   // rank order and publishes {sum, step} in its own ag slot, which the others read (every rank
   // writes only its own region).  Per-link bytes drop from E to 2 E / N granules.
+  // + 4: bf16 granules - a lane's elements travel in pairs as {bf16 | bf16, step} words (half
+  // the granules per link; every rank sums the same bf16-rounded values in fp32, rank order).
   int xp_mode = 0;
   long long xp_ag_off = 0;
   // diagnostic / accounting: per-step exchange wait (max over lanes, s_memrealtime ticks) as
-  // {step << 32 | ticks} words in a ring of XP_WAIT_RING entries (64-bit atomic max)
+  // {step << 32 | ticks} words in a ring of XP_WAIT_RING entries (one plain store per wave)
   unsigned long long* xp_wait = nullptr;
 };
 

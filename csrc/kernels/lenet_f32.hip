@@ -69,15 +69,26 @@ constexpr int L_F2 = L_DA0 + 1600;      // f32 fc2 [84][120]                    
 constexpr int L_F3 = L_F2 + 40320;      // f32 fc3 [10][84]                              3360
 constexpr int L_PART = L_F3 + 3360;     // f32 partial sums: conv2 fwd / fc1 dgrad / dW1 25600
 constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][20] dY2 zero-padded (4 left/top)  23040
-constexpr int L_DP1 = L_DY2 + 23040;    // f32 [6][196] masked d(pooled conv1)           4704
-constexpr int LDS_TOTAL = L_DP1 + 4704;  // 151,472 B
+// conv weight-gradient tables, built from the pool codes while wave 0 runs fc3 + the loss:
+// the ACTIVE windows (ReLU passed) of each channel, compacted in window order, as {dY value,
+// pixel offset}; the offsets are known from the forward pass, the values are filled in by the
+// data-gradient epilogues.  Inactive windows carry no gradient, so the weight-gradient loops
+// walk only the active ones (about half) without a branch.
+constexpr int T1_LD = 207;               // <= 196 active windows + 11 zero pad entries
+constexpr int L_T1 = L_DY2 + 23040;      // f2 [6][T1_LD] {dP1, offset in XW}               9936
+constexpr int L_T2 = L_T1 + 6 * T1_LD * 8;  // f2 [16][25] {dA0, offset in P1}             3200
+constexpr int L_PS1 = L_T2 + 3200;       // u8 [6][196] window -> table slot (255: inactive) 1176
+constexpr int L_PS2 = L_PS1 + 1176;      // u8 [400]                                         400
+constexpr int L_NACT = L_PS2 + 400;      // i32 [6 conv1 | 16 conv2] active-window counts     88
+constexpr int LDS_TOTAL = L_NACT + 88;   // 161,568 B
 static_assert(L_WT1 % 16 == 0 && L_WT2 % 16 == 0 && L_WD % 16 == 0 && L_F2 % 16 == 0 && L_DY2 % 16 == 0,
               "16-B aligned b128 regions");
+static_assert(L_T1 % 8 == 0 && L_T2 % 8 == 0 && L_NACT % 4 == 0, "table alignment");
 static_assert(3 * XW_CH * 4 <= 40320, "XW fits the dead fc2 region");
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 constexpr int B_C1 = 0, B_C2 = 6, B_F1 = 22, B_F2 = 142, B_F3 = 226;  // bias offsets (floats)
 constexpr int DY2_LD = 20, DY2_CH = 18 * DY2_LD;  // rows of 20: 16-B aligned 8-wide windows
-constexpr int W1_PARTS = 11;  // conv1 weight gradient: q split in 11 slices of 18 windows
+constexpr int W1_PARTS = 11;  // conv1 weight gradient: the active windows in 11 slices
 static_assert(16 * 400 * 4 <= 25600 && W1_PARTS * 450 * 4 <= 25600 && 200 * 8 * 4 <= 25600, "partials");
 
 // ToTensor + Normalize((.5,.5,.5),(.5,.5,.5)) exactly as PyTorch's fp32 ops: u / 255 correctly
@@ -94,6 +105,13 @@ __device__ __forceinline__ float u8norm(uint32_t u) {
 // vmcnt) - so a row store or the in-flight fc1 stream would stall every barrier behind it.  The
 // compiler still waits for each global load before the first use of its register.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// v if keep, else +0 - as a bit mask, so the compiler cannot turn the (always safe) LDS load
+// into a branch per element (a select makes it load only under the condition: one LDS round
+// trip per element)
+__device__ __forceinline__ float masked(float v, bool keep) {
+  return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -116,6 +134,14 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   const int b = blockIdx.x;
   const bool stamp = stamps != nullptr && b == 0 && tid == 0;
 #define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+  // (diagnostic: when lane t of block 0 finished its part of a concurrent phase)
+#define LANE_STAMP(i, t)                                                                   \
+  do {                                                                                     \
+    if (stamps != nullptr && b == 0 && tid == (t)) {                                       \
+      __builtin_amdgcn_s_waitcnt(0);                                                       \
+      stamps[i] = (long long)__builtin_amdgcn_s_memrealtime();                             \
+    }                                                                                      \
+  } while (0)
   STAMP(0);
   int bvalid = 1, sample;
   bool valid;
@@ -158,7 +184,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   float* F3 = reinterpret_cast<float*>(smem + L_F3);
   float* PART = reinterpret_cast<float*>(smem + L_PART);
   float* DY2 = reinterpret_cast<float*>(smem + L_DY2);
-  float* DP1 = reinterpret_cast<float*>(smem + L_DP1);
+  f2* T1 = reinterpret_cast<f2*>(smem + L_T1);
+  f2* T2 = reinterpret_cast<f2*>(smem + L_T2);
+  uint8_t* PS1 = smem + L_PS1;
+  uint8_t* PS2 = smem + L_PS2;
+  int* NACT = reinterpret_cast<int*>(smem + L_NACT);
 
   // ============ phase A: ingest + weight staging ========================================
   {
@@ -401,6 +431,42 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       correct_out[b] = pred == label ? 1 : 0;
     }
     if (TRAIN && lane < 16) DZ3[lane] = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
+  } else if (TRAIN && wave <= 6) {
+    // meanwhile: the conv1 weight-gradient table of channel c - its active windows compacted in
+    // window order (ballot prefix counts), each with the offset of its argmax pixel in XW
+    const int c = wave - 1;
+    int base = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 64 * k + lane;
+      const int code = q < 196 ? C1[c * 196 + q] : 4;
+      const unsigned long long m = __ballot(code < 4);
+      if (q < 196) {
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        PS1[c * 196 + q] = code < 4 ? (uint8_t)pos : (uint8_t)255;
+        if (code < 4) {
+          const int qy = q / 14, qx = q - 14 * qy;
+          T1[c * T1_LD + pos] = f2{0.f, __int_as_float((2 * qy + (code >> 1)) * XW_RS + 2 * qx + (code & 1))};
+        }
+      }
+      base += __popcll(m);
+    }
+    if (lane < W1_PARTS) T1[c * T1_LD + base + lane] = f2{0.f, 0.f};  // slices round up: zero pad
+    if (lane == 0) NACT[c] = base;
+  } else if (TRAIN && wave <= 14) {
+    // and the conv2 table: channels o = 2 (wave - 7) + (lane >= 32), one per half wave
+    const int h = lane >> 5, w = lane & 31, o = 2 * (wave - 7) + h;
+    const int code = w < 25 ? C2[o * 25 + w] : 4;
+    const unsigned int hm = (unsigned int)(__ballot(code < 4) >> (32 * h));
+    if (w < 25) {
+      const int pos = __popc(hm & ((1u << w) - 1u));
+      PS2[o * 25 + w] = code < 4 ? (uint8_t)pos : (uint8_t)255;
+      if (code < 4) {
+        const int wy = w / 5, wx = w - 5 * wy;
+        T2[o * 25 + pos] = f2{0.f, __int_as_float((2 * wy + (code >> 1)) * 14 + 2 * wx + (code & 1))};
+      }
+    }
+    if (w == 0) NACT[6 + o] = __popc(hm);
   }
   if (!TRAIN) return;
   lds_barrier();
@@ -445,8 +511,16 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     float d = PART[tid];
 #pragma unroll
     for (int w = 1; w < 16; ++w) d += PART[w * 400 + tid];
-    DA0[tid] = d;  // (the pool2 / ReLU2 mask is applied through C2)
+    DA0[tid] = d;
     a0_out[(size_t)b * A0_LD + tid] = A0[tid];
+    // pool2 / ReLU2 backward: dY2 at the argmax pixel (zero-padded copy for the data gradient)
+    // and the value of the window's entry in the conv2 weight-gradient table
+    const int o = tid / 25, w = tid - 25 * o, wy = w / 5, wx = w - 5 * wy;
+    const int code = C2[tid];
+    if (code < 4) {
+      DY2[o * DY2_CH + (4 + 2 * wy + (code >> 1)) * DY2_LD + 4 + 2 * wx + (code & 1)] = d;
+      reinterpret_cast<float*>(T2 + o * 25 + PS2[tid])[0] = d;
+    }
   } else if (tid < 520) {
     h1_out[(size_t)b * H1_LD + tid - 400] = H1[tid - 400];
     z1_out[(size_t)b * Z1_LD + tid - 400] = DZ1[tid - 400];
@@ -461,34 +535,6 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 
   // ============ phase E: conv2 backward ===================================================
   float* slab = slab_out + (size_t)b * SLAB;
-  if (tid < 400) {  // dY2 = unpool(dA0) at the argmax pixel (zero padding of 4 for the dgrad)
-    const int o = tid / 25, w = tid - 25 * o, wy = w / 5, wx = w - 5 * wy;
-    const int code = C2[tid];
-    if (code < 4) DY2[o * DY2_CH + (4 + 2 * wy + (code >> 1)) * DY2_LD + 4 + 2 * wx + (code & 1)] = DA0[tid];
-  } else if (tid < 416) {  // conv2 bias gradient
-    const int o = tid - 400;
-    float s = 0.f;
-    for (int w = 0; w < 25; ++w) s += C2[o * 25 + w] < 4 ? DA0[o * 25 + w] : 0.f;
-    slab[SLAB_C2B + o] = s;
-  }
-  if (tid >= 512 && tid < 992) {  // conv2 weight gradient over the 25 argmax pixels of channel o
-    const int t = tid - 512, o = t / 30, rem = t - 30 * o, c = rem / 5, ky = rem - 5 * c;
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int w = 0; w < 25; ++w) {
-      const int code = C2[o * 25 + w];
-      if (code < 4) {
-        const int wy = w / 5, wx = w - 5 * wy;
-        const float v = DA0[o * 25 + w];
-        const float* pr = P1 + c * P1_CH + (2 * wy + (code >> 1) + ky) * 14 + 2 * wx + (code & 1);
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, pr[kx], acc[kx]);
-      }
-    }
-#pragma unroll
-    for (int kx = 0; kx < 5; ++kx) slab[SLAB_C2W + o * 150 + c * 25 + ky * 5 + kx] = acc[kx];
-  }
-  lds_barrier();
-  STAMP(12);
   // conv2 data gradient: full correlation of the padded dY2 with the kernel.  A lane owns a
   // 2 x 4 pixel block of one input channel for a quarter of the output channels: per channel o
   // one 6 x 8 dY2 window (12 aligned 16-B reads) and 25 weights (7 16-B reads, broadcast over the
@@ -532,14 +578,55 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) part[k] = dacc[k >> 1][k & 1];
     }
-  } else {  // idle lanes: the re-strided image copy for the conv1 weight gradient (fc2 is dead)
-    float* XW = reinterpret_cast<float*>(smem + L_F2);
-    for (int i = tid - 672; i < 3072; i += NT - 672) {
-      const int c = i >> 10, y = (i >> 5) & 31, x = i & 31;
-      XW[c * XW_CH + y * XW_RS + x] = X[c * X_CH + y * X_RS + x];
+    LANE_STAMP(16, 0);
+  }
+  // the conv2 weight gradient over the active argmax pixels of each output channel (table T2):
+  // tasks (o, c, ky) of 5 taps, 352 on lanes 672..1023 (concurrently with the data gradient),
+  // the last 128 on lanes 0..127 once their data gradient is done; lanes 128..671 then build
+  // the re-strided image copy for the conv1 weight gradient
+  {
+    const int t = tid >= 672 ? tid - 672 : (tid < 128 ? tid + 352 : -1);
+    if (t >= 0) {
+      const int o = t / 30, rem = t - 30 * o, c = rem / 5, ky = rem - 5 * c, n = NACT[6 + o];
+      const float* pr = P1 + c * P1_CH + ky * 14;
+      float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int w = 0; w < n; ++w) {  // unrolled: the table and pixel reads overlap
+        const f2 e = T2[o * 25 + w];
+        const float* r = pr + __float_as_int(e.y);
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(e.x, r[kx], acc[kx]);
+      }
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx) slab[SLAB_C2W + o * 150 + c * 25 + ky * 5 + kx] = acc[kx];
     }
+    LANE_STAMP(17, 672);
+    if (tid >= 1008) {  // conv2 bias gradient
+      const int o = tid - 1008;
+      float sb = 0.f;
+      const int n = NACT[6 + o];
+#pragma unroll
+      for (int w = 0; w < 25; ++w) sb += masked(T2[o * 25 + w].x, w < n);  // fixed trip: reads in flight
+      slab[SLAB_C2B + o] = sb;
+    }
+    if (tid >= 128 && tid < 672) {  // 3072 pixels over 544 lanes: 6 reads in flight, then 6 writes
+      float* XW = reinterpret_cast<float*>(smem + L_F2);
+      float v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int i = min(tid - 128 + 544 * k, 3071), c = i >> 10, y = (i >> 5) & 31, x = i & 31;
+        v[k] = X[c * X_CH + y * X_RS + x];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int i = tid - 128 + 544 * k, c = i >> 10, y = (i >> 5) & 31, x = i & 31;
+        if (i < 3072) XW[c * XW_CH + y * XW_RS + x] = v[k];
+      }
+    }
+    LANE_STAMP(18, 128);
   }
   lds_barrier();
+  STAMP(12);
   if (tid < 168) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -553,9 +640,14 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       for (int pp = 0; pp < 2; ++pp) {
         const int x = d_x0 + 2 * pp;
         if (x < 14) {
-          const int q = (d_y0 + dy) * 14 + x;
-          DP1[d_c * 196 + q] = C1[d_c * 196 + q] < 4 ? dacc[dy][pp].x : 0.f;  // ReLU1 mask (pool codes)
-          DP1[d_c * 196 + q + 1] = C1[d_c * 196 + q + 1] < 4 ? dacc[dy][pp].y : 0.f;
+          // ReLU1 + pool1 backward: dP1 of an active window is the value of its entry in the
+          // conv1 weight-gradient table
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int q = (d_y0 + dy) * 14 + x + e;
+            const int pos = PS1[d_c * 196 + q];
+            if (pos != 255) reinterpret_cast<float*>(T1 + d_c * T1_LD + pos)[0] = e ? dacc[dy][pp].y : dacc[dy][pp].x;
+          }
         }
       }
   }
@@ -563,30 +655,36 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   STAMP(13);
 
   // ============ phase F: conv1 weight + bias gradient =====================================
-  static_assert(W1_PARTS * 90 + 6 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
-  if (tid >= W1_PARTS * 90 && tid < W1_PARTS * 90 + 6) {
-    const int c = tid - W1_PARTS * 90;
-    float s = 0.f;
-    for (int q = 0; q < 196; ++q) s += DP1[c * 196 + q];
-    slab[SLAB_C1B + c] = s;
+  static_assert(W1_PARTS * 90 <= 992 && 992 + 24 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
+  if (tid >= 992 && tid < 992 + 24) {  // conv1 bias gradient: 4 lanes per channel, fixed trip counts
+    const int c = (tid - 992) >> 2, l = tid & 3, n = NACT[c];
+    float sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < 49; ++i) sb += masked(T1[c * T1_LD + 4 * i + l].x, 4 * i + l < n);
+    sb += __shfl_xor(sb, 1);
+    sb += __shfl_xor(sb, 2);
+    if (l == 0) slab[SLAB_C1B + c] = sb;
+    LANE_STAMP(19, 992);
   }
   const float* XW = reinterpret_cast<const float*>(smem + L_F2);
-  if (tid < W1_PARTS * 90) {  // dW1 over the 196 argmax pixels, in 11 slices
-    const int t = tid, part = t / 90, rem = t - 90 * part, o = rem / 15, c = (rem / 5) % 3, ky = rem % 5;
-    const int q0 = 18 * part, q1 = min(q0 + 18, 196);
+  if (tid < W1_PARTS * 90) {
+    // dW1 over the active argmax pixels (table T1) of channel o, in 11 slices of s windows (the
+    // zero pad entries round the last slices up); lanes of one channel share a wave
+    const int o = tid / (15 * W1_PARTS), r = tid - 15 * W1_PARTS * o, part = r / 15, ck = r - 15 * part;
+    const int c = ck / 5, ky = ck - 5 * c, s = (NACT[o] + W1_PARTS - 1) / W1_PARTS;
+    const f2* tb = T1 + o * T1_LD + s * part;
+    const float* xb = XW + c * XW_CH + ky * XW_RS;
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int q = q0; q < q1; ++q) {
-      const int code = C1[o * 196 + q];
-      if (code < 4) {
-        const int qy = q / 14, qx = q - 14 * qy;
-        const float v = DP1[o * 196 + q];
-        const float* xr = XW + c * XW_CH + (2 * qy + (code >> 1) + ky) * XW_RS + 2 * qx + (code & 1);
+#pragma unroll 6
+    for (int q = 0; q < s; ++q) {  // unrolled: six windows' table + pixel reads in flight
+      const f2 e = tb[q];
+      const float* xr = xb + __float_as_int(e.y);
 #pragma unroll
-        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(v, xr[kx], acc[kx]);
-      }
+      for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(e.x, xr[kx], acc[kx]);
     }
 #pragma unroll
     for (int kx = 0; kx < 5; ++kx) PART[part * 450 + o * 75 + c * 25 + ky * 5 + kx] = acc[kx];
+    LANE_STAMP(20, 0);
   }
   lds_barrier();
   STAMP(14);
@@ -601,6 +699,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     STAMP(15);
   }
 #undef STAMP
+#undef LANE_STAMP
 }
 
 }  // namespace f32k

@@ -32,7 +32,10 @@ struct DirectSink {
     sgd_finish(e, g, p, m, a);
   }
 };
-struct XpSink {
+//    PK (bf16 granules, xp_mode bit 4): the lane's elements travel in pairs (0, 1) and (2, 3)
+//    as ONE granule {bf16 | bf16, step} each, published by the exchange once both are known.
+template <bool PK>
+struct XpSinkT {
   unsigned long long* own;  // where the granules go: this rank's pull slot (null: not published)
   unsigned long long tag;   // step << 32
   int e[4] = {0, 0, 0, 0};
@@ -41,10 +44,11 @@ struct XpSink {
   __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
     g_ *= a.grad_scale;
     e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
-    if (own != nullptr)  // (two-hop form: null on the owner of the block's elements)
+    if (!PK && own != nullptr)  // (two-hop form: null on the owner of the block's elements)
       __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 };
+using XpSink = XpSinkT<false>;
 
 // fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
 // output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).

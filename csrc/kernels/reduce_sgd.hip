@@ -112,7 +112,8 @@ __device__ __forceinline__ long long poll_granules(const ReduceArgs& a, const un
   return wall_clock64() - t0;
 }
 
-__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSink& sk, const float (&s)[4]) {
+template <bool PK>
+__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSinkT<PK>& sk, const float (&s)[4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (!sk.v[j]) continue;
@@ -122,6 +123,45 @@ __device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSink& 
     a.mom[sk.e[j]] = m;
     a.master[sk.e[j]] = p;
     write_shadow(a.shadow, sk.e[j], p);
+  }
+}
+
+// bf16 granules (PK): round the pairs (0, 1) and (2, 3) of x to bf16 IN PLACE - a lane's own
+// contribution included, so every rank sums the same numbers - and, if dst, publish each pair
+// as one granule {lo | hi << 16, step} at the index of its first element (unique: an element
+// has one owner lane)
+template <bool PK>
+__device__ __forceinline__ void pack_pairs(float (&x)[4], const bool (&valid)[4], const int (&e)[4],
+                                           unsigned long long* dst, unsigned long long tag) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+      if (!valid[k]) continue;
+      const unsigned lo = bf16_bits(x[k]), hi = valid[k + 1] ? bf16_bits(x[k + 1]) : 0u;
+      x[k] = bf16_lo(lo);
+      x[k + 1] = bf16_lo(hi);
+      if (dst != nullptr)
+        __hip_atomic_store(dst + e[k], tag | (unsigned long long)(lo | (hi << 16)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// which of a lane's elements are polled as granules: all valid ones, or (PK) each pair's first
+template <bool PK>
+__device__ __forceinline__ bool polled(const bool (&valid)[4], int j) { return valid[j] && (!PK || (j & 1) == 0); }
+
+// PK: a polled pair's raw word (in x[k]) -> its two values
+template <bool PK>
+__device__ __forceinline__ void unpack_pairs(float (&x)[4], const bool (&valid)[4]) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2)
+      if (valid[k]) {
+        const unsigned w = __float_as_uint(x[k]);
+        x[k] = bf16_lo(w);
+        x[k + 1] = bf16_hi(w);
+      }
   }
 }
 
@@ -135,10 +175,12 @@ __device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSink& 
 // s + 2 only after it read every peer's step s + 1 granule of e, which each peer wrote only
 // after it had read the owner's step s granule of e.
 // NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
-// group does not pay for 8 ranks' loads in flight.
-template <int NR>
-__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+// group does not pay for 8 ranks' loads in flight.  PK: bf16 granules (half the link bytes;
+// the sum stays fp32 in rank order).
+template <int NR, bool PK>
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed) {
   const int par = step & 1u;
+  pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);
   float v[NR][4];
   unsigned pending = 0;
   const unsigned long long* src[NR];
@@ -148,10 +190,13 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       v[r][j] = sk.g[j];
-      if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
+      if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
     }
   }
   record_wait(a, step, poll_granules<NR>(a, src, sk.e, pending, step, failed, v));
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
   float s[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -163,17 +208,19 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, const XpSink& s
   apply_update(a, sk, s);
 }
 
-// The two-hop pull form (xp_mode 2): reduce-scatter + all-gather where every rank writes only
-// its OWN region.  Block k's elements belong to rank k % N.  A non-owner lane has stored its
-// granules into its own pull slot (XpSink::put); the owner lane reads them from the N - 1 peers'
-// pull slots, sums the N values in RANK ORDER (the same fp32 additions as xp_exchange, so both
-// forms give bit-identical parameters), stores {sum, step} into its own ag slot and applies SGD;
-// the other ranks read that slot.  2 E / N granules per link instead of E, one more dependent
-// remote read.
-template <int NR>
-__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSink& sk, unsigned step, bool failed) {
+// The two-hop pull form (xp_mode bit 2): reduce-scatter + all-gather where every rank writes
+// only its OWN region.  Block k's elements belong to rank k % N.  A non-owner lane has stored
+// its granules into its own pull slot (XpSink::put); the owner lane reads them from the N - 1
+// peers' pull slots, sums the N values in RANK ORDER (the same fp32 additions as xp_exchange,
+// so both forms give bit-identical parameters), stores {sum, step} into its own ag slot and
+// applies SGD; the other ranks read that slot.  2 E / N granules per link instead of E, one
+// more dependent remote read.  PK: the sum is all-gathered as bf16 too (every rank, the owner
+// included, applies the rounded sum).
+template <int NR, bool PK>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed) {
   const int par = step & 1u;
   const int owner = blockIdx.x % a.xp_nranks;
+  pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);  // (null own on the owner: rounding only)
   float s[4];
   long long waited;
   if (owner == a.xp_rank) {
@@ -186,10 +233,13 @@ __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSi
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         v[r][j] = sk.g[j];
-        if (r < a.xp_nranks && r != a.xp_rank && sk.v[j]) pending |= 1u << (4 * r + j);
+        if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
       }
     }
     waited = poll_granules<NR>(a, src, sk.e, pending, step, failed, v);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       s[j] = v[0][j];
@@ -200,10 +250,14 @@ __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSi
     const unsigned long long tag = (unsigned long long)step << 32;
     unsigned long long* dst =
         reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
+    if constexpr (PK) {
+      pack_pairs<PK>(s, sk.v, sk.e, dst, tag);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (sk.v[j])
-        __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int j = 0; j < 4; ++j)
+        if (sk.v[j])
+          __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   } else {
     const unsigned long long* src[1] = {
         reinterpret_cast<const unsigned long long*>(a.xp_region[owner] + a.xp_ag_off + par * a.xp_gslot_bytes)};
@@ -212,9 +266,10 @@ __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, const XpSi
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       v[0][j] = 0.f;
-      if (sk.v[j]) pending |= 1u << j;
+      if (polled<PK>(sk.v, j)) pending |= 1u << j;
     }
     waited = poll_granules<1>(a, src, sk.e, pending, step, failed, v);
+    unpack_pairs<PK>(v[0], sk.v);
 #pragma unroll
     for (int j = 0; j < 4; ++j) s[j] = v[0][j];
   }
@@ -234,23 +289,23 @@ __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
 // NR = 1: local reduction (+ SGD, or gradients out); NR = 2 / 4 / 8: the one-launch
 // exchange for groups of up to NR ranks (separate instances keep the local step's registers
 // at its own need).
-template <int NR>
+template <int NR, bool PK = false>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(const ReduceArgs a) {
   reduce_stamp(a, 0);
   if constexpr (NR > 1) {  // one-launch all-reduce: reduce -> exchange -> SGD, per lane
     const unsigned step = a.xp_ctr[blockIdx.x] + 1u;
     const bool failed = *a.xp_err != 0u;
-    XpSink sk;
+    XpSinkT<PK> sk;
     sk.tag = (unsigned long long)step << 32;
     // pull: every lane's granules go to this rank's slot; two-hop: only non-owners' (the owner
     // publishes the SUM in its ag slot instead)
-    const bool publish = a.xp_mode == 0 || (int)(blockIdx.x % a.xp_nranks) != a.xp_rank;
+    const bool publish = (a.xp_mode & 2) == 0 || (int)(blockIdx.x % a.xp_nranks) != a.xp_rank;
     sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
                                                              (step & 1u) * a.xp_gslot_bytes)
                      : nullptr;
     if (grad_reduce_body(a, sk)) {
-      if (a.xp_mode == 0) xp_exchange<NR>(a, sk, step, failed);
-      else xp_exchange_rsag<NR>(a, sk, step, failed);
+      if ((a.xp_mode & 2) == 0) xp_exchange<NR, PK>(a, sk, step, failed);
+      else xp_exchange_rsag<NR, PK>(a, sk, step, failed);
     }
     __syncthreads();  // every thread read this block's counter before it advances
     if (threadIdx.x == 0) a.xp_ctr[blockIdx.x] = step;
@@ -343,8 +398,11 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
     throw std::runtime_error("grad_reduce exchange needs the whole-arena grid");
   const int nr = args.xp_nranks;
   if (nr > XG_MAX_RANKS) throw std::runtime_error("grad_reduce exchange: at most 8 ranks");
+  const bool pk = (args.xp_mode & 4) != 0;
   auto* kern = nr == 0 ? &grad_reduce_kernel<1>
-                       : (nr <= 2 ? &grad_reduce_kernel<2> : (nr <= 4 ? &grad_reduce_kernel<4> : &grad_reduce_kernel<8>));
+               : pk ? (nr <= 2 ? &grad_reduce_kernel<2, true>
+                               : (nr <= 4 ? &grad_reduce_kernel<4, true> : &grad_reduce_kernel<8, true>))
+                    : (nr <= 2 ? &grad_reduce_kernel<2> : (nr <= 4 ? &grad_reduce_kernel<4> : &grad_reduce_kernel<8>));
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(RT), 0, stream, args);
   HIP_CHECK(hipGetLastError());
 }

@@ -28,6 +28,10 @@ from typing import Callable
 import torch
 
 ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+# opt-in (--grad-comm bf16): the xGMI exchanges with bf16 gradient granules - half the link
+# bytes, lower-precision gradients, so never a candidate unless asked for
+BF16_PATHS = ("xgmi-pull-bf16", "xgmi-rsag-bf16")
+RANK = ORDER + BF16_PATHS  # tie-break order
 
 
 def choose(results: dict[str, dict]) -> str | None:
@@ -37,7 +41,7 @@ def choose(results: dict[str, dict]) -> str | None:
           if k != "local" and v.get("ok") and v.get("us_per_step") is not None and math.isfinite(v["us_per_step"])}
     if not ok:
         return None
-    return min(ok, key=lambda k: (ok[k], ORDER.index(k) if k in ORDER else len(ORDER)))
+    return min(ok, key=lambda k: (ok[k], RANK.index(k) if k in RANK else len(RANK)))
 
 
 def _sync(engine) -> None:
@@ -118,4 +122,4 @@ def allreduce_ab(policy, engine, run: Callable[[int], None], steps: int = 300, w
             "failed": sorted(k for k, v in results.items() if not v.get("ok"))}
 
 
-__all__ = ["ORDER", "allreduce_ab", "choose"]
+__all__ = ["BF16_PATHS", "ORDER", "allreduce_ab", "choose"]

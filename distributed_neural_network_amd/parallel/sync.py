@@ -132,8 +132,10 @@ class StepAllReduce(SyncPolicy):
     # rccl: ncclAllReduce of the fused gradient bucket + sgd_apply; rccl-overlap: the MLP bucket
     # all-reduced on a side stream while the conv bucket is reduced; local: no all-reduce (A/B
     # baseline only: replicas diverge)
-    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+    # (xgmi-pull-bf16 / xgmi-rsag-bf16: the same exchanges with bf16 gradient granules, opt-in)
+    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-bf16", "xgmi-rsag-bf16")
     path: str | None = None
+    grad_comm = "fp32"  # "bf16": the default xGMI path uses bf16 gradient granules (--grad-comm)
     record_waits = False  # xGMI paths: record every step's exchange wait (XgmiGroup.wait_stats)
 
     def attach(self, engine) -> None:
@@ -143,7 +145,7 @@ class StepAllReduce(SyncPolicy):
             return
         name = self.path or self.default_path(engine)
         chain = [name]
-        if name == "xgmi-rsag":
+        if name.startswith("xgmi") and name != "xgmi-pull":
             chain.append("xgmi-pull")
         if name.startswith("xgmi"):
             chain.append("rccl" if self.comm.backend == "nccl" else "torch-pg")
@@ -164,7 +166,8 @@ class StepAllReduce(SyncPolicy):
             return ("rccl-overlap" if getattr(engine, "overlap", False) else "rccl") \
                 if self.comm.backend == "nccl" else "torch-pg"
         if xgmi.wanted(self.comm) and engine.grad.numel() <= self.XGMI_MAX_ELEMS:
-            return "xgmi-rsag" if xgmi.exchange_mode() == 2 else "xgmi-pull"
+            mode = xgmi.exchange_mode() | (4 if self.grad_comm == "bf16" else 0)
+            return "xgmi-" + xgmi.MODE_NAMES[mode]
         return "rccl" if self.comm.backend == "nccl" else "torch-pg"
 
     def installed(self, engine) -> str | None:
@@ -174,7 +177,9 @@ class StepAllReduce(SyncPolicy):
             return None if not self.comm.distributed else "local"
         kind = type(gs).__name__
         if kind == "XgmiGradSync":
-            form = {0: "pull", 2: "rsag"}[gs.group.xp_mode]
+            from .xgmi import MODE_NAMES
+
+            form = MODE_NAMES[gs.group.xp_mode]
             return f"xgmi-{form}" + ("" if gs.group.one_launch else "-two-launch")
         if kind == "NativeGradAllReduce":
             return "rccl-overlap" if gs.overlap else "rccl"
@@ -191,7 +196,9 @@ class StepAllReduce(SyncPolicy):
         if name == "local":
             return True
         if name.startswith("xgmi"):
-            return self._install_xgmi(engine, 2 if name == "xgmi-rsag" else 0)
+            from .xgmi import EXCHANGE_MODES
+
+            return self._install_xgmi(engine, EXCHANGE_MODES[name[len("xgmi-"):]])
         if name in ("rccl", "rccl-overlap"):
             if self.comm.backend != "nccl":
                 return False

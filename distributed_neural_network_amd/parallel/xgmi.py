@@ -78,7 +78,12 @@ def one_launch_wanted() -> bool:
     return v == "1"
 
 
-EXCHANGE_MODES = {"pull": 0, "rsag": 2}
+# xp_mode / all-reduce kernel form: bit 2 = two-hop, bit 4 = bf16 granules (a lane's elements
+# travel in pairs as {bf16 | bf16, step} words: half the link bytes; every rank sums the same
+# bf16-rounded gradients in fp32, rank order - opt-in lower-precision communication, like a
+# bf16 compression hook, never chosen unless asked for: ``--grad-comm bf16``)
+EXCHANGE_MODES = {"pull": 0, "rsag": 2, "pull-bf16": 4, "rsag-bf16": 6}
+MODE_NAMES = {v: k for k, v in EXCHANGE_MODES.items()}
 
 
 def exchange_mode(grp: "XgmiGroup | None" = None) -> int:
@@ -138,7 +143,7 @@ class XgmiGroup:
         # set when a self-test pass raised or timed out on some rank: the per-block step counters
         # may then be out of step across ranks, so the group must be rebuilt before any use
         self.broken = False
-        self.xp_mode = 0  # one-launch exchange form (exchange_mode + self-test): 0 pull, 2 rsag
+        self.xp_mode = 0  # one-launch exchange form (EXCHANGE_MODES, self-tested): 0 pull, 2 rsag, + 4 bf16
         self.ar_mode = 0  # form of the all-reduce kernel (build_group: exchange_mode + self-test)
         # per-step exchange-wait records (ReduceArgs::xp_wait): [ring][block][wave] words of
         # {step << 32 | ticks}; None = not recorded (enable_wait_stats)
@@ -359,7 +364,7 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
     if all(v == 1.0 for v in votes):
         # the all-reduce kernel's two-hop form where it is wanted, kept only if its own exact
         # self-test passes on every rank
-        mode = exchange_mode(grp)
+        mode = exchange_mode(grp) & 2  # (bf16 granules: only with their one-launch exchange)
         if mode != 0:
             grp.ar_mode = mode
             try:

@@ -72,6 +72,7 @@ class TrainConfig:
     use_graphs: bool = True
     bucket_kb: int = 0
     allreduce: str = "default"           # step-allreduce transport: default | ab | a StepAllReduce.PATHS name
+    grad_comm: str = "fp32"              # step-allreduce gradient communication precision: fp32 | bf16
     extra: dict = field(default_factory=dict)
 
 
@@ -126,10 +127,16 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
                    help="step-allreduce: split the flat gradient into all-reduce buckets of at most this many "
                         "KB (0 = one fused bucket, latency-optimal for the 248 KB reference gradient)")
     g.add_argument("--allreduce", default="default",
-                   choices=("default", "ab", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"),
+                   choices=("default", "ab", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-bf16",
+                            "xgmi-rsag-bf16"),
                    help="step-allreduce transport: default (one-launch xGMI exchange on one node, else RCCL), "
                         "ab (time every candidate at start-up and keep the fastest; parallel/autotune.py) or a "
                         "path name")
+    g.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                   help="step-allreduce gradient communication precision: fp32 (default) or bf16 = the xGMI "
+                        "exchange carries bf16 gradient pairs per granule (half the link bytes; every rank sums "
+                        "the same rounded values in fp32) - the default path becomes its -bf16 form and --allreduce "
+                        "ab also times the -bf16 forms")
     g.add_argument("--check-sync", action="store_true",
                    help="after every synchronisation assert that all ranks hold bit-identical parameters "
                         "(cross-rank checksum)")

@@ -228,6 +228,7 @@ class Trainer:
         if c.mode == "single":
             self.policy.reset_momentum_each_epoch = bool(c.momentum_reset)
         self.policy.bucket_kb = c.bucket_kb
+        self.policy.grad_comm = getattr(c, "grad_comm", "fp32")
         if c.allreduce not in ("default", "ab") and hasattr(self.policy, "PATHS"):
             self.policy.path = c.allreduce
         self.policy.attach(self.engine)
@@ -235,11 +236,13 @@ class Trainer:
         self.allreduce_ab = None
         if c.allreduce == "ab" and self.comm.distributed and hasattr(self.policy, "PATHS"):
             # start-up A/B of the per-step all-reduce on this node (parameters restored after)
-            from ..parallel.autotune import allreduce_ab
+            from ..parallel.autotune import BF16_PATHS, ORDER, allreduce_ab
             from ..runtime.cursor import EpochCursor
 
             cur = EpochCursor(self.engine, self.sampler, self.policy, c.batch_size)
-            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur.run, steps=100, warmup=20)
+            cands = ORDER + (BF16_PATHS if self.policy.grad_comm == "bf16" else ())
+            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur.run, steps=100, warmup=20,
+                                             candidates=cands)
             self._say(f"[allreduce] start-up A/B (us/step, max over ranks): {self.allreduce_ab['allreduce_ab']}; "
                       f"using {self.allreduce_ab['allreduce']}")
             self.run_log.record(event="allreduce_ab", **self.allreduce_ab)

@@ -230,3 +230,20 @@ def test_bench_two_ranks_xgmi(tmp_path):
     assert out["local_step_us"] > 0, out
     w = out["exchange_wait_us"]
     assert w is not None and 0 <= w["median"] <= w["p99"] <= w["max"], out
+
+
+def test_xgmi_bf16_granule_exchanges_two_ranks(tmp_path):
+    """2 ranks on the box's GPU: the bf16-granule forms of the one-launch exchange (pairs of
+    bf16 gradients per {value, step} word, --grad-comm bf16) pass their self-test against the
+    all-reduce kernel's bf16 form (a separate implementation with different element pairs) bit
+    for bit, keep the replicas identical, and stay within bf16 rounding of the fp32 exchange."""
+    import torch
+
+    fp, r0 = _two_ranks(tmp_path, "xgmi", "1", 29681, exchange="pull")
+    for port, xch, mode in ((29683, "pull-bf16", 4), (29685, "rsag-bf16", 6)):
+        res, r = _two_ranks(tmp_path, "xgmi", "1", port, exchange=xch)
+        assert all(x["kind"] == "XgmiGradSync" and x["one_launch"] and x["xp_mode"] == mode for x in res), \
+            r.stderr[-2000:]
+        assert torch.equal(res[0]["master"], res[1]["master"])
+        d = (res[0]["master"] - fp[0]["master"]).abs().max().item()
+        assert 0 < d < 1e-4, (xch, d)  # rounded (not the fp32 bits), but only by bf16 gradient rounding

@@ -21,13 +21,51 @@ def test_auto_mode_is_pull(monkeypatch):
 
 
 def test_explicit_modes(monkeypatch):
-    for name, want in (("pull", 0), ("rsag", 2)):
+    for name, want in (("pull", 0), ("rsag", 2), ("pull-bf16", 4), ("rsag-bf16", 6)):
         monkeypatch.setenv("DNN_XGMI_EXCHANGE", name)
         assert xgmi.exchange_mode() == want
     for bad in ("push", "ring"):
         monkeypatch.setenv("DNN_XGMI_EXCHANGE", bad)
         with pytest.raises(ValueError):
             xgmi.exchange_mode()
+
+
+def test_path_names_map_to_exchange_modes(monkeypatch):
+    """Every xGMI path name of the policy maps to its exchange form and back; --grad-comm bf16
+    turns the default xGMI path into its bf16-granule form; the bf16 forms are A/B candidates only
+    when asked for."""
+    from distributed_neural_network_amd.parallel.sync import StepAllReduce
+
+    for name in StepAllReduce.PATHS:
+        if name.startswith("xgmi-"):
+            mode = xgmi.EXCHANGE_MODES[name[len("xgmi-"):]]
+            assert "xgmi-" + xgmi.MODE_NAMES[mode] == name
+    assert set(autotune.BF16_PATHS) <= set(StepAllReduce.PATHS)
+    assert not set(autotune.BF16_PATHS) & set(autotune.ORDER)
+
+    class _Comm:
+        backend, distributed = "nccl", True
+
+    class _Eng:
+        overlap = False
+        grad = torch.zeros(62006)
+
+    pol = StepAllReduce.__new__(StepAllReduce)
+    pol.comm, pol.bucket_kb = _Comm(), 0
+    monkeypatch.setattr(xgmi, "wanted", lambda comm: True)
+    monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
+    assert pol.default_path(_Eng()) == "xgmi-pull"
+    pol.grad_comm = "bf16"
+    assert pol.default_path(_Eng()) == "xgmi-pull-bf16"
+    monkeypatch.setenv("DNN_XGMI_EXCHANGE", "rsag")
+    assert pol.default_path(_Eng()) == "xgmi-rsag-bf16"
+
+
+def test_choose_bf16_tie_prefers_fp32():
+    res = {"xgmi-pull-bf16": _r(20.0), "xgmi-pull": _r(20.0)}
+    assert autotune.choose(res) == "xgmi-pull"
+    res["xgmi-pull-bf16"] = _r(19.0)
+    assert autotune.choose(res) == "xgmi-pull-bf16"
 
 
 def _r(us, ok=True):

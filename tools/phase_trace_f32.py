@@ -14,17 +14,18 @@ from distributed_neural_network_amd.data import synthetic  # noqa: E402
 from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
 
 NAMES = ["A ingest + weights", "B conv1 fwd", "C conv2 fwd (halves)", "C' conv2 epilogue + fc1 issue",
-         "D fc1 fwd", "D fc2 fwd", "D fc3 + CE", "D' dh2", "D' dh1", "D' dA0 partials", "D' dA0 sum + rows",
-         "E dY2 + dW2", "E conv2 dgrad", "F dW1 slices", "F dW1 sum + end"]
+         "D fc1 fwd", "D fc2 fwd", "D fc3 + CE", "D' dh2", "D' dh1", "D' dA0 partials",
+         "D' dA0 sum + rows + dY2/T2", "E dgrad || dW2 + XW copy", "E dgrad sum + T1 values", "F dW1 slices",
+         "F dW1 sum + end"]
 
 
 def main(reps: int = 50, batch: int = 64):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, dtype="fp32")
     eng.attach(tr)
-    stamps = torch.zeros(16, dtype=torch.int64, device=eng.device)
+    stamps = torch.zeros(21, dtype=torch.int64, device=eng.device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rows, walls = [], []
+    rows, walls, lanes = [], [], []
     e = eng
     for r in range(reps):
         eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
@@ -36,11 +37,17 @@ def main(reps: int = 50, batch: int = 64):
         ev1.record()
         torch.cuda.synchronize()
         walls.append(ev0.elapsed_time(ev1) * 1000)
-        rows.append(np.diff(stamps.cpu().numpy()) * 0.01)
+        st = stamps.cpu().numpy()
+        rows.append(np.diff(st[:16]) * 0.01)
+        lanes.append((st[16:21] - st[[11, 11, 11, 13, 13]]) * 0.01)
     med = np.median(np.array(rows[5:]), axis=0)
     for name, v in zip(NAMES, med):
         print(f"{name:30s} {v:8.2f} us")
     print(f"{'sum (block 0)':30s} {med.sum():8.2f} us")
+    lm = np.median(np.array(lanes[5:]), axis=0)
+    for name, v in zip(["E: dgrad lanes done", "E: dW2 lanes done", "E: + XW copy done", "F: db1 lanes done",
+                        "F: dW1 lanes done"], lm):
+        print(f"  {name:28s} {v:8.2f} us after the phase start")
     print(f"{'kernel wall (event)':30s} {np.median(walls[5:]):8.2f} us")
 
 
