@@ -45,7 +45,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int X_RS = 46, X_CH = 32 * X_RS;        // normalised image [3][32][46]
 constexpr int XW_RS = 33, XW_CH = 1061;           // its copy for the conv1 weight gradient
 constexpr int P1_CH = 198;                        // pooled conv1 output [6][198] (14 x 14 used)
-constexpr int WD_LD = 28;                         // conv2 dgrad weights [6 c][16 o][28] (25 used)
+constexpr int WD_LD = 28;                         // conv2 dgrad weights [6 c][16 o][28] (25 used),
+constexpr int WD_CPAD = 4;                        // + 4 floats per c: c and c + 1 rows 16 B apart in the banks
 constexpr int L_X = 0;                  // f32 [3][X_CH] normalised image                17664
 // forward weights by output-channel PAIR p: [p][c][ky][6 (kx, padded)][2 (o = 2p, 2p + 1)], so
 // one 16-B read delivers two taps of both channels (the packed-fma operand pairs), a kernel row
@@ -53,8 +54,8 @@ constexpr int L_X = 0;                  // f32 [3][X_CH] normalised image       
 constexpr int WP_R = 12, WP_C = 5 * WP_R;  // floats per (pair, c, ky) / per (pair, c)
 constexpr int L_WT1 = L_X + 17664;      // f32 [3 p][3 c][WP_C] conv1 weights             2160
 constexpr int L_WT2 = L_WT1 + 2160;     // f32 [8 p][6 c][WP_C] conv2 weights            11520
-constexpr int L_WD = L_WT2 + 11520;     // f32 [6][16][WD_LD] conv2 dgrad weights      10752
-constexpr int L_P1 = L_WD + 10752;      // f32 [6][P1_CH] pooled conv1 output          4752
+constexpr int L_WD = L_WT2 + 11520;     // f32 [6][16][WD_LD] (+ c pad) conv2 dgrad weights 10848
+constexpr int L_P1 = L_WD + 10848;      // f32 [6][P1_CH] pooled conv1 output          4752
 constexpr int L_C1 = L_P1 + 4752;       // u8  [6][196] conv1 pool codes                1184
 constexpr int L_A0 = L_C1 + 1184;       // f32 [400] pooled conv2 output (flatten order) 1600
 constexpr int L_C2 = L_A0 + 1600;       // u8  [400] conv2 pool codes                     400
@@ -74,16 +75,16 @@ constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][20] dY2 zero-padded (4 l
 // pixel offset}; the offsets are known from the forward pass, the values are filled in by the
 // data-gradient epilogues.  Inactive windows carry no gradient, so the weight-gradient loops
 // walk only the active ones (about half) without a branch.
-constexpr int T1_LD = 207;               // <= 196 active windows + 11 zero pad entries
-constexpr int L_T1 = L_DY2 + 23040;      // f2 [6][T1_LD] {dP1, offset in XW}               9936
+constexpr int T1_LD = 218;               // <= 196 active windows + 22 zero pad entries (even: 16-B pairs)
+constexpr int L_T1 = L_DY2 + 23040;      // f2 [6][T1_LD] {dP1, offset in XW}              10464
 constexpr int L_T2 = L_T1 + 6 * T1_LD * 8;  // f2 [16][25] {dA0, offset in P1}             3200
 constexpr int L_PS1 = L_T2 + 3200;       // u8 [6][196] window -> table slot (255: inactive) 1176
 constexpr int L_PS2 = L_PS1 + 1176;      // u8 [400]                                         400
 constexpr int L_NACT = L_PS2 + 400;      // i32 [6 conv1 | 16 conv2] active-window counts     88
-constexpr int LDS_TOTAL = L_NACT + 88;   // 161,568 B
+constexpr int LDS_TOTAL = L_NACT + 88;   // 162,192 B
 static_assert(L_WT1 % 16 == 0 && L_WT2 % 16 == 0 && L_WD % 16 == 0 && L_F2 % 16 == 0 && L_DY2 % 16 == 0,
               "16-B aligned b128 regions");
-static_assert(L_T1 % 8 == 0 && L_T2 % 8 == 0 && L_NACT % 4 == 0, "table alignment");
+static_assert(L_T1 % 16 == 0 && L_T2 % 8 == 0 && L_NACT % 4 == 0, "table alignment");
 static_assert(3 * XW_CH * 4 <= 40320, "XW fits the dead fc2 region");
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 constexpr int B_C1 = 0, B_C2 = 6, B_F1 = 22, B_F2 = 142, B_F3 = 226;  // bias offsets (floats)
@@ -141,6 +142,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       __builtin_amdgcn_s_waitcnt(0);                                                       \
       stamps[i] = (long long)__builtin_amdgcn_s_memrealtime();                             \
     }                                                                                      \
+  } while (0)
+  // (diagnostic: when each wave of block 0 reached a barrier, stamps[base + wave])
+#define WAVE_STAMP(base)                                                                      \
+  do {                                                                                     \
+    if (stamps != nullptr && b == 0 && lane == 0) stamps[(base) + wave] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
   STAMP(0);
   int bvalid = 1, sample;
@@ -208,16 +214,6 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       const int t = k - 25 * c, ky = t / 5;
       WT1[((o >> 1) * 3 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = master[OFF_C1W + i];
     }
-    for (int i = tid; i < 2400; i += NT) {
-      const float v = master[OFF_C2W + i];
-      const int o = i / 150, k = i - 150 * o, c = k / 25;
-      const int t = k - 25 * c, ky = t / 5;
-      WT2[((o >> 1) * 6 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = v;
-      WD[(c * 16 + o) * WD_LD + k - 25 * c] = v;
-    }
-    const f4* f2src = reinterpret_cast<const f4*>(master + OFF_F2W);
-    for (int i = tid; i < 2520; i += NT) reinterpret_cast<f4*>(F2)[i] = f2src[i];
-    if (tid < 210) reinterpret_cast<f4*>(F3)[tid] = reinterpret_cast<const f4*>(master + OFF_F3W)[tid];
     if (tid < 236) {
       int src;
       if (tid < B_C2) src = OFF_C1B + tid;
@@ -227,8 +223,18 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       else src = OFF_F3B + tid - B_F3;
       BIAS[tid] = master[src];
     }
-    if (TRAIN)
-      for (int i = tid; i < 16 * DY2_CH; i += NT) DY2[i] = 0.f;  // dY2 padding (phase E fills the argmaxes)
+  }
+  // the weights conv1 does not need are loaded into registers now and stored to LDS after the
+  // conv1 products: their global-load latency hides under conv1 instead of phase A's barrier
+  f4 lf2[3], lf3;
+  float lw2[3];
+  {
+    const f4* f2src = reinterpret_cast<const f4*>(master + OFF_F2W);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) lf2[k] = f2src[min(tid + NT * k, 2519)];
+    lf3 = reinterpret_cast<const f4*>(master + OFF_F3W)[min(tid, 209)];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) lw2[k] = master[OFF_C2W + min(tid + NT * k, 2399)];
   }
   lds_barrier();
   STAMP(1);
@@ -285,6 +291,17 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       C1[o * 196 + q] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = tid + NT * k;
+    if (i < 2400) {
+      const int o = i / 150, kk = i - 150 * o, c = kk / 25;
+      const int t = kk - 25 * c, ky = t / 5;
+      WT2[((o >> 1) * 6 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = lw2[k];
+      WD[(c * 16 + o) * WD_LD + WD_CPAD * c + kk - 25 * c] = lw2[k];
+    }
+  }
+  if (tid < 210) reinterpret_cast<f4*>(F3)[tid] = lf3;
   lds_barrier();
   STAMP(2);
 
@@ -384,6 +401,13 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       if (lane == 0 && o < 120) H1[o] = fmaxf(s + BIAS[B_F1 + o], 0.f);
     }
   }
+  // fc1 waits on L2 and leaves the LDS idle: the fc2 weights (in registers since phase A)
+  // and the zero padding of dY2 go in now
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (tid + NT * k < 2520) reinterpret_cast<f4*>(F2)[tid + NT * k] = lf2[k];
+  if (TRAIN)
+    for (int i = tid; i < 16 * DY2_CH; i += NT) DY2[i] = 0.f;  // dY2 padding (phase E fills the argmaxes)
   lds_barrier();
   STAMP(5);
   if (tid < 672) {  // fc2: 84 outputs x 8 lanes (15 inputs each)
@@ -451,7 +475,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       }
       base += __popcll(m);
     }
-    if (lane < W1_PARTS) T1[c * T1_LD + base + lane] = f2{0.f, 0.f};  // slices round up: zero pad
+    if (lane < 2 * W1_PARTS) T1[c * T1_LD + base + lane] = f2{0.f, 0.f};  // slices round up: zero pad
     if (lane == 0) NACT[c] = base;
   } else if (TRAIN && wave <= 14) {
     // and the conv2 table: channels o = 2 (wave - 7) + (lane >= 32), one per half wave
@@ -557,7 +581,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
           D[r][4 * j] = t.x; D[r][4 * j + 1] = t.y; D[r][4 * j + 2] = t.z; D[r][4 * j + 3] = t.w;
         }
       float w[28];
-      const f4* wr = reinterpret_cast<const f4*>(WD + (d_c * 16 + o) * WD_LD);
+      const f4* wr = reinterpret_cast<const f4*>(WD + (d_c * 16 + o) * WD_LD + WD_CPAD * d_c);
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
         const f4 t = wr[j];
@@ -625,9 +649,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     }
     LANE_STAMP(18, 128);
   }
+  WAVE_STAMP(24);
   lds_barrier();
   STAMP(12);
   if (tid < 168) {
+    float db1 = 0.f;  // this lane's 8 windows' share of the conv1 bias gradient
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const f2* part = reinterpret_cast<const f2*>(PART) + (q * 168 + d_r) * 4;
@@ -641,29 +667,33 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
         const int x = d_x0 + 2 * pp;
         if (x < 14) {
           // ReLU1 + pool1 backward: dP1 of an active window is the value of its entry in the
-          // conv1 weight-gradient table
+          // conv1 weight-gradient table (and part of the conv1 bias gradient)
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int q = (d_y0 + dy) * 14 + x + e;
             const int pos = PS1[d_c * 196 + q];
-            if (pos != 255) reinterpret_cast<float*>(T1 + d_c * T1_LD + pos)[0] = e ? dacc[dy][pp].y : dacc[dy][pp].x;
+            const float v = e ? dacc[dy][pp].y : dacc[dy][pp].x;
+            if (pos != 255) {
+              reinterpret_cast<float*>(T1 + d_c * T1_LD + pos)[0] = v;
+              db1 += v;
+            }
           }
         }
       }
+    DY2[tid] = db1;  // (dY2 is dead after the data gradient) partials in a fixed order: lane d_r = 28 c + yx
   }
   lds_barrier();
   STAMP(13);
 
   // ============ phase F: conv1 weight + bias gradient =====================================
-  static_assert(W1_PARTS * 90 <= 992 && 992 + 24 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
-  if (tid >= 992 && tid < 992 + 24) {  // conv1 bias gradient: 4 lanes per channel, fixed trip counts
-    const int c = (tid - 992) >> 2, l = tid & 3, n = NACT[c];
-    float sb = 0.f;
+  static_assert(W1_PARTS * 90 <= 992 && 992 + 6 <= NT, "conv1 weight-gradient tasks + bias lanes fit the block");
+  if (tid >= 992 && tid < 992 + 6) {  // conv1 bias gradient: the 28 epilogue partials of channel c
+    const int c = tid - 992;
+    const f4* pp = reinterpret_cast<const f4*>(DY2 + 28 * c);
+    f4 t = pp[0];
 #pragma unroll
-    for (int i = 0; i < 49; ++i) sb += masked(T1[c * T1_LD + 4 * i + l].x, 4 * i + l < n);
-    sb += __shfl_xor(sb, 1);
-    sb += __shfl_xor(sb, 2);
-    if (l == 0) slab[SLAB_C1B + c] = sb;
+    for (int i = 1; i < 7; ++i) t += pp[i];
+    slab[SLAB_C1B + c] = (t.x + t.y) + (t.z + t.w);
     LANE_STAMP(19, 992);
   }
   const float* XW = reinterpret_cast<const float*>(smem + L_F2);
@@ -671,21 +701,26 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     // dW1 over the active argmax pixels (table T1) of channel o, in 11 slices of s windows (the
     // zero pad entries round the last slices up); lanes of one channel share a wave
     const int o = tid / (15 * W1_PARTS), r = tid - 15 * W1_PARTS * o, part = r / 15, ck = r - 15 * part;
-    const int c = ck / 5, ky = ck - 5 * c, s = (NACT[o] + W1_PARTS - 1) / W1_PARTS;
-    const f2* tb = T1 + o * T1_LD + s * part;
+    // slices of an even number of windows: the table is read two entries per 16-B read
+    const int c = ck / 5, ky = ck - 5 * c, s2 = (NACT[o] + 2 * W1_PARTS - 1) / (2 * W1_PARTS);
+    const f4* tb = reinterpret_cast<const f4*>(T1 + o * T1_LD) + s2 * part;
     const float* xb = XW + c * XW_CH + ky * XW_RS;
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 6
-    for (int q = 0; q < s; ++q) {  // unrolled: six windows' table + pixel reads in flight
-      const f2 e = tb[q];
-      const float* xr = xb + __float_as_int(e.y);
+#pragma unroll 3
+    for (int q = 0; q < s2; ++q) {  // unrolled: six windows' table + pixel reads in flight
+      const f4 ee = tb[q];
+      const float* xr0 = xb + __float_as_int(ee.y);
+      const float* xr1 = xb + __float_as_int(ee.w);
 #pragma unroll
-      for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(e.x, xr[kx], acc[kx]);
+      for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(ee.x, xr0[kx], acc[kx]);
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(ee.z, xr1[kx], acc[kx]);
     }
 #pragma unroll
     for (int kx = 0; kx < 5; ++kx) PART[part * 450 + o * 75 + c * 25 + ky * 5 + kx] = acc[kx];
     LANE_STAMP(20, 0);
   }
+  WAVE_STAMP(40);
   lds_barrier();
   STAMP(14);
   if (tid < 450) {
@@ -700,6 +735,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   }
 #undef STAMP
 #undef LANE_STAMP
+#undef WAVE_STAMP
 }
 
 }  // namespace f32k

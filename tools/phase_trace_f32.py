@@ -23,9 +23,9 @@ def main(reps: int = 50, batch: int = 64):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, dtype="fp32")
     eng.attach(tr)
-    stamps = torch.zeros(21, dtype=torch.int64, device=eng.device)
+    stamps = torch.zeros(56, dtype=torch.int64, device=eng.device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rows, walls, lanes = [], [], []
+    rows, walls, lanes, waves = [], [], [], []
     e = eng
     for r in range(reps):
         eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
@@ -40,6 +40,7 @@ def main(reps: int = 50, batch: int = 64):
         st = stamps.cpu().numpy()
         rows.append(np.diff(st[:16]) * 0.01)
         lanes.append((st[16:21] - st[[11, 11, 11, 13, 13]]) * 0.01)
+        waves.append(np.concatenate([st[24:40] - st[11], st[40:56] - st[13]]) * 0.01)
     med = np.median(np.array(rows[5:]), axis=0)
     for name, v in zip(NAMES, med):
         print(f"{name:30s} {v:8.2f} us")
@@ -48,6 +49,9 @@ def main(reps: int = 50, batch: int = 64):
     for name, v in zip(["E: dgrad lanes done", "E: dW2 lanes done", "E: + XW copy done", "F: db1 lanes done",
                         "F: dW1 lanes done"], lm):
         print(f"  {name:28s} {v:8.2f} us after the phase start")
+    wm = np.median(np.array(waves[5:]), axis=0)
+    print("  E: wave w at the barrier (us after the phase start):", " ".join(f"{x:.2f}" for x in wm[:16]))
+    print("  F: wave w at the barrier (us after the phase start):", " ".join(f"{x:.2f}" for x in wm[16:]))
     print(f"{'kernel wall (event)':30s} {np.median(walls[5:]):8.2f} us")
 
 
