@@ -26,6 +26,7 @@ void rccl_abort(uintptr_t comm);
 void rccl_destroy(uintptr_t comm);
 // one-shot xGMI all-reduce (comm/xgmi_allreduce.hip)
 std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
+uintptr_t uncached_alloc(long long bytes);
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
 std::string xgmi_device_id();
@@ -45,6 +46,10 @@ using u = uintptr_t;
 template <typename T>
 static T* P(u x) { return reinterpret_cast<T*>(x); }
 static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
+// early-MLP overlap, in-launch form: grad_reduce(defer=1) stores the MLP reduction's arguments
+// here and the next fused_train(inlaunch_mlp=1) launches them as extra workgroups
+static dnn::ReduceArgs g_pending_mlp{};
+static bool g_pending_set = false;
 
 PYBIND11_MODULE(_dnn_hip, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
@@ -62,18 +67,24 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("fused_train",
         [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
-           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage) {
+           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage, u rowg,
+           u rowg_ctr, int inlaunch_mlp) {
+          if (inlaunch_mlp && !g_pending_set)
+            throw std::runtime_error("fused_train(inlaunch_mlp=1) needs a grad_reduce(defer=1) call first");
+          const dnn::ReduceArgs* red = inlaunch_mlp ? &g_pending_mlp : nullptr;
+          g_pending_set = false;
           dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order),
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
                                   P<long long>(stamps), P<const int32_t>(next_ids), P<unsigned char>(stage),
-                                  S(stream));
+                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red);
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
-        py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0);
+        py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0,
+        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch_mlp") = 0);
   m.def("fused_train_f32", [](u images, u labels, u order, int order_len, int batch, u state, u master, u a0, u h1,
                               u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
     dnn::launch_fused_train_f32(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), order_len,
@@ -98,7 +109,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
                           u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode,
-                          u xp_wait) {
+                          u xp_wait, u rg, u rg_ctr, u rg_err, double rg_timeout_s, int defer) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -106,11 +117,21 @@ PYBIND11_MODULE(_dnn_hip, m) {
                       P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping,
                       P<long long>(stamps)};
     a.next_ids = P<int32_t>(next_ids);
+    a.rg = P<const unsigned long long>(rg);
+    a.rg_ctr = P<unsigned>(rg_ctr);
+    a.rg_err = P<unsigned>(rg_err);
+    a.rg_timeout_ticks = (long long)(rg_timeout_s * 1.0e8);
     if (!xp_regions.empty()) {
       if ((int)xp_regions.size() > dnn::XG_MAX_RANKS || xp_rank < 0 || xp_rank >= (int)xp_regions.size())
         throw std::runtime_error("grad_reduce exchange: 1..8 ranks, rank in range");
-      if (lo != 0 || hi < dnn::ARENA || xp_capacity < dnn::ARENA || !xp_ctr || !xp_err || !xp_abort)
-        throw std::runtime_error("grad_reduce exchange: whole arena, region capacity >= arena, counters set");
+      // the whole arena, or one of the two split launches (early-MLP overlap): MLP range with
+      // counters from block 0, conv range with counters after the MLP launch's blocks
+      const bool whole = lo == 0 && hi >= dnn::ARENA, mlp = lo == dnn::OFF_F1W && hi >= dnn::ARENA,
+                 conv = lo == 0 && hi == dnn::OFF_F1W;
+      if (!(whole || mlp || conv) || xp_capacity < dnn::ARENA || !xp_ctr || !xp_err || !xp_abort)
+        throw std::runtime_error("grad_reduce exchange: whole arena or a split range, region capacity >= arena, "
+                                 "counters set");
+      a.xp_blk_off = conv ? dnn::grad_reduce_mlp_blocks() : 0;
       for (size_t r = 0; r < xp_regions.size(); ++r) a.xp_region[r] = P<unsigned char>(xp_regions[r]);
       a.xp_rank = xp_rank;
       a.xp_nranks = (int)xp_regions.size();
@@ -127,6 +148,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
       a.xp_wait = P<unsigned long long>(xp_wait);
     }
+    if (defer) {  // (early-MLP overlap) kept for the next fused_train(inlaunch_mlp=1) launch
+      g_pending_mlp = a;
+      g_pending_set = true;
+      return;
+    }
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
      py::arg("loss"), py::arg("correct"), py::arg("batch"), py::arg("master"), py::arg("grad"), py::arg("mom"),
@@ -135,7 +161,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("order"), py::arg("order_len"), py::arg("batch_ids"), py::arg("stream"), py::arg("stamps") = 0,
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
-     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0, py::arg("xp_wait") = 0);
+     py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0, py::arg("xp_wait") = 0,
+     py::arg("rg") = 0, py::arg("rg_ctr") = 0, py::arg("rg_err") = 0, py::arg("rg_timeout_s") = 10.0,
+     py::arg("defer") = 0);
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {
@@ -378,6 +406,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_close", &dnn::xgmi_close);
   m.def("xgmi_device_id", &dnn::xgmi_device_id);
   m.def("xgmi_free", &dnn::xgmi_free);
+  m.def("uncached_alloc", &dnn::uncached_alloc);
   m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
   m.def("xgmi_set_abort", &dnn::xgmi_set_abort);
   m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);
@@ -387,6 +416,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_xp_max_blocks", []() { return dnn::XP_MAX_BLOCKS; });
   m.def("xgmi_wait_ring", []() { return py::make_tuple(dnn::XP_WAIT_RING, dnn::XP_MAX_BLOCKS, 4); });
   m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
+  m.def("grad_reduce_mlp_blocks", []() { return dnn::grad_reduce_mlp_blocks(); });
+  m.def("row_granules", []() { return dnn::RG_ROW; });  // granules per sample (early-MLP overlap)
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
                              double timeout_s, u stream, int form, u wait) {

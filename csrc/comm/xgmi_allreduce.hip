@@ -290,6 +290,17 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity) {
   return {reinterpret_cast<uintptr_t>(p), std::string(h.reserved, HIP_IPC_HANDLE_SIZE), kind};
 }
 
+// Uncached (fine-grained) device memory, zeroed, for on-GPU hand-offs by tagged granules
+// between concurrently running kernels (the early-MLP row granules): every access bypasses
+// the per-XCD L2s, as the xGMI regions' do.  Freed with xgmi_free.
+uintptr_t uncached_alloc(long long bytes) {
+  void* p = nullptr;
+  xcheck(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  xcheck(hipMemset(p, 0, bytes), "hipMemset(uncached)");
+  xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return reinterpret_cast<uintptr_t>(p);
+}
+
 uintptr_t xgmi_open(const std::string& handle) {
   if (handle.size() != HIP_IPC_HANDLE_SIZE) throw std::runtime_error("bad IPC handle size");
   hipIpcMemHandle_t h;

@@ -47,6 +47,34 @@ constexpr int H2_LD = 84;   // relu(fc2)
 constexpr int Z1_LD = 120;  // dL/d(fc1 pre-activation)
 constexpr int Z2_LD = 84;   // dL/d(fc2 pre-activation)
 constexpr int Z3_LD = 16;   // dL/dlogits (10 used)
+// Early-MLP overlap (row granules): the six MLP rows of sample b as 8-byte {fp32 value, step}
+// words in one buffer [a0 | h1 | h2 | z1 | z2 | z3] x batch, written by the fused kernel with
+// system-scope stores and polled by the concurrently running MLP reduction (reduce_sgd.hip)
+// until each tag shows the step - no flag, fence or kernel boundary between the two.
+constexpr int RG_ROW = A0_LD + H1_LD + H2_LD + Z1_LD + Z2_LD + Z3_LD;  // granules per sample
+__device__ __forceinline__ long long rg_off(int which, int batch) {  // start of row kind `which`
+  const int ld[6] = {A0_LD, H1_LD, H2_LD, Z1_LD, Z2_LD, Z3_LD};
+  long long o = 0;
+  for (int k = 0; k < which; ++k) o += (long long)batch * ld[k];
+  return o;
+}
+// the fused kernels' side: sample b's six rows (null source: zeros) as {value, tag} words
+__device__ __forceinline__ void put_row_granules(unsigned long long* rg, int batch, int b, unsigned tag, int tid,
+                                                 int nt, const float* a0, const float* h1, const float* h2,
+                                                 const float* z1, const float* z2, const float* z3) {
+  const float* src[6] = {a0, h1, h2, z1, z2, z3};
+  const int ld[6] = {A0_LD, H1_LD, H2_LD, Z1_LD, Z2_LD, Z3_LD};
+  const unsigned long long t = (unsigned long long)tag << 32;
+  long long base = 0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    unsigned long long* row = rg + base + (long long)b * ld[k];
+    for (int i = tid; i < ld[k]; i += nt)
+      __hip_atomic_store(row + i, t | __float_as_uint(src[k] != nullptr ? src[k][i] : 0.f), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    base += (long long)batch * ld[k];
+  }
+}
 
 constexpr int IMG = 3 * 32 * 32;
 

@@ -46,13 +46,26 @@ struct ReduceArgs {
   // diagnostic / accounting: per-step exchange wait (max over lanes, s_memrealtime ticks) as
   // {step << 32 | ticks} words in a ring of XP_WAIT_RING entries (one plain store per wave)
   unsigned long long* xp_wait = nullptr;
+  // split exchange launches (early-MLP overlap): this launch's blocks use step counters and the
+  // two-hop owner mapping of blocks xp_blk_off + blockIdx (the two launches take disjoint
+  // ranges, so every element keeps one counter)
+  int xp_blk_off = 0;
+  // early-MLP overlap (rg != nullptr, MLP-range launch only): the MLP rows are read as
+  // {value, step} granules (common.h RG_ROW) written by the concurrently running fused kernel;
+  // rg_ctr[block] counts this launch's steps (the fused kernel's blocks count theirs), a wait
+  // past rg_timeout_ticks or a set abort word sets *rg_err (sticky) instead of hanging
+  const unsigned long long* rg = nullptr;
+  unsigned* rg_ctr = nullptr;
+  unsigned* rg_err = nullptr;
+  long long rg_timeout_ticks = 0;
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
-                        hipStream_t stream);
+                        hipStream_t stream, unsigned long long* rowg = nullptr, unsigned* rowg_ctr = nullptr,
+                        const ReduceArgs* mlp_red = nullptr);
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);
@@ -72,6 +85,8 @@ void init_kernels();
 void init_kernels_f32();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
 int grad_reduce_blocks();  // grid of a whole-arena grad_reduce launch (with bookkeeping)
+int grad_reduce_mlp_blocks();  // grid of its MLP-range part (the split launches' block offset)
+int inlaunch_mlp_workgroups();  // extra workgroups of a fused launch with the in-launch MLP reduction
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
                         const uint8_t* images, const int32_t* labels, int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream);

@@ -34,7 +34,7 @@
 //    barriers (s_waitcnt lgkmcnt(0); s_barrier) that leave vmcnt alone.
 //  * Every MFMA loop issues all of a tile's operand loads before its MFMA chain
 //    (sched_barrier), so LDS latency is paid once per batch, not once per K-step.
-#include "launchers.h"
+#include "reduce_device.h"
 
 namespace dnn {
 
@@ -227,7 +227,7 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
 }
 
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
-template <bool TRAIN, bool STAGED = false>
+template <bool TRAIN, bool STAGED = false, int RNR = 0>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -241,12 +241,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
     long long* __restrict__ stamps,
     const int32_t* __restrict__ next_ids,  // TRAIN + stage: sample ids of the NEXT step (-1: none)
-    unsigned char* __restrict__ stage) {   // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
+    unsigned char* __restrict__ stage,     // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
+    unsigned long long* __restrict__ rowg,  // TRAIN, early-MLP overlap: the MLP rows as granules
+    unsigned* __restrict__ rowg_ctr,        //   and this block's step counter (common.h RG_ROW)
+    const ReduceArgs ra, int red_wg) {      //   and the in-launch MLP reduction (workgroups >= batch)
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
   // address - one dependent load level (batch id -> image) off the start of phase A.
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if constexpr (TRAIN) {
+    // early-MLP overlap: workgroups past the samples reduce the MLP gradient (+ exchange + SGD),
+    // polling the rows the sample workgroups publish as granules after phase D' - while those
+    // still run the conv backward.  Dispatched after the samples (higher ids), no LDS use.
+    if (RNR > 0 && (int)blockIdx.x >= batch) {
+      inlaunch_mlp_reduce<RNR>(ra, (int)blockIdx.x - batch);
+      return;
+    }
+  }
   // per-block diagnostic trace (stamps != nullptr): stamps[16 + 4 * block + k], k = 0 start,
   // 1 rows published, 2 end, 3 XCC id
   const bool btrace = stamps != nullptr && threadIdx.x == 0;
@@ -289,7 +301,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     valid = gidx < order_len;
     sample = (int)gidx;
   }
+  // early-MLP overlap: this step's row tag, read by every thread before thread 0 advances the
+  // counter (several workgroup barriers later)
+  const unsigned row_tag = (TRAIN && rowg != nullptr) ? rowg_ctr[b] + 1u : 0u;
   if (!valid) {
+    if (TRAIN && rowg != nullptr) {
+      put_row_granules(rowg, batch, b, row_tag, tid, NT, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+      __syncthreads();
+      if (tid == 0) rowg_ctr[b] = row_tag;
+    }
     if (TRAIN) {
       for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
       for (int i = tid; i < H1_LD; i += NT) {
@@ -625,11 +645,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int ks = 0; ks < 4; ++ks) acc = mfma32(av[ks], bv[ks], acc);
     if (fg == 0) DA0[16 * nt + fr] = acc[0];  // (the pool2/ReLU mask is applied via CODE2)
   }
-  // per-sample rows for the batch-reduced fc weight gradients
-  for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
-  if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
-  if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
-  if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
+  // per-sample rows for the batch-reduced fc weight gradients: plain rows for the reduce
+  // launch that follows, or (early-MLP overlap) tagged granules that the concurrently running
+  // MLP reduction polls - it starts on them while this block still runs phases E and F
+  if (rowg != nullptr) {
+    put_row_granules(rowg, batch, b, row_tag, tid, NT, A0, H1, H2, DZ1, DZ2, DZ3);
+    if (tid == 0) rowg_ctr[b] = row_tag;  // (every thread read the counter at the kernel start)
+  } else {
+    for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
+    if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
+    if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
+    if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
+  }
   lds_barrier();
 
   STAMP(5);
@@ -902,12 +929,11 @@ namespace dnn {
 void init_kernels() {
   static bool done = false;
   if (done) return;
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
-  HIP_CHECK(hipFuncSetAttribute((const void*)lenet_fused_kernel<false, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
+  const void* kerns[] = {(const void*)lenet_fused_kernel<true, false, 0>, (const void*)lenet_fused_kernel<true, true, 0>,
+                         (const void*)lenet_fused_kernel<true, false, 1>, (const void*)lenet_fused_kernel<true, true, 1>,
+                         (const void*)lenet_fused_kernel<true, false, 8>, (const void*)lenet_fused_kernel<true, true, 8>,
+                         (const void*)lenet_fused_kernel<false, false, 0>};
+  for (const void* k : kerns) HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   init_kernels_f32();
   done = true;
 }
@@ -916,12 +942,27 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
-                        hipStream_t stream) {
+                        hipStream_t stream, unsigned long long* rowg, unsigned* rowg_ctr, const ReduceArgs* mlp_red) {
   init_kernels();
   if (stage != nullptr && next_ids == nullptr) throw std::runtime_error("fused_train: staging needs next_ids");
-  auto* kern = stage ? &lenet_fused_kernel<true, true> : &lenet_fused_kernel<true, false>;
-  hipLaunchKernelGGL(kern, dim3(batch), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len, batch, 0,
-                     state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, next_ids, stage);
+  if ((rowg == nullptr) != (rowg_ctr == nullptr)) throw std::runtime_error("fused_train: row granules need their counters");
+  ReduceArgs ra{};
+  int red_wg = 0;
+  if (mlp_red != nullptr) {  // in-launch MLP reduction of the early-MLP overlap
+    ra = *mlp_red;
+    if (rowg == nullptr || ra.rg != rowg || ra.lo != OFF_F1W || ra.hi < ARENA || ra.bookkeeping || ra.batch != batch ||
+        ra.rg_ctr == nullptr || ra.rg_err == nullptr || ra.xp_blk_off != 0)
+      throw std::runtime_error("fused_train: the in-launch MLP reduction reads this launch's row granules (MLP range)");
+    red_wg = INLAUNCH_MLP_WG;
+  }
+  const int rnr = red_wg == 0 ? 0 : (ra.xp_nranks == 0 ? 1 : 8);
+  if (rnr == 8 && (ra.xp_mode & 4)) throw std::runtime_error("fused_train: the in-launch MLP reduction has fp32 granules only");
+  auto* kern = rnr == 0 ? (stage ? &lenet_fused_kernel<true, true, 0> : &lenet_fused_kernel<true, false, 0>)
+               : rnr == 1 ? (stage ? &lenet_fused_kernel<true, true, 1> : &lenet_fused_kernel<true, false, 1>)
+                          : (stage ? &lenet_fused_kernel<true, true, 8> : &lenet_fused_kernel<true, false, 8>);
+  hipLaunchKernelGGL(kern, dim3(batch + red_wg), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len,
+                     batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, next_ids,
+                     stage, rowg, rowg_ctr, ra, red_wg);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -932,7 +973,8 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     ReduceArgs{}, 0);
   HIP_CHECK(hipGetLastError());
 }
 

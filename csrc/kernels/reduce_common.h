@@ -60,8 +60,47 @@ constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
 constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
 constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
 
-template <int LAYER, class Sink>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
+// Early-MLP overlap: poll N row granules (a.rg + off[k]) until each tag shows `tag`, values
+// into v.  Every load of a round is in flight before the first check; bounded (rg_timeout /
+// abort word -> sticky *rg_err, zeros then flow into this step: the host raises at the next
+// check).  The rows were stored by the fused kernel's blocks as ONE 8-byte system-scope word
+// {value, step} each, so a tag match IS the value - no flag or fence orders anything.
+template <int N>
+__device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N], unsigned tag, bool failed,
+                                        float (&v)[N]) {
+  static_assert(N <= 32, "pending mask");
+  unsigned pending = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
+  const long long t0 = wall_clock64();
+  while (true) {
+    unsigned long long x[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (pending & (1u << k)) x[k] = __hip_atomic_load(a.rg + off[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if ((pending & (1u << k)) && (unsigned)(x[k] >> 32) == tag) {
+        v[k] = __uint_as_float((unsigned)x[k]);
+        pending &= ~(1u << k);
+      }
+    if (pending == 0u) break;
+    if (failed) {
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (pending & (1u << k)) v[k] = 0.f;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > a.rg_timeout_ticks ||
+        (a.xp_abort != nullptr && __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      __hip_atomic_store(a.rg_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      failed = true;
+    }
+  }
+}
+
+// GR: rtag = this reduction block's row tag, rfail = an earlier wait failed (skip the waits)
+template <int LAYER, bool GR, class Sink>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
   using L = Fc<LAYER>;
   const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
   const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
@@ -86,11 +125,29 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
     // every operand load is unconditional (clamped address) and issued before the first
     // MFMA; out-of-range operands are zeroed by a select afterwards
     float av[16], bv[16];
+    if constexpr (GR) {  // row granules [a0 | h1 | h2 | z1 | z2 | z3] (common.h)
+      const int zo = (int)rg_off(3 + LAYER, a.batch), xo = (int)rg_off(LAYER, a.batch);
+      int off[32];
+      float v[32];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int b = min(b0 + 4 * s + kq, a.batch - 1);
-      av[s] = z[b * L::ZLD + omc];
-      bv[s] = x[b * L::XLD + inc];
+      for (int s = 0; s < 16; ++s) {
+        const int b = min(b0 + 4 * s + kq, a.batch - 1);
+        off[s] = zo + b * L::ZLD + omc;
+        off[16 + s] = xo + b * L::XLD + inc;
+      }
+      rg_poll<32>(a, off, rtag, rfail, v);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        av[s] = v[s];
+        bv[s] = v[16 + s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int b = min(b0 + 4 * s + kq, a.batch - 1);
+        av[s] = z[b * L::ZLD + omc];
+        bv[s] = x[b * L::XLD + inc];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -115,12 +172,23 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk) {
 // reproducible), 16-load chains
 // instead of 64, 4x the threads in flight.
 constexpr int SPLIT = 4;
-__device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q) {
+// GR (early-MLP overlap): src is a row-granule offset into a.rg instead of a float pointer
+template <bool GR = false>
+__device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q,
+                                                  const ReduceArgs* ga = nullptr, int gbase = 0, unsigned rtag = 0,
+                                                  bool rfail = false) {
   float g = 0.f;
   for (int b0 = 0; b0 < batch; b0 += 64) {
     float v[16];
+    if constexpr (GR) {
+      int off[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = src[min(b0 + 16 * q + k, batch - 1) * ld + col];
+      for (int k = 0; k < 16; ++k) off[k] = gbase + min(b0 + 16 * q + k, batch - 1) * ld + col;
+      rg_poll<16>(*ga, off, rtag, rfail, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = src[min(b0 + 16 * q + k, batch - 1) * ld + col];
+    }
     __builtin_amdgcn_sched_barrier(0);  // all 16 loads in flight before the first wait
 #pragma unroll
     for (int k = 0; k < 16; ++k) g += (b0 + 16 * q + k < batch) ? v[k] : 0.f;
@@ -136,21 +204,22 @@ __device__ __forceinline__ float column_sum_split(const float* src, int ld, int 
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
-template <class Sink>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk) {
+template <bool GR, class Sink>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
   const float* zp;
-  int ld, col, n, off;
-  if (grp < 8) { zp = a.z1; ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; }
-  else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; }
-  else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; }
+  int ld, col, n, off, kind;
+  if (grp < 8) { zp = a.z1; ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; kind = 3; }
+  else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; kind = 4; }
+  else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; kind = 5; }
   const float* src = zp;
   const int cc = min(col, n - 1);  // padding lanes recompute a real column (no divergence)
   const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split(src, ld, cc, a.batch, q);  // every lane shuffles: no early exit
+  const float g = column_sum_split<GR>(src, ld, cc, a.batch, q, &a, GR ? (int)rg_off(kind, a.batch) : 0, rtag,
+                                       rfail);  // every lane shuffles: no early exit
   if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
 

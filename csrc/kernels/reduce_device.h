@@ -1,0 +1,339 @@
+// Device code of the batch reduction + momentum SGD + one-launch xGMI exchange, shared by the
+// grad_reduce kernel (reduce_sgd.hip) and the fused kernel's in-launch MLP reduction
+// (lenet_fused.hip, early-MLP overlap).  See reduce_sgd.hip for the parity notes.
+#pragma once
+#include "reduce_common.h"
+
+namespace dnn {
+
+constexpr int RT = 256;
+static_assert(RT % SPLIT == 0, "split column lanes stay inside a wave");
+
+
+
+// One launch's blocks: [MLP tile blocks][MLP bias blocks][conv element blocks][bookkeeping].
+// Returns true (block-uniform) when this block reduced arena elements.
+// rblk / rtid: the reduction block and its thread (grad_reduce_kernel: blockIdx / threadIdx;
+// the fused kernel's in-launch MLP reduction: two 256-thread reduction blocks per workgroup).
+// GR: rtag / rfail as fc_tile's.
+template <bool GR, class Sink>
+__device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk, int rblk, int rtid, unsigned rtag = 0,
+                                                 bool rfail = false) {
+  const bool mlp = a.hi > OFF_F1W;
+  const bool conv = a.lo < OFF_F1W;
+  int blk = rblk;
+  if (mlp) {
+    if (blk < TILE_BLOCKS) {
+      const int t = blk * 4 + (rtid >> 6);
+      if (t < FC_T0) fc_tile<0, GR>(t, a, sk, rtag, rfail);
+      else if (t < FC_T0 + FC_T1) fc_tile<1, GR>(t - FC_T0, a, sk, rtag, rfail);
+      else if (t < FC_TILES) fc_tile<2, GR>(t - FC_T0 - FC_T1, a, sk, rtag, rfail);
+      return true;
+    }
+    blk -= TILE_BLOCKS;
+    constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
+    if (blk < FB) {
+      fcb_task<GR>(blk * RT + rtid, a, sk, rtag, rfail);
+      return true;
+    }
+    blk -= FB;
+  }
+  if (conv) {
+    constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
+    if (blk < CB) { conv_task(blk * RT + rtid, a, sk); return true; }
+    blk -= CB;
+  }
+  if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping(a, rtid);
+  return false;
+}
+
+constexpr int GRAD_REDUCE_BLOCKS =
+    TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT + (CONV_SLOTS + RT - 1) / RT + 1;
+static_assert(GRAD_REDUCE_BLOCKS <= XP_MAX_BLOCKS, "one exchange step counter per reduce block");
+
+__device__ __forceinline__ unsigned long long xp_ld(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Exchange-wait accounting (ReduceArgs::xp_wait, optional): every wave stores the longest wait
+// of its lanes for this step (s_memrealtime ticks, 100 MHz) into its own word of the ring entry
+// [step % XP_WAIT_RING][block][wave] as {step << 32 | ticks} - a plain store per wave, no
+// atomics; the host takes the max over blocks and waves (parallel/xgmi.py wait_stats).
+__device__ __forceinline__ void record_wait(const ReduceArgs& a, unsigned step, long long ticks, int rblk, int rtid) {
+  if (a.xp_wait == nullptr) return;
+  unsigned t = (unsigned)min(ticks, 0xffffffffll);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t = max(t, (unsigned)__shfl_xor((int)t, off));
+  if ((rtid & 63) == 0) {
+    const int w = rtid >> 6;
+    a.xp_wait[((size_t)(step % XP_WAIT_RING) * XP_MAX_BLOCKS + rblk + a.xp_blk_off) * (RT / 64) + w] =
+        ((unsigned long long)step << 32) | t;
+  }
+}
+
+// Poll the granules in `pending` (bit 4 r + j: element j of source r) until each tag shows
+// `step`; the values land in v[r][j].  Every load of a round is in flight before the first
+// check.  Bounded: timeout / abort word -> sticky error word, never a hang.  Returns the wait.
+template <int NR>
+__device__ __forceinline__ long long poll_granules(const ReduceArgs& a, const unsigned long long* const (&src)[NR],
+                                                   const int (&e)[4], unsigned pending, unsigned step, bool failed,
+                                                   float (&v)[NR][4]) {
+  const long long t0 = wall_clock64();
+  while (pending != 0u) {
+    unsigned long long x[NR][4];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (pending & (1u << (4 * r + j))) x[r][j] = xp_ld(src[r] + e[j]);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((pending & (1u << (4 * r + j))) && (unsigned)(x[r][j] >> 32) == step) {
+          v[r][j] = __uint_as_float((unsigned)x[r][j]);
+          pending &= ~(1u << (4 * r + j));
+        }
+    if (pending == 0u || failed) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > a.xp_timeout_ticks ||
+        __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      __hip_atomic_store(a.xp_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  return wall_clock64() - t0;
+}
+
+template <bool PK>
+__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSinkT<PK>& sk, const float (&s)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!sk.v[j]) continue;
+    const float gr = s[j] * a.xp_scale;
+    float p, m;
+    sgd_update(gr, sk.p[j], sk.m[j], a.lr, a.momentum, p, m);
+    a.mom[sk.e[j]] = m;
+    a.master[sk.e[j]] = p;
+    write_shadow(a.shadow, sk.e[j], p);
+  }
+}
+
+// bf16 granules (PK): round the pairs (0, 1) and (2, 3) of x to bf16 IN PLACE - a lane's own
+// contribution included, so every rank sums the same numbers - and, if dst, publish each pair
+// as one granule {lo | hi << 16, step} at the index of its first element (unique: an element
+// has one owner lane)
+template <bool PK>
+__device__ __forceinline__ void pack_pairs(float (&x)[4], const bool (&valid)[4], const int (&e)[4],
+                                           unsigned long long* dst, unsigned long long tag) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+      if (!valid[k]) continue;
+      const unsigned lo = bf16_bits(x[k]), hi = valid[k + 1] ? bf16_bits(x[k + 1]) : 0u;
+      x[k] = bf16_lo(lo);
+      x[k + 1] = bf16_lo(hi);
+      if (dst != nullptr)
+        __hip_atomic_store(dst + e[k], tag | (unsigned long long)(lo | (hi << 16)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// which of a lane's elements are polled as granules: all valid ones, or (PK) each pair's first
+template <bool PK>
+__device__ __forceinline__ bool polled(const bool (&valid)[4], int j) { return valid[j] && (!PK || (j & 1) == 0); }
+
+// PK: a polled pair's raw word (in x[k]) -> its two values
+template <bool PK>
+__device__ __forceinline__ void unpack_pairs(float (&x)[4], const bool (&valid)[4]) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2)
+      if (valid[k]) {
+        const unsigned w = __float_as_uint(x[k]);
+        x[k] = bf16_lo(w);
+        x[k + 1] = bf16_hi(w);
+      }
+  }
+}
+
+// The one-launch all-reduce exchange of ONE lane's (<= 4) reduced elements.  Each element
+// was stored as a granule {value, step} (XpSink::put); the lane reads the same element's
+// granule from every peer's slot over xGMI (7 links at once) until each tag shows this step,
+// sums the N values in RANK ORDER (bit-identical replicas), scales by 1/N and applies momentum
+// SGD + the bf16 images.  The value and its tag are one 8-byte atomic word, so no flag, fence or
+// barrier orders anything: a tag match IS the data.
+// Double buffering by step parity: the owner overwrites its element e of slot (s & 1) at step
+// s + 2 only after it read every peer's step s + 1 granule of e, which each peer wrote only
+// after it had read the owner's step s granule of e.
+// NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
+// group does not pay for 8 ranks' loads in flight.  PK: bf16 granules (half the link bytes;
+// the sum stays fp32 in rank order).
+template <int NR, bool PK>
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed, int rblk,
+                                            int rtid) {
+  const int par = step & 1u;
+  pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);
+  float v[NR][4];
+  unsigned pending = 0;
+  const unsigned long long* src[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[r][j] = sk.g[j];
+      if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
+    }
+  }
+  record_wait(a, step, poll_granules<NR>(a, src, sk.e, pending, step, failed, v), rblk, rtid);
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
+  float s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[j] = v[0][j];
+#pragma unroll
+    for (int r = 1; r < NR; ++r)
+      if (r < a.xp_nranks) s[j] += v[r][j];
+  }
+  apply_update(a, sk, s);
+}
+
+// The two-hop pull form (xp_mode bit 2): reduce-scatter + all-gather where every rank writes
+// only its OWN region.  Block k's elements belong to rank k % N.  A non-owner lane has stored
+// its granules into its own pull slot (XpSink::put); the owner lane reads them from the N - 1
+// peers' pull slots, sums the N values in RANK ORDER (the same fp32 additions as xp_exchange,
+// so both forms give bit-identical parameters), stores {sum, step} into its own ag slot and
+// applies SGD; the other ranks read that slot.  2 E / N granules per link instead of E, one
+// more dependent remote read.  PK: the sum is all-gathered as bf16 too (every rank, the owner
+// included, applies the rounded sum).
+template <int NR, bool PK>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed,
+                                                 int rblk, int rtid) {
+  const int par = step & 1u;
+  const int owner = (rblk + a.xp_blk_off) % a.xp_nranks;
+  pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);  // (null own on the owner: rounding only)
+  float s[4];
+  long long waited;
+  if (owner == a.xp_rank) {
+    float v[NR][4];
+    unsigned pending = 0;
+    const unsigned long long* src[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[r][j] = sk.g[j];
+        if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
+      }
+    }
+    waited = poll_granules<NR>(a, src, sk.e, pending, step, failed, v);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = v[0][j];
+#pragma unroll
+      for (int r = 1; r < NR; ++r)
+        if (r < a.xp_nranks) s[j] += v[r][j];
+    }
+    const unsigned long long tag = (unsigned long long)step << 32;
+    unsigned long long* dst =
+        reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
+    if constexpr (PK) {
+      pack_pairs<PK>(s, sk.v, sk.e, dst, tag);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (sk.v[j])
+          __hip_atomic_store(dst + sk.e[j], tag | __float_as_uint(s[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else {
+    const unsigned long long* src[1] = {
+        reinterpret_cast<const unsigned long long*>(a.xp_region[owner] + a.xp_ag_off + par * a.xp_gslot_bytes)};
+    float v[1][4];
+    unsigned pending = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[0][j] = 0.f;
+      if (polled<PK>(sk.v, j)) pending |= 1u << j;
+    }
+    waited = poll_granules<1>(a, src, sk.e, pending, step, failed, v);
+    unpack_pairs<PK>(v[0], sk.v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = v[0][j];
+  }
+  record_wait(a, step, waited, rblk, rtid);
+  apply_update(a, sk, s);
+}
+
+
+// One reduction block's work (rblk, rtid as grad_reduce_body's).  NR = 1: local reduction
+// (+ SGD, or gradients out); NR = 2 / 4 / 8: the one-launch exchange for groups of up to NR
+// ranks (separate instances keep the local step's registers at its own need).  GR: the MLP
+// reduction of the early-MLP overlap (rows as granules from the fused kernel's sample blocks).
+// Every thread of the workgroup calls it once (it has a workgroup barrier).
+template <int NR, bool PK, bool GR>
+__device__ __forceinline__ void reduce_block(const ReduceArgs& a, int rblk, int rtid) {
+  unsigned rtag = 0;
+  bool rfail = false;
+  if constexpr (GR) {
+    rtag = a.rg_ctr[rblk] + 1u;
+    rfail = *a.rg_err != 0u;
+  }
+  if constexpr (NR > 1) {  // one-launch all-reduce: reduce -> exchange -> SGD, per lane
+    const int gb = rblk + a.xp_blk_off;  // (split launches: disjoint counter ranges)
+    const unsigned step = a.xp_ctr[gb] + 1u;
+    const bool failed = *a.xp_err != 0u;
+    XpSinkT<PK> sk;
+    sk.tag = (unsigned long long)step << 32;
+    // pull: every lane's granules go to this rank's slot; two-hop: only non-owners' (the owner
+    // publishes the SUM in its ag slot instead)
+    const bool publish = (a.xp_mode & 2) == 0 || gb % a.xp_nranks != a.xp_rank;
+    sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                             (step & 1u) * a.xp_gslot_bytes)
+                     : nullptr;
+    if (grad_reduce_body<GR>(a, sk, rblk, rtid, rtag, rfail)) {
+      if ((a.xp_mode & 2) == 0) xp_exchange<NR, PK>(a, sk, step, failed, rblk, rtid);
+      else xp_exchange_rsag<NR, PK>(a, sk, step, failed, rblk, rtid);
+    }
+    __syncthreads();  // every thread read this block's counters before they advance
+    if (rtid == 0) {
+      a.xp_ctr[gb] = step;
+      if constexpr (GR) a.rg_ctr[rblk] = rtag;
+    }
+  } else {
+    DirectSink d;
+    grad_reduce_body<GR>(a, d, rblk, rtid, rtag, rfail);
+    if constexpr (GR) {
+      __syncthreads();
+      if (rtid == 0) a.rg_ctr[rblk] = rtag;
+    }
+  }
+}
+
+
+// The fused kernel's in-launch MLP reduction (early-MLP overlap): workgroups batch .. of the
+// fused launch run reduction blocks 2 (w - batch) and 2 (w - batch) + 1, one per 256-thread
+// half.  RNR: 1 = local step, 8 = the one-launch exchange of up to 8 ranks (pull or two-hop,
+// fp32 granules) - one instance per fused-kernel instance (a run-time choice among several
+// would make the compiler copy the argument block to scratch).
+template <int RNR>
+__device__ __forceinline__ void inlaunch_mlp_reduce(const ReduceArgs& a, int wg) {
+  const int half = threadIdx.x >> 8, rblk = 2 * wg + half, rtid = threadIdx.x & 255;
+  const int nblk = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
+  // (an odd block count leaves the last half idle; it still meets the workgroup barrier)
+  if (rblk >= nblk) {
+    __syncthreads();
+    return;
+  }
+  reduce_block<RNR, false, true>(a, rblk, rtid);
+}
+constexpr int INLAUNCH_MLP_WG = (TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT + 1) / 2;
+
+}  // namespace dnn

@@ -211,7 +211,7 @@ class HipEngine(Engine):
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
                  use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None,
-                 dtype: str = "bf16") -> None:
+                 dtype: str = "bf16", early_mlp: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if dtype not in ("bf16", "fp32"):
             raise ValueError(f"HipEngine dtype must be bf16 or fp32, not {dtype!r}")
@@ -264,6 +264,20 @@ class HipEngine(Engine):
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
+        # early-MLP overlap (bf16 kernel, local step or one-launch xGMI exchange): the MLP
+        # reduction (+ its exchange + SGD) runs in extra workgroups of the fused launch,
+        # CONCURRENTLY with the samples, polling the rows they publish as {value, step} granules
+        # after phase D' while they still run the conv backward; the conv reduction follows as
+        # its own launch.  Bit-identical to the serial step (same sums, same order).  (A side-
+        # stream form with a graph fork/join measured 28.3 vs 19.8 us/step: profiles/r3/early_mlp.)
+        if early_mlp is None:
+            early_mlp = os.environ.get("DNN_EARLY_MLP", "0") == "1" and dtype == "bf16"
+        if early_mlp and dtype != "bf16":
+            raise ValueError("early-MLP overlap is a feature of the bf16 kernel")
+        self.early_mlp = bool(early_mlp)
+        self._rg: dict | None = None
+        if dtype == "bf16":
+            self._rg_buffers()  # (allocated up front: never inside a graph capture)
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.params_changed()
@@ -340,8 +354,65 @@ class HipEngine(Engine):
                              self.order_len, self._p(self.batch_ids), s,
                              next_ids=self._p(self.next_ids) if self._staged else 0, **xg)
 
+    RG_TIMEOUT_S = 10.0  # bound of one early-MLP row wait (then a sticky error word, raised at epoch_stats)
+
+    def _rg_buffers(self) -> dict:
+        """Row-granule buffer (uncached device memory: every access bypasses the per-XCD L2s),
+        the fused blocks' and the MLP-reduction blocks' step counters and the error word."""
+        if self._rg is None:
+            ptr = self.ext.uncached_alloc(self.batch * self.ext.row_granules() * 8)
+            i32 = dict(device=self.device, dtype=torch.int32)
+            self._rg = dict(ptr=ptr, fctr=torch.zeros(self.batch, **i32),
+                            rctr=torch.zeros(self.ext.grad_reduce_mlp_blocks(), **i32), err=torch.zeros(1, **i32))
+        return self._rg
+
+    def early_failed(self) -> bool:
+        return self._rg is not None and int(self._rg["err"].item()) != 0
+
+    def __del__(self) -> None:
+        rg = getattr(self, "_rg", None)
+        if rg is not None:
+            try:
+                torch.cuda.synchronize(self.device)
+                self.ext.xgmi_free(rg["ptr"])
+            except Exception:
+                pass
+
+    def _early_ok(self) -> bool:
+        if not self.early_mlp or self.dtype != "bf16":
+            return False
+        if self.grad_sync is None:
+            return True
+        # (the in-launch MLP reduction carries fp32 granules only)
+        return (getattr(self.grad_sync, "fuses_sgd", False) and self.grad_sync.group.one_launch
+                and not self.grad_sync.group.xp_mode & 4)
+
+    def _launch_step_early(self) -> None:
+        """ONE launch: the fused kernel's sample workgroups + extra workgroups that reduce the MLP
+        gradient (+ exchange + SGD), polling the rows the samples publish as {value, step}
+        granules after phase D' - while the samples still run the conv backward; then the conv
+        reduction + bookkeeping (split launch) on the same stream."""
+        rg = self._rg_buffers()
+        xg = self.grad_sync.group.exchange() if self.grad_sync is not None else {}
+        s = self._stream()
+        mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
+        self._reduce(1, mlp[0], mlp[1], 0, s, rg=rg["ptr"], rg_ctr=self._p(rg["rctr"]), rg_err=self._p(rg["err"]),
+                     rg_timeout_s=self.RG_TIMEOUT_S, defer=1, **xg)
+        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
+                             self.order_len, self.batch, self._p(self.state), self._p(self.master),
+                             self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
+                             self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
+                             self._p(self.loss), self._p(self.correct), s,
+                             next_ids=self._p(self.next_ids) if self._staged else 0,
+                             stage=self._p(self.stage) if self._staged else 0,
+                             rowg=rg["ptr"], rowg_ctr=self._p(rg["fctr"]), inlaunch_mlp=1)
+        self._reduce(1, conv[0], conv[1], 1, s, **xg)
+
     def _launch_step(self) -> None:
         assert self.train is not None
+        if self._early_ok():
+            self._launch_step_early()
+            return
         s = self._stream()
         if self.dtype == "fp32":
             self.ext.fused_train_f32(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
@@ -458,7 +529,7 @@ class HipEngine(Engine):
         return all(v == 1.0 for v in votes)
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, id(self.grad_sync), self.overlap, self.order_len,
+        key = (nsteps, id(self.grad_sync), self.overlap, self.early_mlp, self.order_len,
                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
                getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged)
         g = self._graphs.get(key)
@@ -521,6 +592,9 @@ class HipEngine(Engine):
 
     def epoch_stats(self, reset: bool = True) -> StepStats:
         v = self.stats.cpu().tolist()
+        if self.early_failed():
+            raise RuntimeError("early-MLP overlap: a row-granule wait timed out (the MLP reduction of a step "
+                               "did not see the fused kernel's rows); rerun with DNN_EARLY_MLP=0")
         if reset:
             self.stats.zero_()
         return StepStats(v[0], int(round(v[1])), int(round(v[2])), int(round(v[3])))

@@ -165,3 +165,34 @@ def test_rank_drop_recovery_on_gpu_engine(tmp_path, sync):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "communicator re-formed (generation 1, 2 ranks)" in r.stdout
     assert r.stdout.count("Validation loss of updated master model:") == 3
+
+
+def test_early_mlp_overlap_matches_serial_step():
+    """Early-MLP overlap (the MLP reduction + SGD on a side stream, concurrent with the fused
+    kernel, polling its row granules) gives the serial step's parameters, momentum, bf16
+    images and epoch statistics bit for bit - graphs and eager, tail batches included - and
+    its row waits never time out."""
+    import numpy as np
+    import torch
+
+    from distributed_neural_network_amd.data import synthetic
+    from distributed_neural_network_amd.models.network import init_arena
+    from distributed_neural_network_amd.runtime import HipEngine
+
+    data = synthetic(1000, 7)  # 15 full batches + a tail of 40
+    a = init_arena(seed=3)
+    res = []
+    for early, graphs in ((False, True), (True, True), (True, False)):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, early_mlp=early)
+        eng.attach(data)
+        stats = []
+        for ep in range(2):
+            eng.begin_epoch(np.random.default_rng(ep).permutation(1000).astype(np.int32))
+            eng.run_steps(16)
+            stats.append(eng.epoch_stats())
+        torch.cuda.synchronize()
+        assert not eng.early_failed()
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
+    for m, mo, sh, st in res[1:]:
+        assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo) and torch.equal(res[0][2], sh)
+        assert [(x.loss_sum, x.samples, x.correct) for x in st] == [(x.loss_sum, x.samples, x.correct) for x in res[0][3]]
