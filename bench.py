@@ -91,9 +91,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="bf16: bf16 MFMA operands, fp32 accumulation / master weights (lenet_fused.hip); fp32: "
                          "fp32 operands throughout, the reference's arithmetic (lenet_f32.hip)")
-    ap.add_argument("--early-mlp", default="off", choices=("on", "off"),
-                    help="bf16 fused engine: run the MLP reduction (+ exchange + SGD) on a side stream concurrently "
-                         "with the fused kernel, polling its row granules (bit-identical to the serial step)")
+    ap.add_argument("--early-mlp", default="off", choices=("off", "mlp", "full"),
+                    help="bf16 fused engine, in-launch reduction (bit-identical to the serial step): mlp = the MLP "
+                         "reduction (+ exchange + SGD) in extra workgroups of the fused launch, polling the rows the "
+                         "samples publish as granules; full = the conv reduction + bookkeeping too (one launch/step)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
@@ -121,7 +122,8 @@ def main():
     if args.model == "lenet" and args.engine in ("auto", "fused"):
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
                            overlap=args.overlap, use_graphs=not args.no_graphs, dtype=args.dtype,
-                           early_mlp=args.early_mlp == "on" and args.dtype == "bf16")
+                           early_mlp=(args.early_mlp if args.early_mlp != "off" else False) if args.dtype == "bf16"
+                           else False)
     else:  # modular layer engine (other models / fp32)
         engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
                              dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16), use_graphs=not args.no_graphs)
@@ -254,7 +256,7 @@ def main():
                "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)"
                           if args.model == "lenet" else args.model,
                           "engine": type(engine).__name__,
-                          "early_mlp": bool(getattr(engine, "early_mlp", False)),
+                          "early_mlp": getattr(engine, "early_mlp", False) or "off",
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",

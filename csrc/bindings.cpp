@@ -46,10 +46,10 @@ using u = uintptr_t;
 template <typename T>
 static T* P(u x) { return reinterpret_cast<T*>(x); }
 static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
-// early-MLP overlap, in-launch form: grad_reduce(defer=1) stores the MLP reduction's arguments
-// here and the next fused_train(inlaunch_mlp=1) launches them as extra workgroups
-static dnn::ReduceArgs g_pending_mlp{};
-static bool g_pending_set = false;
+// in-launch reduction (one launch per step): grad_reduce(defer=1) stores the MLP and the conv
+// reduction's arguments here and the next fused_train(inlaunch=1) runs them as extra workgroups
+static dnn::ReduceArgs g_pending_mlp{}, g_pending_conv{};
+static bool g_pending_mlp_set = false, g_pending_conv_set = false;
 
 PYBIND11_MODULE(_dnn_hip, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
@@ -68,23 +68,26 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("fused_train",
         [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
            u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage, u rowg,
-           u rowg_ctr, int inlaunch_mlp) {
-          if (inlaunch_mlp && !g_pending_set)
-            throw std::runtime_error("fused_train(inlaunch_mlp=1) needs a grad_reduce(defer=1) call first");
-          const dnn::ReduceArgs* red = inlaunch_mlp ? &g_pending_mlp : nullptr;
-          g_pending_set = false;
+           u rowg_ctr, int inlaunch) {
+          // inlaunch 1: the MLP reduction in-launch (conv reduction: its own launch after);
+          // 2: both (the whole step in one launch) - from the grad_reduce(defer=1) calls before
+          if (inlaunch && !(g_pending_mlp_set && (inlaunch == 1 || g_pending_conv_set)))
+            throw std::runtime_error("fused_train(inlaunch) needs the grad_reduce(defer=1) calls of its ranges first");
+          const dnn::ReduceArgs* red = inlaunch ? &g_pending_mlp : nullptr;
+          const dnn::ReduceArgs* redc = inlaunch == 2 ? &g_pending_conv : nullptr;
+          g_pending_mlp_set = g_pending_conv_set = false;
           dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order),
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
                                   P<long long>(stamps), P<const int32_t>(next_ids), P<unsigned char>(stage),
-                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red);
+                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red, redc);
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0,
-        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch_mlp") = 0);
+        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch") = 0);
   m.def("fused_train_f32", [](u images, u labels, u order, int order_len, int batch, u state, u master, u a0, u h1,
                               u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
     dnn::launch_fused_train_f32(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), order_len,
@@ -148,9 +151,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
       a.xp_wait = P<unsigned long long>(xp_wait);
     }
-    if (defer) {  // (early-MLP overlap) kept for the next fused_train(inlaunch_mlp=1) launch
-      g_pending_mlp = a;
-      g_pending_set = true;
+    if (defer) {  // (in-launch reduction) kept for the next fused_train(inlaunch=1) launch
+      if (lo == dnn::OFF_F1W) { g_pending_mlp = a; g_pending_mlp_set = true; }
+      else if (lo == 0 && hi == dnn::OFF_F1W) { g_pending_conv = a; g_pending_conv_set = true; }
+      else throw std::runtime_error("grad_reduce(defer=1): the MLP range or the conv range");
       return;
     }
     dnn::launch_grad_reduce(a, S(stream));

@@ -65,7 +65,7 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream, unsigned long long* rowg = nullptr, unsigned* rowg_ctr = nullptr,
-                        const ReduceArgs* mlp_red = nullptr);
+                        const ReduceArgs* mlp_red = nullptr, const ReduceArgs* conv_red = nullptr);
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);

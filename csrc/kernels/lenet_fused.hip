@@ -244,27 +244,31 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     unsigned char* __restrict__ stage,     // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
     unsigned long long* __restrict__ rowg,  // TRAIN, early-MLP overlap: the MLP rows as granules
     unsigned* __restrict__ rowg_ctr,        //   and this block's step counter (common.h RG_ROW)
-    const ReduceArgs ra, int red_wg) {      //   and the in-launch MLP reduction (workgroups >= batch)
+    const ReduceArgs ra, const ReduceArgs rc) {  //   and the in-launch reduction: MLP (ra), conv + bookkeeping (rc)
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
   // address - one dependent load level (batch id -> image) off the start of phase A.
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if constexpr (TRAIN) {
-    // early-MLP overlap: workgroups past the samples reduce the MLP gradient (+ exchange + SGD),
-    // polling the rows the sample workgroups publish as granules after phase D' - while those
-    // still run the conv backward.  Dispatched after the samples (higher ids), no LDS use.
-    if (RNR > 0 && (int)blockIdx.x >= batch) {
-      inlaunch_mlp_reduce<RNR>(ra, (int)blockIdx.x - batch);
-      return;
-    }
-  }
   // per-block diagnostic trace (stamps != nullptr): stamps[16 + 4 * block + k], k = 0 start,
-  // 1 rows published, 2 end, 3 XCC id
+  // 1 rows published, 2 end, 3 XCC id (reduction workgroups: start, end)
   const bool btrace = stamps != nullptr && threadIdx.x == 0;
   if (btrace) {
     stamps[16 + 4 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
     stamps[16 + 4 * blockIdx.x + 3] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+  }
+  if constexpr (TRAIN) {
+    // in-launch reduction: workgroups past the samples reduce the MLP gradient, then the conv
+    // gradient + bookkeeping (+ exchange + SGD), polling the rows, slab and {loss, correct} the
+    // sample workgroups publish as granules - the MLP part while the samples still run the
+    // conv backward.  Dispatched after the samples (higher ids), no LDS use.
+    if (RNR > 0 && (int)blockIdx.x >= batch) {
+      const int wg = (int)blockIdx.x - batch;
+      if (wg < INLAUNCH_MLP_WG) inlaunch_reduce<RNR>(ra, wg, INLAUNCH_MLP_BLOCKS);  // (rc only if launched)
+      else inlaunch_reduce<RNR>(rc, wg - INLAUNCH_MLP_WG, INLAUNCH_CONV_BLOCKS);
+      if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+      return;
+    }
   }
   // diagnostic phase timeline (block 0, thread 0): s_memrealtime ticks (100 MHz)
   const bool stamp = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
@@ -304,11 +308,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // early-MLP overlap: this step's row tag, read by every thread before thread 0 advances the
   // counter (several workgroup barriers later)
   const unsigned row_tag = (TRAIN && rowg != nullptr) ? rowg_ctr[b] + 1u : 0u;
+  // in-launch conv reduction too (rc set): the slab and {loss, correct} go out as granules
+  const bool conv_g = TRAIN && RNR > 0 && rc.rg != nullptr;
+  float my_loss = 0.f;
+  int my_correct = 0;
   if (!valid) {
     if (TRAIN && rowg != nullptr) {
       put_row_granules(rowg, batch, b, row_tag, tid, NT, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+      if (conv_g)
+        for (int i = tid; i < SLAB; i += NT) rg_put(rowg, rg_off(RG_SLAB, batch) + (long long)b * SLAB + i, row_tag, 0.f);
       __syncthreads();
-      if (tid == 0) rowg_ctr[b] = row_tag;
+      if (tid == 0) {
+        rowg_ctr[b] = row_tag;
+        if (conv_g) {
+          const long long lc = rg_off(RG_LCK, batch) + (long long)RG_LC * b;
+          rg_put(rowg, lc, row_tag, 0.f);
+          rg_put(rowg, lc + 1, row_tag, 0.f);
+        }
+      }
     }
     if (TRAIN) {
       for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
@@ -600,6 +617,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (lane == 0) {
       loss_out[b] = lse - ll;
       correct_out[b] = pred == label ? 1 : 0;
+      my_loss = lse - ll;  // (thread 0: also the in-launch bookkeeping's granule)
+      my_correct = pred == label ? 1 : 0;
     }
     if (TRAIN && lane < 32) {
       const float dz = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
@@ -669,6 +688,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
   //    flipped kernel WF - no col2im scratch, no gather pass.
   float* slab = slab_out + (size_t)b * SLAB;
+  // the conv gradient slab: plain rows, or (in-launch reduction) {value, step} granules
+  unsigned long long* const slab_g = conv_g ? rowg + rg_off(RG_SLAB, batch) + (long long)b * SLAB : nullptr;
+#define SLAB_PUT(i, v)                                   \
+  do {                                                   \
+    if (slab_g != nullptr) rg_put(slab_g, (i), row_tag, (v)); \
+    else slab[i] = (v);                                  \
+  } while (0)
   bf16x8* R3 = reinterpret_cast<bf16x8*>(smem + L_REGA + A_R3);
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
@@ -738,7 +764,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int k = 0; k < 3; ++k) t += (part + 4 * k < 10) ? RS[o * 10 + min(part + 4 * k, 9)] : 0.f;
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
-    if (part == 0) slab[SLAB_C2B + o] = t;
+    if (part == 0) SLAB_PUT(SLAB_C2B + o, t);
   }
   // conv2 data gradient: 14 tiles (one output row each, lanes x >= 14 duplicate x = 13)
   // x 20 K-steps in two halves.  Waves 0-5 run rows w and w + 8 TOGETHER (one WF
@@ -815,7 +841,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       for (int u = 0; u < 2; ++u) {
         if ((u == 0 || two) && n[u] < 150) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) slab[SLAB_C2W + (4 * fg + i) * 150 + n[u]] = acc[u][i];
+          for (int i = 0; i < 4; ++i) SLAB_PUT(SLAB_C2W + (4 * fg + i) * 150 + n[u], acc[u][i]);
         }
       }
     }
@@ -883,7 +909,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
     t += __shfl_xor(t, 4);
-    if (part == 0 && lane < 48) slab[SLAB_C1B + c] = t;
+    if (part == 0 && lane < 48) SLAB_PUT(SLAB_C1B + c, t);
   }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
     const int n = wave * 16 + fr, nc = min(n, 74);
@@ -909,8 +935,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = 4 * fg + i;
-        if (o < 6) slab[SLAB_C1W + o * 75 + n] = acc[i];
+        if (o < 6) SLAB_PUT(SLAB_C1W + o * 75 + n, acc[i]);
       }
+    }
+  }
+  if (conv_g) {
+    // {loss, correct} granules LAST: every wave of this sample is past its reads of the sample
+    // ids, next_ids and cursor that the in-launch bookkeeping advances once it has them all
+    __syncthreads();
+    if (tid == 0) {
+      const long long lc = rg_off(RG_LCK, batch) + (long long)RG_LC * b;
+      rg_put(rowg, lc, row_tag, my_loss);
+      rg_put(rowg, lc + 1, row_tag, __int_as_float(my_correct));
     }
   }
   if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -919,6 +955,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     STAMP(7);
   }
 #undef STAMP
+#undef SLAB_PUT
 }
 
 }  // namespace dnn
@@ -942,18 +979,29 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
-                        hipStream_t stream, unsigned long long* rowg, unsigned* rowg_ctr, const ReduceArgs* mlp_red) {
+                        hipStream_t stream, unsigned long long* rowg, unsigned* rowg_ctr, const ReduceArgs* mlp_red,
+                        const ReduceArgs* conv_red) {
   init_kernels();
   if (stage != nullptr && next_ids == nullptr) throw std::runtime_error("fused_train: staging needs next_ids");
   if ((rowg == nullptr) != (rowg_ctr == nullptr)) throw std::runtime_error("fused_train: row granules need their counters");
-  ReduceArgs ra{};
+  ReduceArgs ra{}, rc{};
   int red_wg = 0;
-  if (mlp_red != nullptr) {  // in-launch MLP reduction of the early-MLP overlap
+  if (conv_red != nullptr && mlp_red == nullptr)
+    throw std::runtime_error("fused_train: an in-launch conv reduction needs the in-launch MLP reduction");
+  if (mlp_red != nullptr) {  // in-launch reduction: MLP (early-MLP overlap), + conv = the whole step
     ra = *mlp_red;
     if (rowg == nullptr || ra.rg != rowg || ra.lo != OFF_F1W || ra.hi < ARENA || ra.bookkeeping || ra.batch != batch ||
         ra.rg_ctr == nullptr || ra.rg_err == nullptr || ra.xp_blk_off != 0)
       throw std::runtime_error("fused_train: the in-launch MLP reduction reads this launch's row granules (MLP range)");
     red_wg = INLAUNCH_MLP_WG;
+    if (conv_red != nullptr) {
+      rc = *conv_red;
+      if (rc.rg != rowg || rc.lo != 0 || rc.hi != OFF_F1W || !rc.bookkeeping || rc.batch != batch ||
+          rc.rg_ctr == nullptr || rc.rg_err == nullptr || rc.xp_nranks != ra.xp_nranks ||
+          (rc.xp_nranks > 0 && rc.xp_blk_off != INLAUNCH_MLP_BLOCKS))
+        throw std::runtime_error("fused_train: the in-launch conv reduction reads this launch's slab granules");
+      red_wg += INLAUNCH_CONV_WG;
+    }
   }
   const int rnr = red_wg == 0 ? 0 : (ra.xp_nranks == 0 ? 1 : 8);
   if (rnr == 8 && (ra.xp_mode & 4)) throw std::runtime_error("fused_train: the in-launch MLP reduction has fp32 granules only");
@@ -962,7 +1010,7 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                           : (stage ? &lenet_fused_kernel<true, true, 8> : &lenet_fused_kernel<true, false, 8>);
   hipLaunchKernelGGL(kern, dim3(batch + red_wg), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len,
                      batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, next_ids,
-                     stage, rowg, rowg_ctr, ra, red_wg);
+                     stage, rowg, rowg_ctr, ra, rc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -974,7 +1022,7 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
                      nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     ReduceArgs{}, 0);
+                     ReduceArgs{}, ReduceArgs{});
   HIP_CHECK(hipGetLastError());
 }
 

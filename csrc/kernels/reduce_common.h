@@ -8,7 +8,7 @@ namespace dnn {
 
 // SGD epilogue with the master/momentum values already in registers (prefetched
 // together with the gradient operands, so the update costs no extra memory latency).
-__device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs a) {
+__device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs& a) {
   g *= a.grad_scale;
   if (a.fuse_sgd) {
     float p, m;
@@ -71,6 +71,19 @@ __device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N]
   static_assert(N <= 32, "pending mask");
   unsigned pending = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
   const long long t0 = wall_clock64();
+  // first wait on ONE granule (this lane's first operand), polling every ~0.2 us: the rows
+  // arrive together per sample, and a full round of every lane's loads would put several TB/s
+  // of uncached polling traffic next to the samples' own memory accesses
+  while (!failed) {
+    const unsigned long long x = __hip_atomic_load(a.rg + off[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((unsigned)(x >> 32) == tag) break;
+    __builtin_amdgcn_s_sleep(8);
+    if (wall_clock64() - t0 > a.rg_timeout_ticks ||
+        (a.xp_abort != nullptr && __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      __hip_atomic_store(a.rg_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      failed = true;
+    }
+  }
   while (true) {
     unsigned long long x[N];
 #pragma unroll
@@ -89,7 +102,7 @@ __device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N]
         if (pending & (1u << k)) v[k] = 0.f;
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(4);
     if (wall_clock64() - t0 > a.rg_timeout_ticks ||
         (a.xp_abort != nullptr && __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
       __hip_atomic_store(a.rg_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -100,7 +113,7 @@ __device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N]
 
 // GR: rtag = this reduction block's row tag, rfail = an earlier wait failed (skip the waits)
 template <int LAYER, bool GR, class Sink>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
   using L = Fc<LAYER>;
   const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
   const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
@@ -205,7 +218,7 @@ constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
 template <bool GR, class Sink>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
@@ -231,24 +244,41 @@ __device__ __forceinline__ int conv_dst(int e) {
   if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
   return OFF_C2B + (e - SLAB_C2B);
 }
-template <class Sink>
-__device__ __forceinline__ void conv_task(int t, const ReduceArgs a, Sink& sk) {
+template <bool GR, class Sink>
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
   const float* src = a.slab;
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split(src, SLAB, e, a.batch, q);
+  const float g = column_sum_split<GR>(src, SLAB, e, a.batch, q, &a, GR ? (int)rg_off(RG_SLAB, a.batch) : 0, rtag,
+                                      rfail);
   if (t < CONV_SLOTS && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
 
 // Epoch statistics of the step that just ran + publication of the next step's cursor,
 // valid count and sample ids.  One wave (lanes 0..63), fixed summation order.
-__device__ __forceinline__ void bookkeeping(const ReduceArgs a, int lane) {
+// GR (in-launch reduction): {loss, correct} from the row granules, which every sample workgroup
+// publishes as its LAST action - so the cursor, sample ids and next_ids below are advanced only
+// after every sample of this launch read them
+template <bool GR = false>
+__device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsigned rtag = 0, bool rfail = false) {
     const float* loss = a.loss;
     const int32_t* correct = a.correct;
     float ls = 0.f;
     int cs = 0;
-    for (int b = lane; b < a.batch; b += 64) { ls += loss[b]; cs += correct[b]; }
+    for (int b = lane; b < a.batch; b += 64) {
+      if constexpr (GR) {
+        const int lo = (int)rg_off(RG_LCK, a.batch) + RG_LC * b;
+        const int off[2] = {lo, lo + 1};
+        float v[2];
+        rg_poll<2>(a, off, rtag, rfail, v);
+        ls += v[0];
+        cs += __float_as_int(v[1]);
+      } else {
+        ls += loss[b];
+        cs += correct[b];
+      }
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
     const int bv = a.state[ST_BVALID];

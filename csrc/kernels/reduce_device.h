@@ -40,10 +40,10 @@ __device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk, 
   }
   if (conv) {
     constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
-    if (blk < CB) { conv_task(blk * RT + rtid, a, sk); return true; }
+    if (blk < CB) { conv_task<GR>(blk * RT + rtid, a, sk, rtag, rfail); return true; }
     blk -= CB;
   }
-  if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping(a, rtid);
+  if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping<GR>(a, rtid, rtag, rfail);
   return false;
 }
 
@@ -318,15 +318,14 @@ __device__ __forceinline__ void reduce_block(const ReduceArgs& a, int rblk, int 
 }
 
 
-// The fused kernel's in-launch MLP reduction (early-MLP overlap): workgroups batch .. of the
-// fused launch run reduction blocks 2 (w - batch) and 2 (w - batch) + 1, one per 256-thread
-// half.  RNR: 1 = local step, 8 = the one-launch exchange of up to 8 ranks (pull or two-hop,
+// The fused kernel's in-launch reduction (one launch per step): the reduction workgroups of
+// the fused launch (after the samples) run reduction blocks 2 wg and 2 wg + 1 of one launch
+// range (MLP, then conv + bookkeeping), one per 256-thread half.  RNR: 1 = local step, 8 = the one-launch exchange of up to 8 ranks (pull or two-hop,
 // fp32 granules) - one instance per fused-kernel instance (a run-time choice among several
 // would make the compiler copy the argument block to scratch).
 template <int RNR>
-__device__ __forceinline__ void inlaunch_mlp_reduce(const ReduceArgs& a, int wg) {
+__device__ __forceinline__ void inlaunch_reduce(const ReduceArgs& a, int wg, int nblk) {
   const int half = threadIdx.x >> 8, rblk = 2 * wg + half, rtid = threadIdx.x & 255;
-  const int nblk = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
   // (an odd block count leaves the last half idle; it still meets the workgroup barrier)
   if (rblk >= nblk) {
     __syncthreads();
@@ -334,6 +333,9 @@ __device__ __forceinline__ void inlaunch_mlp_reduce(const ReduceArgs& a, int wg)
   }
   reduce_block<RNR, false, true>(a, rblk, rtid);
 }
-constexpr int INLAUNCH_MLP_WG = (TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT + 1) / 2;
+constexpr int INLAUNCH_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
+constexpr int INLAUNCH_MLP_WG = (INLAUNCH_MLP_BLOCKS + 1) / 2;
+constexpr int INLAUNCH_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT + 1;  // + the bookkeeping block
+constexpr int INLAUNCH_CONV_WG = (INLAUNCH_CONV_BLOCKS + 1) / 2;
 
 }  // namespace dnn

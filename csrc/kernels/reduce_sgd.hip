@@ -125,23 +125,15 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
     if (args.xp_blk_off + nblk > XP_MAX_BLOCKS || !(whole || split_mlp || split_conv))
       throw std::runtime_error("grad_reduce exchange needs the whole-arena grid or one of the two split launches");
   }
-  if (args.rg != nullptr && (!mlp || conv || args.bookkeeping || args.rg_ctr == nullptr || args.rg_err == nullptr))
-    throw std::runtime_error("grad_reduce: row granules are read by the MLP-range launch only (no bookkeeping)");
+  if (args.rg != nullptr)
+    throw std::runtime_error("grad_reduce: row granules are read by the fused kernel's in-launch reduction only");
   const int nr = args.xp_nranks;
   if (nr > XG_MAX_RANKS) throw std::runtime_error("grad_reduce exchange: at most 8 ranks");
   const bool pk = (args.xp_mode & 4) != 0;
-  decltype(&grad_reduce_kernel<1>) kern;
-  if (args.rg != nullptr)
-    kern = nr == 0 ? &grad_reduce_kernel<1, false, true>
-           : pk ? (nr <= 2 ? &grad_reduce_kernel<2, true, true>
-                           : (nr <= 4 ? &grad_reduce_kernel<4, true, true> : &grad_reduce_kernel<8, true, true>))
-                : (nr <= 2 ? &grad_reduce_kernel<2, false, true>
-                           : (nr <= 4 ? &grad_reduce_kernel<4, false, true> : &grad_reduce_kernel<8, false, true>));
-  else
-    kern = nr == 0 ? &grad_reduce_kernel<1>
-           : pk ? (nr <= 2 ? &grad_reduce_kernel<2, true>
-                           : (nr <= 4 ? &grad_reduce_kernel<4, true> : &grad_reduce_kernel<8, true>))
-                : (nr <= 2 ? &grad_reduce_kernel<2> : (nr <= 4 ? &grad_reduce_kernel<4> : &grad_reduce_kernel<8>));
+  auto* kern = nr == 0 ? &grad_reduce_kernel<1>
+               : pk ? (nr <= 2 ? &grad_reduce_kernel<2, true>
+                               : (nr <= 4 ? &grad_reduce_kernel<4, true> : &grad_reduce_kernel<8, true>))
+                    : (nr <= 2 ? &grad_reduce_kernel<2> : (nr <= 4 ? &grad_reduce_kernel<4> : &grad_reduce_kernel<8>));
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(RT), 0, stream, args);
   HIP_CHECK(hipGetLastError());
 }

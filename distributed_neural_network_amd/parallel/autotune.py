@@ -27,7 +27,7 @@ from typing import Callable
 
 import torch
 
-ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl")
 # opt-in (--grad-comm bf16): the xGMI exchanges with bf16 gradient granules - half the link
 # bytes, lower-precision gradients, so never a candidate unless asked for
 BF16_PATHS = ("xgmi-pull-bf16", "xgmi-rsag-bf16")

@@ -133,7 +133,10 @@ class StepAllReduce(SyncPolicy):
     # all-reduced on a side stream while the conv bucket is reduced; local: no all-reduce (A/B
     # baseline only: replicas diverge)
     # (xgmi-pull-bf16 / xgmi-rsag-bf16: the same exchanges with bf16 gradient granules, opt-in)
-    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-bf16", "xgmi-rsag-bf16")
+    # (xgmi-pull-ovl / xgmi-rsag-ovl: the same exchanges run by the fused launch's in-launch MLP
+    # reduction, overlapped with the conv backward - HipEngine early_mlp="mlp"; bit-identical)
+    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl", "xgmi-pull-bf16",
+             "xgmi-rsag-bf16")
     path: str | None = None
     grad_comm = "fp32"  # "bf16": the default xGMI path uses bf16 gradient granules (--grad-comm)
     record_waits = False  # xGMI paths: record every step's exchange wait (XgmiGroup.wait_stats)
@@ -180,7 +183,8 @@ class StepAllReduce(SyncPolicy):
             from .xgmi import MODE_NAMES
 
             form = MODE_NAMES[gs.group.xp_mode]
-            return f"xgmi-{form}" + ("" if gs.group.one_launch else "-two-launch")
+            ovl = "-ovl" if getattr(engine, "early_mlp", False) and engine._early_ok() else ""
+            return f"xgmi-{form}{ovl}" + ("" if gs.group.one_launch else "-two-launch")
         if kind == "NativeGradAllReduce":
             return "rccl-overlap" if gs.overlap else "rccl"
         return "torch-pg"
@@ -192,13 +196,24 @@ class StepAllReduce(SyncPolicy):
             engine.invalidate_graphs()
         if hasattr(engine, "overlap"):
             engine.overlap = name == "rccl-overlap"
+        if hasattr(engine, "early_mlp"):
+            # the -ovl paths switch the in-launch MLP reduction on; other paths restore the
+            # engine's own setting
+            if not hasattr(self, "_early0"):
+                self._early0 = engine.early_mlp
+            ovl = name.endswith("-ovl")
+            if ovl and getattr(engine, "dtype", "bf16") != "bf16":
+                return False
+            engine.early_mlp = "mlp" if ovl else self._early0
+        elif name.endswith("-ovl"):
+            return False
         engine.grad_sync = None
         if name == "local":
             return True
         if name.startswith("xgmi"):
             from .xgmi import EXCHANGE_MODES
 
-            return self._install_xgmi(engine, EXCHANGE_MODES[name[len("xgmi-"):]])
+            return self._install_xgmi(engine, EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-ovl")])
         if name in ("rccl", "rccl-overlap"):
             if self.comm.backend != "nccl":
                 return False

@@ -270,11 +270,18 @@ class HipEngine(Engine):
         # after phase D' while they still run the conv backward; the conv reduction follows as
         # its own launch.  Bit-identical to the serial step (same sums, same order).  (A side-
         # stream form with a graph fork/join measured 28.3 vs 19.8 us/step: profiles/r3/early_mlp.)
+        # early_mlp: False | True / "mlp" (MLP reduction in-launch, conv reduction its own launch)
+        # | "full" (both in-launch: the whole step in one launch)
         if early_mlp is None:
-            early_mlp = os.environ.get("DNN_EARLY_MLP", "0") == "1" and dtype == "bf16"
+            early_mlp = {"0": False, "1": "mlp", "mlp": "mlp", "2": "full", "full": "full"}[
+                os.environ.get("DNN_EARLY_MLP", "0")] if dtype == "bf16" else False
+        if early_mlp is True:
+            early_mlp = "mlp"
+        if early_mlp not in (False, "mlp", "full"):
+            raise ValueError(f"early_mlp must be False, 'mlp' or 'full', not {early_mlp!r}")
         if early_mlp and dtype != "bf16":
             raise ValueError("early-MLP overlap is a feature of the bf16 kernel")
-        self.early_mlp = bool(early_mlp)
+        self.early_mlp = early_mlp
         self._rg: dict | None = None
         if dtype == "bf16":
             self._rg_buffers()  # (allocated up front: never inside a graph capture)
@@ -363,7 +370,7 @@ class HipEngine(Engine):
             ptr = self.ext.uncached_alloc(self.batch * self.ext.row_granules() * 8)
             i32 = dict(device=self.device, dtype=torch.int32)
             self._rg = dict(ptr=ptr, fctr=torch.zeros(self.batch, **i32),
-                            rctr=torch.zeros(self.ext.grad_reduce_mlp_blocks(), **i32), err=torch.zeros(1, **i32))
+                            rctr=torch.zeros(self.ext.grad_reduce_blocks(), **i32), err=torch.zeros(1, **i32))
         return self._rg
 
     def early_failed(self) -> bool:
@@ -388,16 +395,21 @@ class HipEngine(Engine):
                 and not self.grad_sync.group.xp_mode & 4)
 
     def _launch_step_early(self) -> None:
-        """ONE launch: the fused kernel's sample workgroups + extra workgroups that reduce the MLP
-        gradient (+ exchange + SGD), polling the rows the samples publish as {value, step}
-        granules after phase D' - while the samples still run the conv backward; then the conv
-        reduction + bookkeeping (split launch) on the same stream."""
+        """The whole step in ONE launch: the fused kernel's sample workgroups + reduction
+        workgroups that reduce the MLP gradient (polling the rows the samples publish as {value,
+        step} granules after phase D', while the samples still run the conv backward) and the
+        conv gradient + bookkeeping (polling the slab and {loss, correct} granules), each with
+        its exchange + SGD - no kernel boundary inside the step."""
         rg = self._rg_buffers()
         xg = self.grad_sync.group.exchange() if self.grad_sync is not None else {}
         s = self._stream()
         mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
-        self._reduce(1, mlp[0], mlp[1], 0, s, rg=rg["ptr"], rg_ctr=self._p(rg["rctr"]), rg_err=self._p(rg["err"]),
-                     rg_timeout_s=self.RG_TIMEOUT_S, defer=1, **xg)
+        nm = self.ext.grad_reduce_mlp_blocks()
+        common = dict(rg=rg["ptr"], rg_err=self._p(rg["err"]), rg_timeout_s=self.RG_TIMEOUT_S, defer=1, **xg)
+        full = self.early_mlp == "full"
+        self._reduce(1, mlp[0], mlp[1], 0, s, rg_ctr=self._p(rg["rctr"]), **common)
+        if full:
+            self._reduce(1, conv[0], conv[1], 1, s, rg_ctr=self._p(rg["rctr"]) + 4 * nm, **common)
         self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
                              self.order_len, self.batch, self._p(self.state), self._p(self.master),
                              self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
@@ -405,8 +417,9 @@ class HipEngine(Engine):
                              self._p(self.loss), self._p(self.correct), s,
                              next_ids=self._p(self.next_ids) if self._staged else 0,
                              stage=self._p(self.stage) if self._staged else 0,
-                             rowg=rg["ptr"], rowg_ctr=self._p(rg["fctr"]), inlaunch_mlp=1)
-        self._reduce(1, conv[0], conv[1], 1, s, **xg)
+                             rowg=rg["ptr"], rowg_ctr=self._p(rg["fctr"]), inlaunch=2 if full else 1)
+        if not full:
+            self._reduce(1, conv[0], conv[1], 1, s, **xg)
 
     def _launch_step(self) -> None:
         assert self.train is not None

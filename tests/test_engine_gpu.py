@@ -168,10 +168,11 @@ def test_rank_drop_recovery_on_gpu_engine(tmp_path, sync):
 
 
 def test_early_mlp_overlap_matches_serial_step():
-    """Early-MLP overlap (the MLP reduction + SGD on a side stream, concurrent with the fused
-    kernel, polling its row granules) gives the serial step's parameters, momentum, bf16
-    images and epoch statistics bit for bit - graphs and eager, tail batches included - and
-    its row waits never time out."""
+    """In-launch reduction - the MLP reduction + SGD ("mlp"), and also the conv reduction +
+    bookkeeping ("full": one launch per step), in extra workgroups of the fused launch polling
+    the row / slab / {loss, correct} granules its samples publish - gives the serial step's
+    parameters, momentum, bf16 images and epoch statistics bit for bit, graphs and eager, tail
+    batches included, and its waits never time out."""
     import numpy as np
     import torch
 
@@ -182,7 +183,7 @@ def test_early_mlp_overlap_matches_serial_step():
     data = synthetic(1000, 7)  # 15 full batches + a tail of 40
     a = init_arena(seed=3)
     res = []
-    for early, graphs in ((False, True), (True, True), (True, False)):
+    for early, graphs in ((False, True), ("mlp", True), ("mlp", False), ("full", True), ("full", False)):
         eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, early_mlp=early)
         eng.attach(data)
         stats = []

@@ -225,9 +225,11 @@ def test_bench_two_ranks_xgmi(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
-    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag"), out
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag", "xgmi-pull-ovl",
+                                                                   "xgmi-rsag-ovl"), out
     ab = out["allreduce_ab"]
-    assert set(ab) == {"xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"}, out
+    assert set(ab) == {"xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl"}, out
+    assert ab["xgmi-pull-ovl"] is not None, out
     assert ab["xgmi-pull"] is not None and ab["rccl"] is None and "rccl" in out["allreduce_failed"], out
     assert out["local_step_us"] > 0, out
     w = out["exchange_wait_us"]
@@ -252,15 +254,16 @@ def test_xgmi_bf16_granule_exchanges_two_ranks(tmp_path):
 
 
 def test_xgmi_early_mlp_two_ranks(tmp_path):
-    """2 ranks on the box's GPU, early-MLP overlap: the MLP reduction + its xGMI exchange + SGD
-    run on a side stream concurrently with the fused kernel (polling its row granules), the conv
-    reduction + exchange follow it as a second split launch (own counter range).  Pull and
-    two-hop forms give the serial one-launch exchange's parameters bit for bit on both ranks."""
+    """2 ranks on the box's GPU, in-launch reduction: the MLP reduction + its xGMI exchange + SGD
+    run in extra workgroups of the fused launch (polling its row granules), the conv reduction +
+    exchange follow as a split launch with its own counter range (or, "full", in the same launch).
+    Pull and two-hop forms give the serial one-launch exchange's parameters bit for bit on both
+    ranks."""
     import torch
 
     ref, r0 = _two_ranks(tmp_path, "xgmi", "1", 29687, exchange="pull")
-    for port, xch, mode in ((29689, "pull", 0), (29691, "rsag", 2)):
-        res, r = _two_ranks(tmp_path, "xgmi", "1", port, exchange=xch, early="1")
+    for port, xch, mode, early in ((29689, "pull", 0, "1"), (29691, "rsag", 2, "1"), (29693, "pull", 0, "2")):
+        res, r = _two_ranks(tmp_path, "xgmi", "1", port, exchange=xch, early=early)
         assert all(x["kind"] == "XgmiGradSync" and x["one_launch"] and x["xp_mode"] == mode for x in res), \
             r.stderr[-2000:]
         for i in range(2):
