@@ -18,7 +18,7 @@
 namespace dnn {
 int rccl_open(const std::string& path);
 std::string rccl_unique_id();
-uintptr_t rccl_init(const std::string& id_bytes, int nranks, int rank, int device);
+uintptr_t rccl_init(const std::string& id_bytes, int nranks, int rank, int device, int blocking, double timeout_s);
 void rccl_allreduce(uintptr_t comm, uintptr_t buf, size_t count, int dtype, int op, uintptr_t stream);
 void rccl_broadcast(uintptr_t comm, uintptr_t buf, size_t count, int root, uintptr_t stream);
 int rccl_async_error(uintptr_t comm);
@@ -391,10 +391,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
   // native RCCL communicator (comm/rccl_comm.cpp)
   m.def("rccl_open", &dnn::rccl_open, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dnn::rccl_unique_id()); });
-  m.def("rccl_init", [](py::bytes id, int nranks, int rank, int device) {
-    py::gil_scoped_release nogil;  // blocks until every rank joined
-    return dnn::rccl_init(std::string(id), nranks, rank, device);
-  });
+  m.def(
+      "rccl_init",
+      [](py::bytes id, int nranks, int rank, int device, int blocking, double timeout_s) {
+        const std::string idb(id);      // (converted under the GIL)
+        py::gil_scoped_release nogil;   // waits until every rank joined (non-blocking: <= timeout_s)
+        return dnn::rccl_init(idb, nranks, rank, device, blocking, timeout_s);
+      },
+      py::arg("id"), py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("blocking") = 0,
+      py::arg("timeout_s") = 120.0);
   m.def("rccl_allreduce", &dnn::rccl_allreduce, py::arg("comm"), py::arg("buf"), py::arg("count"),
         py::arg("dtype"), py::arg("op"), py::arg("stream"));
   m.def("rccl_broadcast", &dnn::rccl_broadcast);

@@ -23,9 +23,12 @@
 //    same registers for the fc1 data gradient - no second pass over fc1;
 //  * ReLU + 2x2 maxpool fused into the conv epilogues with a 2-bit argmax code (4 = no
 //    gradient), exactly as lenet_fused.hip (first max wins, like torch.max_pool2d);
-//  * the conv weight gradients exploit the max-pool sparsity: dY = unpool(d pooled) has ONE
-//    nonzero per 2x2 window, so dW2 / dW1 sum over the 25 / 196 argmax pixels instead of the
-//    100 / 784 dense ones (4x fewer products; zeros add nothing in fp32);
+//  * the conv1 weight gradient exploits the max-pool sparsity: dY = unpool(d pooled) has ONE
+//    nonzero per 2x2 window, so dW1 sums over the <= 196 active argmax pixels instead of the 784
+//    dense ones (4x fewer products; zeros add nothing in fp32);
+//  * the conv2 weight gradient is the one GEMM whose M (16 output channels) fills an MFMA tile:
+//    it runs dense (k = the 100 unpooled pixels) on v_mfma_f32_16x16x4_f32 in 5 waves, beside the
+//    data gradient's VALU work in the other 11;
 //  * fixed summation orders everywhere (no atomics): bitwise reproducible run to run.
 #include "launchers.h"
 
@@ -69,28 +72,30 @@ constexpr int L_DA0 = L_DZ1 + 512;      // f32 [400]                            
 constexpr int L_F2 = L_DA0 + 1600;      // f32 fc2 [84][120]                            40320
 constexpr int L_F3 = L_F2 + 40320;      // f32 fc3 [10][84]                              3360
 constexpr int L_PART = L_F3 + 3360;     // f32 partial sums: conv2 fwd / fc1 dgrad / dW1 25600
-constexpr int L_DY2 = L_PART + 25600;   // f32 [16][18][20] dY2 zero-padded (4 left/top)  23040
+constexpr int DY2_LD = 20;              // dY2 rows of 20: 16-B aligned 8-wide windows
+constexpr int DY2_CH = 18 * DY2_LD + 4;  //   channels 364 floats apart: the conv2 weight gradient's
+                                         //   b32 reads of 16 channels are 2-way, not 4-way
+constexpr int L_DY2 = L_PART + 25600;   // f32 [16][DY2_CH] dY2 zero-padded (4 left/top)  23296
 // conv weight-gradient tables, built from the pool codes while wave 0 runs fc3 + the loss:
 // the ACTIVE windows (ReLU passed) of each channel, compacted in window order, as {dY value,
 // pixel offset}; the offsets are known from the forward pass, the values are filled in by the
 // data-gradient epilogues.  Inactive windows carry no gradient, so the weight-gradient loops
 // walk only the active ones (about half) without a branch.
 constexpr int T1_LD = 218;               // <= 196 active windows + 22 zero pad entries (even: 16-B pairs)
-constexpr int L_T1 = L_DY2 + 23040;      // f2 [6][T1_LD] {dP1, offset in XW}              10464
+constexpr int L_T1 = L_DY2 + 16 * DY2_CH * 4;  // f2 [6][T1_LD] {dP1, offset in XW}        10464
 constexpr int L_T2 = L_T1 + 6 * T1_LD * 8;  // f2 [16][25] {dA0, offset in P1}             3200
 constexpr int L_PS1 = L_T2 + 3200;       // u8 [6][196] window -> table slot (255: inactive) 1176
 constexpr int L_PS2 = L_PS1 + 1176;      // u8 [400]                                         400
 constexpr int L_NACT = L_PS2 + 400;      // i32 [6 conv1 | 16 conv2] active-window counts     88
-constexpr int LDS_TOTAL = L_NACT + 88;   // 162,192 B
+constexpr int LDS_TOTAL = L_NACT + 88;   // 162,448 B
 static_assert(L_WT1 % 16 == 0 && L_WT2 % 16 == 0 && L_WD % 16 == 0 && L_F2 % 16 == 0 && L_DY2 % 16 == 0,
               "16-B aligned b128 regions");
 static_assert(L_T1 % 16 == 0 && L_T2 % 8 == 0 && L_NACT % 4 == 0, "table alignment");
 static_assert(3 * XW_CH * 4 <= 40320, "XW fits the dead fc2 region");
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 constexpr int B_C1 = 0, B_C2 = 6, B_F1 = 22, B_F2 = 142, B_F3 = 226;  // bias offsets (floats)
-constexpr int DY2_LD = 20, DY2_CH = 18 * DY2_LD;  // rows of 20: 16-B aligned 8-wide windows
 constexpr int W1_PARTS = 11;  // conv1 weight gradient: the active windows in 11 slices
-static_assert(16 * 400 * 4 <= 25600 && W1_PARTS * 450 * 4 <= 25600 && 200 * 8 * 4 <= 25600, "partials");
+static_assert(16 * 400 * 4 <= 25600 && W1_PARTS * 450 * 4 <= 25600 && 4 * 168 * 4 * 8 <= 25600, "partials");
 
 // ToTensor + Normalize((.5,.5,.5),(.5,.5,.5)) exactly as PyTorch's fp32 ops: u / 255 correctly
 // rounded (the double quotient of u / 255 is never within a double ulp of a float rounding
@@ -559,15 +564,42 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 
   // ============ phase E: conv2 backward ===================================================
   float* slab = slab_out + (size_t)b * SLAB;
-  // conv2 data gradient: full correlation of the padded dY2 with the kernel.  A lane owns a
-  // 2 x 4 pixel block of one input channel for a quarter of the output channels: per channel o
-  // one 6 x 8 dY2 window (12 aligned 16-B reads) and 25 weights (7 16-B reads, broadcast over the
-  // lanes of the same c and o) feed 8 outputs; the quarters' partial sums meet through LDS in a
-  // fixed order
+  // conv2 data gradient: full correlation of the padded dY2 with the kernel.  A task owns a
+  // 2 x 4 pixel block (yx: row pair yh = yx >> 2, column quad yx & 3) of one input channel c for
+  // a quarter q of the output channels: per channel o one 6 x 8 dY2 window (12 aligned 16-B
+  // reads) and 25 weights (7 16-B reads, broadcast over the lanes of the same c and o) feed 8
+  // outputs; the quarters' partial sums meet through LDS in a fixed order.
+  // Task -> lane map from the b128 bank model (tools/lds_banks.py rules): a 16-lane read group
+  // of ds_read_b128 covers all 64 banks once only if its windows fall on 16 distinct 4-bank
+  // slots, slot = (10 yh + (yx & 3)) mod 16 (+ a group-uniform shift).  The 16 blocks of even yh
+  // have distinct slots, the 12 of odd yh too, and lanes of the same yx (other c) read the
+  // same address (broadcast).  So each quarter fills 11 groups: 6 groups of one channel's even
+  // blocks, then its 72 odd-yh tasks in channel order, 16 per group (44 groups = waves 0..10).
+  // The plain tid order put 2 windows on one slot in most groups: 4416 vs 2112 LDS cycles.
   f2 dacc[2][2] = {{{0.f, 0.f}, {0.f, 0.f}}, {{0.f, 0.f}, {0.f, 0.f}}};
-  const int d_q = tid / 168, d_r = tid - 168 * d_q, d_c = d_r / 28, d_yx = d_r - 28 * d_c;
-  const int d_y0 = 2 * (d_yx >> 2), d_x0 = 4 * (d_yx & 3);
-  if (tid < 672) {
+  bool d_on;
+  int d_q, d_r, d_c, d_y0, d_x0;
+  {
+    const int l32 = lane & 31;
+    const int gi = 4 * wave + 2 * (lane >> 5) + ((0xf00f0ff0u >> l32) & 1);  // read group of the wave
+    const int pi = (int)(((l32 < 16 ? 0x7654765432103210ull : 0xfedcfedcba98ba98ull) >> (4 * (l32 & 15))) & 15);
+    d_q = gi / 11;
+    const int kg = gi - 11 * d_q, t = 16 * (kg - 6) + pi;
+    int yx;
+    if (kg < 6) {
+      d_c = kg;
+      yx = 8 * (pi >> 2) + (pi & 3);
+    } else {
+      d_c = t / 12;
+      const int m = t - 12 * d_c;
+      yx = 8 * (m >> 2) + 4 + (m & 3);
+    }
+    d_on = tid < 704 && (kg < 6 || t < 72);
+    d_r = 28 * d_c + yx;
+    d_y0 = 2 * (yx >> 2);
+    d_x0 = 4 * (yx & 3);
+  }
+  if (d_on) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int o = 4 * d_q + i;
@@ -597,53 +629,71 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
             for (int pp = 0; pp < 2; ++pp)
               dacc[dy][pp] += w[ky * 5 + kx] * f2{D[dy - ky + 4][2 * pp + 4 - kx], D[dy - ky + 4][2 * pp + 5 - kx]};
     }
-    if (d_q > 0) {
-      f2* part = reinterpret_cast<f2*>(PART) + ((d_q - 1) * 168 + d_r) * 4;
+    f2* part = reinterpret_cast<f2*>(PART) + (d_q * 168 + d_r) * 4;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) part[k] = dacc[k >> 1][k & 1];
-    }
+    for (int k = 0; k < 4; ++k) part[k] = dacc[k >> 1][k & 1];
     LANE_STAMP(16, 0);
   }
-  // the conv2 weight gradient over the active argmax pixels of each output channel (table T2):
-  // tasks (o, c, ky) of 5 taps, 352 on lanes 672..1023 (concurrently with the data gradient),
-  // the last 128 on lanes 0..127 once their data gradient is done; lanes 128..671 then build
-  // the re-strided image copy for the conv1 weight gradient
-  {
-    const int t = tid >= 672 ? tid - 672 : (tid < 128 ? tid + 352 : -1);
-    if (t >= 0) {
-      const int o = t / 30, rem = t - 30 * o, c = rem / 5, ky = rem - 5 * c, n = NACT[6 + o];
-      const float* pr = P1 + c * P1_CH + ky * 14;
-      float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int w = 0; w < n; ++w) {  // unrolled: the table and pixel reads overlap
-        const f2 e = T2[o * 25 + w];
-        const float* r = pr + __float_as_int(e.y);
+  // the conv2 weight gradient on the MATRIX cores, waves 11..15, concurrently with the data
+  // gradient's VALU work on waves 0..10: dW2[o][n] = sum_k dY2[o][k] * im2col(P1)[k][n] with
+  // n = (c, ky, kx) < 150 and k = (y, x) over the DENSE 10 x 10 unpooled dY2 (the zeros outside
+  // the argmax pixels add exact zeros) - a 16 x 150 x 100 GEMM whose M = 16 output channels fill
+  // the v_mfma_f32_16x16x4_f32 tile exactly.  Each wave owns two 16-column tiles, reads one dY2
+  // fragment and two im2col fragments per K-step (no table, no dependent address), and runs two
+  // interleaved accumulator chains of 25 MFMAs.  The sparse VALU form (tasks (o, c, ky) walking
+  // the active-window table) took 5.5 us of LDS round trips after the data gradient's 2.1 us.
+  if (wave >= 11) {
+    const int wv = wave - 11, col = lane & 15, q = lane >> 4;
+    const float* ab = DY2 + col * DY2_CH + 4 * DY2_LD + 4;  // A: dY2[o = col][k]
+    int nb[2];
 #pragma unroll
-        for (int kx = 0; kx < 5; ++kx) acc[kx] = __builtin_fmaf(e.x, r[kx], acc[kx]);
-      }
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx) slab[SLAB_C2W + o * 150 + c * 25 + ky * 5 + kx] = acc[kx];
+    for (int t = 0; t < 2; ++t) {  // B: im2col column n = 32 wv + 16 t + col (clamped: n >= 150 unstored)
+      const int n = min(32 * wv + 16 * t + col, 149), c = n / 25, r = n - 25 * c, ky = r / 5;
+      nb[t] = c * P1_CH + ky * 14 + (r - 5 * ky);
     }
-    LANE_STAMP(17, 672);
-    if (tid >= 1008) {  // conv2 bias gradient
-      const int o = tid - 1008;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 25; ++s) {  // k = 4 s + q: (y, x) from the compile-time (4 s) / 10
+      const int y0 = (4 * s) / 10, x0 = (4 * s) % 10;
+      const int xs = x0 + q, wrap = xs >= 10 ? 1 : 0;
+      const int y = y0 + wrap, x = xs - 10 * wrap;
+      const float a = ab[y * DY2_LD + x];
+      const float b0 = P1[nb[0] + y * 14 + x];
+      const float b1 = P1[nb[1] + y * 14 + x];
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1, acc1, 0, 0, 0);
+    }
+    // D[i = 4 q + r][j = col]: output channel o = 4 q + r, column n
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = 32 * wv + 16 * t + col;
+      if (n < 150) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slab[SLAB_C2W + (4 * q + r) * 150 + n] = t ? acc1[r] : acc0[r];
+      }
+    }
+  }
+  LANE_STAMP(17, 704);
+  {
+    if (tid >= 960 && tid < 976) {  // conv2 bias gradient (after wave 15's MFMA tiles)
+      const int o = tid - 960;
       float sb = 0.f;
       const int n = NACT[6 + o];
 #pragma unroll
       for (int w = 0; w < 25; ++w) sb += masked(T2[o * 25 + w].x, w < n);  // fixed trip: reads in flight
       slab[SLAB_C2B + o] = sb;
     }
-    if (tid >= 128 && tid < 672) {  // 3072 pixels over 544 lanes: 6 reads in flight, then 6 writes
+    if (tid < 704) {  // the re-strided image copy for the conv1 weight gradient: 3072 pixels over 704 lanes
       float* XW = reinterpret_cast<float*>(smem + L_F2);
-      float v[6];
+      float v[5];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int i = min(tid - 128 + 544 * k, 3071), c = i >> 10, y = (i >> 5) & 31, x = i & 31;
+      for (int k = 0; k < 5; ++k) {
+        const int i = min(tid + 704 * k, 3071), c = i >> 10, y = (i >> 5) & 31, x = i & 31;
         v[k] = X[c * X_CH + y * X_RS + x];
       }
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int i = tid - 128 + 544 * k, c = i >> 10, y = (i >> 5) & 31, x = i & 31;
+      for (int k = 0; k < 5; ++k) {
+        const int i = tid + 704 * k, c = i >> 10, y = (i >> 5) & 31, x = i & 31;
         if (i < 3072) XW[c * XW_CH + y * XW_RS + x] = v[k];
       }
     }
@@ -652,10 +702,19 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   WAVE_STAMP(24);
   lds_barrier();
   STAMP(12);
-  if (tid < 168) {
+  if (tid < 168) {  // lane = block d_r = 28 c + yx: the quarters' partials in the order 0, 1, 2, 3
+    d_r = tid;
+    d_c = tid / 28;
+    d_y0 = 2 * ((tid - 28 * d_c) >> 2);
+    d_x0 = 4 * ((tid - 28 * d_c) & 3);
     float db1 = 0.f;  // this lane's 8 windows' share of the conv1 bias gradient
+    {
+      const f2* part = reinterpret_cast<const f2*>(PART) + d_r * 4;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+      for (int k = 0; k < 4; ++k) dacc[k >> 1][k & 1] = part[k];
+    }
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
       const f2* part = reinterpret_cast<const f2*>(PART) + (q * 168 + d_r) * 4;
 #pragma unroll
       for (int k = 0; k < 4; ++k) dacc[k >> 1][k & 1] += part[k];

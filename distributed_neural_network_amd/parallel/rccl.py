@@ -6,7 +6,12 @@ for two bucketed all-reduces even at world size 1.  The hot path therefore calls
 ``ncclAllReduce`` from C++ (csrc/comm/rccl_comm.cpp) directly on the engine's stream;
 inside the step hipGraph it is one kernel node.  The communicator is bootstrapped
 through the job's TCPStore (rank 0 publishes the ncclUniqueId under the current
-generation prefix) and re-created after a rank drop (ncclCommAbort + new InitRank).
+generation prefix) and re-created after a rank drop (ncclCommAbort + a new communicator).
+
+Communicators are non-blocking (``ncclCommInitRankConfig`` with ``blocking = 0``): the init is
+polled through ``ncclCommGetAsyncError`` against ``DNN_RCCL_INIT_TIMEOUT_S`` (default 120 s), so
+a peer that dies while the group (re-)forms raises ``CommError`` instead of hanging inside
+RCCL.  ``DNN_RCCL_BLOCKING=1`` restores the blocking ``ncclCommInitRank``.
 
 Bucketing at this model size: the whole gradient is 248 KB (fp32) - a few
 microseconds of xGMI wire time, so the collective is latency-bound.  The default is
@@ -51,7 +56,9 @@ class RcclComm:
             c.store.set(key, self.ext.rccl_unique_id())
         uid = c.store.get(key)
         try:
-            self.handle = self.ext.rccl_init(uid, c.world, c.rank, c.device.index)
+            self.handle = self.ext.rccl_init(uid, c.world, c.rank, c.device.index,
+                                             int(os.environ.get("DNN_RCCL_BLOCKING", "0") == "1"),
+                                             float(os.environ.get("DNN_RCCL_INIT_TIMEOUT_S", "120")))
         except RuntimeError as e:
             raise CommError(f"ncclCommInitRank failed: {e}") from e
         self.generation = c.generation
