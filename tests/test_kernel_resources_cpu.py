@@ -13,7 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
-SOURCES = ["kernels/lenet_fused.hip", "kernels/reduce_sgd.hip", "kernels/layers.hip", "kernels/conv_igemm.hip",
+SOURCES = ["kernels/lenet_fused.hip", "kernels/lenet_f32.hip", "kernels/reduce_sgd.hip", "kernels/layers.hip", "kernels/conv_igemm.hip",
            "kernels/linear.hip", "comm/xgmi_allreduce.hip"]
 
 

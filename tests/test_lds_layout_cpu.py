@@ -1,0 +1,73 @@
+"""LDS bank model checks of kernel lane maps (CPU; gfx950 rules of MI355X_MICROARCH.md §LDS as
+coded in tools/lds_banks.py).  The fp32 kernel's conv2 data gradient (csrc/kernels/lenet_f32.hip,
+phase E) maps its 672 tasks (quarter q, channel c, 2 x 4 pixel block yx) to lanes so that every
+16-lane read group of its 16-B dY2 window reads hits 16 distinct 4-bank slots (or broadcasts);
+this replicates the kernel's formula and pins both properties."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+from lds_banks import G128, cycles  # noqa: E402
+
+DY2_LD, DY2_CH = 20, 18 * 20 + 4
+G1_MASK, PI_LO, PI_HI = 0xF00F0FF0, 0x7654765432103210, 0xFEDCFEDCBA98BA98
+
+
+def dgrad_task(tid):
+    """(q, c, yx) of lane tid, or None - lenet_f32.hip phase E, verbatim in Python."""
+    wave, lane = tid >> 6, tid & 63
+    l32 = lane & 31
+    gi = 4 * wave + 2 * (lane >> 5) + ((G1_MASK >> l32) & 1)
+    pi = ((PI_LO if l32 < 16 else PI_HI) >> (4 * (l32 & 15))) & 15
+    q = gi // 11
+    kg = gi - 11 * q
+    t = 16 * (kg - 6) + pi
+    if kg < 6:
+        c, yx = kg, 8 * (pi >> 2) + (pi & 3)
+    else:
+        c = t // 12
+        m = t - 12 * c
+        yx = 8 * (m >> 2) + 4 + (m & 3)
+    if not (tid < 704 and (kg < 6 or t < 72)):
+        return None
+    return q, c, yx
+
+
+def test_lane_groups_match_the_read_groups():
+    # the bit tables give each lane its ds_read_b128 group and a unique position in it
+    for base in (0, 32):
+        seen = {}
+        for l in range(base, base + 32):
+            l32 = l & 31
+            g = (G1_MASK >> l32) & 1
+            pi = ((PI_LO if l32 < 16 else PI_HI) >> (4 * (l32 & 15))) & 15
+            assert l in G128[g + (2 if base else 0)]
+            assert (g, pi) not in seen
+            seen[(g, pi)] = l
+
+
+def test_dgrad_map_is_a_bijection_onto_the_tasks():
+    tasks = [dgrad_task(t) for t in range(1024)]
+    real = [x for x in tasks if x is not None]
+    assert len(real) == 672 and len(set(real)) == 672
+    assert set(real) == {(q, c, yx) for q in range(4) for c in range(6) for yx in range(28)}
+    assert all(tasks[t] is None for t in range(704, 1024))  # waves 11-15: the MFMA weight gradient
+
+
+def test_dgrad_window_reads_are_conflict_free():
+    total = ideal = 0
+    for w in range(11):
+        for i in range(4):
+            for r in range(6):
+                for j in range(2):
+                    a = [None] * 64
+                    for l in range(64):
+                        task = dgrad_task(64 * w + l)
+                        if task is None:
+                            continue
+                        q, _, yx = task
+                        y0, x0 = 2 * (yx >> 2), 4 * (yx & 3)
+                        a[l] = 4 * ((4 * q + i) * DY2_CH + (y0 + r) * DY2_LD + x0 + 4 * j)
+                    total += cycles(a, G128, 16, 64)
+                    ideal += 4
+    assert total == ideal  # one LDS cycle per 16-lane group: 2112 per sample (the tid order took 4416)
