@@ -321,7 +321,10 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) r0[j] = w1[min(wave + 16 * j, 119) * 100 + lane];
   f2 cacc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-  const int c_hh = tid / 200, c_r = tid - 200 * c_hh, c_pp = c_r / 25, c_w = c_r - 25 * c_pp;
+  // task c_r = (window c_w, channel pair c_pp), pair-minor: a 32-lane read group covers 4
+  // windows x 8 pairs, so its 8-B image reads are 4 broadcast addresses and its 16-B weight reads
+  // 8 distinct slots (bank model: 756 LDS cycles per sample, the window-minor order took 1458)
+  const int c_hh = tid / 200, c_r = tid - 200 * c_hh, c_w = c_r >> 3, c_pp = c_r & 7;
   if (tid < 400) {
     const int wy = c_w / 5, wx = c_w - 5 * wy;
 #pragma unroll
