@@ -315,7 +315,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   // sums meet the first half's through LDS (fixed order: c 0-2, then + c 3-5)
   // fc1 rows of this wave (o = wave + 16 j): streamed from L2 ONCE, kept in registers through
   // the loss for the data gradient.  Issued now: the loads fly under conv2.
-  // (the first 64 columns of the rows now, the remaining 36 after conv2: register budget)
+  // (the first 64 columns of the rows now, the remaining 36 after the conv2 products: register
+  // budget)
   f4 r0[8], r1[8];
   const f4* w1 = reinterpret_cast<const f4*>(master + OFF_F1W);
 #pragma unroll
@@ -365,6 +366,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       for (int i = 0; i < 4; ++i) reinterpret_cast<f2*>(PART)[c_r * 4 + i] = cacc[i];
     }
   }
+  // the remaining 36 columns of the fc1 rows: issued as soon as the conv2 products are done
+  // (their patch and weight registers are dead; waves 7-15 have no conv2 work and issue them
+  // at once), so they land under the epilogue instead of at the start of phase D
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r1[j] = w1[min(wave + 16 * j, 119) * 100 + 64 + min(lane, 35)];
   lds_barrier();
   STAMP(3);
   if (tid < 200) {
@@ -385,8 +391,6 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       C2[o * 25 + c_w] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r1[j] = w1[min(wave + 16 * j, 119) * 100 + 64 + min(lane, 35)];
   lds_barrier();
   STAMP(4);
 
