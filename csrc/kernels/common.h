@@ -141,6 +141,46 @@ constexpr int ST_BVALID = 1;
 // device stats (fp64): [0] sum of batch-mean losses, [1] batches, [2] correct, [3] samples
 constexpr int STAT_LOSS = 0, STAT_BATCHES = 1, STAT_CORRECT = 2, STAT_SAMPLES = 3;
 
+// Cross-lane reductions on DPP (VALU lane permutes, a few cycles) instead of __shfl_xor (a
+// ds_bpermute through the LDS unit, ~100+ cycles of latency per dependent step).  Pairings:
+// quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror (i <-> 7 - i in each 8) and
+// row_mirror (i <-> 15 - i in each 16).  After the quad steps every lane of a quad holds the
+// bit-identical quad total, so pairing by mirror instead of xor 4 / xor 8 gives bit-identical
+// sums (fp32 + is commutative), and every lane of the group ends with the same value.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_XOR1 = 0xb1, DPP_XOR2 = 0x4e, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+__device__ __forceinline__ float sum4(float v) {
+  v += dppf<DPP_XOR1>(v);
+  return v + dppf<DPP_XOR2>(v);
+}
+__device__ __forceinline__ float sum8(float v) {
+  v = sum4(v);
+  return v + dppf<DPP_HALF_MIRROR>(v);
+}
+__device__ __forceinline__ float sum16(float v) {
+  v = sum8(v);
+  return v + dppf<DPP_MIRROR>(v);
+}
+__device__ __forceinline__ float max16(float v) {
+  v = fmaxf(v, dppf<DPP_XOR1>(v));
+  v = fmaxf(v, dppf<DPP_XOR2>(v));
+  v = fmaxf(v, dppf<DPP_HALF_MIRROR>(v));
+  return fmaxf(v, dppf<DPP_MIRROR>(v));
+}
+__device__ __forceinline__ int min16(int v) {
+  v = min(v, dppi<DPP_XOR1>(v));
+  v = min(v, dppi<DPP_XOR2>(v));
+  v = min(v, dppi<DPP_HALF_MIRROR>(v));
+  return min(v, dppi<DPP_MIRROR>(v));
+}
+
 }  // namespace dnn
 
 #define HIP_CHECK(x)                                                                      \

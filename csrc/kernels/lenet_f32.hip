@@ -119,12 +119,6 @@ __device__ __forceinline__ float masked(float v, bool keep) {
   return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
 template <bool TRAIN>
 __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
@@ -398,9 +392,9 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   {
     const f4 a0v = reinterpret_cast<const f4*>(A0)[lane];
     const f4 a1v = lane < 36 ? reinterpret_cast<const f4*>(A0)[64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+    float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int o = wave + 16 * j;
       float s = r0[j].x * a0v.x;
       s = __builtin_fmaf(r0[j].y, a0v.y, s);
       s = __builtin_fmaf(r0[j].z, a0v.z, s);
@@ -408,10 +402,21 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       s = __builtin_fmaf(r1[j].x, a1v.x, s);
       s = __builtin_fmaf(r1[j].y, a1v.y, s);
       s = __builtin_fmaf(r1[j].z, a1v.z, s);
-      s = __builtin_fmaf(r1[j].w, a1v.w, s);
-      s = wave_sum(s);
-      if (lane == 0 && o < 120) H1[o] = fmaxf(s + BIAS[B_F1 + o], 0.f);
+      v[j] = __builtin_fmaf(r1[j].w, a1v.w, s);
     }
+    // the wave's 8 row sums as a reduce-scatter: the xor 32 / 16 / 8 exchanges halve the rows
+    // each lane carries (7 ds_bpermute, 3 deep - 8 separate wave sums were 48, 6 deep each),
+    // then DPP finishes inside groups of 8 lanes; lane group (lane >> 3) holds row
+    // j = 4 h5 + 2 h4 + h3 (a fixed summation tree: deterministic)
+    const bool h5 = (lane & 32) != 0, h4 = (lane & 16) != 0, h3 = (lane & 8) != 0;
+    float u[4], w2[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = (h5 ? v[k + 4] : v[k]) + __shfl_xor(h5 ? v[k] : v[k + 4], 32);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) w2[k] = (h4 ? u[k + 2] : u[k]) + __shfl_xor(h4 ? u[k] : u[k + 2], 16);
+    const float t = sum8((h3 ? w2[1] : w2[0]) + __shfl_xor(h3 ? w2[0] : w2[1], 8));
+    const int o = wave + 16 * ((h5 ? 4 : 0) + (h4 ? 2 : 0) + (h3 ? 1 : 0));
+    if ((lane & 7) == 0 && o < 120) H1[o] = fmaxf(t + BIAS[B_F1 + o], 0.f);
   }
   // fc1 waits on L2 and leaves the LDS idle: the fc2 weights (in registers since phase A)
   // and the zero padding of dY2 go in now
@@ -429,9 +434,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 15; ++i) acc = __builtin_fmaf(row[i], h[i], acc);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    acc += __shfl_xor(acc, 4);
+    acc = sum8(acc);
     if (s == 0) H2[o] = fmaxf(acc + BIAS[B_F2 + o], 0.f);
   }
   lds_barrier();
@@ -445,21 +448,14 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 21; ++i) acc = __builtin_fmaf(row[i], h[i], acc);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
+    acc = sum4(acc);
     const float logit = __shfl(acc, 4 * min(lane, 9)) + BIAS[B_F3 + min(lane, 9)];
     const bool act = lane < 10;
     const float lg = act ? logit : -INFINITY;
-    float mx = lg;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 16));
+    const float mx = max16(lg);
     const float e = act ? expf(lg - mx) : 0.f;
-    float sum = e;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
-    int pred = (act && lg == mx) ? lane : 64;  // first max wins (torch.argmax)
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) pred = min(pred, __shfl_xor(pred, off, 16));
+    const float sum = sum16(e);
+    const int pred = min16((act && lg == mx) ? lane : 64);  // first max wins (torch.argmax)
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
@@ -522,8 +518,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     float d = 0.f;
 #pragma unroll
     for (int k = 0; k < 21; ++k) d = __builtin_fmaf(F2[(21 * s + k) * 120 + i], DZ2[21 * s + k], d);
-    d += __shfl_xor(d, 1);
-    d += __shfl_xor(d, 2);
+    d = sum4(d);
     if (s == 0) DZ1[i] = H1[i] > 0.f ? d : 0.f;
   }
   lds_barrier();

@@ -602,16 +602,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     // row 0 of the tile lives in lanes 0..15 (fg == 0): lane o holds logit o
     const bool act = lane < 10;
     const float lg = act ? acc[0] + bias_f3 : -INFINITY;
-    float mx = lg;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 16));
+    // row reductions on DPP (common.h): bit-identical to xor-shuffle butterflies, without a
+    // ds_bpermute round trip per step on the loss's critical path
+    const float mx = max16(lg);
     const float e = act ? expf(lg - mx) : 0.f;
-    float sum = e;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
-    int pred = (act && lg == mx) ? lane : 64;  // first max wins (torch.argmax)
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) pred = min(pred, __shfl_xor(pred, off, 16));
+    const float sum = sum16(e);
+    const int pred = min16((act && lg == mx) ? lane : 64);  // first max wins (torch.argmax)
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
@@ -762,8 +758,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) t += (part + 4 * k < 10) ? RS[o * 10 + min(part + 4 * k, 9)] : 0.f;
-    t += __shfl_xor(t, 1);
-    t += __shfl_xor(t, 2);
+    t = sum4(t);
     if (part == 0) SLAB_PUT(SLAB_C2B + o, t);
   }
   // conv2 data gradient: 14 tiles (one output row each, lanes x >= 14 duplicate x = 13)
@@ -906,9 +901,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) t += (part + 8 * k < 28) ? RS1[c * 28 + min(part + 8 * k, 27)] : 0.f;
-    t += __shfl_xor(t, 1);
-    t += __shfl_xor(t, 2);
-    t += __shfl_xor(t, 4);
+    t = sum8(t);
     if (part == 0 && lane < 48) SLAB_PUT(SLAB_C1B + c, t);
   }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
