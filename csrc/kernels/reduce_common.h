@@ -51,7 +51,7 @@ struct XpSinkT {
 using XpSink = XpSinkT<false>;
 
 // fc weight-gradient tiles: dW[o][i] = sum_b z[b][o] * x[b][i]  (K = batch), one 16x16
-// output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, fixed order).
+// output tile per wave on v_mfma_f32_16x16x4_f32 (exact fp32 fma chains, fixed order).
 template <int LAYER> struct Fc;
 template <> struct Fc<0> { static constexpr int O = 120, I = 400, IT = 25, OFF = OFF_F1W, ZLD = Z1_LD, XLD = A0_LD; };
 template <> struct Fc<1> { static constexpr int O = 84, I = 120, IT = 8, OFF = OFF_F2W, ZLD = Z2_LD, XLD = H1_LD; };
@@ -132,7 +132,9 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) { pv[j] = a.master[e[j]]; mv[j] = a.mom[e[j]]; }  // (unused if !fuse_sgd)
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // two interleaved accumulator chains (even / odd K-steps, summed at the end): the dependent
+  // MFMA chain per tile is 8 deep instead of 16 (this tile is the reduce launch's critical path)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const int omc = ov ? om : 0, inc = iv ? in : 0;
   for (int b0 = 0; b0 < a.batch; b0 += 64) {
     // every operand load is unconditional (clamped address) and issued before the first
@@ -170,8 +172,12 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
       bv[s] = (bvld && iv) ? bv[s] : 0.f;
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    for (int s = 0; s < 16; s += 2) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s + 1], bv[s + 1], acc1, 0, 0, 0);
+    }
   }
+  acc += acc1;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + 4 * kq + j;
