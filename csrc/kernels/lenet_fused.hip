@@ -179,6 +179,35 @@ __device__ __forceinline__ void build_r1_part(const uint8_t* img, bf16x8* R1, in
   }
 }
 
+// Half of build_r1_part: records x = 4h .. 4h+3 (x < 29) of input row `row` (bit-identical
+// records).  Phase F's R1 rebuild runs on these finer tasks so it balances over all 512 threads
+// next to the dY1 rows.  Task u -> row (u & 7) + 8 (u >> 6), h = (u >> 3) & 7: the 8 lanes of a
+// ds_write_b128 group take 8 consecutive rows of the same h (record stride 29 = 5 mod 8: 8
+// distinct 4-dword slots).
+__device__ __forceinline__ void build_r1_half(const uint8_t* img, bf16x8* R1, int u) {
+  const int row = (u & 7) + 8 * (u >> 6), h = (u >> 3) & 7;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(img + row * 32);
+  uint32_t w[3];  // pixels 4h .. 4h+11 (zero past the row end)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[k] = src[min(h + k, 7)];
+  bf16 v[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    const uint32_t px = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    const bf16 t = u8norm_bf16(px);
+    v[k] = (4 * h + k < 32) ? t : (bf16)0.f;
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    if (4 * h + x < 29) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = v[x + j];
+      R1[row * 29 + 4 * h + x] = r;
+    }
+  }
+}
+
 // R1 builder thread -> (row, quarter): the 8 lanes of a ds_write_b128 group take 8
 // different rows (row stride 29 records = 116 dwords -> 8 distinct 4-dword bank slots),
 // conflict-free; the natural (row = t / 4) map put 4 lanes on one slot (tools/lds_banks.py).
@@ -879,13 +908,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       drow[g8] = r;
     }
     RS1[c * 28 + y] = rs;
+    // the R1 rebuild (R2 is dead) in 768 half-row tasks: 2 on each thread past the dY1 rows,
+    // the last 80 on threads 0..79 after their dY1 row (whole-row tasks left threads 168..207
+    // with two full rows, 16 records, on the phase's critical path)
+    static_assert(2 * (NT - 168) <= 768 && 768 - 2 * (NT - 168) <= 168, "R1 half-task split");
+    if (tid < 768 - 2 * (NT - 168)) build_r1_half(IMGS, R1, 2 * (NT - 168) + tid);
   } else {
     if (staged && wave >= 5) {  // a vector load: the lgkmcnt(0) of the barriers does not wait for it
       const int32_t* p = next_ids + b;
       asm volatile("" : "+v"(p));
       ns_next = *p;
     }
-    for (int t = tid - 168; t < 384; t += NT - 168) build_r1_part(IMGS, R1, r1_row(t), r1_q(t));  // R2 dead
+    build_r1_half(IMGS, R1, tid - 168);
+    build_r1_half(IMGS, R1, tid - 168 + (NT - 168));
   }
   lds_barrier();
   STAMP(10);
