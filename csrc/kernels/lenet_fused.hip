@@ -471,28 +471,35 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         CODE1[fr * 196 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
       }
     };
-    // 49 tiles = 6 per wave + 1: three tiles per round (12 loads in flight) -> 2 rounds on
-    // waves 1-7, 3 on wave 0 (two-tile rounds needed 3 and 4)
-    for (int t0 = wave; t0 < 49; t0 += 24) {
-      const int t1 = t0 + 8 < 49 ? t0 + 8 : t0, t2 = t0 + 16 < 49 ? t0 + 16 : t0;
-      bf16x8 a0[4], a1[4], a2[4];
+    // 49 tiles = 6 per wave + 1: two rounds of three tiles (12 loads in flight) on every wave;
+    // the 49th tile rides along as a fourth in wave 0's second round (a third round of its own
+    // put one more LDS round trip + MFMA chain on wave 0, the phase's critical path)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int t0 = wave + 24 * r, t1 = t0 + 8, t2 = t0 + 16;
+      const bool four = wave == 0 && r == 1;  // wave-uniform
+      bf16x8 a0[4], a1[4], a2[4], a3[4];
 #pragma unroll
       for (int sk = 0; sk < 4; ++sk) {
         a0[sk] = R1[a_index(t0, sk)];
         a1[sk] = R1[a_index(t1, sk)];
         a2[sk] = R1[a_index(t2, sk)];
+        if (four) a3[sk] = R1[a_index(48, sk)];
       }
       __builtin_amdgcn_sched_barrier(0);
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int sk = 0; sk < 4; ++sk) {
         acc0 = mfma32(a0[sk], bw1[sk], acc0);
         acc1 = mfma32(a1[sk], bw1[sk], acc1);
         acc2 = mfma32(a2[sk], bw1[sk], acc2);
+        if (four) acc3 = mfma32(a3[sk], bw1[sk], acc3);
       }
       epilogue(t0, acc0);
-      if (t0 + 8 < 49) epilogue(t1, acc1);
-      if (t0 + 16 < 49) epilogue(t2, acc2);
+      epilogue(t1, acc1);
+      epilogue(t2, acc2);
+      if (four) epilogue(48, acc3);
     }
   }
   lds_barrier();
