@@ -682,19 +682,34 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   lds_barrier();
-  // fc1 dgrad: dA0 = W1^T dz1 (400 x 120), B fragments by transposed LDS reads of fc1
-  for (int nt = wave; nt < 25; nt += 8) {
-    bf16x8 av[4], bv[4];
+  // fc1 dgrad: dA0 = W1^T dz1 (400 x 120), B fragments by transposed LDS reads of fc1.  The 25
+  // column tiles of a wave (3, wave 0: 4) run as ONE batch: the A fragments (dz1, the same for
+  // every tile) once, every tile's transposed reads in flight together, then the MFMA chains -
+  // one LDS round trip per wave instead of one per tile (wave 0's fourth tile was a round of its
+  // own on the phase's critical path)
+  {
+    bf16x8 av[4], bv[4][4];
+    const bool four = wave == 0;  // wave-uniform: tile 24
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      bv[ks] = tr_frag(fc1s, 400, 32 * ks, 16 * nt, 120, lane);
       av[ks] = row0(DZ1B, 32 * ks + 8 * fg, fr);
+#pragma unroll
+      for (int u = 0; u < 3; ++u) bv[u][ks] = tr_frag(fc1s, 400, 32 * ks, 16 * (wave + 8 * u), 120, lane);
+      if (four) bv[3][ks] = tr_frag(fc1s, 400, 32 * ks, 16 * 24, 120, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) acc = mfma32(av[ks], bv[ks], acc);
-    if (fg == 0) DA0[16 * nt + fr] = acc[0];  // (the pool2/ReLU mask is applied via CODE2)
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) acc[u] = mfma32(av[ks], bv[u][ks], acc[u]);
+      if (four) acc[3] = mfma32(av[ks], bv[3][ks], acc[3]);
+    }
+    if (fg == 0) {  // (the pool2/ReLU mask is applied via CODE2)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) DA0[16 * (wave + 8 * u) + fr] = acc[u][0];
+      if (four) DA0[16 * 24 + fr] = acc[3][0];
+    }
   }
   // per-sample rows for the batch-reduced fc weight gradients: plain rows for the reduce
   // launch that follows, or (early-MLP overlap) tagged granules that the concurrently running
