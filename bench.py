@@ -10,7 +10,8 @@ with fp32 master weights/accumulation, momentum SGD (lr 0.001, m 0.9) every step
 
 Synchronisation defaults to a per-step gradient all-reduce inside the step hipGraph.  At N > 1
 the bench first MEASURES its transport (--allreduce ab, parallel/autotune.py): in the untimed
-set-up it times a few hundred real steps of every candidate - the one-launch xGMI exchange in
+set-up it times every candidate with the timed window's own shape (one exact-size graph of K
+steps inside one epoch, W warmup steps, 3 windows, median) - the one-launch xGMI exchange in
 its one-hop (xgmi-pull) and two-hop (xgmi-rsag) forms inside the batch-reduction kernel, native
 ncclAllReduce of one fused bucket (rccl) and of two buckets with the MLP bucket on a side stream
 (rccl-overlap) - plus the no-all-reduce step as the baseline, takes the max over ranks, and all
@@ -22,10 +23,14 @@ max over ranks).  --sync epoch-avg runs the reference algorithm
 buffer per epoch and an RCCL parameter all-reduce at every epoch end (epoch boundaries fall
 inside the timed window: 50,000 / N samples per rank and epoch).
 
-For N > 1 run under torchrun (one rank per GPU, RCCL over xGMI).  W untimed warmup
-steps, then EXACTLY K timed optimizer steps bracketed by barrier + device sync;
-epoch boundaries inside the window re-shuffle and continue (no step is skipped).
-The max over ranks is reported.  Rank 0 prints one JSON line.
+For N > 1 it runs one rank per GPU (RCCL over xGMI): under torchrun / mpiexec /
+parallel/launch.py, or - plain ``python bench.py --gpus N`` - it launches its own N ranks
+before anything touches the GPU (parallel/selflaunch.py) and relays rank 0's JSON line.
+W untimed warmup steps, then EXACTLY K timed optimizer steps bracketed by barrier + device
+sync; epoch boundaries inside the window re-shuffle and continue (no step is skipped).
+The max over ranks is reported.  Rank 0 prints one JSON line; every rank prints a stamped
+start-up trace to stderr (store / process group, native RCCL, xGMI IPC map, each A/B
+candidate), so a stalled multi-GPU start shows where it sits.
 """
 from __future__ import annotations
 
@@ -43,12 +48,19 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
+from distributed_neural_network_amd.parallel import selflaunch  # noqa: E402
 from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, allreduce_ab  # noqa: E402
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
 BASELINE_IMG_S = 1261.0  # BASELINE.md headline: bs64, "4 procs", training-phase whole-node img/s
 METRIC = "images/sec (whole node) + epoch time, CIFAR-10 CNN bs=64 at 1/2/4/8 MI355X"
+_T0 = time.time()
+
+
+def stamp(rank: int, msg: str) -> None:
+    """Start-up trace line on stderr (seconds since this process started)."""
+    print(f"[bench r{rank} +{time.time() - _T0:.3f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def _reserve_stdout() -> int:
@@ -82,7 +94,10 @@ def main():
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
                     help="bf16: the A/B also times the xGMI exchanges with bf16 gradient granules (opt-in "
                          "lower-precision gradient communication; the default path becomes its -bf16 form)")
-    ap.add_argument("--ab-steps", type=int, default=300, help="timed steps per candidate and round of the A/B")
+    ap.add_argument("--ab-steps", type=int, default=0,
+                    help="timed steps per A/B window (0: the timed window's own --steps, capped at 256); every "
+                         "candidate is timed exactly like the reported window (parallel/autotune.py)")
+    ap.add_argument("--ab-reps", type=int, default=3, help="A/B windows per candidate and round (median)")
     ap.add_argument("--noise", type=int, default=SYNTH_NOISE_HARD,
                     help="synthetic data noise amplitude (255: the hard split of tools/convergence.py, so the "
                          "epoch's val_acc / val_loss carry signal; 96: the easy template set)")
@@ -106,14 +121,21 @@ def main():
                          "inside the timed window (diagnostic)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and not selflaunch.launcher_present():
+        # no launcher: become one (nothing has touched the GPU yet; children, never an exec)
+        sys.exit(selflaunch.run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
+                                out_fd=out_fd))
+    os.environ.setdefault("DNN_STARTUP_TRACE", "1")
     env = detect()
     if env.world != args.gpus:
-        if env.world == 1 and args.gpus > 1:
-            sys.exit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks (found WORLD_SIZE=1)")
+        stamp(env.rank, f"note: --gpus {args.gpus} but the launcher started {env.world} ranks; using {env.world}")
     dev_index = env.local_rank % torch.cuda.device_count()  # 1 GPU per rank (wraps only in tests)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
+    stamp(env.rank, f"rank {env.rank}/{env.world} on cuda:{dev_index}; rendezvous {env.master_addr}:{env.master_port}")
     comm = Communicator(env, device)
+    if comm.distributed:
+        stamp(env.rank, f"store + process group ({comm.backend}) up")
     B = args.batch_size
 
     train = synthetic(args.train_samples, args.seed, True, noise=args.noise)
@@ -135,16 +157,20 @@ def main():
     policy.grad_comm = args.grad_comm
     if args.allreduce in ORDER + BF16_PATHS:
         policy.path = args.allreduce
+    stamp(comm.rank, f"engine {type(engine).__name__} ready; installing the all-reduce path")
     policy.attach(engine)
     policy.initial_broadcast(engine)
+    if comm.distributed:
+        stamp(comm.rank, f"all-reduce path {policy.installed(engine) if hasattr(policy, 'installed') else None}; "
+                         "initial broadcast done")
     cur = EpochCursor(engine, sampler, policy, B)
     ab = {}
     if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
-        cur._next_epoch()
-        ab = allreduce_ab(policy, engine, cur.run, steps=args.ab_steps,
-                          candidates=ORDER + (BF16_PATHS if args.grad_comm == "bf16" else ()))
-        if comm.rank == 0:
-            print(f"[bench] all-reduce A/B (us/step, max over ranks): {ab}", file=sys.stderr, flush=True)
+        ab_steps = args.ab_steps or min(args.steps, 256)
+        ab = allreduce_ab(policy, engine, cur, steps=ab_steps, warmup=args.warmup, reps=args.ab_reps,
+                          candidates=ORDER + (BF16_PATHS if args.grad_comm == "bf16" else ()),
+                          log=lambda m: stamp(comm.rank, m) if comm.rank == 0 else None)
+        stamp(comm.rank, f"all-reduce A/B (us/step, max over ranks): {ab}")
         cur.left = 0  # the timed run starts on a fresh epoch
 
     # untimed set-up: capture every chunk graph, first-call costs of the eval path (kernel,
@@ -181,6 +207,7 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
+    stamp(comm.rank, f"timed window done: {1e6 * dt / args.steps:.3f} us/step on this rank")
     if diag:
         print(f"[bench] reported window: {1e6 * dt / args.steps:.2f} us/step wall, "
               f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
@@ -265,7 +292,10 @@ def main():
         if ab:
             out["allreduce_ab"] = ab["allreduce_ab"]
             out["allreduce_failed"] = ab["failed"]
+            out["allreduce_failed_why"] = ab["why"]
             out["local_step_us"] = ab["local_us_per_step"]  # same steps with no all-reduce (A/B baseline)
+            # the reported window's us/step next to the A/B's number for the same path (same shape)
+            out["chosen_timed_us"] = round(1000.0 * ms_per_step, 3)
         if comm.distributed and args.sync == "step-allreduce":
             out["exchange_wait_us"] = waits
         os.write(out_fd, (json.dumps(out) + "\n").encode())

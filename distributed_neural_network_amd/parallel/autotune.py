@@ -1,4 +1,4 @@
-"""Start-up A/B of the per-step gradient all-reduce (multi-GPU bench, trainer ``--allreduce auto``).
+"""Start-up A/B of the per-step gradient all-reduce (multi-GPU bench, trainer ``--allreduce ab``).
 
 Why measure instead of guess: at 62,006 parameters the per-step collective is a few
 microseconds of xGMI wire time next to a ~20 us step, so which transport wins is decided by
@@ -8,22 +8,33 @@ timed its own communication (data_parallelism_train.py:116-120, 209-213, 228-231
 measures the candidates on the real node, in the real captured step, before the timed run:
 
 * every candidate path (``StepAllReduce.PATHS``) is installed collectively - its own self-test
-  included - on the same start parameters, graphs captured, ``warmup`` steps run, then
-  ``steps`` steps timed between barrier + device sync; the per-rank time's MAX over ranks is
-  the candidate's cost, and a candidate counts only if it installed and finished without a
-  failed wait on EVERY rank;
+  included - on the same start parameters;
+* it is timed with EXACTLY the shape of bench.py's timed window: inside one epoch (a fresh one
+  when the rest of the current epoch cannot hold the window), the window's step count as ONE
+  exact-size graph replay, ``warmup`` steps right before it, bracketed by barrier + device
+  sync on both sides; ``reps`` windows per round, the median per-rank time, MAX over ranks.
+  (Round 3 timed 300 steps as power-of-two chunk replays across epoch boundaries and read
+  3.5-4x the timed window's cost for the same path);
 * ``local`` (no all-reduce at all) is timed the same way as the baseline that the
   communication overhead of each path is read against; it is never selectable;
 * two rounds in alternating order (the min per path), so clock ramp-up does not favour the
   path that happens to run last;
+* FAULT-CONTAINED: a candidate whose install, self-test or timing raises on any rank (an RCCL
+  init error or timeout, a failed xGMI wait) is voted failed on every rank and lands in
+  ``failed`` with its reason; the epoch-boundary error vote is deferred for the whole A/B
+  (``lazy_check``) so it cannot escape mid-candidate.  Only "no path at all" is fatal;
 * every rank adopts the same winner (the decision is made from all-reduced numbers only), the
   parameters and momentum are restored, and the losing paths leave nothing installed.
 """
 from __future__ import annotations
 
+import inspect
 import math
+import os
+import statistics
+import sys
 import time
-from typing import Callable
+from typing import Callable, Optional
 
 import torch
 
@@ -49,32 +60,63 @@ def _sync(engine) -> None:
         torch.cuda.synchronize(engine.device)
 
 
-def _measure(comm, engine, run: Callable[[int], None], steps: int, warmup: int) -> tuple[float, bool]:
-    """(max-over-ranks us/step, passed on every rank) of the installed path."""
-    if hasattr(engine, "prepare_graphs"):
-        engine.prepare_graphs()
-    run(warmup)
+def window(comm, engine, cur, steps: int) -> float:
+    """One timed window exactly as bench.py times it: barrier + device sync, ``steps`` steps,
+    device sync + barrier + device sync.  Returns this rank's seconds."""
     comm.barrier()
     _sync(engine)
     t0 = time.perf_counter()
-    run(steps)
+    cur.run(steps)
     _sync(engine)
     comm.barrier()
     _sync(engine)
-    dt = time.perf_counter() - t0
+    return time.perf_counter() - t0
+
+
+def prepare_window(engine, cur, steps: int, warmup: int) -> None:
+    """Put the cursor where a ``warmup + steps`` window fits inside one epoch (a fresh epoch if
+    the rest of this one is too short) and capture the chunk graphs + the exact-size graph of
+    the window (bench.py:153-157).  Capture happens here, outside any timed region."""
+    if cur.left < warmup + steps and cur.steps_per_epoch >= warmup + steps:
+        cur.left = 0
+        cur._next_epoch()
+    elif cur.left == 0:
+        cur._next_epoch()
+    if hasattr(engine, "prepare_graphs"):
+        fits = steps <= min(512, cur.left - warmup)
+        if "exact" in inspect.signature(engine.prepare_graphs).parameters:
+            engine.prepare_graphs(exact=(steps,) if fits else ())
+        else:  # engines without exact-size graphs (layer engine)
+            engine.prepare_graphs()
+
+
+def _measure(comm, engine, cur, steps: int, warmup: int, reps: int) -> tuple[float, bool]:
+    """(max-over-ranks us/step, passed on every rank) of the installed path."""
+    times = []
+    for _ in range(reps):
+        prepare_window(engine, cur, steps, warmup)
+        cur.run(warmup)
+        times.append(window(comm, engine, cur, steps))
+    dt = statistics.median(times)
     failed = getattr(engine.grad_sync, "failed", None)
     bad = bool(failed()) if failed is not None else False
     ok = all(v == 0.0 for v in comm.gather_scalars(1.0 if bad else 0.0))
     return 1e6 * comm.reduce_scalar(dt, "max") / steps, ok
 
 
-def allreduce_ab(policy, engine, run: Callable[[int], None], steps: int = 300, warmup: int = 40,
-                 rounds: int = 2, candidates: tuple[str, ...] = ORDER) -> dict:
-    """Collective (every rank calls it with the same arguments).  Times every candidate,
-    installs the winner on ``engine`` (``policy.path`` pins it for later re-attaches) and
-    returns {"allreduce_ab": {path: us_per_step | None}, "allreduce": winner,
-    "local_us_per_step": ..., "failed": [...]}."""
+def _agree(comm, ok: bool) -> bool:
+    return all(v == 1.0 for v in comm.gather_scalars(1.0 if ok else 0.0))
+
+
+def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: int = 2, reps: int = 3,
+                 candidates: tuple[str, ...] = ORDER, log: Optional[Callable[[str], None]] = None,
+                 rccl_init_timeout_s: float = 60.0) -> dict:
+    """Collective (every rank calls it with the same arguments).  ``cur`` is the run's
+    ``EpochCursor``.  Times every candidate, installs the winner on ``engine`` (``policy.path``
+    pins it for later re-attaches) and returns {"allreduce_ab": {path: us_per_step | None},
+    "allreduce": winner, "local_us_per_step": ..., "failed": [...], "why": {path: reason}}."""
     comm = policy.comm
+    say = log or (lambda s: None)
     snap = (engine.master.detach().clone(), engine.mom.detach().clone())
 
     def restore() -> None:
@@ -86,40 +128,95 @@ def allreduce_ab(policy, engine, run: Callable[[int], None], steps: int = 300, w
 
     results: dict[str, dict] = {}
     names = ("local",) + tuple(candidates)
-    for rnd in range(rounds):
-        seq = names if rnd % 2 == 0 else tuple(reversed(names))
-        for name in seq:
-            if results.get(name, {}).get("ok") is False:
-                continue  # failed once: not tried again
-            ok = policy.install(engine, name)
-            if not ok:
-                results[name] = {"ok": False, "us_per_step": None, "why": "install / self-test failed"}
-                continue
-            restore()
-            us, passed = _measure(comm, engine, run, steps, warmup)
-            if not passed:
-                # a wait timed out somewhere: the sticky error words stay set and the group's
-                # step counters may be out of step - drop the group (rebuilt if chosen later)
-                policy._drop_xgmi_group()
-                results[name] = {"ok": False, "us_per_step": None, "why": "a wait failed during the timed steps"}
-                continue
-            prev = results.get(name, {}).get("us_per_step")
-            results[name] = {"ok": True, "us_per_step": us if prev is None else min(prev, us)}
-    win = choose(results)
-    engine.grad_sync = None
-    if win is None or not policy.install(engine, win):
-        win = None
-        policy.path = None
-        policy.attach(engine)  # the default path (and its fallbacks)
-    else:
-        policy.path = win
-    restore()
+    lazy = getattr(policy, "lazy_check", False)
+    policy.lazy_check = True  # an xGMI wait failure is voted per candidate below, not at an epoch end
+    tmo = os.environ.get("DNN_RCCL_INIT_TIMEOUT_S")
+    os.environ["DNN_RCCL_INIT_TIMEOUT_S"] = str(min(float(tmo or 1e9), rccl_init_timeout_s))
+    try:
+        for rnd in range(rounds):
+            seq = names if rnd % 2 == 0 else tuple(reversed(names))
+            for name in seq:
+                if results.get(name, {}).get("ok") is False:
+                    continue  # failed once: not tried again
+                t0 = time.perf_counter()
+                why = ""
+                try:
+                    ok = bool(policy.install(engine, name))
+                    if not ok:
+                        why = "install / self-test failed"
+                except Exception as e:  # contained: this candidate fails, the A/B goes on
+                    ok, why = False, f"install raised {type(e).__name__}: {e}"
+                if not _agree(comm, ok):
+                    why = why or "failed on another rank"
+                    results[name] = {"ok": False, "us_per_step": None, "why": why}
+                    _drop(policy, engine, name)
+                    say(f"A/B {name}: FAILED ({why}) after {time.perf_counter() - t0:.2f}s")
+                    continue
+                restore()
+                passed, us = True, None
+                try:
+                    us, passed = _measure(comm, engine, cur, steps, warmup, reps)
+                    if not passed:
+                        why = "a wait failed during the timed steps"
+                except Exception as e:
+                    passed, why = False, f"timing raised {type(e).__name__}: {e}"
+                if not _agree(comm, passed):
+                    results[name] = {"ok": False, "us_per_step": None, "why": why or "failed on another rank"}
+                    # sticky error words stay set and the group's step counters may be out of
+                    # step: drop the group (rebuilt if another xGMI path is tried later)
+                    _drop(policy, engine, name)
+                    say(f"A/B {name}: FAILED ({results[name]['why']})")
+                    continue
+                prev = results.get(name, {}).get("us_per_step")
+                results[name] = {"ok": True, "us_per_step": us if prev is None else min(prev, us)}
+                say(f"A/B {name}: {us:.3f} us/step (round {rnd}, {time.perf_counter() - t0:.2f}s incl. install)")
+        win = choose(results)
+        engine.grad_sync = None
+        installed = False
+        if win is not None:
+            try:
+                installed = bool(policy.install(engine, win))
+            except Exception as e:
+                say(f"A/B winner {win} could not be re-installed: {type(e).__name__}: {e}")
+            installed = _agree(comm, installed)
+        if not installed:
+            win = None
+            policy.path = None
+            policy.attach(engine)  # the default path (and its fallback chain)
+        else:
+            policy.path = win
+        restore()
+    finally:
+        policy.lazy_check = lazy
+        if tmo is None:
+            os.environ.pop("DNN_RCCL_INIT_TIMEOUT_S", None)
+        else:
+            os.environ["DNN_RCCL_INIT_TIMEOUT_S"] = tmo
     return {"allreduce_ab": {k: (round(v["us_per_step"], 3) if v.get("us_per_step") is not None else None)
                              for k, v in results.items() if k != "local"},
             "local_us_per_step": (round(results["local"]["us_per_step"], 3)
                                   if results.get("local", {}).get("us_per_step") is not None else None),
             "allreduce": policy.installed(engine),
-            "failed": sorted(k for k, v in results.items() if not v.get("ok"))}
+            "failed": sorted(k for k, v in results.items() if not v.get("ok")),
+            "why": {k: v["why"] for k, v in results.items() if not v.get("ok")}}
 
 
-__all__ = ["BF16_PATHS", "ORDER", "allreduce_ab", "choose"]
+def _drop(policy, engine, name: str) -> None:
+    """Leave nothing of a failed candidate installed."""
+    engine.grad_sync = None
+    if name.startswith("xgmi") and hasattr(policy, "_drop_xgmi_group"):
+        try:
+            policy._drop_xgmi_group()
+        except Exception as e:
+            print(f"[ab] dropping the xGMI group after {name} failed: {e}", file=sys.stderr, flush=True)
+    if name.startswith("rccl"):
+        nat = getattr(policy.comm, "native", None)
+        if nat is not None:
+            try:
+                nat.abort()
+            except Exception:
+                pass
+            policy.comm.native = None
+
+
+__all__ = ["BF16_PATHS", "ORDER", "allreduce_ab", "choose", "prepare_window", "window"]

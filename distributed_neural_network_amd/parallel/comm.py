@@ -37,6 +37,19 @@ class CommError(RuntimeError):
     """A collective failed (peer died, communicator aborted, timeout)."""
 
 
+_TRACE_T0 = time.time()
+
+
+def trace(msg: str) -> None:
+    """Stamped start-up trace on stderr (``DNN_STARTUP_TRACE=1``; bench.py sets it): process
+    group, native RCCL init, xGMI IPC map - so a stalled multi-GPU start shows where it sits."""
+    if os.environ.get("DNN_STARTUP_TRACE") == "1":
+        import sys
+
+        print(f"[trace r{os.environ.get('RANK', '0')} +{time.time() - _TRACE_T0:.3f}s] {msg}", file=sys.stderr,
+              flush=True)
+
+
 class Communicator:
     def __init__(self, env: DistEnv | None = None, device: torch.device | str = "cpu",
                  backend: str | None = None, timeout_s: float = 300.0) -> None:
@@ -60,8 +73,11 @@ class Communicator:
         # even at world size 1 (exercises the RCCL + hipGraph-capture path on one GPU)
         self.force = os.environ.get("DNN_FORCE_COLLECTIVES", "0") == "1"
         if self.env.world > 1 or self.force:
+            trace(f"store {self.env.master_addr}:{self.env.master_port} ...")
             self._init_store()
+            trace(f"store connected; process group ({self.backend}, generation {self.generation}) ...")
             self._init_group()
+            trace("process group up")
 
     # -- identity ----------------------------------------------------------------------
     @property
@@ -88,14 +104,53 @@ class Communicator:
         elif self.env.world > 1 and os.environ.get("DNN_STORE_IN_RANK0", "0") != "1":
             # no agent (mpiexec / plain env launch): rank 0 starts a stand-alone store process and
             # every rank is a client, so the store survives rank 0 (parallel/store_server.py)
+            token = None
             if self.env.rank == 0:
-                self._store_proc = _spawn_store_server(self.env.master_port, self.env.world)
+                token = f"{os.getpid()}-{os.urandom(6).hex()}"
+                self._store_proc = _spawn_store_server(self.env.master_port, self.env.world, token)
             self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
                                        is_master=False, timeout=self.timeout)
+            self._check_fresh_store(token)
         else:
             self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
                                        is_master=self.env.rank == 0, timeout=self.timeout,
                                        wait_for_workers=False)
+
+    STALE_BEAT_S = 30.0
+
+    def _check_fresh_store(self, token: str | None) -> None:
+        """Fail loudly if the store on MASTER_PORT is a server left over from an earlier job
+        (ADVICE r3): its keys - recovery leaders, member lists, RCCL ids, closed counters -
+        would steer this job.  Rank 0 checks that the server answering is the child it just
+        started (job token, and the child is still running: a second server on a taken port
+        exits at once); every rank checks that nothing has checked out of this store yet and
+        that no rank's heartbeat in it is older than ``STALE_BEAT_S`` (a left-over server exits
+        on its own after that long without beats, parallel/store_server.py)."""
+        st = self.store
+        assert st is not None
+        where = f"{self.env.master_addr}:{self.env.master_port}"
+        if token is not None:
+            st.wait(["dnn/store_server"])
+            got = st.get("dnn/store_server").decode()
+            proc = getattr(self, "_store_proc", None)
+            if got != token or (proc is not None and proc.poll() is not None):
+                raise CommError(f"the rendezvous store on {where} is not this job's (token {got!r}, expected "
+                                f"{token!r}; store child exit code {proc.poll() if proc is not None else None}): "
+                                "a server from an earlier job still holds the port - wait for it to exit "
+                                f"(<= {self.STALE_BEAT_S:.0f} s after its job's last heartbeat) or use another MASTER_PORT")
+        if st.add("dnn/closed", 0) != 0 or st.add("dnn/dropped", 0) != 0:
+            raise CommError(f"the rendezvous store on {where} belongs to a finished job (ranks have checked out)")
+        now = time.time()
+        for r in range(self.env.world):
+            k = f"dnn/hb/{r}"
+            if st.check([k]):
+                try:
+                    age = now - float(st.get(k).decode())
+                except ValueError:
+                    continue
+                if age > self.STALE_BEAT_S:
+                    raise CommError(f"the rendezvous store on {where} holds a {age:.0f} s old heartbeat of rank {r}: "
+                                    "it belongs to an earlier job")
 
     def _init_group(self) -> None:
         assert self.store is not None
@@ -354,16 +409,17 @@ class Communicator:
 _REAPERS: list[threading.Thread] = []
 
 
-def _spawn_store_server(port: int, world: int):
+def _spawn_store_server(port: int, world: int, token: str):
     """Start parallel/store_server.py as a child in its own session (a signal to this rank's
     process group does not reach it) and return the Popen.  A child process, never an exec of
-    this one; it imports no GPU runtime."""
+    this one; it imports no GPU runtime.  ``token`` identifies this job's server."""
     import subprocess
     import sys
 
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     return subprocess.Popen([sys.executable, "-m", "distributed_neural_network_amd.parallel.store_server",
-                             "--port", str(port), "--world", str(world)], env=env, start_new_session=True,
+                             "--port", str(port), "--world", str(world), "--token", token], env=env,
+                            start_new_session=True,
                             stdin=subprocess.DEVNULL, cwd=os.path.dirname(os.path.dirname(os.path.dirname(
                                 os.path.abspath(__file__)))))
 

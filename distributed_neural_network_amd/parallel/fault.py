@@ -31,6 +31,7 @@ Capability parity:
 from __future__ import annotations
 
 import os
+import socket
 import threading
 import time
 from dataclasses import dataclass
@@ -87,11 +88,17 @@ class Heartbeat:
 
         self.comm = comm
         self.period = period_s
-        # DNN_HEARTBEAT_TIMEOUT: seconds without a beat before a peer is declared dead.  A live
-        # rank whose beat thread was starved past it (a loaded host) is flagged, but it still
-        # announces itself alive in the recovery agreement: the recovery is then an all-alive
-        # retry, and the agreement clears the flag (``clear``)
-        self.timeout = float(os.environ.get("DNN_HEARTBEAT_TIMEOUT", "1.0")) if timeout_s is None else timeout_s
+        # DNN_HEARTBEAT_TIMEOUT: seconds without a beat before a peer is flagged (default
+        # 1 s + 0.1 s per rank: more ranks on one host, more beat-thread contention).  The
+        # effective timeout also follows the beat jitter actually observed: at least 4x the p99
+        # gap between a peer's consecutive beats (``timeout``).  A flag only starts a recovery;
+        # a live rank whose beat was late still announces itself alive in the agreement and
+        # keeps its place (an all-alive retry; ``clear`` drops the flag).  Launcher-reported
+        # deaths (dnn/dead/<r>) bypass all of this and are flagged within one period.
+        env_t = os.environ.get("DNN_HEARTBEAT_TIMEOUT")
+        self.base_timeout = (float(env_t) if env_t else 1.0 + 0.1 * comm.world) if timeout_s is None else timeout_s
+        self._gaps: list[float] = []  # recent gaps between a peer's consecutive beat stamps (s)
+        self._last_val: dict[int, float] = {}
         self.dead: set[int] = set()
         self.detected_at: dict[int, float] = {}  # rank -> time.time() when the watchdog flagged it
         # rank -> time its flag was cleared by a recovery agreement: staleness counts from here,
@@ -103,10 +110,33 @@ class Heartbeat:
         # a private client connection for the thread
         self.store = dist.TCPStore(env.master_addr, env.master_port, env.world, is_master=False,
                                    timeout=comm.timeout)
+        # process identity: a peer on the same host whose process is gone is dead at once, even
+        # with no launcher to report it (mpiexec / plain env launches) - a stale beat alone only
+        # starts the (patient) agreement
+        self.host = socket.gethostname()
+        self.store.set(f"dnn/pid/{comm.orig_rank}", f"{self.host}:{os.getpid()}")
+        self._pids: dict[int, Optional[int]] = {}
         self._beat()
         comm.watch = lambda: tuple(self.dead)  # makes host-blocking collectives interruptible
         self._thread = threading.Thread(target=self._run, name="dnn-heartbeat", daemon=True)
         self._thread.start()
+
+    JITTER_FACTOR = 4.0
+
+    @property
+    def timeout(self) -> float:
+        """Base timeout, raised to JITTER_FACTOR x the p99 observed beat gap (last 256 gaps)."""
+        g = sorted(self._gaps)
+        p99 = g[min(len(g) - 1, int(0.99 * len(g)))] if g else 0.0
+        return max(self.base_timeout, self.JITTER_FACTOR * p99)
+
+    def _observe(self, rank: int, stamp: float) -> None:
+        prev = self._last_val.get(rank)
+        if prev is not None and stamp > prev:
+            self._gaps.append(stamp - prev)
+            if len(self._gaps) > 256:
+                del self._gaps[:-256]
+        self._last_val[rank] = stamp
 
     def _beat(self) -> None:
         if time.time() < self.paused_until:
@@ -122,14 +152,36 @@ class Heartbeat:
             return 0.0
 
     def stale(self, rank: int) -> bool:
-        return time.time() - max(self.last_seen(rank), self.grace.get(rank, 0.0)) > self.timeout
+        seen = self.last_seen(rank)
+        if seen and rank not in self.dead:
+            self._observe(rank, seen)
+        return time.time() - max(seen, self.grace.get(rank, 0.0)) > self.timeout
 
     def reported_dead(self, rank: int) -> bool:
-        """The launcher saw this rank's process exit (parallel/launch.py publishes it)."""
+        """The rank's process is known to be gone: the launcher saw it exit (parallel/launch.py,
+        selflaunch.py, torchrun's agent publish ``dnn/dead/<r>``), or it ran on this host and its
+        pid no longer names a live process."""
         try:
-            return bool(self.store.check([f"dnn/dead/{rank}"]))
+            if self.store.check([f"dnn/dead/{rank}"]):
+                return True
         except Exception:
             return False
+        return self._local_pid_gone(rank)
+
+    def _local_pid_gone(self, rank: int) -> bool:
+        if rank not in self._pids:
+            pid = None
+            try:
+                if self.store.check([f"dnn/pid/{rank}"]):
+                    host, _, p = self.store.get(f"dnn/pid/{rank}").decode().rpartition(":")
+                    pid = int(p) if host == self.host else None
+                else:
+                    return False  # not registered yet: ask again later
+            except Exception:
+                return False
+            self._pids[rank] = pid
+        pid = self._pids[rank]
+        return pid is not None and not pid_alive(pid)
 
     def _flag(self, r: int, why: str) -> None:
         self.dead.add(r)
@@ -182,6 +234,21 @@ class Heartbeat:
         self._thread.join(timeout=2.0)
 
 
+def pid_alive(pid: int) -> bool:
+    """Does ``pid`` name a live (not zombie) process on this host?"""
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except OSError:
+        return True  # no /proc: kill(0) said it exists
+
+
 def announce_alive(comm: Communicator) -> None:
     """Mark this rank alive for generation g's agreement.  Called BEFORE tearing the broken
     group down: destroying a gloo group can block until a collective pending on the dead
@@ -192,20 +259,30 @@ def announce_alive(comm: Communicator) -> None:
     comm.store.set(f"dnn/recover/{comm.generation}/begun", str(comm.orig_rank))
 
 
+def exclusion_grace(hb: Heartbeat) -> float:
+    """Seconds a heartbeat-only-stale rank gets to announce itself before it is excluded
+    (``DNN_EXCLUDE_GRACE_S``, default max(10 s, 2 heartbeat timeouts)).  Separate from the
+    flagging timeout: a whole-process stall of a few seconds (swap, a long GIL hold, SIGSTOP,
+    host contention) costs an all-alive retry, never the rank's place."""
+    env = os.environ.get("DNN_EXCLUDE_GRACE_S")
+    return float(env) if env else max(10.0, 2.0 * hb.timeout)
+
+
 def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0, grace_s: float | None = None) -> list[int]:
     """Survivors of generation g agree on the member list of generation g+1.
 
     A member is alive once it announced itself (``announce_alive``).  It is dead at once if the
-    launcher reported its process gone, and dead after ``grace_s`` (default: two heartbeat
-    timeouts) if its heartbeat is stale - a live rank whose beat was only late reaches its own
-    recovery (its next collective fails once the others tore their group down) and announces
-    itself within that grace, so it stays in the group: the recovery is an all-alive retry.
-    Ranks neither stale nor announced are waited for up to ``wait_s``."""
+    launcher reported its process gone, and dead after ``grace_s`` (``exclusion_grace``) if its
+    heartbeat is stale - a live rank whose beat was only late reaches its own recovery (its next
+    collective fails once the others tore their group down, or its watchdog sees the recovery
+    begin) and announces itself within that grace, so it stays in the group: the recovery is an
+    all-alive retry.  Ranks neither stale nor announced are waited for up to ``wait_s``."""
     assert comm.store is not None
     st = comm.store
     p = f"dnn/recover/{comm.generation}/"
     st.set(f"{p}alive/{comm.orig_rank}", "1")
-    grace = 2.0 * hb.timeout if grace_s is None else grace_s
+    grace = exclusion_grace(hb) if grace_s is None else grace_s
+    wait_s = max(wait_s, grace + 5.0)
     t0 = time.time()
     deadline = t0 + wait_s
     while True:
@@ -227,6 +304,42 @@ def agree_survivors(comm: Communicator, hb: Heartbeat, wait_s: float = 30.0, gra
     st.wait([f"{p}members"])
     members = [int(x) for x in st.get(f"{p}members").decode().split(",") if x]
     return members
+
+
+def stall_injection(orig_rank: int, epoch: int) -> tuple[str, float]:
+    """Fault injection for tests: a WHOLE-process stall of a live rank at the start of an epoch.
+    ``DNN_INJECT_STALL=rank:epoch:seconds[:kind]``, kind ``sigstop`` (default: the process is
+    stopped, every thread included, and a helper process continues it) or ``gil`` (the main
+    thread holds the GIL - a long C call - so the heartbeat thread cannot beat).  Returns
+    (kind, seconds); seconds 0: none."""
+    spec = os.environ.get("DNN_INJECT_STALL", "")
+    if not spec:
+        return "", 0.0
+    parts = spec.split(":")
+    r, e, d = int(parts[0]), int(parts[1]), float(parts[2])
+    kind = parts[3] if len(parts) > 3 else "sigstop"
+    return (kind, d) if r == orig_rank and e == epoch else ("", 0.0)
+
+
+def stall_process(kind: str, seconds: float) -> None:
+    """Carry out a ``stall_injection``."""
+    import signal
+    import subprocess
+    import sys
+
+    print(f"[fault] injected {kind} stall: this process stops for {seconds} s", flush=True)
+    if kind == "gil":
+        old = sys.getswitchinterval()
+        sys.setswitchinterval(seconds + 1.0)  # no other thread gets the GIL while this one spins
+        t_end = time.time() + seconds
+        try:
+            while time.time() < t_end:
+                pass
+        finally:
+            sys.setswitchinterval(old)
+        return
+    subprocess.Popen(["/bin/sh", "-c", f"sleep {seconds}; kill -CONT {os.getpid()}"], start_new_session=True)
+    os.kill(os.getpid(), signal.SIGSTOP)
 
 
 def beat_pause_injection(orig_rank: int, epoch: int) -> float:

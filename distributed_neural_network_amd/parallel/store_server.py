@@ -9,9 +9,11 @@ not reach it), every rank including rank 0 connects as a client, and the store o
 single rank.
 
 It exits when every rank of the job has checked out (``dnn/closed`` counter, incremented by
-``Communicator.close``; a rank the recovery dropped counts through ``dnn/dropped``), or when
-nothing has changed for ``--idle`` seconds - no new key, no heartbeat (``dnn/hb/<rank>``) -
-i.e. every rank is gone without checking out.
+``Communicator.close``; a rank the recovery dropped counts through ``dnn/dropped``), when every
+heartbeat it has seen is older than ``--stale`` seconds (the ranks are gone without checking
+out: a crash, Ctrl-C, SIGKILL), or when nothing at all has changed for ``--idle`` seconds.  It
+publishes ``dnn/store_server`` = ``--token`` (rank 0's job token), so rank 0 can tell its own
+server from one an earlier job left on the port (Communicator._check_fresh_store).
 
 usage (started by Communicator; not by hand):
     python -m distributed_neural_network_amd.parallel.store_server --port P --world N
@@ -28,14 +30,16 @@ def main(argv=None) -> int:
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, required=True)
     ap.add_argument("--world", type=int, required=True)
-    ap.add_argument("--idle", type=float, default=3600.0)
+    ap.add_argument("--idle", type=float, default=300.0)
+    ap.add_argument("--stale", type=float, default=30.0)
+    ap.add_argument("--token", default="up")
     a = ap.parse_args(argv)
 
     import torch.distributed as dist
 
     store = dist.TCPStore(a.host, a.port, a.world + 1, is_master=True, wait_for_workers=False,
                           timeout=__import__("datetime").timedelta(seconds=30))
-    store.set("dnn/store_server", "up")
+    store.set("dnn/store_server", a.token)
     last_change, last_sig = time.time(), None
     while True:
         time.sleep(0.2)
@@ -51,6 +55,16 @@ def main(argv=None) -> int:
             return 1
         if closed + dropped >= a.world:
             time.sleep(1.0)  # let the last clients finish their final reads
+            return 0
+        stamps = []
+        for v in beats:
+            try:
+                stamps.append(float(v.decode()) if v else None)
+            except ValueError:
+                stamps.append(None)
+        seen = [t for t in stamps if t is not None]
+        if seen and time.time() - max(seen) > a.stale:
+            print(f"[store] no heartbeat for {a.stale:.0f} s: the job is gone, exiting", file=sys.stderr, flush=True)
             return 0
         if sig != last_sig:
             last_sig, last_change = sig, time.time()

@@ -21,7 +21,7 @@ import time
 
 import torch
 
-from .comm import CommError, Communicator, GradAllReduce
+from .comm import CommError, Communicator, GradAllReduce, trace
 
 SYNC_MODES = ("step-allreduce", "epoch-avg", "parent")
 
@@ -220,10 +220,12 @@ class StepAllReduce(SyncPolicy):
             from .rccl import NativeGradAllReduce, RcclComm
 
             rc = getattr(self.comm, "native", None)
+            trace("native RCCL communicator ...")
             if rc is None:
                 rc = self.comm.native = RcclComm(self.comm)
             elif rc.generation != self.comm.generation:
                 rc.reinit()
+            trace("native RCCL communicator up")
             engine.grad_sync = NativeGradAllReduce(rc, engine.device, overlap=name == "rccl-overlap",
                                                    bucket_kb=self.bucket_kb)
             return True
@@ -294,8 +296,10 @@ class StepAllReduce(SyncPolicy):
         if grp is not None and (grp.generation != self.comm.generation or grp.capacity < n):
             stale, grp = grp, None
         if grp is None and not getattr(self.comm, "xgmi_refused", False):
+            trace("xGMI group: IPC regions + self-test ...")
             grp = self.comm.xgmi = xgmi.build_group(self.comm, n)
             self.comm.xgmi_refused = grp is None
+            trace(f"xGMI group {'up' if grp is not None else 'refused / failed'}")
         if stale is not None:
             stale.close()  # after the new regions exist: no address of the old ones is reused
         if hasattr(engine, "invalidate_graphs"):

@@ -26,7 +26,7 @@ import torch
 from ..data import EpochSampler, get_splits
 from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
 from ..parallel.fault import (DropInjector, Heartbeat, agree_survivors, announce_alive, beat_pause_injection,
-                              simulate_failure)
+                              simulate_failure, stall_injection, stall_process)
 from ..runtime import eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
 from ..utils.metrics import Run
@@ -241,8 +241,7 @@ class Trainer:
 
             cur = EpochCursor(self.engine, self.sampler, self.policy, c.batch_size)
             cands = ORDER + (BF16_PATHS if self.policy.grad_comm == "bf16" else ())
-            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur.run, steps=100, warmup=20,
-                                             candidates=cands)
+            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur, steps=64, warmup=16, candidates=cands)
             self._say(f"[allreduce] start-up A/B (us/step, max over ranks): {self.allreduce_ab['allreduce_ab']}; "
                       f"using {self.allreduce_ab['allreduce']}")
             self.run_log.record(event="allreduce_ab", **self.allreduce_ab)
@@ -280,6 +279,10 @@ class Trainer:
             if c.mode != "single":
                 self._say("Starting epoch ", epoch)
             simulate_failure(self.comm.orig_rank, c.failure_probability, c.failure_duration, self.rng)
+            kind, stall = stall_injection(self.comm.orig_rank, epoch)
+            if stall and ("stall", epoch) not in self._paused:
+                self._paused.add(("stall", epoch))
+                stall_process(kind, stall)
             pause = beat_pause_injection(self.comm.orig_rank, epoch)
             if pause and self.hb is not None and epoch not in self._paused:
                 self._paused.add(epoch)
@@ -355,9 +358,15 @@ class Trainer:
                                     seed=c.seed, world=self.comm.world, sync=c.sync, mode=c.mode)
             epoch += 1
 
+        # recoveries with every member alive: heartbeat false positives / transient collective
+        # failures (each cost one epoch redo, never a rank)
+        retries = sum(1 for r in self.recoveries if not r["dead"])
+        if self.rank0:
+            self.run_log.record(event="summary", recoveries=len(self.recoveries), retries_all_alive=retries,
+                                heartbeat_timeout_s=round(self.hb.timeout, 3) if self.hb is not None else None)
         self._finish()
         return {"history": self.history, "recoveries": self.recoveries, "timers": self.timers.as_dict(),
-                "world": self.comm.world, "rank": self.comm.rank}
+                "world": self.comm.world, "rank": self.comm.rank, "retries_all_alive": retries}
 
     def _finish(self) -> None:
         c = self.cfg

@@ -1,0 +1,255 @@
+"""CPU tests of the N>1 bench plumbing (VERDICT r3 "make the N>1 bench unkillable"):
+
+* parallel/selflaunch.py - ``python bench.py --gpus N`` without a launcher spawns its own N
+  ranks (children, never an exec), relays rank 0's JSON line and, when a rank fails, returns
+  non-zero with that rank's stderr tail and terminates the ranks still waiting on it;
+* parallel/autotune.py - the start-up A/B is fault-contained: an RCCL communicator whose init
+  raises (monkeypatched ``RcclComm``) is listed as failed with its reason and the A/B still picks
+  the fastest xGMI path; an xGMI wait failure across an epoch boundary fails only its candidate;
+  every candidate is timed inside one epoch with the window's shape.
+"""
+import io
+import json
+import os
+import sys
+import textwrap
+import time
+
+import pytest
+import torch
+
+from distributed_neural_network_amd.parallel import autotune, selflaunch
+from distributed_neural_network_amd.parallel.comm import CommError
+from distributed_neural_network_amd.parallel.sync import StepAllReduce
+from distributed_neural_network_amd.runtime.cursor import EpochCursor
+
+STUB = textwrap.dedent("""
+    import json, os, sys, time
+    r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1" and os.environ["DNN_STORE_EXTERNAL"] == "1"
+    mode = sys.argv[1]
+    print(f"rank {r} of {n} starting", file=sys.stderr, flush=True)
+    if mode == "fail" and r == 1:
+        print("boom: rank 1 fails", file=sys.stderr, flush=True)
+        sys.exit(3)
+    if mode == "fail":
+        time.sleep(120)  # stuck on the dead peer: the launcher must end it
+    if r == 0:
+        print("banner that is not json")
+        print(json.dumps({"metric": "m", "value": 1.5, "n_gpus": n}))
+""")
+
+
+def _stub(tmp_path):
+    p = tmp_path / "stub.py"
+    p.write_text(STUB)
+    return str(p)
+
+
+def test_launcher_present():
+    assert not selflaunch.launcher_present({})
+    assert selflaunch.launcher_present({"WORLD_SIZE": "4"})
+    assert selflaunch.launcher_present({"OMPI_COMM_WORLD_SIZE": "2"})
+    assert not selflaunch.launcher_present({"WORLD_SIZE": ""})
+
+
+def test_spawn_and_relay(tmp_path, monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    r, w = os.pipe()
+    err = io.StringIO()
+    rc = selflaunch.run([sys.executable, _stub(tmp_path), "ok"], 3, out_fd=w, err=err)
+    os.close(w)
+    out = os.read(r, 1 << 16).decode()
+    os.close(r)
+    assert rc == 0, err.getvalue()
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1 and json.loads(lines[0]) == {"metric": "m", "value": 1.5, "n_gpus": 3}
+    log = err.getvalue()
+    assert "[r1] rank 1 of 3 starting" in log and "[r2] rank 2 of 3 starting" in log
+    assert "banner that is not json" not in out
+
+
+def test_failed_rank_reports_and_ends_the_job(tmp_path):
+    r, w = os.pipe()
+    err = io.StringIO()
+    t0 = time.time()
+    rc = selflaunch.run([sys.executable, _stub(tmp_path), "fail"], 2, out_fd=w, err=err, grace_s=1.0)
+    os.close(w)
+    out = os.read(r, 1 << 16).decode()
+    os.close(r)
+    assert rc == 3, err.getvalue()
+    assert out == ""
+    log = err.getvalue()
+    assert "rank 1 (exit code 3) stderr tail" in log and "boom: rank 1 fails" in log
+    assert "terminating" in log
+    assert time.time() - t0 < 60  # rank 0 (sleeping 120 s) was terminated after the grace
+
+
+# ---- A/B fault containment ------------------------------------------------------------------
+
+
+class _Comm:
+    backend, distributed, rank, world, generation = "nccl", True, 0, 1, 0
+    native = None
+
+    def gather_scalars(self, x):
+        return [float(x)]
+
+    def reduce_scalar(self, x, op="max"):
+        return float(x)
+
+    def barrier(self):
+        pass
+
+
+class _Group:
+    def __init__(self, mode):
+        self.xp_mode, self.one_launch = mode, True
+
+
+class XgmiGradSync:  # (named like the real one: StepAllReduce.installed reads the class name)
+    fuses_sgd = True
+
+    def __init__(self, mode, cost_s, fail=False):
+        self.group, self.cost, self.fail = _Group(mode), cost_s, fail
+
+    def failed(self):
+        return self.fail
+
+
+class _Engine:
+    device = torch.device("cpu")
+
+    def __init__(self):
+        self.master = torch.arange(8, dtype=torch.float32)
+        self.mom = torch.zeros(8)
+        self.grad_sync = None
+        self.windows = []  # (steps left in the epoch when a window of run_steps started)
+        self.epochs = 0
+        self.exact = set()
+
+    def params_changed(self):
+        pass
+
+    def epoch_stats(self, reset=True):
+        return None
+
+    def begin_epoch(self, order):
+        self.epochs += 1
+
+    def prepare_graphs(self, exact=()):
+        self.exact = set(exact)
+
+    def run_steps(self, n):
+        gs = self.grad_sync
+        time.sleep(n * (0.0002 + (gs.cost if gs is not None else 0.0)))
+        self.master.add_(1.0)  # training moves the parameters: the A/B must restore them
+
+
+class _Sampler:
+    def __init__(self, steps):
+        self.n = steps
+
+    def steps(self, batch):
+        return self.n
+
+    def order(self, epoch):
+        return list(range(self.n))
+
+
+class _Policy(StepAllReduce):
+    """The real install() (RCCL paths included); only the xGMI group build is faked."""
+    COST = {0: 0.0003, 2: 0.0006}
+    FAIL = ()
+
+    def _install_xgmi(self, engine, mode):
+        engine.grad_sync = XgmiGradSync(mode, self.COST[mode], fail=mode in self.FAIL)
+        return True
+
+
+def _ab(policy, engine, spe=40, **kw):
+    cur = EpochCursor(engine, _Sampler(spe), policy, 16)
+    return autotune.allreduce_ab(policy, engine, cur, steps=8, warmup=2, reps=2, **kw), cur
+
+
+def test_ab_contains_an_rccl_init_failure(monkeypatch):
+    from distributed_neural_network_amd.parallel import rccl
+
+    class Boom:
+        def __init__(self, comm):
+            raise CommError("ncclCommInitRankConfig did not finish within 60 s")
+
+    monkeypatch.setattr(rccl, "RcclComm", Boom)
+    eng, pol = _Engine(), _Policy(_Comm())
+    start = eng.master.clone()
+    res, _ = _ab(pol, eng, candidates=autotune.ORDER)
+    assert res["allreduce"] == "xgmi-pull" and pol.path == "xgmi-pull", res
+    assert "rccl" in res["failed"] and "rccl-overlap" in res["failed"], res
+    assert "CommError" in res["why"]["rccl"] and "60 s" in res["why"]["rccl"], res
+    assert res["allreduce_ab"]["xgmi-pull"] < res["allreduce_ab"]["xgmi-rsag"], res
+    assert res["allreduce_ab"]["rccl"] is None
+    assert torch.equal(eng.master, start), "parameters not restored"
+    assert pol.comm.native is None
+
+
+def test_ab_wait_failure_across_epoch_boundaries_fails_only_its_candidate():
+    """a failing candidate's error vote at an epoch end must not escape the A/B."""
+    eng, pol = _Engine(), _Policy(_Comm())
+    pol.FAIL = (2,)  # the two-hop exchange's waits fail
+    pol.lazy_check = False
+    res, cur = _ab(pol, eng, spe=11, candidates=("xgmi-pull", "xgmi-rsag"))  # 11 < 2 + 8 + 2: boundaries
+    assert res["failed"] == ["xgmi-rsag"] and "wait failed" in res["why"]["xgmi-rsag"], res
+    assert res["allreduce"] == "xgmi-pull"
+    assert pol.lazy_check is False  # restored
+    assert cur.epoch > 1
+
+
+def test_ab_times_inside_one_epoch_with_an_exact_graph():
+    eng, pol = _Engine(), _Policy(_Comm())
+    seen = []
+    orig = EpochCursor.run
+
+    def run(self, k):
+        if k == 8:
+            seen.append((self.left, set(eng.exact)))
+        return orig(self, k)
+
+    EpochCursor.run = run
+    try:
+        res, _ = _ab(pol, eng, spe=40, candidates=("xgmi-pull",))
+    finally:
+        EpochCursor.run = orig
+    assert res["allreduce"] == "xgmi-pull"
+    assert seen and all(left >= 8 and 8 in exact for left, exact in seen), seen
+
+
+def test_ab_no_path_at_all_falls_back_to_the_policy_default(monkeypatch):
+    """Every candidate failing is not fatal to the A/B itself: the policy's own attach runs."""
+    eng = _Engine()
+
+    class P(_Policy):
+        def install(self, engine, name):
+            if name == "local":
+                return super().install(engine, name)
+            raise RuntimeError(f"{name} broken")
+
+        def attach(self, engine):
+            engine.grad_sync = None
+            self.attached = True
+
+    pol = P(_Comm())
+    res, _ = _ab(pol, eng, candidates=("xgmi-pull", "rccl"))
+    assert res["failed"] == ["rccl", "xgmi-pull"] and getattr(pol, "attached", False), res
+    assert "broken" in res["why"]["rccl"]
+
+
+@pytest.mark.parametrize("n", [2])
+def test_bench_refuses_nothing_without_launcher(n):
+    """bench.py no longer exits at --gpus N>1 without torchrun: it self-launches (source check;
+    the GPU run itself is tools/gpu_run.sh rehearse2)."""
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    assert "needs torchrun" not in src
+    i_launch = src.index("selflaunch.run(")
+    i_gpu = src.index("torch.cuda.set_device")
+    assert i_launch < i_gpu  # children are spawned before the first GPU call

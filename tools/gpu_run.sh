@@ -1,0 +1,63 @@
+#!/usr/bin/env bash
+# One parameterised GPU-box runner (replaces the per-session tools/gpu_r*.sh one-offs).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu_run.sh OUT step [step ...]
+#
+# Every step runs under its own `timeout -k 10`, output goes to gpurun_out/OUT/<step>.*, and
+# the first failing step ends the call (set -e: no GPU work after a fault / abort / timeout).
+# Steps:
+#   smoke            __graft_entry__.smoke()
+#   tests            the whole GPU suite (pytest -m gpu, per-test timeout)
+#   tests:<expr>     GPU tests selected by -k <expr>
+#   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
+#   k20f32           the same, --dtype fp32
+#   long | long32    bench.py default window (5000 / 500), bf16 / fp32
+#   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
+#   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
+#   phase | phase32  per-phase timeline of the fused kernels (tools/phase_trace*.py)
+#   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
+#   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
+#   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
+set -e
+O=gpurun_out/${1:?usage: gpu_run.sh OUT step...}
+shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+stamp() { echo "[gpu_run $(date +%H:%M:%S)] $*"; }
+for s in "$@"; do
+  stamp "step $s"
+  case "$s" in
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+             > "$O/tests.log" 2>&1 ;;
+    tests:*) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+             -k "${s#tests:}" > "$O/tests_k.log" 2>&1 ;;
+    k20|k20b) timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
+    long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
+    prof|prof32)
+      dt=bf16; [ "$s" = prof32 ] && dt=fp32
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d "$O/$s" -o run -- \
+        python3 bench.py --dtype $dt --steps 2000 --warmup 200 --no-epoch > "$O/$s.log" 2>&1
+      db=$(find "$O/$s" -name '*.db' | head -n 1 || true)
+      [ -n "$db" ] && python tools/kstats.py "$db" --steps 2200 > "$O/${s}_kernel_stats.txt" 2>&1 || true ;;
+    pmc:*)
+      c="${s#pmc:}"; n=$(echo "$c" | tr ',' '_' | cut -c1-60)
+      timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- \
+        python3 bench.py --steps 200 --warmup 20 --no-epoch > "$O/pmc_$n.log" 2>&1 ;;
+    phase) timeout -k 10 300 python tools/phase_trace.py > "$O/phase.txt" 2>&1 ;;
+    phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
+    rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
+                 > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;
+    fault2) timeout -k 10 400 python tools/fault_bench.py -n 2 --share-gpu > "$O/fault2.json" 2> "$O/fault2.log" ;;
+    fault4) timeout -k 10 400 python tools/fault_bench.py -n 4 --share-gpu > "$O/fault4.json" 2> "$O/fault4.log" ;;
+    sweep:*)
+      for b in $(echo "${s#sweep:}" | tr ',' ' '); do
+        timeout -k 10 200 python bench.py --batch-size "$b" --steps 2000 --warmup 200 --no-epoch \
+          > "$O/sweep_b$b.json" 2> "$O/sweep_b$b.err"
+      done ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  stamp "done $s"
+done
