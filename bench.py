@@ -284,6 +284,8 @@ def main():
                           if args.model == "lenet" else args.model,
                           "engine": type(engine).__name__,
                           "early_mlp": getattr(engine, "early_mlp", False) or "off",
+                          # pipelined step: step k's reduction + SGD in step k+1's launch (lenet_fused.hip PIPE)
+                          "pipelined_step": bool(getattr(engine, "_pipe_ok", lambda: False)()),
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",

@@ -50,6 +50,10 @@ static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
 // reduction's arguments here and the next fused_train(inlaunch=1) runs them as extra workgroups
 static dnn::ReduceArgs g_pending_mlp{}, g_pending_conv{};
 static bool g_pending_mlp_set = false, g_pending_conv_set = false;
+// pipelined step: grad_reduce(defer=2) stores the previous step's reduction for the next
+// fused_train_pipe launch
+static dnn::ReduceArgs g_pending_pipe{};
+static bool g_pending_pipe_set = false;
 
 PYBIND11_MODULE(_dnn_hip, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
@@ -68,7 +72,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("fused_train",
         [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
            u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage, u rowg,
-           u rowg_ctr, int inlaunch) {
+           u rowg_ctr, int inlaunch, u codes) {
           // inlaunch 1: the MLP reduction in-launch (conv reduction: its own launch after);
           // 2: both (the whole step in one launch) - from the grad_reduce(defer=1) calls before
           if (inlaunch && !(g_pending_mlp_set && (inlaunch == 1 || g_pending_conv_set)))
@@ -81,13 +85,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
                                   P<long long>(stamps), P<const int32_t>(next_ids), P<unsigned char>(stage),
-                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red, redc);
+                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red, redc,
+                                  P<uint8_t>(codes));
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0,
-        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch") = 0);
+        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch") = 0, py::arg("codes") = 0);
   m.def("fused_train_f32", [](u images, u labels, u order, int order_len, int batch, u state, u master, u a0, u h1,
                               u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
     dnn::launch_fused_train_f32(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), order_len,
@@ -112,7 +117,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
                           u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode,
-                          u xp_wait, u rg, u rg_ctr, u rg_err, double rg_timeout_s, int defer) {
+                          u xp_wait, u rg, u rg_ctr, u rg_err, double rg_timeout_s, int defer, u bk_bv_in,
+                          u bk_bv_out, int bk_adv, int bk_stats) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
                       P<const int32_t>(correct), batch, P<float>(master), P<float>(grad), P<float>(mom),
@@ -120,6 +126,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
                       P<int32_t>(batch_ids), lr, momentum, grad_scale, fuse_sgd, lo, hi, bookkeeping,
                       P<long long>(stamps)};
     a.next_ids = P<int32_t>(next_ids);
+    a.bk_bv_in = P<const int32_t>(bk_bv_in);
+    a.bk_bv_out = P<int32_t>(bk_bv_out);
+    if (bk_adv < 0 || bk_adv > 1) throw std::runtime_error("grad_reduce: bk_adv is 0 or 1");
+    a.bk_adv = bk_adv;
+    a.bk_stats = bk_stats;
     a.rg = P<const unsigned long long>(rg);
     a.rg_ctr = P<unsigned>(rg_ctr);
     a.rg_err = P<unsigned>(rg_err);
@@ -151,6 +162,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
       a.xp_ag_off = dnn::xgmi_ag_off(xp_capacity);
       a.xp_wait = P<unsigned long long>(xp_wait);
     }
+    if (defer == 2) {  // (pipelined step) kept for the next fused_train_pipe launch
+      g_pending_pipe = a;
+      g_pending_pipe_set = true;
+      return;
+    }
     if (defer) {  // (in-launch reduction) kept for the next fused_train(inlaunch=1) launch
       if (lo == dnn::OFF_F1W) { g_pending_mlp = a; g_pending_mlp_set = true; }
       else if (lo == 0 && hi == dnn::OFF_F1W) { g_pending_conv = a; g_pending_conv_set = true; }
@@ -167,7 +183,34 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
      py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0, py::arg("xp_wait") = 0,
      py::arg("rg") = 0, py::arg("rg_ctr") = 0, py::arg("rg_err") = 0, py::arg("rg_timeout_s") = 10.0,
-     py::arg("defer") = 0);
+     py::arg("defer") = 0, py::arg("bk_bv_in") = 0, py::arg("bk_bv_out") = 0, py::arg("bk_adv") = 1,
+     py::arg("bk_stats") = 1);
+  // the pipelined step's merged launch (lenet_fused.hip PIPE): the reduction of the previous
+  // step (the last grad_reduce(defer=2) call) + this step's samples
+  m.def("fused_train_pipe", [](u images, u labels, int order_len, int batch, u master, u shadow, u a0, u h1, u h2,
+                               u z1, u z2, u z3, u slab, u loss, u correct, u next_ids, u stage, u ctr, int par,
+                               int wait, int nred, u bvalid, u err, double timeout_s, u stream, u stamps) {
+    if (!g_pending_pipe_set) throw std::runtime_error("fused_train_pipe needs a grad_reduce(defer=2) call first");
+    g_pending_pipe_set = false;
+    dnn::PipeCtl pc;
+    pc.ctr = P<unsigned>(ctr);
+    pc.par = par;
+    pc.wait = wait;
+    pc.nred = nred;
+    pc.bvalid = P<const int32_t>(bvalid);
+    pc.err = P<unsigned>(err);
+    pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
+    dnn::launch_fused_train_pipe(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
+                                 P<const float>(master), P<const bf16>(shadow), P<float>(a0), P<float>(h1),
+                                 P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
+                                 P<float>(loss), P<int32_t>(correct), P<long long>(stamps), P<const int32_t>(next_ids),
+                                 P<unsigned char>(stage), g_pending_pipe, pc, S(stream));
+  }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"),
+     py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
+     py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("next_ids"), py::arg("stage"), py::arg("ctr"),
+     py::arg("par"), py::arg("wait"), py::arg("nred"), py::arg("bvalid"), py::arg("err"), py::arg("timeout_s"),
+     py::arg("stream"), py::arg("stamps") = 0);
+  m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {

@@ -58,6 +58,29 @@ struct ReduceArgs {
   unsigned* rg_ctr = nullptr;
   unsigned* rg_err = nullptr;
   long long rg_timeout_ticks = 0;
+  // Bookkeeping slots (null: the serial layout - bvalid in state[ST_BVALID], ids in next_ids).
+  // The pipelined step (lenet_fused.hip, PIPE) publishes one launch ahead into the other of
+  // two {bvalid, next_ids} slots: bk_bv_in = bvalid of the step whose statistics this launch
+  // adds (read before anything is published), bk_bv_out / next_ids = the slot published,
+  // bk_adv = how far the cursor advances (1; 0 re-publishes the current step's slot: the
+  // launch that ends a pipelined chunk), bk_stats = 0: publish only (no step was reduced).
+  const int32_t* bk_bv_in = nullptr;
+  int32_t* bk_bv_out = nullptr;
+  int bk_adv = 1, bk_stats = 1;
+};
+
+// The pipelined step's per-launch control (lenet_fused.hip, PIPE): launch i of a chunk runs
+// the batch reduction + SGD of step i - 1 (its rows in the other parity buffer set) in its
+// first workgroups and the samples of step i in the rest; the samples wait for the reduction's
+// ready counters before they load the weights it writes.
+struct PipeCtl {
+  unsigned* ctr = nullptr;        // [2 parities][conv, mlp] ready counters (agent-scope adds)
+  int par = 0;                    // this launch's parity (launch index & 1)
+  int wait = 0;                   // 1: a reduction runs in this launch, wait for its counters
+  int nred = 0;                   // reduction blocks of this launch (0, 1 = bookkeeping only, all)
+  const int32_t* bvalid = nullptr;  // this launch's samples' valid count (its bookkeeping slot)
+  unsigned* err = nullptr;          // sticky error word: a ready wait timed out (never a hang)
+  long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
@@ -65,7 +88,16 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream, unsigned long long* rowg = nullptr, unsigned* rowg_ctr = nullptr,
-                        const ReduceArgs* mlp_red = nullptr, const ReduceArgs* conv_red = nullptr);
+                        const ReduceArgs* mlp_red = nullptr, const ReduceArgs* conv_red = nullptr,
+                        uint8_t* codes = nullptr);
+// The pipelined step's merged launch: [reduction of the previous step (red, plain rows of the
+// other parity)] + [samples of this step, writing this parity's rows]; see PipeCtl.
+void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                             const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
+                             float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
+                             const int32_t* next_ids, unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc,
+                             hipStream_t stream);
+int pipe_reduce_blocks();  // reduction blocks of a full PIPE launch (2 per workgroup)
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);

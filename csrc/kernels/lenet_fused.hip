@@ -39,6 +39,7 @@
 namespace dnn {
 
 constexpr int NT = 512;
+constexpr int CODES_PER_SAMPLE = 6 * 196 + 400;  // CODE1 [6][196] | CODE2 [16][25]: 2-bit argmax, 4 = no gradient
 
 // ---- LDS map (bytes) ----------------------------------------------------------------
 constexpr int L_REGA = 0;          // fc1 bf16 [120][400] (A-D) | conv2-bwd scratch (E) | dY1 (F)
@@ -255,8 +256,120 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
   }
 }
 
+// ---- the pipelined step (PIPE) ----------------------------------------------------------
+// Launch i of a pipelined chunk runs step i - 1's batch reduction + momentum SGD in its first
+// workgroups and step i's samples in the rest, so the reduction hides under the samples' phase
+// A (ingest) instead of sitting between two kernel boundaries.  Step i - 1's rows are in the
+// other parity's buffers (written by launch i - 1: visible across the kernel boundary).  The
+// new weights are a hand-off INSIDE the launch (MI355X guide §6 G16, R1): the reduction stores
+// master / bf16 images write-through (sc1), every storing wave drains (vmcnt(0)), a workgroup
+// barrier, then one lane per reduction block adds 1 to its group's ready counter; the samples
+// poll the counter from one lane (a returning atomic add of 0, s_sleep), pass a workgroup barrier
+// and load every weight byte with sc1 loads (buffer loads / LDS-DMA with sc1) - no acquire fence.
+// Reduction blocks in start order: conv slab columns (needed first: phase B), bookkeeping, MLP
+// tiles / bias columns (needed at phase C: the fc1 stream).
+constexpr int PIPE_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
+constexpr int PIPE_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT;
+constexpr int PIPE_BLOCKS = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS + 1;
+static_assert(PIPE_BLOCKS == GRAD_REDUCE_BLOCKS, "the pipelined launch runs the whole grad_reduce");
+int pipe_reduce_blocks() { return PIPE_BLOCKS; }
+
+// Reduction workgroup `wg` of a PIPE launch: two 256-thread reduction blocks.
+__device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
+  const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255;
+  if (wg == 0 && threadIdx.x == 0) {  // the next launch's counters start from zero (kernel boundary)
+    pc.ctr[2 * (pc.par ^ 1)] = 0u;
+    pc.ctr[2 * (pc.par ^ 1) + 1] = 0u;
+  }
+  int grp = -1;  // ready counter this block signals: 0 conv, 1 MLP, -1 none (bookkeeping)
+  if (m < pc.nred) {
+    int rblk = 0;  // (nred == 1: the bookkeeping alone - the launch range holds no elements)
+    if (pc.nred > 1) {
+      if (m < PIPE_CONV_BLOCKS) { rblk = PIPE_MLP_BLOCKS + m; grp = 0; }
+      else if (m == PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS;
+      else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = 1; }
+    }
+    WtSink sk;
+    grad_reduce_body<false>(a, sk, rblk, rtid);
+  }
+  if (stamps != nullptr && threadIdx.x == 0) stamps[16 + 4 * wg + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its write-through stores
+  __syncthreads();
+  if (rtid == 0 && grp >= 0) {
+    if (stamps != nullptr) {  // diagnostic: when the add has been performed
+      const unsigned v = __hip_atomic_fetch_add(pc.ctr + 2 * pc.par + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime() + 0 * v;
+    } else {
+      __hip_atomic_fetch_add(pc.ctr + 2 * pc.par + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// One lane waits until a ready counter reaches `target` (returning-atomic polls).  Bounded: past the
+// timeout it sets the sticky error word and returns (the step then runs on the old weights and
+// the host raises at the next check) - never a hang.
+__device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned target, long long* diag = nullptr) {
+  const unsigned* c = pc.ctr + 2 * pc.par + grp;
+  if (__hip_atomic_load(pc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // failed before: no wait
+  const long long t0 = wall_clock64();
+  if (diag != nullptr) diag[0] = t0;
+  long long polls = 0;
+  // the poll is a returning atomic (add 0): performed where the adds are, never a stale L2 copy
+  // (sc1 load polls of this counter saw its final value ~3 us late: profiles/r4/pipe/)
+  while (__hip_atomic_fetch_add(const_cast<unsigned*>(c), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    ++polls;
+    if (diag != nullptr) diag[1] = polls;
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > pc.timeout_ticks) {
+      __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+// Weight loads: plain, or (WT: the pipelined step) sc1 buffer loads of the write-through bytes
+template <bool WT>
+struct WeightRd {
+  const bf16* sh;
+  const float* ms;
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ WeightRd(const bf16* shadow, const float* master) : sh(shadow), ms(master) {
+    if constexpr (WT) r = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(shadow), 0, SH_TOTAL * 2, 0x00020000);
+  }
+  __device__ __forceinline__ bf16x8 w8(int e) const {  // 8 bf16 at element e (16-B aligned)
+    if constexpr (WT) return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, e * 2, 0, 16));
+    else return *reinterpret_cast<const bf16x8*>(sh + e);
+  }
+  __device__ __forceinline__ bf16x4 w4(int e) const {  // 4 bf16 at element e (8-B aligned)
+    if constexpr (WT) return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(r, e * 2, 0, 16));
+    else return *reinterpret_cast<const bf16x4*>(sh + e);
+  }
+  __device__ __forceinline__ float f(int i) const {  // fp32 master element (biases)
+    if constexpr (WT)
+      return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(ms + i), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT));
+    else return ms[i];
+  }
+};
+
+// LDS-DMA with the sc1 cache policy (the pipelined step's weight streams; see dma16)
+__device__ __forceinline__ void dma16_sc1(const void* gsrc, uint32_t lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+template <bool WT>
+__device__ __forceinline__ void dma_w(const void* gsrc, uint32_t lds_base) {
+  if constexpr (WT) dma16_sc1(gsrc, lds_base);
+  else dma16(gsrc, lds_base);
+}
+
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
-template <bool TRAIN, bool STAGED = false, int RNR = 0>
+// PIPE (TRAIN + STAGED only): the pipelined step's merged launch (above)
+template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -269,11 +382,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
     float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
     long long* __restrict__ stamps,
+    uint8_t* __restrict__ codes_out,       // TRAIN, diagnostic (tests): [batch][6*196 + 400] pool argmax codes
     const int32_t* __restrict__ next_ids,  // TRAIN + stage: sample ids of the NEXT step (-1: none)
     unsigned char* __restrict__ stage,     // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
     unsigned long long* __restrict__ rowg,  // TRAIN, early-MLP overlap: the MLP rows as granules
     unsigned* __restrict__ rowg_ctr,        //   and this block's step counter (common.h RG_ROW)
-    const ReduceArgs ra, const ReduceArgs rc) {  //   and the in-launch reduction: MLP (ra), conv + bookkeeping (rc)
+    const ReduceArgs ra, const ReduceArgs rc,  //   and the in-launch reduction: MLP (ra), conv + bookkeeping (rc)
+    const PipeCtl pc) {                     // PIPE: ra = the previous step's reduction, pc its control
+  static_assert(!PIPE || (TRAIN && STAGED && RNR == 0), "the pipelined step is a staged training launch");
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
@@ -285,6 +401,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (btrace) {
     stamps[16 + 4 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
     stamps[16 + 4 * blockIdx.x + 3] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+  }
+  // PIPE: the first workgroups run the previous step's reduction; the samples follow
+  const int nrw = PIPE ? (pc.nred + 1) / 2 : 0;
+  if constexpr (PIPE) {
+    if ((int)blockIdx.x < nrw) {
+      pipe_reduce(ra, pc, blockIdx.x, stamps);
+      if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+      return;
+    }
   }
   if constexpr (TRAIN) {
     // in-launch reduction: workgroups past the samples reduce the MLP gradient, then the conv
@@ -299,8 +424,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       return;
     }
   }
-  // diagnostic phase timeline (block 0, thread 0): s_memrealtime ticks (100 MHz)
-  const bool stamp = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  // diagnostic phase timeline (sample block 0, thread 0): s_memrealtime ticks (100 MHz)
+  const bool stamp = stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0;
 #define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
   STAMP(0);
   const int tid = threadIdx.x;
@@ -308,7 +433,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int wave = tid >> 6;
   const int fr = lane & 15;   // MFMA fragment row/col within the 16-tile
   const int fg = lane >> 4;   // MFMA k-group (0..3)
-  const int b = blockIdx.x;
+  const int b = (int)blockIdx.x - nrw;
+  const WeightRd<PIPE> wr(shadow, master);
 
   // TRAIN: the sample ids and valid count of this step were published by the previous
   // step's reduce kernel (begin_epoch for the first step): one dependent load level less
@@ -327,7 +453,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     } else {
       sample = order[b];  // `order` = the published batch ids [batch]
     }
-    bvalid = state[ST_BVALID];
+    bvalid = PIPE ? *pc.bvalid : state[ST_BVALID];  // (PIPE: this launch's bookkeeping slot)
     valid = b < bvalid;
   } else {
     const long gidx = (long)base_index + b;
@@ -409,12 +535,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if constexpr (staged) im = st_im;
   else im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
+  float bias_c1 = 0.f, bias_c2 = 0.f;
+  auto load_conv_w = [&]() {
 #pragma unroll
-  for (int sk = 0; sk < 4; ++sk) bw1[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W1F)[(4 * sk + fg) * 16 + fr];
+    for (int sk = 0; sk < 4; ++sk) bw1[sk] = wr.w8(SH_W1F + ((4 * sk + fg) * 16 + fr) * 8);
 #pragma unroll
-  for (int sk = 0; sk < 8; ++sk) bw2[sk] = reinterpret_cast<const bf16x8*>(shadow + SH_W2F)[(4 * sk + fg) * 16 + fr];
-  float bias_c1 = master[OFF_C1B + min(fr, 5)];
-  float bias_c2 = master[OFF_C2B + fr];
+    for (int sk = 0; sk < 8; ++sk) bw2[sk] = wr.w8(SH_W2F + ((4 * sk + fg) * 16 + fr) * 8);
+    bias_c1 = wr.f(OFF_C1B + min(fr, 5));
+    bias_c2 = wr.f(OFF_C2B + fr);
+  };
+  if constexpr (PIPE) {
+    // the conv weights are the previous step's reduction's: one lane waits for its conv
+    // blocks; the barrier below releases the other waves, whose loads follow it
+    if (pc.wait && tid == 0) pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr);
+    STAMP(12);
+  } else {
+    load_conv_w();
+  }
   for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = (bf16)0.f;
   if (tid < 16) A0B[400 + tid] = (bf16)0.f;                                   // MLP operand padding
   else if (tid < 24) H1B[120 + tid - 16] = (bf16)0.f;
@@ -425,6 +562,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
   lds_barrier();
   STAMP(9);
+  if constexpr (PIPE) load_conv_w();  // (sc1: written in this launch, ready since the barrier)
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
 #pragma unroll
   for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
@@ -433,17 +571,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   consume(bias_c1);
   consume(bias_c2);
   STAMP(11);
-  {
-    // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all
-    // in-arena); 12 per wave with the index clamped (a duplicate copies identical bytes)
+  // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all in-arena);
+  // 12 per wave with the index clamped (a duplicate copies identical bytes).  Issued here, or
+  // (PIPE) once the MLP reduction is ready, at the start of phase C
+  auto stream_fc1 = [&]() {
     const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
       const int i = min(wave + 8 * k, 93);
-      dma16(f1src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
+      dma_w<PIPE>(f1src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
     }
-  }
+  };
+  if constexpr (!PIPE) stream_fc1();
   lds_barrier();
   STAMP(1);
 
@@ -502,7 +642,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       if (four) epilogue(48, acc3);
     }
   }
+  if constexpr (PIPE) {
+    if (pc.wait && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS);  // the MLP weights (released by the barrier)
+    STAMP(13);
+  }
   lds_barrier();
+  if constexpr (PIPE) stream_fc1();  // first, so the fragment loads below are waited for after it
 
   STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============
@@ -511,25 +656,25 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int ncol = 16 * wave + fr;
   bf16x8 w2f[4], w2t[3], w3t, w3f[3];
   {
-    const bf16* r2 = shadow + OFF_F2W + min(ncol, 83) * 120;             // fc2 row (forward)
+    const int r2 = OFF_F2W + min(ncol, 83) * 120;             // fc2 row (forward)
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) w2f[ks] = *reinterpret_cast<const bf16x8*>(r2 + 32 * ks + 8 * fg);
-    const bf16* t2 = shadow + SH_W2T + min(ncol, 119) * 96;               // fc2^T row (dgrad)
+    for (int ks = 0; ks < 4; ++ks) w2f[ks] = wr.w8(r2 + 32 * ks + 8 * fg);
+    const int t2 = SH_W2T + min(ncol, 119) * 96;               // fc2^T row (dgrad)
 #pragma unroll
-    for (int ks = 0; ks < 3; ++ks) w2t[ks] = *reinterpret_cast<const bf16x8*>(t2 + 32 * ks + 8 * fg);
-    w3t = *reinterpret_cast<const bf16x8*>(shadow + SH_W3T + min(ncol, 83) * 16 + 8 * fg);  // fc3^T (dgrad)
-    const bf16* r3 = shadow + OFF_F3W + min(fr, 9) * 84;                  // fc3 row (forward; 8-B aligned)
+    for (int ks = 0; ks < 3; ++ks) w2t[ks] = wr.w8(t2 + 32 * ks + 8 * fg);
+    w3t = wr.w8(SH_W3T + min(ncol, 83) * 16 + 8 * fg);         // fc3^T (dgrad)
+    const int r3 = OFF_F3W + min(fr, 9) * 84;                  // fc3 row (forward; 8-B aligned)
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
-      const bf16x4 lo = *reinterpret_cast<const bf16x4*>(r3 + 32 * ks + 8 * fg);
-      const bf16x4 hi = *reinterpret_cast<const bf16x4*>(r3 + 32 * ks + 8 * fg + 4);
+      const bf16x4 lo = wr.w4(r3 + 32 * ks + 8 * fg);
+      const bf16x4 hi = wr.w4(r3 + 32 * ks + 8 * fg + 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { w3f[ks][j] = lo[j]; w3f[ks][4 + j] = hi[j]; }
     }
   }
-  float bias_f1 = master[OFF_F1B + min(ncol, 119)];
-  float bias_f2 = master[OFF_F2B + min(ncol, 83)];
-  float bias_f3 = master[OFF_F3B + min(fr, 9)];
+  float bias_f1 = wr.f(OFF_F1B + min(ncol, 119));
+  float bias_f2 = wr.f(OFF_F2B + min(ncol, 83));
+  float bias_f3 = wr.f(OFF_F3B + min(fr, 9));
   if (tid < 168) {  // window records of P1 rows (overwrite R1: dead until phase F); 2 threads per row
     const int row = tid >> 1, h = tid & 1;  // row = c*14 + y; half h builds records 7h .. 7h+6 (< 13)
     bf16 v[14];
@@ -598,7 +743,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int i = min(wave + 8 * k, 19);
-      dma16(src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
+      dma_w<PIPE>(src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
     }
   }
   {  // fc1: h1 = relu(W1 a0 + b1), 120 x 400; wave w -> output tile w
@@ -999,6 +1144,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       rg_put(rowg, lc + 1, row_tag, __int_as_float(my_correct));
     }
   }
+  if (codes_out != nullptr) {  // the ReLU + max-pool decisions of this sample (mask-aware oracle tests)
+    for (int i = tid; i < CODES_PER_SAMPLE; i += NT)
+      codes_out[(size_t)b * CODES_PER_SAMPLE + i] = i < 6 * 196 ? CODE1[i] : CODE2[i - 6 * 196];
+  }
   if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1019,7 +1168,7 @@ void init_kernels() {
   const void* kerns[] = {(const void*)lenet_fused_kernel<true, false, 0>, (const void*)lenet_fused_kernel<true, true, 0>,
                          (const void*)lenet_fused_kernel<true, false, 1>, (const void*)lenet_fused_kernel<true, true, 1>,
                          (const void*)lenet_fused_kernel<true, false, 8>, (const void*)lenet_fused_kernel<true, true, 8>,
-                         (const void*)lenet_fused_kernel<false, false, 0>};
+                         (const void*)lenet_fused_kernel<false, false, 0>, (const void*)lenet_fused_kernel<true, true, 0, true>};
   for (const void* k : kerns) HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   init_kernels_f32();
   done = true;
@@ -1030,7 +1179,7 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream, unsigned long long* rowg, unsigned* rowg_ctr, const ReduceArgs* mlp_red,
-                        const ReduceArgs* conv_red) {
+                        const ReduceArgs* conv_red, uint8_t* codes) {
   init_kernels();
   if (stage != nullptr && next_ids == nullptr) throw std::runtime_error("fused_train: staging needs next_ids");
   if ((rowg == nullptr) != (rowg_ctr == nullptr)) throw std::runtime_error("fused_train: row granules need their counters");
@@ -1059,8 +1208,32 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                : rnr == 1 ? (stage ? &lenet_fused_kernel<true, true, 1> : &lenet_fused_kernel<true, false, 1>)
                           : (stage ? &lenet_fused_kernel<true, true, 8> : &lenet_fused_kernel<true, false, 8>);
   hipLaunchKernelGGL(kern, dim3(batch + red_wg), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len,
-                     batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, next_ids,
-                     stage, rowg, rowg_ctr, ra, rc);
+                     batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, codes,
+                     next_ids, stage, rowg, rowg_ctr, ra, rc, PipeCtl{});
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                             const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
+                             float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
+                             const int32_t* next_ids, unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc,
+                             hipStream_t stream) {
+  init_kernels();
+  // the shapes the kernel assumes: every reduction block of a full launch (conv first), or the
+  // bookkeeping alone; staged images; a ready wait only behind a full reduction
+  if (stage == nullptr || next_ids == nullptr || pc.bvalid == nullptr || pc.ctr == nullptr || pc.err == nullptr)
+    throw std::runtime_error("fused_train_pipe: needs the stage, its next_ids / bvalid slot, the counters and error word");
+  if (!(pc.nred == PIPE_BLOCKS || pc.nred == 1) || (pc.wait && pc.nred != PIPE_BLOCKS) || (pc.par & ~1))
+    throw std::runtime_error("fused_train_pipe: nred must be the whole reduction or the bookkeeping alone");
+  if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || red.rg != nullptr || !red.fuse_sgd)
+    throw std::runtime_error("fused_train_pipe: a local fused-SGD reduction with bookkeeping of this batch");
+  if (pc.nred == PIPE_BLOCKS ? !(red.lo == 0 && red.hi >= ARENA) : !(red.lo == OFF_F1W && red.hi == OFF_F1W))
+    throw std::runtime_error("fused_train_pipe: whole-arena reduction, or an empty range for the bookkeeping alone");
+  if (batch < 1 || batch > 1024) throw std::runtime_error("fused_train_pipe: batch out of range");
+  const int nrw = (pc.nred + 1) / 2;
+  hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true>), dim3(nrw + batch), dim3(NT), LDS_TOTAL, stream, images,
+                     labels, nullptr, order_len, batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab,
+                     loss, correct, stamps, nullptr, next_ids, stage, nullptr, nullptr, red, ReduceArgs{}, pc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1071,8 +1244,8 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     ReduceArgs{}, ReduceArgs{});
+                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     ReduceArgs{}, ReduceArgs{}, PipeCtl{});
   HIP_CHECK(hipGetLastError());
 }
 

@@ -6,16 +6,62 @@
 
 namespace dnn {
 
+// The pipelined step's reduction (lenet_fused.hip, PIPE): the new parameters and their bf16
+// images are stored WRITE-THROUGH (sc1), because the sample workgroups of the same launch load
+// them (sc1 loads) once the storing block has drained its stores and added to its ready counter
+// (MI355X guide §6 G16 R1).  The momentum is read by the next launch only: plain stores.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(bf16* p, bf16 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned short*>(p), __builtin_bit_cast(unsigned short, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// write_shadow (common.h) with write-through stores: the same positions, the same values
+__device__ __forceinline__ void write_shadow_wt(bf16* __restrict__ sh, int e, float p) {
+  const bf16 v = (bf16)p;
+  st_wt(sh + e, v);
+  if (e >= OFF_C1W && e < OFF_C1W + 450) {
+    const int r = e - OFF_C1W, n = r / 75, rem = r - 75 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
+    st_wt(sh + SH_W1F + ((c * 5 + ky) * 16 + n) * 8 + kx, v);
+  } else if (e >= OFF_C2W && e < OFF_C2W + 2400) {
+    const int r = e - OFF_C2W, n = r / 150, rem = r - 150 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
+    st_wt(sh + SH_W2F + ((c * 5 + ky) * 16 + n) * 8 + kx, v);
+    st_wt(sh + SH_WF + (((4 - ky) * 16 + n) * 16 + c) * 8 + (4 - kx), v);
+  } else if (e >= OFF_F2W && e < OFF_F2W + 10080) {
+    const int r = e - OFF_F2W, o = r / 120, i = r - 120 * o;
+    st_wt(sh + SH_W2T + i * 96 + o, v);
+  } else if (e >= OFF_F3W && e < OFF_F3W + 840) {
+    const int r = e - OFF_F3W, o = r / 84, i = r - 84 * o;
+    st_wt(sh + SH_W3T + i * 16 + o, v);
+  }
+}
+
+__device__ __forceinline__ bool is_bias(int e) {
+  return (e >= OFF_C1B && e < OFF_C1B + 6) || (e >= OFF_C2B && e < OFF_C2B + 16) || (e >= OFF_F1B && e < OFF_F1B + 120) ||
+         (e >= OFF_F2B && e < OFF_F2B + 84) || (e >= OFF_F3B && e < OFF_F3B + 10);
+}
+
 // SGD epilogue with the master/momentum values already in registers (prefetched
 // together with the gradient operands, so the update costs no extra memory latency).
+// WT: write-through parameter / image stores (the pipelined step).
+template <bool WT = false>
 __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_old, const ReduceArgs& a) {
   g *= a.grad_scale;
   if (a.fuse_sgd) {
     float p, m;
     sgd_update(g, p_old, m_old, a.lr, a.momentum, p, m);
     a.mom[e] = m;
-    a.master[e] = p;
-    write_shadow(a.shadow, e, p);
+    if constexpr (WT) {
+      // the samples read the biases from the fp32 master, every weight from the bf16 images:
+      // only those bytes go write-through; the rest of master is read by the next launch
+      if (is_bias(e)) st_wt(a.master + e, p);
+      else a.master[e] = p;
+      write_shadow_wt(a.shadow, e, p);
+    } else {
+      a.master[e] = p;
+      write_shadow(a.shadow, e, p);
+    }
   } else {
     a.grad[e] = g;
   }
@@ -23,15 +69,19 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
 
 // Where a lane's reduced elements go (at most 4 per lane; j is a compile-time index once the
 // callers' loops are unrolled, so the exchange sink's arrays stay in registers).
-//  * DirectSink: finish at once (local SGD step, or gradient output).
+//  * DirectSink: finish at once (local SGD step, or gradient output); WtSink: the same with
+//    write-through stores (the pipelined step's in-launch reduction).
 //  * XpSink (one-launch xGMI all-reduce, reduce_sgd.hip): the gradient goes to this rank's
 //    granule slot now as one 8-byte {value, step} word (system-coherent store); the update
 //    runs after the lane has read the same element from every peer.
-struct DirectSink {
+template <bool WT>
+struct DirectSinkT {
   __device__ __forceinline__ void put(int, int e, float g, float p, float m, const ReduceArgs& a) {
-    sgd_finish(e, g, p, m, a);
+    sgd_finish<WT>(e, g, p, m, a);
   }
 };
+using DirectSink = DirectSinkT<false>;
+using WtSink = DirectSinkT<true>;
 //    PK (bf16 granules, xp_mode bit 4): the lane's elements travel in pairs (0, 1) and (2, 3)
 //    as ONE granule {bf16 | bf16, step} each, published by the exchange once both are known.
 template <bool PK>
@@ -272,7 +322,10 @@ __device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsig
     const int32_t* correct = a.correct;
     float ls = 0.f;
     int cs = 0;
-    for (int b = lane; b < a.batch; b += 64) {
+    // bvalid of the step whose statistics are added: read before any slot is published (the
+    // pipelined step's bk_bv_in and bk_bv_out may be the same word)
+    const int bv = a.bk_bv_in != nullptr ? *a.bk_bv_in : a.state[ST_BVALID];
+    for (int b = lane; b < (a.bk_stats ? a.batch : 0); b += 64) {
       if constexpr (GR) {
         const int lo = (int)rg_off(RG_LCK, a.batch) + RG_LC * b;
         const int off[2] = {lo, lo + 1};
@@ -287,9 +340,8 @@ __device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsig
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
-    const int bv = a.state[ST_BVALID];
-    const int next = a.state[ST_CURSOR] + 1;
-    if (lane == 0 && bv > 0) {
+    const int next = a.state[ST_CURSOR] + a.bk_adv;
+    if (lane == 0 && bv > 0 && a.bk_stats) {
       a.stats[STAT_LOSS] += (double)ls / (double)bv;
       a.stats[STAT_BATCHES] += 1.0;
       a.stats[STAT_CORRECT] += (double)cs;
@@ -312,7 +364,7 @@ __device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsig
     const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
     if (lane == 0) {
       a.state[ST_CURSOR] = next;
-      a.state[ST_BVALID] = nbv;
+      *(a.bk_bv_out != nullptr ? a.bk_bv_out : a.state + ST_BVALID) = nbv;
     }
 }
 

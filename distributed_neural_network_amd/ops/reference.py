@@ -144,3 +144,69 @@ def per_sample_outputs_bf16(shadow: torch.Tensor, master: torch.Tensor, images_u
     z3p[:, :10] = z3
     return {"a0": a0, "h1": h1, "h2": h2, "z1": z1, "z2": z2, "z3": z3p, "slab": slab, "loss": loss,
             "correct": correct, "logits": logits}
+
+
+CODES_PER_SAMPLE = 6 * 196 + 400  # lenet_fused.hip: CODE1 [6][14*14] | CODE2 [16][5*5]
+
+
+def _pool_by_code(c: torch.Tensor, code: torch.Tensor, h: int) -> torch.Tensor:
+    """ReLU + 2x2 max-pool of ``c`` [B, C, 2h, 2h] with the window decisions ``code`` [B, C, h*h]
+    (the pixel index dy * 2 + dx the kernel picked, 4 = max <= 0: output 0, no gradient)."""
+    B, C = c.shape[:2]
+    win = c.reshape(B, C, h, 2, h, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, h * h, 4)
+    idx = code.long().clamp(max=3).unsqueeze(-1)
+    return torch.where(code < 4, win.gather(3, idx).squeeze(-1), torch.zeros(()))
+
+
+def _unpool_by_code(d: torch.Tensor, code: torch.Tensor, h: int) -> torch.Tensor:
+    """Route the pooled gradient ``d`` [B, C, h*h] to the chosen pixel of each window."""
+    B, C = d.shape[:2]
+    out = torch.zeros(B, C, h * h, 4)
+    out.scatter_(3, code.long().clamp(max=3).unsqueeze(-1), (d * (code < 4).float()).unsqueeze(-1))
+    return out.reshape(B, C, h, h, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, 2 * h, 2 * h)
+
+
+def per_sample_outputs_masked(weights: torch.Tensor, master: torch.Tensor, images_u8: torch.Tensor,
+                              labels: torch.Tensor, codes: torch.Tensor, h1_mask: torch.Tensor,
+                              h2_mask: torch.Tensor, bvalid: int | None = None) -> Dict[str, torch.Tensor]:
+    """The fp32 oracle (every operand and accumulator fp32, no rounding) evaluated with the
+    KERNEL'S OWN decisions: its ReLU + max-pool argmax codes (``codes``, written by the fused
+    kernel's diagnostic output) and its fc ReLU masks (h1 > 0, h2 > 0 of its rows).  A near-tie
+    that bf16 operands flip then cannot turn a 1e-3 difference into a 15 % one, so the bf16
+    kernel can be held to ~1e-2 of fp32 per tensor.  ``weights``: the arena the
+    kernel multiplies by (the bf16 shadow as fp32); biases come from ``master``, as in the kernel."""
+    w = LAYOUT.views(weights.detach().float().cpu())
+    bm = LAYOUT.views(master.detach().float().cpu())
+    x = normalize_u8(images_u8.cpu())
+    y = labels.cpu().long()
+    B = x.shape[0]
+    bvalid = B if bvalid is None else bvalid
+    codes = codes.cpu()
+    code1 = codes[:, :6 * 196].reshape(B, 6, 196)
+    code2 = codes[:, 6 * 196:].reshape(B, 16, 25)
+    m1, m2 = h1_mask.cpu().float(), h2_mask.cpu().float()
+    W1, W2 = w["conv1.weight"], w["conv2.weight"]
+    c1 = F.conv2d(x, W1, bm["conv1.bias"])
+    p1 = _pool_by_code(c1, code1, 14).reshape(B, 6, 14, 14)
+    c2 = F.conv2d(p1, W2, bm["conv2.bias"])
+    a0 = _pool_by_code(c2, code2, 5).reshape(B, 400)
+    h1 = F.linear(a0, w["fc1.weight"], bm["fc1.bias"]) * m1
+    h2 = F.linear(h1, w["fc2.weight"], bm["fc2.bias"]) * m2
+    logits = F.linear(h2, w["fc3.weight"], bm["fc3.bias"])
+    loss = F.cross_entropy(logits, y, reduction="none")
+    z3 = (torch.softmax(logits, 1) - F.one_hot(y, 10).float()) / bvalid
+    z2 = (z3 @ w["fc3.weight"]) * m2
+    z1 = (z2 @ w["fc2.weight"]) * m1
+    da0 = z1 @ w["fc1.weight"]
+    dy2 = _unpool_by_code(da0.reshape(B, 16, 25), code2, 5)
+    db2 = dy2.sum((2, 3))
+    dW2 = torch.stack([torch.nn.grad.conv2d_weight(p1[b:b + 1], W2.shape, dy2[b:b + 1]) for b in range(B)])
+    dp1 = torch.nn.grad.conv2d_input(p1.shape, W2, dy2)
+    dy1 = _unpool_by_code(dp1.reshape(B, 6, 196), code1, 14)
+    db1 = dy1.sum((2, 3))
+    dW1 = torch.stack([torch.nn.grad.conv2d_weight(x[b:b + 1], W1.shape, dy1[b:b + 1]) for b in range(B)])
+    slab = torch.cat([dW1.flatten(1), db1, dW2.flatten(1), db2], 1)
+    z3p = torch.zeros(B, 16)
+    z3p[:, :10] = z3
+    return {"a0": a0, "h1": h1, "h2": h2, "z1": z1, "z2": z2, "z3": z3p, "slab": slab, "loss": loss,
+            "logits": logits}

@@ -9,7 +9,8 @@ measures the candidates on the real node, in the real captured step, before the 
 
 * every candidate path (``StepAllReduce.PATHS``) is installed collectively - its own self-test
   included - on the same start parameters;
-* it is timed with EXACTLY the shape of bench.py's timed window: inside one epoch (a fresh one
+* after ``spin`` untimed steps (the GPU's clocks ramp up, as they have before bench.py's window),
+  it is timed with EXACTLY the shape of bench.py's timed window: inside one epoch (a fresh one
   when the rest of the current epoch cannot hold the window), the window's step count as ONE
   exact-size graph replay, ``warmup`` steps right before it, bracketed by barrier + device
   sync on both sides; ``reps`` windows per round, the median per-rank time, MAX over ranks.
@@ -90,8 +91,13 @@ def prepare_window(engine, cur, steps: int, warmup: int) -> None:
             engine.prepare_graphs()
 
 
-def _measure(comm, engine, cur, steps: int, warmup: int, reps: int) -> tuple[float, bool]:
-    """(max-over-ranks us/step, passed on every rank) of the installed path."""
+def _measure(comm, engine, cur, steps: int, warmup: int, reps: int, spin: int) -> tuple[float, bool]:
+    """(max-over-ranks us/step, passed on every rank) of the installed path.  ``spin`` steps run
+    first, untimed: a candidate installed on an idle GPU would otherwise be timed at low clocks
+    (bench.py's window follows the full-test-set evaluation, a clocked-up GPU; the 2-rank
+    rehearsal timed the same path 3.4x slower in the A/B than in the window without this)."""
+    prepare_window(engine, cur, steps, warmup)
+    cur.run(spin)
     times = []
     for _ in range(reps):
         prepare_window(engine, cur, steps, warmup)
@@ -110,7 +116,7 @@ def _agree(comm, ok: bool) -> bool:
 
 def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: int = 2, reps: int = 3,
                  candidates: tuple[str, ...] = ORDER, log: Optional[Callable[[str], None]] = None,
-                 rccl_init_timeout_s: float = 60.0) -> dict:
+                 rccl_init_timeout_s: float = 60.0, spin: int = 200) -> dict:
     """Collective (every rank calls it with the same arguments).  ``cur`` is the run's
     ``EpochCursor``.  Times every candidate, installs the winner on ``engine`` (``policy.path``
     pins it for later re-attaches) and returns {"allreduce_ab": {path: us_per_step | None},
@@ -155,7 +161,7 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
                 restore()
                 passed, us = True, None
                 try:
-                    us, passed = _measure(comm, engine, cur, steps, warmup, reps)
+                    us, passed = _measure(comm, engine, cur, steps, warmup, reps, spin)
                     if not passed:
                         why = "a wait failed during the timed steps"
                 except Exception as e:

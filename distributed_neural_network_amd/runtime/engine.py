@@ -211,7 +211,7 @@ class HipEngine(Engine):
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
                  use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None,
-                 dtype: str = "bf16", early_mlp: bool | None = None) -> None:
+                 dtype: str = "bf16", early_mlp: bool | None = None, pipeline: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if dtype not in ("bf16", "fp32"):
             raise ValueError(f"HipEngine dtype must be bf16 or fp32, not {dtype!r}")
@@ -282,9 +282,31 @@ class HipEngine(Engine):
         if early_mlp and dtype != "bf16":
             raise ValueError("early-MLP overlap is a feature of the bf16 kernel")
         self.early_mlp = early_mlp
+        # Pipelined step (lenet_fused.hip PIPE; bf16, staged images, local step): launch i of a
+        # step chunk runs step i - 1's batch reduction + SGD in its first workgroups and step i's
+        # samples in the rest, which wait (in-launch ready counters) for the new weights before
+        # they load them - the reduction hides under the samples' image ingest, and a chunk of n
+        # steps is n + 1 launches instead of 2 n.  Bit-identical to the serial step (the same
+        # kernels' arithmetic).  Opt-in (DNN_PIPELINE=1) until it measures faster than the serial
+        # step (profiles/r4/pipe_v1/).
+        if pipeline is None:
+            pipeline = os.environ.get("DNN_PIPELINE", "0") != "0"
+        self.pipeline = bool(pipeline) and dtype == "bf16" and stage_images
         self._rg: dict | None = None
         if dtype == "bf16":
             self._rg_buffers()  # (allocated up front: never inside a graph capture)
+        if self.pipeline:
+            # the second parity's per-sample rows (the first is a0 .. correct above), the second
+            # {bvalid, next_ids} bookkeeping slot (bvalid in state[2]), the ready counters
+            # [parity][conv, mlp] and the sticky wait-timeout word
+            self._rows2 = dict(a0=torch.zeros_like(self.a0), h1=torch.zeros_like(self.h1),
+                               h2=torch.zeros_like(self.h2), z1=torch.zeros_like(self.z1),
+                               z2=torch.zeros_like(self.z2), z3=torch.zeros_like(self.z3),
+                               slab=torch.zeros_like(self.slab), loss=torch.zeros_like(self.loss),
+                               correct=torch.zeros_like(self.correct))
+            self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
+            self.pipe_ctr = torch.zeros(4, device=dev, dtype=torch.int32)
+            self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.params_changed()
@@ -375,6 +397,72 @@ class HipEngine(Engine):
 
     def early_failed(self) -> bool:
         return self._rg is not None and int(self._rg["err"].item()) != 0
+
+    def pipe_failed(self) -> bool:
+        return self.pipeline and int(self.pipe_err.item()) != 0
+
+    def _pipe_ok(self) -> bool:
+        """The pipelined step runs: bf16 with staged images, no all-reduce installed (one rank)
+        and no in-launch reduction."""
+        return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
+
+    PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
+    _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
+
+    def _rows(self, par: int) -> dict:
+        if par == 0:
+            return dict(a0=self.a0, h1=self.h1, h2=self.h2, z1=self.z1, z2=self.z2, z3=self.z3, slab=self.slab,
+                        loss=self.loss, correct=self.correct)
+        return self._rows2
+
+    def _launch_steps_pipe(self, n: int) -> None:
+        """n steps as n + 1 launches: launch i (< n) = [step i - 1's reduction] + [step i's
+        samples]; launch n = step n - 1's reduction alone (grad_reduce), which also re-publishes
+        the bookkeeping slot the next chunk's first launch reads (slot 0).  Bookkeeping slots:
+        slot 0 = (state[ST_BVALID], next_ids) - the serial layout epoch_begin writes -, slot 1 =
+        (state[2], next_ids2); launch i's samples read slot i & 1 and its bookkeeping publishes
+        slot (i + 1) & 1 one launch ahead."""
+        s = self._stream()
+        sp = self._p(self.state)
+        slot_bv = (sp + 4, sp + 8)
+        slot_nid = (self._p(self.next_ids), self._p(self.next_ids2))
+        f1w = LAYOUT.offsets["fc1.weight"]
+        for i in range(n + 1):
+            par = i & 1
+            prev = self._rows((i - 1) & 1)
+            red = dict(a0=self._p(prev["a0"]), h1=self._p(prev["h1"]), h2=self._p(prev["h2"]), z1=self._p(prev["z1"]),
+                       z2=self._p(prev["z2"]), z3=self._p(prev["z3"]), slab=self._p(prev["slab"]),
+                       loss=self._p(prev["loss"]), correct=self._p(prev["correct"]), batch=self.batch,
+                       master=self._p(self.master), grad=self._p(self.grad), mom=self._p(self.mom),
+                       shadow=self._p(self.shadow), state=sp, stats=self._p(self.stats), lr=self.lr,
+                       momentum=self.momentum, grad_scale=1.0, fuse_sgd=1, bookkeeping=1, order=self._p(self.order),
+                       order_len=self.order_len, batch_ids=self._p(self.batch_ids), stream=s)
+            if i == n:  # the chunk's last reduction: its own launch, re-publishing slot 0
+                self.ext.grad_reduce(lo=0, hi=LAYOUT.total, next_ids=slot_nid[0], bk_bv_in=slot_bv[(i - 1) & 1],
+                                     bk_bv_out=slot_bv[0], bk_adv=0, **red)
+                break
+            first = i == 0
+            self.ext.grad_reduce(lo=f1w if first else 0, hi=f1w if first else LAYOUT.total, defer=2,
+                                 next_ids=slot_nid[par ^ 1], bk_bv_in=slot_bv[(i - 1) & 1],
+                                 bk_bv_out=slot_bv[par ^ 1], bk_adv=1, bk_stats=0 if first else 1, **red)
+            rows = self._rows(par)
+            self.ext.fused_train_pipe(self._p(self.train.images), self._p(self.train.labels), self.order_len,
+                                      self.batch, self._p(self.master), self._p(self.shadow), self._p(rows["a0"]),
+                                      self._p(rows["h1"]), self._p(rows["h2"]), self._p(rows["z1"]),
+                                      self._p(rows["z2"]), self._p(rows["z3"]), self._p(rows["slab"]),
+                                      self._p(rows["loss"]), self._p(rows["correct"]), slot_nid[par],
+                                      self._p(self.stage), self._p(self.pipe_ctr), par, 0 if first else 1,
+                                      1 if first else self.ext.pipe_reduce_blocks(), slot_bv[par],
+                                      self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
+                                      stamps=0 if first else self._pipe_stamps)
+
+    def _launch_steps(self, n: int) -> None:
+        """n training steps' launches (what a chunk graph captures)."""
+        if self._pipe_ok():
+            self._launch_steps_pipe(n)
+            return
+        for _ in range(n):
+            self._launch_step()
 
     def __del__(self) -> None:
         rg = getattr(self, "_rg", None)
@@ -544,7 +632,7 @@ class HipEngine(Engine):
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
         key = (nsteps, id(self.grad_sync), self.overlap, self.early_mlp, self.order_len,
                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
-               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged)
+               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok())
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.  The wait before it is
@@ -552,8 +640,7 @@ class HipEngine(Engine):
             self._wait()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
-                for _ in range(nsteps):
-                    self._launch_step()
+                self._launch_steps(nsteps)
             torch.cuda.synchronize(self.device)
             self._graphs[key] = g
         return g
@@ -583,6 +670,11 @@ class HipEngine(Engine):
         poll = self.poll
         if not self.use_graphs:
             with torch.cuda.device(self.device):
+                if self._pipe_ok():
+                    if poll is not None:
+                        poll()
+                    self._launch_steps_pipe(n)
+                    return
                 for _ in range(n):
                     if poll is not None:
                         poll()
@@ -608,6 +700,9 @@ class HipEngine(Engine):
         if self.early_failed():
             raise RuntimeError("early-MLP overlap: a row-granule wait timed out (the MLP reduction of a step "
                                "did not see the fused kernel's rows); rerun with DNN_EARLY_MLP=0")
+        if self.pipe_failed():
+            raise RuntimeError("pipelined step: a ready wait timed out (the samples did not see their launch's "
+                               "reduction finish); rerun with DNN_PIPELINE=0")
         if reset:
             self.stats.zero_()
         return StepStats(v[0], int(round(v[1])), int(round(v[2])), int(round(v[3])))

@@ -73,7 +73,7 @@ def ab(out: str) -> None:
     start = eng.master.clone()
     samp = EpochSampler.for_rank(256, comm.rank, comm.world, seed=1, mode="shard")
     cur = EpochCursor(eng, samp, policy, 16)
-    res = allreduce_ab(policy, eng, cur, steps=6, warmup=2, reps=2, candidates=("torch-pg", "slow", "flaky"))
+    res = allreduce_ab(policy, eng, cur, steps=6, warmup=2, reps=2, spin=4, candidates=("torch-pg", "slow", "flaky"))
     restored = bool(torch.equal(eng.master, start))
     cur.run(3)  # the adopted path trains: replicas stay identical
     torch.save({"master": eng.master, "res": res, "restored": restored, "path": policy.path},

@@ -197,3 +197,63 @@ def test_early_mlp_overlap_matches_serial_step():
     for m, mo, sh, st in res[1:]:
         assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo) and torch.equal(res[0][2], sh)
         assert [(x.loss_sum, x.samples, x.correct) for x in st] == [(x.loss_sum, x.samples, x.correct) for x in res[0][3]]
+
+
+@pytest.mark.parametrize("graphs,chunk", [(True, 8), (True, 1), (False, 4), (True, 64)])
+def test_pipelined_step_matches_serial_step(graphs, chunk):
+    """The pipelined step (launch i = step i - 1's reduction + step i's samples, the samples
+    waiting on in-launch ready counters for the weights the reduction writes through) gives the
+    serial step's parameters, momentum, bf16 images and epoch statistics BIT FOR BIT: shuffled
+    epochs with a tail batch, steps past an epoch's end, chunk graphs of 1 / 8 / 64 steps (odd
+    and even launch counts) and eager launches; 3 epochs x 17 steps re-read every weight after
+    every hand-off (a stale L1 / L2 line would show as a mismatch), and no wait times out."""
+    data = synthetic(1000, 11)  # 15 full batches + a tail of 40
+    a = init_arena(seed=5)
+    rng = np.random.default_rng(3)
+    orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
+    res = []
+    for pipe in (False, True):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe)
+        eng.attach(data)
+        stats = []
+        for ep, order in enumerate(orders):
+            eng.begin_epoch(order)
+            if ep == 0:
+                assert eng._pipe_ok() == pipe
+            eng.run_steps(5)
+            eng.run_steps(12 if ep != 1 else 13)  # epoch 1 runs a step past its end (a no-op)
+            stats.append(eng.epoch_stats())
+        torch.cuda.synchronize()
+        assert not (pipe and eng.pipe_failed())
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
+    (m0, mo0, sh0, st0), (m1, mo1, sh1, st1) = res
+    assert torch.equal(m0, m1), f"master differs at {int((m0 != m1).sum())} elements"
+    assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1)
+    assert [(x.loss_sum, x.samples, x.correct, x.batches) for x in st0] == \
+        [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1]
+    assert all(x.samples == 1000 and x.batches == 16 for x in st1)
+
+
+def test_pipelined_long_run_under_load():
+    """600 pipelined steps next to a second stream of GPU work (uneven load on the CUs the
+    hand-off crosses) against the serial step, bit for bit."""
+    data = synthetic(4096, 12)
+    a = init_arena(seed=6)
+    order = np.random.default_rng(4).permutation(4096).astype(np.int32)
+    res = []
+    for pipe in (False, True):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=32, pipeline=pipe)
+        eng.attach(data)
+        side = torch.cuda.Stream()
+        x = torch.randn(2048, 2048, device="cuda")
+        for ep in range(10):
+            eng.begin_epoch(order)
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    x = torch.tanh(x @ x * 1e-3)
+            eng.run_steps(60)
+        torch.cuda.synchronize()
+        assert not (pipe and eng.pipe_failed())
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert res[0][2].loss_sum == res[1][2].loss_sum

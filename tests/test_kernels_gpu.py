@@ -30,11 +30,12 @@ def test_fused_rows_match_oracle(B, n):
     eng.begin_epoch(order)
     s = eng._stream()
     ext = eng.ext
+    codes = torch.full((B, reference.CODES_PER_SAMPLE), 255, device=eng.device, dtype=torch.uint8)
     with torch.cuda.device(eng.device):
         ext.fused_train(eng._p(eng.train.images), eng._p(eng.train.labels), eng._p(eng.batch_ids), eng.order_len,
                         eng.batch, eng._p(eng.state), eng._p(eng.master), eng._p(eng.shadow), eng._p(eng.a0),
                         eng._p(eng.h1), eng._p(eng.h2), eng._p(eng.z1), eng._p(eng.z2), eng._p(eng.z3),
-                        eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), s)
+                        eng._p(eng.slab), eng._p(eng.loss), eng._p(eng.correct), s, codes=eng._p(codes))
     torch.cuda.synchronize()
     bvalid = min(B, n)
     assert int(eng.state[1]) == bvalid
@@ -54,13 +55,22 @@ def test_fused_rows_match_oracle(B, n):
     print("vs bf16-emulating oracle:", {k: f"{v:.2e}" for k, v in eerrs.items()})
     for k, v in eerrs.items():
         assert v < 1e-3, f"{k}: rel err vs bf16 emulation {v:.3e}"
-    # (2) end-to-end precision vs the pure fp32 oracle
-    #     (bf16 operands: ReLU-mask / argmax flips make small batches noisy)
-    #     a single flipped mask is not averaged away below a few samples: looser there
-    loose = 3.0 if bvalid < 4 else 1.0
-    for k, tol in [("a0", 1e-2), ("h1", 1e-2), ("h2", 1e-2), ("loss", 1e-2), ("z3", 1e-2), ("z2", 0.15),
-                   ("z1", 0.15), ("dW2", 0.15), ("dW1", 0.2)]:
-        assert errs[k] < tol * loose, f"{k}: rel err {errs[k]:.3e}"
+    # (2) end-to-end precision vs the pure fp32 oracle, MASK-AWARE: the oracle runs in fp32 with
+    #     the kernel's own max-pool argmax codes and fc ReLU masks, so a near-tie that bf16
+    #     operands flip is excluded and every tensor is held to 1e-2 of fp32
+    cd = codes[:bvalid].cpu()
+    assert int(cd.max()) <= 4, "every sample's codes were written"
+    msk = reference.per_sample_outputs_masked(eng.shadow.float().cpu(), eng.master, split.images[idx], split.labels[idx],
+                                              cd, got["h1"] > 0, got["h2"] > 0, bvalid)
+    merrs = {k: _rel(got[k], msk[k]) for k in got}
+    for lo, hi, name in [(0, 450, "dW1"), (450, 456, "db1"), (456, 2856, "dW2"), (2856, 2872, "db2")]:
+        merrs[name] = _rel(got["slab"][:, lo:hi], msk["slab"][:, lo:hi])
+    print("vs mask-aware fp32 oracle:", {k: f"{v:.2e}" for k, v in merrs.items()})
+    for k, v in merrs.items():
+        assert v < 1e-2, f"{k}: rel err vs the mask-aware fp32 oracle {v:.3e}"
+    #     and the unmasked fp32 oracle agrees where no decision flipped: the masks differ rarely
+    flips = float(((got["h1"] > 0) != (ref["h1"] > 0)).float().mean())
+    assert flips < 0.05, f"fc1 ReLU decisions differ from fp32 on {100 * flips:.1f} % of units"
     if B > n:  # tail rows must be zero
         assert float(eng.a0[bvalid:].abs().sum()) == 0.0
         assert float(eng.slab[bvalid:].abs().sum()) == 0.0

@@ -73,3 +73,33 @@ def test_fma_normalisation_matches_totensor_normalize_in_bf16():
     exact = (u / np.float32(255) - np.float32(0.5)) / np.float32(0.5)
     fma = (u.astype(np.float64) * np.float64(np.float32(2.0 / 255.0)) - 1.0).astype(np.float32)
     assert torch.equal(torch.from_numpy(exact).bfloat16(), torch.from_numpy(fma).bfloat16())
+
+
+def test_masked_oracle_reproduces_fp32_oracle_with_its_own_decisions():
+    """ops/reference.per_sample_outputs_masked (the bf16 kernel's mask-aware fp32 oracle) fed
+    with the pool argmax codes / ReLU masks of an exact fp32 pass equals per_sample_outputs."""
+    import torch.nn.functional as F
+
+    from distributed_neural_network_amd.data import synthetic
+    from distributed_neural_network_amd.models.network import init_arena
+    from distributed_neural_network_amd.ops import reference as R
+
+    d = synthetic(16, 3)
+    a = init_arena(seed=1)
+    x, y = R.normalize_u8(d.images[:8]), d.labels[:8]
+    p = R.LAYOUT.views(a)
+
+    def codes_of(c, h):
+        B, C = c.shape[:2]
+        win = F.relu(c).reshape(B, C, h, 2, h, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, h * h, 4)
+        mx, idx = win.max(-1)
+        return torch.where(mx > 0, idx, torch.full_like(idx, 4)).to(torch.uint8)
+
+    c1 = F.conv2d(x, p["conv1.weight"], p["conv1.bias"])
+    c2 = F.conv2d(F.max_pool2d(F.relu(c1), 2, 2), p["conv2.weight"], p["conv2.bias"])
+    codes = torch.cat([codes_of(c1, 14).reshape(8, -1), codes_of(c2, 5).reshape(8, -1)], 1)
+    assert codes.shape[1] == R.CODES_PER_SAMPLE
+    ref = R.per_sample_outputs(a, d.images[:8], y, 8)
+    got = R.per_sample_outputs_masked(a, a, d.images[:8], y, codes, ref["h1"] > 0, ref["h2"] > 0, 8)
+    for k in ["a0", "h1", "h2", "z1", "z2", "z3", "slab", "loss"]:
+        assert float((got[k] - ref[k]).norm() / (ref[k].norm() + 1e-30)) < 1e-5, k

@@ -170,7 +170,7 @@ class _Policy(StepAllReduce):
 
 def _ab(policy, engine, spe=40, **kw):
     cur = EpochCursor(engine, _Sampler(spe), policy, 16)
-    return autotune.allreduce_ab(policy, engine, cur, steps=8, warmup=2, reps=2, **kw), cur
+    return autotune.allreduce_ab(policy, engine, cur, steps=8, warmup=2, reps=2, spin=3, **kw), cur
 
 
 def test_ab_contains_an_rccl_init_failure(monkeypatch):

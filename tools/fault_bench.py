@@ -52,6 +52,9 @@ def main() -> int:
     ap.add_argument("--device", default="cuda", help="cuda (default) | cpu (plumbing check without a GPU)")
     ap.add_argument("--timeout", type=int, default=900)
     ap.add_argument("--log", default=None, help="also write the stamped per-rank output here")
+    ap.add_argument("--no-check-sync", dest="check_sync", action="store_false",
+                    help="skip the cross-rank parameter checksum after every sync (default: on, so the survivors' "
+                         "parameters are asserted bit-identical after the re-form)")
     a = ap.parse_args()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_FAULT_TRACE="1")
     env.setdefault("DNN_FAULTHANDLER_S", "60")
@@ -68,7 +71,7 @@ def main() -> int:
                str(a.batch_size), "--sync", a.sync, "--drop-rank", str(a.drop_rank), "--drop-at-epoch",
                str(a.drop_at_epoch), "--drop-at-step", str(a.drop_at_step), "--train-samples", str(a.train_samples),
                "--test-samples", str(a.test_samples), "--device", a.device, "--nb-proc", str(a.n), "--metrics",
-               metrics, "--allreduce", a.allreduce]
+               metrics, "--allreduce", a.allreduce] + (["--check-sync"] if a.check_sync else [])
         t0 = time.perf_counter()
         p = subprocess.Popen(cmd, cwd=tmp, env=dict(env, PYTHONUNBUFFERED="1"), stdout=subprocess.PIPE,
                              stderr=subprocess.STDOUT, text=True, bufsize=1)
@@ -115,6 +118,7 @@ def main() -> int:
                      "(BASELINE config 5)",
            "n_ranks": a.n, "share_gpu": a.share_gpu, "allreduce": a.allreduce, "dropped": rv["dead"],
            "generation": rv["generation"], "all_alive_retries": len([x for x in recov if not x["dead"]]),
+           "check_sync": a.check_sync,
            "detect_s": round(t_det - kill, 4) if kill and t_det else None,
            "recovery_s": round(rv["recovery_s"], 4), "stages_s": rv.get("stages_s"),
            "time_to_resume_s": round(res["t_resumed"] - kill, 4) if kill and res else None,

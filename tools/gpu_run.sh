@@ -11,10 +11,12 @@
 #   tests:<expr>     GPU tests selected by -k <expr>
 #   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
 #   k20f32           the same, --dtype fp32
+#   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
+#   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32    bench.py default window (5000 / 500), bf16 / fp32
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
-#   phase | phase32  per-phase timeline of the fused kernels (tools/phase_trace*.py)
+#   phase | phase32 | phasepipe  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
@@ -33,20 +35,28 @@ for s in "$@"; do
     tests:*) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
              -k "${s#tests:}" > "$O/tests_k.log" 2>&1 ;;
     k20|k20b) timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    k20pipe) DNN_PIPELINE=1 timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    longpipe) DNN_PIPELINE=1 timeout -k 10 300 python bench.py > "$O/$s.json" 2> "$O/$s.err" ;;
+    k20serial) DNN_PIPELINE=0 timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    longserial) DNN_PIPELINE=0 timeout -k 10 300 python bench.py > "$O/$s.json" 2> "$O/$s.err" ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
-    prof|prof32)
+    prof|prof32|profserial|profpipe)
       dt=bf16; [ "$s" = prof32 ] && dt=fp32
+      [ "$s" = profserial ] && export DNN_PIPELINE=0
+      [ "$s" = profpipe ] && export DNN_PIPELINE=1
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d "$O/$s" -o run -- \
         python3 bench.py --dtype $dt --steps 2000 --warmup 200 --no-epoch > "$O/$s.log" 2>&1
       db=$(find "$O/$s" -name '*.db' | head -n 1 || true)
-      [ -n "$db" ] && python tools/kstats.py "$db" --steps 2200 > "$O/${s}_kernel_stats.txt" 2>&1 || true ;;
+      [ -n "$db" ] && python tools/kstats.py "$db" --steps 2200 > "$O/${s}_kernel_stats.txt" 2>&1 || true
+      unset DNN_PIPELINE ;;
     pmc:*)
       c="${s#pmc:}"; n=$(echo "$c" | tr ',' '_' | cut -c1-60)
       timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- \
         python3 bench.py --steps 200 --warmup 20 --no-epoch > "$O/pmc_$n.log" 2>&1 ;;
     phase) timeout -k 10 300 python tools/phase_trace.py > "$O/phase.txt" 2>&1 ;;
+    phasepipe) timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe.txt" 2>&1 ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;

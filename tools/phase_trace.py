@@ -22,6 +22,50 @@ PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' 
           "  A1 image landed", "  A2 R1 build + weights landed", "  A3 fc1 DMA issue + barrier"]
 
 
+def pipe_main(reps: int = 50, batch: int = 64):
+    """--pipe: the pipelined step's merged launch (lenet_fused.hip PIPE): reduction workgroups
+    (start / end), the samples' ready waits (conv: before phase B, MLP: before phase C) and the
+    sample phases, medians over repeats of 1-step chunks (launch 1 = reduction + samples)."""
+    tr = synthetic(4096, 0)
+    eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True)
+    eng.attach(tr)
+    stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
+    eng._pipe_stamps = stamps.data_ptr()
+    nrw = (eng.ext.pipe_reduce_blocks() + 1) // 2
+    recs = []
+    for r in range(reps):
+        eng.begin_epoch(np.roll(np.arange(4096, dtype=np.int32), -64 * (r % 60)))
+        stamps.zero_()
+        eng.run_steps(2)  # launches: [bookkeeping + S0] [R0 + S1] [R1]; stamps from the middle one
+        torch.cuda.synchronize()
+        s = stamps.cpu().numpy().astype(np.float64)
+        nb = nrw + batch
+        bl = s[16:16 + 4 * nb].reshape(nb, 4)
+        t0 = bl[:, 0].min()
+        recs.append(dict(red_body=(bl[:nrw, 1] - t0) * 0.01, red_add=(bl[:nrw, 3] - t0) * 0.01,
+                         poll0=(s[14] - t0) * 0.01, polls=s[15],
+                         red_start=(bl[:nrw, 0] - t0) * 0.01, red_end=(bl[:nrw, 2] - t0) * 0.01,
+                         smp_start=(bl[nrw:, 0] - t0) * 0.01, smp_end=(bl[nrw:, 2] - t0) * 0.01,
+                         conv_ready=(s[12] - t0) * 0.01, mlp_ready=(s[13] - t0) * 0.01,
+                         a_done=(s[1] - t0) * 0.01, b_done=(s[2] - t0) * 0.01, c_done=(s[3] - t0) * 0.01,
+                         img=(s[9] - t0) * 0.01, end0=(s[7] - t0) * 0.01))
+    rr = recs[5:]
+    med = lambda f: float(np.median([f(x) for x in rr]))  # noqa: E731
+    # reduction WG order: conv blocks 0..44 (WGs 0..22), bookkeeping (WG 22 half 1), MLP (WGs 23..56)
+    print(f"reduction WGs start med {med(lambda x: np.median(x['red_start'])):.2f} max {med(lambda x: x['red_start'].max()):.2f} us")
+    print(f"  conv WGs (0-22) end med {med(lambda x: np.median(x['red_end'][:23])):.2f} max {med(lambda x: x['red_end'][:23].max()):.2f}")
+    print(f"  MLP WGs (23-56) end med {med(lambda x: np.median(x['red_end'][23:])):.2f} max {med(lambda x: x['red_end'][23:].max()):.2f}")
+    print(f"  conv WGs body done med {med(lambda x: np.median(x['red_body'][:23])):.2f} max {med(lambda x: x['red_body'][:23].max()):.2f}"
+          f"; add performed med {med(lambda x: np.median(x['red_add'][:23])):.2f} max {med(lambda x: x['red_add'][:23].max()):.2f}")
+    print(f"  MLP WGs body done med {med(lambda x: np.median(x['red_body'][23:])):.2f} max {med(lambda x: x['red_body'][23:].max()):.2f}"
+          f"; add performed med {med(lambda x: np.median(x['red_add'][23:])):.2f} max {med(lambda x: x['red_add'][23:].max()):.2f}")
+    print(f"  sample block 0 first conv poll {med(lambda x: x['poll0']):.2f} us, polls {med(lambda x: x['polls']):.0f}")
+    print(f"sample blocks start med {med(lambda x: np.median(x['smp_start'])):.2f} max {med(lambda x: x['smp_start'].max()):.2f}"
+          f"  end med {med(lambda x: np.median(x['smp_end'])):.2f} max {med(lambda x: x['smp_end'].max()):.2f} us")
+    for k in ("img", "conv_ready", "a_done", "b_done", "mlp_ready", "c_done", "end0"):
+        print(f"  sample block 0 {k:10s} {med(lambda x: x[k]):8.2f} us")
+
+
 def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, early_mlp="full" if inlaunch else False)
@@ -92,4 +136,7 @@ def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
 
 
 if __name__ == "__main__":
-    main(inlaunch="--inlaunch" in sys.argv)
+    if "--pipe" in sys.argv:
+        pipe_main()
+    else:
+        main(inlaunch="--inlaunch" in sys.argv)
