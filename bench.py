@@ -164,6 +164,13 @@ def main():
         stamp(comm.rank, f"all-reduce path {policy.installed(engine) if hasattr(policy, 'installed') else None}; "
                          "initial broadcast done")
     cur = EpochCursor(engine, sampler, policy, B)
+    # first-call costs of the eval path (kernel, D2H, host ops) - before the A/B too: a full-chip
+    # kernel, after which the A/B's candidates run on the GPU state the timed window will see
+    if not args.no_epoch:
+        wl, wc = engine.evaluate_samples(test_dev, 0, len(test))
+        wl2, wc2 = torch.zeros_like(wl), torch.zeros_like(wc, dtype=torch.float32)
+        comm.allreduce_(wl2, "sum")
+        eval_metrics(wl + wl2, wc.float() + wc2, B)
     ab = {}
     if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
         ab_steps = args.ab_steps or min(args.steps, 256)
@@ -235,6 +242,11 @@ def main():
         torch.cuda.synchronize(device)
         print(f"[bench] extra window: {1e6 * (time.perf_counter() - t1) / args.steps:.2f} us/step wall, "
               f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
+    if diag and ab and comm.distributed:
+        # diagnostic: the A/B's own measurement of the installed path, after the timed window
+        from distributed_neural_network_amd.parallel.autotune import _measure
+        us, _ = _measure(comm, engine, cur, min(args.steps, 256), args.warmup, 3, 200)
+        stamp(comm.rank, f"A/B-style re-measure of {policy.installed(engine)} after the timed window: {us:.3f} us/step")
     dt = comm.reduce_scalar(dt, "max")
     ms_per_step = 1000.0 * dt / args.steps
     value = comm.world * B * args.steps / dt

@@ -74,13 +74,14 @@ struct ReduceArgs {
 // first workgroups and the samples of step i in the rest; the samples wait for the reduction's
 // ready counters before they load the weights it writes.
 struct PipeCtl {
-  unsigned* ctr = nullptr;        // [2 parities][conv, mlp] ready counters (agent-scope adds)
+  unsigned* ctr = nullptr;        // [2 parities][conv, mlp] ready counters, 128 B apart, in uncached memory
   int par = 0;                    // this launch's parity (launch index & 1)
   int wait = 0;                   // 1: a reduction runs in this launch, wait for its counters
   int nred = 0;                   // reduction blocks of this launch (0, 1 = bookkeeping only, all)
   const int32_t* bvalid = nullptr;  // this launch's samples' valid count (its bookkeeping slot)
   unsigned* err = nullptr;          // sticky error word: a ready wait timed out (never a hang)
   long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
+  int flags = 0;                    // & 3: poll form; & 4: stream fc1 in phase A when the MLP is ready
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

@@ -271,6 +271,7 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
 constexpr int PIPE_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
 constexpr int PIPE_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT;
 constexpr int PIPE_BLOCKS = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS + 1;
+constexpr int PIPE_CTR_STRIDE = 32;  // ready counters 128 B apart: [parity][conv, mlp] = 4 lines
 static_assert(PIPE_BLOCKS == GRAD_REDUCE_BLOCKS, "the pipelined launch runs the whole grad_reduce");
 int pipe_reduce_blocks() { return PIPE_BLOCKS; }
 
@@ -278,8 +279,8 @@ int pipe_reduce_blocks() { return PIPE_BLOCKS; }
 __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255;
   if (wg == 0 && threadIdx.x == 0) {  // the next launch's counters start from zero (kernel boundary)
-    pc.ctr[2 * (pc.par ^ 1)] = 0u;
-    pc.ctr[2 * (pc.par ^ 1) + 1] = 0u;
+    pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1))] = 0u;
+    pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1) + 1)] = 0u;
   }
   int grp = -1;  // ready counter this block signals: 0 conv, 1 MLP, -1 none (bookkeeping)
   if (m < pc.nred) {
@@ -297,10 +298,11 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
   __syncthreads();
   if (rtid == 0 && grp >= 0) {
     if (stamps != nullptr) {  // diagnostic: when the add has been performed
-      const unsigned v = __hip_atomic_fetch_add(pc.ctr + 2 * pc.par + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned v = __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
       if (half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime() + 0 * v;
     } else {
-      __hip_atomic_fetch_add(pc.ctr + 2 * pc.par + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -309,14 +311,47 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
 // timeout it sets the sticky error word and returns (the step then runs on the old weights and
 // the host raises at the next check) - never a hang.
 __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned target, long long* diag = nullptr) {
-  const unsigned* c = pc.ctr + 2 * pc.par + grp;
+  const unsigned* c = pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp);
   if (__hip_atomic_load(pc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // failed before: no wait
   const long long t0 = wall_clock64();
   if (diag != nullptr) diag[0] = t0;
   long long polls = 0;
-  // the poll is a returning atomic (add 0): performed where the adds are, never a stale L2 copy
-  // (sc1 load polls of this counter saw its final value ~3 us late: profiles/r4/pipe/)
-  while (__hip_atomic_fetch_add(const_cast<unsigned*>(c), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  // The counters live in UNCACHED memory, each on its own 128-B line: a poll is a plain sc1 load
+  // that goes to memory every time.  (In cached memory an sc1 poll saw the final count ~3 us late -
+  // its first read left the line in this XCD's L2 - and a returning atomic add of 0 from 64 pollers
+  // took ~1.2 us per poll on the contended line: profiles/r4/pipe_v1.)
+  // flags & 3 (the poll form, measured in profiles/r4/pipe_v2): 0 = one load, s_sleep, the next;
+  // 1 = two in flight (a new load is issued before the previous one is checked); 2 = four loads
+  // ~0.1 us apart per round, checked together
+  const int form = pc.flags & 3;
+  if (form == 1) {
+    unsigned prev = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+      __builtin_amdgcn_s_sleep(8);
+      const unsigned cur = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev >= target) break;
+      prev = cur;
+      ++polls;
+      if (diag != nullptr) diag[1] = polls;
+      if (wall_clock64() - t0 > pc.timeout_ticks) {
+        __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    return;
+  }
+  while (true) {
+    unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (form == 2) {
+      __builtin_amdgcn_s_sleep(4);
+      const unsigned v1 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_sleep(4);
+      const unsigned v2 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_sleep(4);
+      const unsigned v3 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = max(max(v, v1), max(v2, v3));
+    }
+    if (v >= target) break;
     ++polls;
     if (diag != nullptr) diag[1] = polls;
     __builtin_amdgcn_s_sleep(2);
@@ -536,6 +571,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
   float bias_c1 = 0.f, bias_c2 = 0.f;
+  bool fc1_early = false;  // PIPE: the fc1 stream left in phase A (the MLP reduction was ready)
   auto load_conv_w = [&]() {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) bw1[sk] = wr.w8(SH_W1F + ((4 * sk + fg) * 16 + fr) * 8);
@@ -544,14 +580,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     bias_c1 = wr.f(OFF_C1B + min(fr, 5));
     bias_c2 = wr.f(OFF_C2B + fr);
   };
-  if constexpr (PIPE) {
-    // the conv weights are the previous step's reduction's: one lane waits for its conv
-    // blocks; the barrier below releases the other waves, whose loads follow it
-    if (pc.wait && tid == 0) pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr);
-    STAMP(12);
-  } else {
-    load_conv_w();
-  }
+  if constexpr (!PIPE) load_conv_w();  // (PIPE: after the conv reduction is ready, below)
   for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = (bf16)0.f;
   if (tid < 16) A0B[400 + tid] = (bf16)0.f;                                   // MLP operand padding
   else if (tid < 24) H1B[120 + tid - 16] = (bf16)0.f;
@@ -562,14 +591,34 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
   lds_barrier();
   STAMP(9);
-  if constexpr (PIPE) load_conv_w();  // (sc1: written in this launch, ready since the barrier)
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
+  if constexpr (PIPE) {
+    // the conv weights are the previous step's reduction's: one lane waits for its conv blocks
+    // (the image and its records need none of it, so they are done first); the barrier releases
+    // the other waves, then every wave loads its fragments (sc1) - waited for at phase B's first
+    // MFMA, so the R1 records' barrier below is this one
+    if (tid == 0) {
+      int early = 1;  // the MLP weights are ready too: stream fc1 now, as the serial step does
+      if (pc.wait) {
+        pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr);
+        early = (pc.flags & 4) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                           (unsigned)PIPE_MLP_BLOCKS;
+      }
+      *reinterpret_cast<int*>(smem + L_MISC) = early;
+    }
+    STAMP(12);
+    lds_barrier();
+    load_conv_w();
+    fc1_early = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + L_MISC)) != 0;
+  } else {
 #pragma unroll
-  for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
+    for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
 #pragma unroll
-  for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
-  consume(bias_c1);
-  consume(bias_c2);
+    for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+    consume(bias_c1);
+    consume(bias_c2);
+  }
   STAMP(11);
   // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all in-arena);
   // 12 per wave with the index clamped (a duplicate copies identical bytes).  Issued here, or
@@ -583,8 +632,21 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       dma_w<PIPE>(f1src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
     }
   };
-  if constexpr (!PIPE) stream_fc1();
-  lds_barrier();
+  if constexpr (!PIPE) {
+    stream_fc1();
+    lds_barrier();
+  } else if (fc1_early) {
+    // (the MLP weights were ready when the conv weights were: the sc1 stream, as above; the conv
+    // fragments are waited for first - vmcnt counts in issue order, so a fragment wait after the
+    // DMA would wait for the whole 96 KB)
+#pragma unroll
+    for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
+#pragma unroll
+    for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+    consume(bias_c1);
+    consume(bias_c2);
+    stream_fc1();
+  }
   STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
@@ -643,11 +705,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   if constexpr (PIPE) {
-    if (pc.wait && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS);  // the MLP weights (released by the barrier)
+    if (!fc1_early && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS);  // the MLP weights (released by the barrier)
     STAMP(13);
   }
   lds_barrier();
-  if constexpr (PIPE) stream_fc1();  // first, so the fragment loads below are waited for after it
+  if constexpr (PIPE) {
+    if (!fc1_early) stream_fc1();  // first, so the fragment loads below are waited for after it
+  }
 
   STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============

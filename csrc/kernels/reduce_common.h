@@ -76,16 +76,88 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
 //    runs after the lane has read the same element from every peer.
 template <bool WT>
 struct DirectSinkT {
+  static constexpr bool kTile = WT;  // fc1 / fc2 tiles finish in put_tile (below)
   __device__ __forceinline__ void put(int, int e, float g, float p, float m, const ReduceArgs& a) {
     sgd_finish<WT>(e, g, p, m, a);
   }
+  // A finished fc1 / fc2 weight-gradient tile (lane (i, kq) holds rows o0 + 4 kq + j of column
+  // i0 + i): SGD per element (master / momentum plain: the samples read no fc weight from the
+  // fp32 master), then the bf16 images with 8-byte write-through stores instead of one 2-byte
+  // store per element - a 4 x 4 transpose inside each lane quad (DPP rotations) gives lane u
+  // the 4 consecutive columns of row o0 + 4 kq + u for the row-major copy; the transposed fc2
+  // image [i][o] takes the lane's own 4 consecutive rows as they are.
+  template <int LAYER>
+  __device__ __forceinline__ void put_tile(const f32x4& acc, const float (&pv)[4], const float (&mv)[4],
+                                           const int (&e)[4], int o0, int i0, int lane, const ReduceArgs& a);
 };
 using DirectSink = DirectSinkT<false>;
 using WtSink = DirectSinkT<true>;
+
+// lane u of a quad reads lane (u + R) & 3's value
+template <int R>
+__device__ __forceinline__ unsigned qrot(unsigned v) {
+  constexpr int c = (R & 3) | (((1 + R) & 3) << 2) | (((2 + R) & 3) << 4) | (((3 + R) & 3) << 6);
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, c, 0xf, 0xf, false);
+}
+__device__ __forceinline__ unsigned sel4(const unsigned (&x)[4], int k) {
+  return k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
+}
+// b[u][v] = a[v][u] over the 4 lanes u of a quad (a[lane][element])
+// (lane u receives a[k][u] from lane k = (u + r) & 3, which sends its element (k - r) & 3 = u)
+__device__ __forceinline__ void quad_transpose(const unsigned (&x)[4], unsigned (&y)[4], int u) {
+  const unsigned r0 = sel4(x, u), r1 = qrot<1>(sel4(x, (u - 1) & 3)), r2 = qrot<2>(sel4(x, (u - 2) & 3)),
+                 r3 = qrot<3>(sel4(x, (u - 3) & 3));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = (k - u) & 3;
+    y[k] = r == 0 ? r0 : r == 1 ? r1 : r == 2 ? r2 : r3;
+  }
+}
+
+__device__ __forceinline__ void st_wt8(bf16* p, unsigned lo, unsigned hi) {  // 4 bf16, 8-B aligned
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)lo | ((unsigned long long)hi << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool WT>
+template <int LAYER>
+__device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, const float (&pv)[4], const float (&mv)[4],
+                                                         const int (&e)[4], int o0, int i0, int lane,
+                                                         const ReduceArgs& a) {
+  constexpr int O = LAYER == 0 ? 120 : 84, I = LAYER == 0 ? 400 : 120, OFF = LAYER == 0 ? OFF_F1W : OFF_F2W;
+  const int i = lane & 15, kq = lane >> 4, u = lane & 3;
+  const bool iv = i0 + i < I;
+  unsigned bv[4];  // this lane's column, rows o0 + 4 kq + j: bf16 bits (0 outside the layer)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool ok = iv && o0 + 4 * kq + j < O;
+    float p = 0.f;
+    if (ok) {
+      float m;
+      sgd_update(acc[j] * a.grad_scale, pv[j], mv[j], a.lr, a.momentum, p, m);
+      a.mom[e[j]] = m;
+      a.master[e[j]] = p;
+    }
+    bv[j] = ok ? (unsigned)__builtin_bit_cast(unsigned short, (bf16)p) : 0u;
+  }
+  // row-major bf16 copy: lane u of the quad -> row o0 + 4 kq + u, columns i0 + (i & ~3) .. + 3
+  unsigned t[4];
+  quad_transpose(bv, t, u);
+  const int row = o0 + 4 * kq + u, c0 = i0 + (i & ~3);
+  if (row < O && c0 < I) st_wt8(a.shadow + OFF + row * I + c0, t[0] | (t[1] << 16), t[2] | (t[3] << 16));
+  if constexpr (LAYER == 1) {  // fc2^T image [i][96]: this lane's 4 consecutive rows o0 + 4 kq ..
+    if (iv && o0 + 4 * kq < O) st_wt8(a.shadow + SH_W2T + (i0 + i) * 96 + o0 + 4 * kq, bv[0] | (bv[1] << 16),
+                                      bv[2] | (bv[3] << 16));
+  }
+}
 //    PK (bf16 granules, xp_mode bit 4): the lane's elements travel in pairs (0, 1) and (2, 3)
 //    as ONE granule {bf16 | bf16, step} each, published by the exchange once both are known.
 template <bool PK>
 struct XpSinkT {
+  static constexpr bool kTile = false;
+  template <int LAYER>
+  __device__ __forceinline__ void put_tile(const f32x4&, const float (&)[4], const float (&)[4], const int (&)[4], int,
+                                           int, int, const ReduceArgs&) {}
   unsigned long long* own;  // where the granules go: this rank's pull slot (null: not published)
   unsigned long long tag;   // step << 32
   int e[4] = {0, 0, 0, 0};
@@ -228,6 +300,10 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
     }
   }
   acc += acc1;
+  if constexpr (Sink::kTile && LAYER < 2) {  // the pipelined step: wide write-through image stores
+    sk.template put_tile<LAYER>(acc, pv, mv, e, o0, i0, lane, a);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + 4 * kq + j;

@@ -103,6 +103,9 @@ def _measure(comm, engine, cur, steps: int, warmup: int, reps: int, spin: int) -
         prepare_window(engine, cur, steps, warmup)
         cur.run(warmup)
         times.append(window(comm, engine, cur, steps))
+    if os.environ.get("DNN_AB_DEBUG") == "1":
+        print(f"[ab] rank {comm.rank}: windows {[round(1e6 * t / steps, 2) for t in times]} us/step", file=sys.stderr,
+              flush=True)
     dt = statistics.median(times)
     failed = getattr(engine.grad_sync, "failed", None)
     bad = bool(failed()) if failed is not None else False

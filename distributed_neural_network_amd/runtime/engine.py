@@ -305,7 +305,8 @@ class HipEngine(Engine):
                                slab=torch.zeros_like(self.slab), loss=torch.zeros_like(self.loss),
                                correct=torch.zeros_like(self.correct))
             self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
-            self.pipe_ctr = torch.zeros(4, device=dev, dtype=torch.int32)
+            # (uncached memory: every poll reads memory, lenet_fused.hip pipe_wait)
+            self._pipe_ctr_ptr = self.ext.uncached_alloc(4 * 128)
             self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -408,6 +409,8 @@ class HipEngine(Engine):
 
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
+    # lenet_fused.hip PipeCtl.flags: & 3 the ready-poll form, & 4 the early fc1 stream
+    pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "0"))
 
     def _rows(self, par: int) -> dict:
         if par == 0:
@@ -451,10 +454,10 @@ class HipEngine(Engine):
                                       self._p(rows["h1"]), self._p(rows["h2"]), self._p(rows["z1"]),
                                       self._p(rows["z2"]), self._p(rows["z3"]), self._p(rows["slab"]),
                                       self._p(rows["loss"]), self._p(rows["correct"]), slot_nid[par],
-                                      self._p(self.stage), self._p(self.pipe_ctr), par, 0 if first else 1,
+                                      self._p(self.stage), self._pipe_ctr_ptr, par, 0 if first else 1,
                                       1 if first else self.ext.pipe_reduce_blocks(), slot_bv[par],
                                       self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                      stamps=0 if first else self._pipe_stamps)
+                                      stamps=0 if first else self._pipe_stamps, flags=self.pipe_flags)
 
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
@@ -466,10 +469,14 @@ class HipEngine(Engine):
 
     def __del__(self) -> None:
         rg = getattr(self, "_rg", None)
-        if rg is not None:
+        pc = getattr(self, "_pipe_ctr_ptr", None)
+        if rg is not None or pc is not None:
             try:
                 torch.cuda.synchronize(self.device)
-                self.ext.xgmi_free(rg["ptr"])
+                if rg is not None:
+                    self.ext.xgmi_free(rg["ptr"])
+                if pc is not None:
+                    self.ext.xgmi_free(pc)
             except Exception:
                 pass
 

@@ -57,9 +57,19 @@ for s in "$@"; do
         python3 bench.py --steps 200 --warmup 20 --no-epoch > "$O/pmc_$n.log" 2>&1 ;;
     phase) timeout -k 10 300 python tools/phase_trace.py > "$O/phase.txt" 2>&1 ;;
     phasepipe) timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe.txt" 2>&1 ;;
+    pipeflags:*)  # the pipelined step's variants: phase trace + 2000-step bench per DNN_PIPE_FLAGS value
+      for f in $(echo "${s#pipeflags:}" | tr ',' ' '); do
+        DNN_PIPE_FLAGS=$f timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe_f$f.txt" 2>&1
+        DNN_PIPE_FLAGS=$f DNN_PIPELINE=1 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch \
+          > "$O/b2k_pipe_f$f.json" 2> "$O/b2k_pipe_f$f.err"
+      done
+      DNN_PIPELINE=0 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k_serial.json" \
+        2> "$O/b2k_serial.err" ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;
+    rehearse2diag) DNN_BACKEND=gloo DNN_AB_DEBUG=1 timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
+                 --diag-windows 3 > "$O/$s.json" 2> "$O/$s.err" ;;
     fault2) timeout -k 10 400 python tools/fault_bench.py -n 2 --share-gpu > "$O/fault2.json" 2> "$O/fault2.log" ;;
     fault4) timeout -k 10 400 python tools/fault_bench.py -n 4 --share-gpu > "$O/fault4.json" 2> "$O/fault4.log" ;;
     sweep:*)
