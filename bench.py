@@ -196,6 +196,16 @@ def main():
         comm.allreduce_(wl2, "sum")
         eval_metrics(wl + wl2, wc.float() + wc2, B)
     cur.run(args.warmup)
+    if getattr(engine, "pipeline", False) and engine._pipe_ok():
+        torch.cuda.synchronize(device)
+        if engine.pipe_failed():  # a ready wait timed out (never seen): time the serial step instead
+            stamp(comm.rank, "pipelined step: a ready wait timed out in the warmup; using the serial step")
+            engine.pipeline = False
+            engine.pipe_err.zero_()
+            cur.left = 0
+            cur._next_epoch()
+            engine.prepare_graphs(exact=(args.steps,) if args.steps <= min(512, cur.left - args.warmup) else ())
+            cur.run(args.warmup)
     xg = getattr(engine.grad_sync, "group", None)
     if xg is not None:
         xg.reset_wait_stats()

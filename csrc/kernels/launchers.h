@@ -81,7 +81,7 @@ struct PipeCtl {
   const int32_t* bvalid = nullptr;  // this launch's samples' valid count (its bookkeeping slot)
   unsigned* err = nullptr;          // sticky error word: a ready wait timed out (never a hang)
   long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
-  int flags = 0;                    // & 3: poll form; & 4: stream fc1 in phase A when the MLP is ready
+  int flags = 0;  // & 3: poll form; & 4: stream fc1 in phase A when the MLP is ready (& 8: by wave 7 alone)
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

@@ -601,9 +601,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       int early = 1;  // the MLP weights are ready too: stream fc1 now, as the serial step does
       if (pc.wait) {
         pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr);
-        early = (pc.flags & 4) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                           (unsigned)PIPE_MLP_BLOCKS;
+        early = (pc.flags & 12) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                            (unsigned)PIPE_MLP_BLOCKS;
       }
       *reinterpret_cast<int*>(smem + L_MISC) = early;
     }
@@ -635,6 +635,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if constexpr (!PIPE) {
     stream_fc1();
     lds_barrier();
+  } else if (fc1_early && (pc.flags & 8)) {
+    // (flags & 8: wave 7 alone streams the whole of fc1 - 94 wave-instructions - once its own conv
+    // fragments have landed; the other waves start phase B without waiting for theirs here)
+    if (wave == 7) {
+#pragma unroll
+      for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
+#pragma unroll
+      for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+      consume(bias_c1);
+      consume(bias_c2);
+      const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
+      const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
+      for (int i = 0; i < 94; ++i) dma16_sc1(f1src + i * 64 + lane, base + (uint32_t)i * 1024u);
+    }
   } else if (fc1_early) {
     // (the MLP weights were ready when the conv weights were: the sc1 stream, as above; the conv
     // fragments are waited for first - vmcnt counts in issue order, so a fragment wait after the

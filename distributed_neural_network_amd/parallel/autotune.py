@@ -152,7 +152,7 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
                 try:
                     ok = bool(policy.install(engine, name))
                     if not ok:
-                        why = "install / self-test failed"
+                        why = getattr(policy, "install_why", "") or "install / self-test failed"
                 except Exception as e:  # contained: this candidate fails, the A/B goes on
                     ok, why = False, f"install raised {type(e).__name__}: {e}"
                 if not _agree(comm, ok):

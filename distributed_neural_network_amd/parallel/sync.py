@@ -192,6 +192,7 @@ class StepAllReduce(SyncPolicy):
     def install(self, engine, name: str) -> bool:
         """Collective: put path ``name`` on the engine.  Returns the agreed outcome (False on
         every rank if it failed on any; the engine then has no all-reduce installed)."""
+        self.install_why = ""  # why the last install returned False (the A/B's failure reason)
         if hasattr(engine, "invalidate_graphs"):
             engine.invalidate_graphs()
         if hasattr(engine, "overlap"):
@@ -203,9 +204,11 @@ class StepAllReduce(SyncPolicy):
                 self._early0 = engine.early_mlp
             ovl = name.endswith("-ovl")
             if ovl and getattr(engine, "dtype", "bf16") != "bf16":
+                self.install_why = "the in-launch (-ovl) reduction is a bf16-kernel feature"
                 return False
             engine.early_mlp = "mlp" if ovl else self._early0
         elif name.endswith("-ovl"):
+            self.install_why = "the in-launch (-ovl) reduction needs the fused engine"
             return False
         engine.grad_sync = None
         if name == "local":
@@ -216,6 +219,7 @@ class StepAllReduce(SyncPolicy):
             return self._install_xgmi(engine, EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-ovl")])
         if name in ("rccl", "rccl-overlap"):
             if self.comm.backend != "nccl":
+                self.install_why = f"RCCL needs the nccl backend (this run's host collectives: {self.comm.backend})"
                 return False
             from .rccl import NativeGradAllReduce, RcclComm
 
@@ -242,6 +246,7 @@ class StepAllReduce(SyncPolicy):
 
         xg = self._xgmi_group(engine)
         if xg is None:
+            self.install_why = "no xGMI group (not one node, refused, or its self-test failed)"
             return False
         engine.grad_sync = XgmiGradSync(xg)
         xg.one_launch, xg.xp_mode = False, mode
@@ -258,11 +263,13 @@ class StepAllReduce(SyncPolicy):
                     # step across ranks - this group must not be used again
                     self._drop_xgmi_group()
                     engine.grad_sync = None
+                    self.install_why = "the one-launch exchange self-test raised or timed out"
                     return False
             xg.one_launch = cache[mode]
             if not xg.one_launch:
                 if mode != 0:
                     engine.grad_sync = None
+                    self.install_why = "the one-launch exchange self-test did not match the two-launch path"
                     return False  # the two-hop form exists only as the one-launch exchange
                 if self.comm.rank == 0:
                     import sys

@@ -287,10 +287,10 @@ class HipEngine(Engine):
         # samples in the rest, which wait (in-launch ready counters) for the new weights before
         # they load them - the reduction hides under the samples' image ingest, and a chunk of n
         # steps is n + 1 launches instead of 2 n.  Bit-identical to the serial step (the same
-        # kernels' arithmetic).  Opt-in (DNN_PIPELINE=1) until it measures faster than the serial
-        # step (profiles/r4/pipe_v1/).
+        # kernels' arithmetic).  On by default: 18.5 vs 18.9 us per step over 2000 steps, 19.9
+        # vs 20.4 in the 20-step window (profiles/r4/pipe_v2, pipe_v3); DNN_PIPELINE=0 turns it off.
         if pipeline is None:
-            pipeline = os.environ.get("DNN_PIPELINE", "0") != "0"
+            pipeline = os.environ.get("DNN_PIPELINE", "1") != "0"
         self.pipeline = bool(pipeline) and dtype == "bf16" and stage_images
         self._rg: dict | None = None
         if dtype == "bf16":
