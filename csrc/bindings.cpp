@@ -190,7 +190,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("fused_train_pipe", [](u images, u labels, int order_len, int batch, u master, u shadow, u a0, u h1, u h2,
                                u z1, u z2, u z3, u slab, u loss, u correct, u next_ids, u stage, u ctr, int par,
                                int wait, int nred, u bvalid, u err, double timeout_s, u stream, u stamps,
-                               int flags) {
+                               int flags, u flg) {
     if (!g_pending_pipe_set) throw std::runtime_error("fused_train_pipe needs a grad_reduce(defer=2) call first");
     g_pending_pipe_set = false;
     dnn::PipeCtl pc;
@@ -202,6 +202,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     pc.err = P<unsigned>(err);
     pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
     pc.flags = flags;
+    pc.flg = P<unsigned>(flg);
     dnn::launch_fused_train_pipe(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
                                  P<const float>(master), P<const bf16>(shadow), P<float>(a0), P<float>(h1),
                                  P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
@@ -211,13 +212,18 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
      py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("next_ids"), py::arg("stage"), py::arg("ctr"),
      py::arg("par"), py::arg("wait"), py::arg("nred"), py::arg("bvalid"), py::arg("err"), py::arg("timeout_s"),
-     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0);
+     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0, py::arg("flg") = 0);
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {
     dnn::launch_linear_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), B, K, N, relu,
                            S(stream));
+  });
+  m.def("linear_splitk_splits", [](int B, int K, int N) { return dnn::linear_splitk_splits(B, K, N); });
+  m.def("linear_fwd_splitk", [](u x, u w, u b, u y, u part, int splits, int B, int K, int N, int relu, u stream) {
+    dnn::launch_linear_fwd_splitk(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), P<float>(part),
+                                  splits, B, K, N, relu, S(stream));
   });
   m.def("linear_dgrad", [](u dy, u y, u w, u dx, int B, int K, int N, u stream) {
     dnn::launch_linear_dgrad(P<const float>(dy), P<const float>(y), P<const float>(w), P<float>(dx), B, K, N,

@@ -80,6 +80,7 @@ struct PipeCtl {
   int nred = 0;                   // reduction blocks of this launch (0, 1 = bookkeeping only, all)
   const int32_t* bvalid = nullptr;  // this launch's samples' valid count (its bookkeeping slot)
   unsigned* err = nullptr;          // sticky error word: a ready wait timed out (never a hang)
+  unsigned* flg = nullptr;          // optional broadcast flags (uncached, [2][2][batch] x 128 B): see pipe_reduce
   long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
   int flags = 0;  // & 3: poll form; & 4: stream fc1 in phase A when the MLP is ready (& 8: by wave 7 alone)
 };
@@ -238,6 +239,9 @@ void launch_sgd_tail(float* p, float* g, float* m, long n, float lr, float momen
 // dz = dy masked by y > 0 when y != nullptr (fused ReLU)
 void launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int B, int K, int N, int relu,
                        hipStream_t s);
+int linear_splitk_splits(int B, int K, int N);
+void launch_linear_fwd_splitk(const float* x, const float* w, const float* b, float* y, float* part, int S, int B,
+                              int K, int N, int relu, hipStream_t s);
 void launch_linear_dgrad(const float* dy, const float* y, const float* w, float* dx, int B, int K, int N,
                          hipStream_t s);
 void launch_linear_wgrad(const float* dy, const float* y, const float* x, float* dw, float* db, int B, int K, int N,

@@ -275,6 +275,11 @@ constexpr int PIPE_CTR_STRIDE = 32;  // ready counters 128 B apart: [parity][con
 static_assert(PIPE_BLOCKS == GRAD_REDUCE_BLOCKS, "the pipelined launch runs the whole grad_reduce");
 int pipe_reduce_blocks() { return PIPE_BLOCKS; }
 
+// broadcast flags (PipeCtl::flg): [parity][conv, mlp][sample], one 128-B line each
+__device__ __forceinline__ long pipe_flag_index(int par, int grp, int b, int batch) {
+  return ((long)(2 * par + grp) * batch + b) * PIPE_CTR_STRIDE;
+}
+
 // Reduction workgroup `wg` of a PIPE launch: two 256-thread reduction blocks.
 __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255;
@@ -282,6 +287,9 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
     pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1))] = 0u;
     pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1) + 1)] = 0u;
   }
+  if (wg == 0 && pc.flg != nullptr)  // ... and its broadcast flags
+    for (int i = threadIdx.x; i < 2 * a.batch; i += blockDim.x)
+      pc.flg[pipe_flag_index(pc.par ^ 1, i / a.batch, i % a.batch, a.batch)] = 0u;
   int grp = -1;  // ready counter this block signals: 0 conv, 1 MLP, -1 none (bookkeeping)
   if (m < pc.nred) {
     int rblk = 0;  // (nred == 1: the bookkeeping alone - the launch range holds no elements)
@@ -291,11 +299,35 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
       else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = 1; }
     }
     WtSink sk;
+    if (grp == 1 && (pc.flags & 32)) {  // MLP tiles store after the conv weights are out
+      sk.gate = pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par);
+      sk.gate_target = PIPE_CONV_BLOCKS;
+    }
     grad_reduce_body<false>(a, sk, rblk, rtid);
   }
   if (stamps != nullptr && threadIdx.x == 0) stamps[16 + 4 * wg + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its write-through stores
   __syncthreads();
+  if (pc.flg != nullptr) {
+    // broadcast form: the LAST block of a group (its returning add saw every other block's add,
+    // each made after that block drained its stores) stores one flag per sample workgroup, each on
+    // a line of its own - 64 pollers of ONE counter word serialize at its memory channel (a poll
+    // took 1-2 us there: profiles/r4/pipe_v5, pipe_v6)
+    if ((rtid >> 6) == 0 && grp >= 0) {  // wave 0 of the block
+      unsigned old = 0;
+      if (rtid == 0)
+        old = __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (stamps != nullptr && rtid == 0 && half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime();
+      const unsigned last = grp == 0 ? PIPE_CONV_BLOCKS - 1 : PIPE_MLP_BLOCKS - 1;
+      if (old == last)
+        for (int b = rtid; b < a.batch; b += 64)
+          __hip_atomic_store(pc.flg + pipe_flag_index(pc.par, grp, b, a.batch), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (rtid == 0 && grp >= 0) {
     if (stamps != nullptr) {  // diagnostic: when the add has been performed
       const unsigned v = __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED,
@@ -310,8 +342,14 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
 // One lane waits until a ready counter reaches `target` (returning-atomic polls).  Bounded: past the
 // timeout it sets the sticky error word and returns (the step then runs on the old weights and
 // the host raises at the next check) - never a hang.
-__device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned target, long long* diag = nullptr) {
-  const unsigned* c = pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp);
+// also != nullptr: each poll round also reads the MLP counter (in flight with the first), so its
+// value at the round that saw `target` costs no extra round trip
+__device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned target, long long* diag = nullptr,
+                                          unsigned* also = nullptr, int b = 0, int batch = 0) {
+  // (broadcast form: this sample workgroup's own flag, set to 1 by the group's last block)
+  const unsigned* c = pc.flg != nullptr ? pc.flg + pipe_flag_index(pc.par, grp, b, batch)
+                                        : pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp);
+  if (pc.flg != nullptr) target = 1u;
   if (__hip_atomic_load(pc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // failed before: no wait
   const long long t0 = wall_clock64();
   if (diag != nullptr) diag[0] = t0;
@@ -342,6 +380,12 @@ __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned t
   }
   while (true) {
     unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (also != nullptr)
+      *also = __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (diag != nullptr && polls < 12) {  // (t, value) of each poll's return: stamps[4096 + 2 k]
+      diag[4082 + 2 * polls] = (long long)__builtin_amdgcn_s_memrealtime();
+      diag[4083 + 2 * polls] = v;
+    }
     if (form == 2) {
       __builtin_amdgcn_s_sleep(4);
       const unsigned v1 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -571,7 +615,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
   float bias_c1 = 0.f, bias_c2 = 0.f;
-  bool fc1_early = false;  // PIPE: the fc1 stream left in phase A (the MLP reduction was ready)
+  bool fc1_early = false;  // PIPE: the fc1 stream left early (the MLP reduction was ready) -
+  bool fc1_mid = false;    //   in phase A, or (fc1_mid) after phase B's first round
   auto load_conv_w = [&]() {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) bw1[sk] = wr.w8(SH_W1F + ((4 * sk + fg) * 16 + fr) * 8);
@@ -600,17 +645,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (tid == 0) {
       int early = 1;  // the MLP weights are ready too: stream fc1 now, as the serial step does
       if (pc.wait) {
-        pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr);
-        early = (pc.flags & 12) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                            (unsigned)PIPE_MLP_BLOCKS;
+        unsigned mlp_seen = 0;
+        pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr, (pc.flags & 16) ? &mlp_seen : nullptr, b,
+                  batch);
+        if (pc.flags & 16) early = mlp_seen >= (unsigned)PIPE_MLP_BLOCKS ? 2 : 0;  // (2: stream mid-phase B)
+        else
+          early = (pc.flags & 12) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                              (unsigned)PIPE_MLP_BLOCKS;
       }
       *reinterpret_cast<int*>(smem + L_MISC) = early;
     }
     STAMP(12);
     lds_barrier();
     load_conv_w();
-    fc1_early = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + L_MISC)) != 0;
+    const int how = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + L_MISC));
+    fc1_early = how != 0;
+    fc1_mid = how == 2;
   } else {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
@@ -635,6 +686,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if constexpr (!PIPE) {
     stream_fc1();
     lds_barrier();
+  } else if (fc1_mid) {
+    // (streamed after phase B's first MFMA round, below: its fragments have landed by then)
   } else if (fc1_early && (pc.flags & 8)) {
     // (flags & 8: wave 7 alone streams the whole of fc1 - 94 wave-instructions - once its own conv
     // fragments have landed; the other waves start phase B without waiting for theirs here)
@@ -716,10 +769,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       epilogue(t1, acc1);
       epilogue(t2, acc2);
       if (four) epilogue(48, acc3);
+      if (PIPE && fc1_mid && r == 0) {
+        // the MLP weights were ready when the conv weights were: stream fc1 now, behind this
+        // round's MFMAs (which waited for bw1); bw2 / the biases are waited for first (issued with
+        // bw1, so already in) - vmcnt counts in issue order, a later wait would drain the DMA
+#pragma unroll
+        for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+        consume(bias_c1);
+        consume(bias_c2);
+        stream_fc1();
+      }
     }
   }
   if constexpr (PIPE) {
-    if (!fc1_early && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS);  // the MLP weights (released by the barrier)
+    if (!fc1_early && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS, nullptr, nullptr, b, batch);  // (released by the barrier)
     STAMP(13);
   }
   lds_barrier();

@@ -214,6 +214,39 @@ __global__ void __launch_bounds__(64 * LIN_MAX_WAVES) small_gemm_fwd_vec_kernel(
   small_gemm_tile<false, false, true>(g, red);
 }
 
+// Split-K forward for long reductions (cifar-vgg's fc1: 64 x 4096 x 256 has only 64 output tiles,
+// so one workgroup per tile fills 64 CUs and walks K = 4096 alone): grid z = split s takes
+// k in [s Ks, (s + 1) Ks) of every tile and writes its fp32 partial tile to part[s]; a combine
+// launch sums the S partials per output IN SPLIT ORDER (deterministic, no atomics) and applies
+// the bias and the ReLU.
+template <bool VEC>
+__global__ void __launch_bounds__(64 * LIN_MAX_WAVES) splitk_gemm_kernel(const GemmArgs g, int ks, float* part) {
+  extern __shared__ f32x4 red[];
+  const int s = blockIdx.z, k0 = s * ks;
+  GemmArgs gs = g;
+  gs.a = g.a + (long)k0 * g.a_k;
+  gs.b = g.b + (long)k0 * g.b_k;
+  gs.K = min(ks, g.K - k0);
+  gs.c = part + (long)s * g.M * g.N;
+  gs.c_m = g.N;
+  gs.bias = nullptr;
+  gs.relu = 0;
+  small_gemm_tile<false, false, VEC>(gs, red);
+}
+
+__global__ void __launch_bounds__(256) splitk_combine_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                             const float* __restrict__ bias, int relu,
+                                                             float* __restrict__ y, long y_m) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * N) return;
+  const int m = i / N, n = i - m * N;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[(long)s * M * N + i];  // split order: deterministic
+  if (bias != nullptr) v += bias[n];
+  if (relu) v = fmaxf(v, 0.f);
+  y[(long)m * y_m + n] = v;
+}
+
 // the forward operands qualify for the vector loads: rows contiguous along k, K a multiple of 4,
 // every row start 16-B aligned
 bool fwd_vec_ok(const GemmArgs& g) {
@@ -292,6 +325,41 @@ void launch_linear_fwd(const float* x, const float* w, const float* b, float* y,
     return;
   }
   launch(g, nullptr, s);
+}
+
+// splits of a split-K forward: enough workgroups to fill the chip (>= 256 over the output tiles),
+// each split a multiple of 64 (one wave batch) and at least 256 deep
+int linear_splitk_splits(int B, int K, int N) {
+  const int tiles = ((N + 15) / 16) * ((B + 15) / 16);
+  int S = 1;
+  while (tiles * S < 256 && K / (2 * S) >= 256) S *= 2;
+  return S;
+}
+
+// y[B][N] = act(x[B][K] W[N][K]^T + b) as S split-K partial GEMMs + one combine launch;
+// part: S * B * N floats of workspace
+void launch_linear_fwd_splitk(const float* x, const float* w, const float* b, float* y, float* part, int S, int B,
+                              int K, int N, int relu, hipStream_t s) {
+  if (S < 1 || K < S) throw std::runtime_error("linear_fwd_splitk: bad split count");
+  GemmArgs g{};
+  g.a = x; g.a_m = K; g.a_k = 1;
+  g.b = w; g.b_k = 1; g.b_n = K;
+  g.M = B; g.N = N; g.K = K; g.ones_col = -1;
+  const int ks = ((K + S - 1) / S + 63) / 64 * 64;
+  const int splits = (K + ks - 1) / ks;
+  GemmArgs gk = g;
+  gk.K = ks;  // (the waves of one split; the last split may be shorter)
+  const int waves = prepare(gk);
+  g.kpw = gk.kpw;
+  g.ncols = g.N;
+  const dim3 grid((unsigned)((N + 15) / 16), (unsigned)((B + 15) / 16), (unsigned)splits);
+  const bool vec = fwd_vec_ok(g) && ks % 4 == 0;
+  if (vec) hipLaunchKernelGGL(splitk_gemm_kernel<true>, grid, dim3(64 * waves), lds_bytes(waves), s, g, ks, part);
+  else hipLaunchKernelGGL(splitk_gemm_kernel<false>, grid, dim3(64 * waves), lds_bytes(waves), s, g, ks, part);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(splitk_combine_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, part, splits, B, N,
+                     b, relu, y, (long)N);
+  HIP_CHECK(hipGetLastError());
 }
 
 // logits[B][N] = x W^T + b with the softmax cross-entropy of every row fused in (N <= 16)

@@ -77,6 +77,11 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
 template <bool WT>
 struct DirectSinkT {
   static constexpr bool kTile = WT;  // fc1 / fc2 tiles finish in put_tile (below)
+  // WT, optional: put_tile's write-through stores wait until *gate >= gate_target (the pipelined
+  // step's conv ready counter): the samples' poll of that counter then does not queue behind the
+  // MLP tiles' write-through traffic (lenet_fused.hip PIPE flags & 32)
+  const unsigned* gate = nullptr;
+  unsigned gate_target = 0;
   __device__ __forceinline__ void put(int, int e, float g, float p, float m, const ReduceArgs& a) {
     sgd_finish<WT>(e, g, p, m, a);
   }
@@ -126,6 +131,12 @@ __device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, cons
                                                          const ReduceArgs& a) {
   constexpr int O = LAYER == 0 ? 120 : 84, I = LAYER == 0 ? 400 : 120, OFF = LAYER == 0 ? OFF_F1W : OFF_F2W;
   const int i = lane & 15, kq = lane >> 4, u = lane & 3;
+  if (gate != nullptr && lane == 0) {  // bounded: the samples' own wait on this counter has the timeout
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gate_target &&
+           wall_clock64() - t0 < 200000000ll)
+      __builtin_amdgcn_s_sleep(4);
+  }
   const bool iv = i0 + i < I;
   unsigned bv[4];  // this lane's column, rows o0 + 4 kq + j: bf16 bits (0 outside the layer)
 #pragma unroll

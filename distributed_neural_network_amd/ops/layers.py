@@ -326,6 +326,10 @@ class ReluFn(torch.autograd.Function):
 # while it runs the small ones as single-workgroup tiles (lenet fc1 forward: 19 us vs 5-9 us;
 # profiles/r2/linear/).  DNN_LINEAR_MFMA_MAX overrides (0: library everywhere).
 LINEAR_MFMA_MAX_MACS = int(os.environ.get("DNN_LINEAR_MFMA_MAX", 16 << 20))
+# forwards past that size with a long reduction (cifar-vgg's fc1: K = 4096) run as split-K MFMA
+# GEMMs + a fixed-order combine (linear.hip) instead of the library GEMM (DNN_LINEAR_SPLITK=0: off)
+LINEAR_SPLITK_MIN_K = 2048
+LINEAR_SPLITK = os.environ.get("DNN_LINEAR_SPLITK", "1") != "0"
 
 
 class XentFusion:
@@ -373,6 +377,12 @@ class LinearFn(torch.autograd.Function):
             elif B * K * N <= LINEAR_MFMA_MAX_MACS:
                 y = torch.empty(B, N, device=x.device, dtype=torch.float32)
                 _ext().linear_fwd(_p(x), _p(w), _p(b), _p(y), B, K, N, int(relu), _s(x))
+            elif LINEAR_SPLITK and K >= LINEAR_SPLITK_MIN_K:
+                ext = _ext()
+                S = ext.linear_splitk_splits(B, K, N)
+                y = torch.empty(B, N, device=x.device, dtype=torch.float32)
+                part = torch.empty(S * B * N, device=x.device, dtype=torch.float32)
+                ext.linear_fwd_splitk(_p(x), _p(w), _p(b), _p(y), _p(part), S, B, K, N, int(relu), _s(x))
             else:
                 y = torch.addmm(b, x, w.t())
                 if relu:

@@ -307,6 +307,8 @@ class HipEngine(Engine):
             self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
             # (uncached memory: every poll reads memory, lenet_fused.hip pipe_wait)
             self._pipe_ctr_ptr = self.ext.uncached_alloc(4 * 128)
+            # broadcast flags [parity][conv, mlp][sample], a 128-B line each (PIPE_FLAGS & 64)
+            self._pipe_flg_ptr = self.ext.uncached_alloc(4 * B * 128) if self.pipe_flags & 64 else 0
             self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -409,8 +411,10 @@ class HipEngine(Engine):
 
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
-    # lenet_fused.hip PipeCtl.flags: & 3 the ready-poll form, & 4 the early fc1 stream
-    pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "0"))
+    # lenet_fused.hip PipeCtl.flags: & 3 the ready-poll form, & 4 / 8 / 16 early fc1 streams, & 64 the
+    # last-arriver broadcast to per-sample flags (default: 17.9 vs 18.9 us/step with counter polls,
+    # profiles/r4/pipe_v7)
+    pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "64"))
 
     def _rows(self, par: int) -> dict:
         if par == 0:
@@ -457,7 +461,8 @@ class HipEngine(Engine):
                                       self._p(self.stage), self._pipe_ctr_ptr, par, 0 if first else 1,
                                       1 if first else self.ext.pipe_reduce_blocks(), slot_bv[par],
                                       self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                      stamps=0 if first else self._pipe_stamps, flags=self.pipe_flags)
+                                      stamps=0 if first else self._pipe_stamps, flags=self.pipe_flags,
+                                      flg=self._pipe_flg_ptr)
 
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
@@ -470,6 +475,7 @@ class HipEngine(Engine):
     def __del__(self) -> None:
         rg = getattr(self, "_rg", None)
         pc = getattr(self, "_pipe_ctr_ptr", None)
+        pf = getattr(self, "_pipe_flg_ptr", None)
         if rg is not None or pc is not None:
             try:
                 torch.cuda.synchronize(self.device)
@@ -477,6 +483,8 @@ class HipEngine(Engine):
                     self.ext.xgmi_free(rg["ptr"])
                 if pc is not None:
                     self.ext.xgmi_free(pc)
+                if pf:
+                    self.ext.xgmi_free(pf)
             except Exception:
                 pass
 

@@ -82,7 +82,7 @@ def test_conv2d_bf16_operands_track_fp32(B, C, H, K, pad, Cout):
 
 
 @pytest.mark.parametrize("B,K,N", [(64, 400, 120), (64, 120, 84), (3, 84, 10), (64, 4096, 256), (17, 130, 33),
-                                   (1, 5, 1)])
+                                   (1, 5, 1), (17, 2180, 33)])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("arena", [False, True])
 @pytest.mark.parametrize("mfma_max", [None, 0])
@@ -90,7 +90,7 @@ def test_linear_mfma_fwd_bwd(B, K, N, relu, arena, mfma_max, monkeypatch):
     """linear.hip (forward + bias + fused ReLU, data gradient, weight gradient with the bias
     gradient from the all-ones column, ReLU mask on the operand loads) vs the fp32 CPU path;
     arena=True writes the parameter gradients into preallocated views (the engine's mode)."""
-    if mfma_max is not None:  # 0: the library-GEMM path for every size
+    if mfma_max is not None:  # 0: past the small-GEMM kernels - split-K forward for K >= 2048, else library
         monkeypatch.setattr(L, "LINEAR_MFMA_MAX_MACS", mfma_max)
     else:  # the MFMA kernels for every size
         monkeypatch.setattr(L, "LINEAR_MFMA_MAX_MACS", 1 << 40)

@@ -20,6 +20,7 @@
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
+#   vgg              layer engine, cifar-vgg bf16 / fp32, split-K fc1 forward on / off
 set -e
 O=gpurun_out/${1:?usage: gpu_run.sh OUT step...}
 shift
@@ -72,6 +73,10 @@ for s in "$@"; do
                  --diag-windows 3 > "$O/$s.json" 2> "$O/$s.err" ;;
     fault2) timeout -k 10 400 python tools/fault_bench.py -n 2 --share-gpu > "$O/fault2.json" 2> "$O/fault2.log" ;;
     fault4) timeout -k 10 400 python tools/fault_bench.py -n 4 --share-gpu > "$O/fault4.json" 2> "$O/fault4.log" ;;
+    vgg) for dt in bf16 fp32; do for sk in 1 0; do
+           DNN_LINEAR_SPLITK=$sk timeout -k 10 200 python bench.py --model cifar-vgg --dtype $dt --steps 300 --warmup 30 \
+             --no-epoch > "$O/vgg_${dt}_splitk$sk.json" 2> "$O/vgg_${dt}_splitk$sk.err"
+         done; done ;;
     sweep:*)
       for b in $(echo "${s#sweep:}" | tr ',' ' '); do
         timeout -k 10 200 python bench.py --batch-size "$b" --steps 2000 --warmup 200 --no-epoch \

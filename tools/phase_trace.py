@@ -29,7 +29,7 @@ def pipe_main(reps: int = 50, batch: int = 64):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True)
     eng.attach(tr)
-    stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
+    stamps = torch.zeros(4096 + 64, dtype=torch.int64, device=eng.device)
     eng._pipe_stamps = stamps.data_ptr()
     nrw = (eng.ext.pipe_reduce_blocks() + 1) // 2
     recs = []
@@ -47,6 +47,8 @@ def pipe_main(reps: int = 50, batch: int = 64):
                          red_start=(bl[:nrw, 0] - t0) * 0.01, red_end=(bl[:nrw, 2] - t0) * 0.01,
                          smp_start=(bl[nrw:, 0] - t0) * 0.01, smp_end=(bl[nrw:, 2] - t0) * 0.01,
                          conv_ready=(s[12] - t0) * 0.01, mlp_ready=(s[13] - t0) * 0.01,
+                         poll_t=[(s[4096 + 2 * k] - t0) * 0.01 if s[4096 + 2 * k] else None for k in range(12)],
+                         poll_v=[int(s[4097 + 2 * k]) for k in range(12)],
                          a_done=(s[1] - t0) * 0.01, b_done=(s[2] - t0) * 0.01, c_done=(s[3] - t0) * 0.01,
                          img=(s[9] - t0) * 0.01, end0=(s[7] - t0) * 0.01))
     rr = recs[5:]
@@ -62,6 +64,10 @@ def pipe_main(reps: int = 50, batch: int = 64):
     print(f"  sample block 0 first conv poll {med(lambda x: x['poll0']):.2f} us, polls {med(lambda x: x['polls']):.0f}")
     print(f"sample blocks start med {med(lambda x: np.median(x['smp_start'])):.2f} max {med(lambda x: x['smp_start'].max()):.2f}"
           f"  end med {med(lambda x: np.median(x['smp_end'])):.2f} max {med(lambda x: x['smp_end'].max()):.2f} us")
+    last = rr[-1]
+    print("  last rep: conv adds performed (sorted):", " ".join(f"{x:.2f}" for x in sorted(last["red_add"][:23])))
+    print("  last rep: conv polls (t us, count):", " ".join(f"({t:.2f},{v})" for t, v in zip(last["poll_t"], last["poll_v"])
+                                                        if t is not None))
     for k in ("img", "conv_ready", "a_done", "b_done", "mlp_ready", "c_done", "end0"):
         print(f"  sample block 0 {k:10s} {med(lambda x: x[k]):8.2f} us")
 
