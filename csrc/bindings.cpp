@@ -214,6 +214,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("par"), py::arg("wait"), py::arg("nred"), py::arg("bvalid"), py::arg("err"), py::arg("timeout_s"),
      py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0, py::arg("flg") = 0);
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });
+  m.def("pipe_groups", []() { return dnn::pipe_groups(); });
   m.def("init", []() { dnn::init_kernels(); });
   // ---- Linear layers on MFMA (kernels/linear.hip) ----
   m.def("linear_fwd", [](u x, u w, u b, u y, int B, int K, int N, int relu, u stream) {

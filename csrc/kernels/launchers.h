@@ -72,17 +72,17 @@ struct ReduceArgs {
 // The pipelined step's per-launch control (lenet_fused.hip, PIPE): launch i of a chunk runs
 // the batch reduction + SGD of step i - 1 (its rows in the other parity buffer set) in its
 // first workgroups and the samples of step i in the rest; the samples wait for the reduction's
-// ready counters before they load the weights it writes.
+// ready flags (conv1, conv2, MLP groups) before they load the weights it writes.
 struct PipeCtl {
-  unsigned* ctr = nullptr;        // [2 parities][conv, mlp] ready counters, 128 B apart, in uncached memory
+  unsigned* ctr = nullptr;        // [2 parities][3 groups] arrival counters, 128 B apart, in uncached memory
   int par = 0;                    // this launch's parity (launch index & 1)
-  int wait = 0;                   // 1: a reduction runs in this launch, wait for its counters
+  int wait = 0;                   // 1: a reduction runs in this launch, wait for its flags
   int nred = 0;                   // reduction blocks of this launch (0, 1 = bookkeeping only, all)
   const int32_t* bvalid = nullptr;  // this launch's samples' valid count (its bookkeeping slot)
   unsigned* err = nullptr;          // sticky error word: a ready wait timed out (never a hang)
-  unsigned* flg = nullptr;          // optional broadcast flags (uncached, [2][2][batch] x 128 B): see pipe_reduce
+  unsigned* flg = nullptr;          // ready flags (uncached, [2][3][batch] x 128 B): see pipe_reduce
   long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
-  int flags = 0;  // & 3: poll form; & 4: stream fc1 in phase A when the MLP is ready (& 8: by wave 7 alone)
+  int flags = 0;                    // & 1: no mid-phase-B fc1 stream (measurement)
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
@@ -100,6 +100,7 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
                              const int32_t* next_ids, unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc,
                              hipStream_t stream);
 int pipe_reduce_blocks();  // reduction blocks of a full PIPE launch (2 per workgroup)
+int pipe_groups();         // ready groups (counters / flags per parity)
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,
                        int count, const float* master, const bf16* shadow, float* loss, int32_t* correct,
                        hipStream_t stream);

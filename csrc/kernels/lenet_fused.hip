@@ -262,140 +262,103 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
 // A (ingest) instead of sitting between two kernel boundaries.  Step i - 1's rows are in the
 // other parity's buffers (written by launch i - 1: visible across the kernel boundary).  The
 // new weights are a hand-off INSIDE the launch (MI355X guide §6 G16, R1): the reduction stores
-// master / bf16 images write-through (sc1), every storing wave drains (vmcnt(0)), a workgroup
-// barrier, then one lane per reduction block adds 1 to its group's ready counter; the samples
-// poll the counter from one lane (a returning atomic add of 0, s_sleep), pass a workgroup barrier
-// and load every weight byte with sc1 loads (buffer loads / LDS-DMA with sc1) - no acquire fence.
-// Reduction blocks in start order: conv slab columns (needed first: phase B), bookkeeping, MLP
-// tiles / bias columns (needed at phase C: the fc1 stream).
+// master biases / bf16 images write-through (sc1), every storing wave drains (vmcnt(0)), a
+// workgroup barrier, then one lane per reduction block adds 1 to its group's counter; the block
+// whose returning add completes the group stores a ready flag for every sample workgroup; the
+// samples poll their own flag from one lane and load every weight byte with sc1 loads (buffer
+// loads / LDS-DMA with sc1) - no acquire fence.
+// Three ready groups, in the order the samples need them (reduction blocks start in this order):
+//   PG_C1  conv1 weights + bias (phase B; with the head of conv2's - the group's last block is
+//          shared), waited for by thread 0 after phase A's record build;
+//   PG_C2  the rest of conv2 (phase C forward, phase E dgrad image), waited for by each wave
+//          after phase B's first MFMA round - its fragments load behind the second;
+//   PG_MLP fc weights + biases (phase C: the fc1 LDS stream; phase D fragments): checked in the
+//          same poll round - a wave streams its part of fc1 mid-phase B if the group is
+//          already complete, else after phase B once it is.
 constexpr int PIPE_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
 constexpr int PIPE_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT;
+constexpr int PIPE_C1_BLOCKS = (SLAB_C2W * SPLIT + RT - 1) / RT;  // conv1 W + b: slab [0, SLAB_C2W)
+constexpr int PIPE_C2_BLOCKS = PIPE_CONV_BLOCKS - PIPE_C1_BLOCKS;
 constexpr int PIPE_BLOCKS = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS + 1;
-constexpr int PIPE_CTR_STRIDE = 32;  // ready counters 128 B apart: [parity][conv, mlp] = 4 lines
+constexpr int PG_C1 = 0, PG_C2 = 1, PG_MLP = 2, PIPE_GROUPS = 3;
+constexpr int PIPE_CTR_STRIDE = 32;  // counters and flags 128 B apart, each on a line of its own
 static_assert(PIPE_BLOCKS == GRAD_REDUCE_BLOCKS, "the pipelined launch runs the whole grad_reduce");
+static_assert(PIPE_C2_BLOCKS > 0, "conv2 keeps blocks of its own");
 int pipe_reduce_blocks() { return PIPE_BLOCKS; }
+int pipe_groups() { return PIPE_GROUPS; }
 
-// broadcast flags (PipeCtl::flg): [parity][conv, mlp][sample], one 128-B line each
+__device__ __forceinline__ int pipe_group_blocks(int grp) {
+  return grp == PG_C1 ? PIPE_C1_BLOCKS : grp == PG_C2 ? PIPE_C2_BLOCKS : PIPE_MLP_BLOCKS;
+}
+// ready counters [parity][group]; broadcast flags [parity][group][sample]
+__device__ __forceinline__ long pipe_ctr_index(int par, int grp) { return (long)(PIPE_GROUPS * par + grp) * PIPE_CTR_STRIDE; }
 __device__ __forceinline__ long pipe_flag_index(int par, int grp, int b, int batch) {
-  return ((long)(2 * par + grp) * batch + b) * PIPE_CTR_STRIDE;
+  return ((long)(PIPE_GROUPS * par + grp) * batch + b) * PIPE_CTR_STRIDE;
 }
 
 // Reduction workgroup `wg` of a PIPE launch: two 256-thread reduction blocks.
 __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255;
-  if (wg == 0 && threadIdx.x == 0) {  // the next launch's counters start from zero (kernel boundary)
-    pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1))] = 0u;
-    pc.ctr[PIPE_CTR_STRIDE * (2 * (pc.par ^ 1) + 1)] = 0u;
-  }
-  if (wg == 0 && pc.flg != nullptr)  // ... and its broadcast flags
-    for (int i = threadIdx.x; i < 2 * a.batch; i += blockDim.x)
+  if (wg == 0) {  // the next launch's counters and flags start from zero (kernel boundary)
+    if (threadIdx.x < PIPE_GROUPS) pc.ctr[pipe_ctr_index(pc.par ^ 1, threadIdx.x)] = 0u;
+    for (int i = threadIdx.x; i < PIPE_GROUPS * a.batch; i += blockDim.x)
       pc.flg[pipe_flag_index(pc.par ^ 1, i / a.batch, i % a.batch, a.batch)] = 0u;
-  int grp = -1;  // ready counter this block signals: 0 conv, 1 MLP, -1 none (bookkeeping)
+  }
+  int grp = -1;  // ready group this block signals (-1: none, the bookkeeping block)
   if (m < pc.nred) {
     int rblk = 0;  // (nred == 1: the bookkeeping alone - the launch range holds no elements)
     if (pc.nred > 1) {
-      if (m < PIPE_CONV_BLOCKS) { rblk = PIPE_MLP_BLOCKS + m; grp = 0; }
+      if (m < PIPE_CONV_BLOCKS) { rblk = PIPE_MLP_BLOCKS + m; grp = m < PIPE_C1_BLOCKS ? PG_C1 : PG_C2; }
       else if (m == PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS;
-      else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = 1; }
+      else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = PG_MLP; }
     }
     WtSink sk;
-    if (grp == 1 && (pc.flags & 32)) {  // MLP tiles store after the conv weights are out
-      sk.gate = pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par);
-      sk.gate_target = PIPE_CONV_BLOCKS;
-    }
     grad_reduce_body<false>(a, sk, rblk, rtid);
   }
   if (stamps != nullptr && threadIdx.x == 0) stamps[16 + 4 * wg + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its write-through stores
   __syncthreads();
-  if (pc.flg != nullptr) {
-    // broadcast form: the LAST block of a group (its returning add saw every other block's add,
-    // each made after that block drained its stores) stores one flag per sample workgroup, each on
-    // a line of its own - 64 pollers of ONE counter word serialize at its memory channel (a poll
-    // took 1-2 us there: profiles/r4/pipe_v5, pipe_v6)
-    if ((rtid >> 6) == 0 && grp >= 0) {  // wave 0 of the block
-      unsigned old = 0;
-      if (rtid == 0)
-        old = __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (stamps != nullptr && rtid == 0 && half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime();
-      const unsigned last = grp == 0 ? PIPE_CONV_BLOCKS - 1 : PIPE_MLP_BLOCKS - 1;
-      if (old == last)
-        for (int b = rtid; b < a.batch; b += 64)
-          __hip_atomic_store(pc.flg + pipe_flag_index(pc.par, grp, b, a.batch), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  if (rtid == 0 && grp >= 0) {
-    if (stamps != nullptr) {  // diagnostic: when the add has been performed
-      const unsigned v = __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      if (half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime() + 0 * v;
-    } else {
-      __hip_atomic_fetch_add(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  // the LAST block of a group (its returning add saw every other block's add, each made after
+  // that block drained its stores) stores one flag per sample workgroup, each on a line of its
+  // own: 64 pollers of ONE counter word serialize at its memory channel (a poll took 1-2 us
+  // there: profiles/r4/pipe_v5, pipe_v6), their own flags return every ~0.3 us (pipe_v7)
+  if ((rtid >> 6) == 0 && grp >= 0) {  // wave 0 of the block
+    unsigned old = 0;
+    if (rtid == 0)
+      old = __hip_atomic_fetch_add(pc.ctr + pipe_ctr_index(pc.par, grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (stamps != nullptr && rtid == 0 && half == 0) stamps[16 + 4 * wg + 3] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (old == (unsigned)pipe_group_blocks(grp) - 1u)
+      for (int b = rtid; b < a.batch; b += 64)
+        __hip_atomic_store(pc.flg + pipe_flag_index(pc.par, grp, b, a.batch), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// One lane waits until a ready counter reaches `target` (returning-atomic polls).  Bounded: past the
-// timeout it sets the sticky error word and returns (the step then runs on the old weights and
-// the host raises at the next check) - never a hang.
-// also != nullptr: each poll round also reads the MLP counter (in flight with the first), so its
-// value at the round that saw `target` costs no extra round trip
-__device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, unsigned target, long long* diag = nullptr,
-                                          unsigned* also = nullptr, int b = 0, int batch = 0) {
-  // (broadcast form: this sample workgroup's own flag, set to 1 by the group's last block)
-  const unsigned* c = pc.flg != nullptr ? pc.flg + pipe_flag_index(pc.par, grp, b, batch)
-                                        : pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + grp);
-  if (pc.flg != nullptr) target = 1u;
+// One lane waits until this sample workgroup's flag of group `grp` is set (uncached sc1 loads
+// ~0.3 us apart).  also >= 0: each poll round also loads that group's flag (in flight with the
+// first), its value at the round that ended the wait returned in *also_set - no extra round trip.
+// Bounded: past the timeout it sets the sticky error word and returns (the step then runs on
+// stale weights and the host raises at the next check) - never a hang.
+__device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int batch, long long* diag = nullptr,
+                                          int also = -1, bool* also_set = nullptr) {
+  const unsigned* f = pc.flg + pipe_flag_index(pc.par, grp, b, batch);
+  const unsigned* g = pc.flg + pipe_flag_index(pc.par, also < 0 ? grp : also, b, batch);
   if (__hip_atomic_load(pc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // failed before: no wait
   const long long t0 = wall_clock64();
   if (diag != nullptr) diag[0] = t0;
   long long polls = 0;
-  // The counters live in UNCACHED memory, each on its own 128-B line: a poll is a plain sc1 load
-  // that goes to memory every time.  (In cached memory an sc1 poll saw the final count ~3 us late -
-  // its first read left the line in this XCD's L2 - and a returning atomic add of 0 from 64 pollers
-  // took ~1.2 us per poll on the contended line: profiles/r4/pipe_v1.)
-  // flags & 3 (the poll form, measured in profiles/r4/pipe_v2): 0 = one load, s_sleep, the next;
-  // 1 = two in flight (a new load is issued before the previous one is checked); 2 = four loads
-  // ~0.1 us apart per round, checked together
-  const int form = pc.flags & 3;
-  if (form == 1) {
-    unsigned prev = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (true) {
-      __builtin_amdgcn_s_sleep(8);
-      const unsigned cur = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev >= target) break;
-      prev = cur;
-      ++polls;
-      if (diag != nullptr) diag[1] = polls;
-      if (wall_clock64() - t0 > pc.timeout_ticks) {
-        __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-    return;
-  }
   while (true) {
-    unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (also != nullptr)
-      *also = __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned w = also >= 0 ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     if (diag != nullptr && polls < 12) {  // (t, value) of each poll's return: stamps[4096 + 2 k]
       diag[4082 + 2 * polls] = (long long)__builtin_amdgcn_s_memrealtime();
       diag[4083 + 2 * polls] = v;
     }
-    if (form == 2) {
-      __builtin_amdgcn_s_sleep(4);
-      const unsigned v1 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_sleep(4);
-      const unsigned v2 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_sleep(4);
-      const unsigned v3 = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v = max(max(v, v1), max(v2, v3));
+    if (v != 0u) {
+      if (also_set != nullptr) *also_set = w != 0u;
+      break;
     }
-    if (v >= target) break;
     ++polls;
     if (diag != nullptr) diag[1] = polls;
     __builtin_amdgcn_s_sleep(2);
@@ -615,17 +578,25 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else im = reinterpret_cast<const uint4*>(img)[min(tid, 191)];
   bf16x8 bw1[4], bw2[8];  // conv1 / conv2 forward B fragments (optimizer-packed images)
   float bias_c1 = 0.f, bias_c2 = 0.f;
-  bool fc1_early = false;  // PIPE: the fc1 stream left early (the MLP reduction was ready) -
-  bool fc1_mid = false;    //   in phase A, or (fc1_mid) after phase B's first round
-  auto load_conv_w = [&]() {
+  auto load_conv1_w = [&]() {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) bw1[sk] = wr.w8(SH_W1F + ((4 * sk + fg) * 16 + fr) * 8);
+    bias_c1 = wr.f(OFF_C1B + min(fr, 5));
+  };
+  auto load_conv2_w = [&]() {
 #pragma unroll
     for (int sk = 0; sk < 8; ++sk) bw2[sk] = wr.w8(SH_W2F + ((4 * sk + fg) * 16 + fr) * 8);
-    bias_c1 = wr.f(OFF_C1B + min(fr, 5));
     bias_c2 = wr.f(OFF_C2B + fr);
   };
-  if constexpr (!PIPE) load_conv_w();  // (PIPE: after the conv reduction is ready, below)
+  auto consume_conv2_w = [&]() {
+#pragma unroll
+    for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
+    consume(bias_c2);
+  };
+  if constexpr (!PIPE) {  // (PIPE: conv1's once its reduction is ready, below; conv2's in phase B)
+    load_conv1_w();
+    load_conv2_w();
+  }
   for (int i = tid; i < 6 * 14 * 20; i += NT) P1[i] = (bf16)0.f;
   if (tid < 16) A0B[400 + tid] = (bf16)0.f;                                   // MLP operand padding
   else if (tid < 24) H1B[120 + tid - 16] = (bf16)0.f;
@@ -638,42 +609,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   STAMP(9);
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
   if constexpr (PIPE) {
-    // the conv weights are the previous step's reduction's: one lane waits for its conv blocks
-    // (the image and its records need none of it, so they are done first); the barrier releases
-    // the other waves, then every wave loads its fragments (sc1) - waited for at phase B's first
-    // MFMA, so the R1 records' barrier below is this one
-    if (tid == 0) {
-      int early = 1;  // the MLP weights are ready too: stream fc1 now, as the serial step does
-      if (pc.wait) {
-        unsigned mlp_seen = 0;
-        pipe_wait(pc, 0, PIPE_CONV_BLOCKS, stamp ? stamps + 14 : nullptr, (pc.flags & 16) ? &mlp_seen : nullptr, b,
-                  batch);
-        if (pc.flags & 16) early = mlp_seen >= (unsigned)PIPE_MLP_BLOCKS ? 2 : 0;  // (2: stream mid-phase B)
-        else
-          early = (pc.flags & 12) != 0 && __hip_atomic_load(pc.ctr + PIPE_CTR_STRIDE * (2 * pc.par + 1),
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                              (unsigned)PIPE_MLP_BLOCKS;
-      }
-      *reinterpret_cast<int*>(smem + L_MISC) = early;
-    }
+    // conv1's weights are the previous step's reduction's: one lane waits for its group (the
+    // image and its records need none of it, so they are done first); the barrier releases the
+    // other waves, then every wave loads its fragments (sc1) - waited for at phase B's first MFMA
+    if (tid == 0 && pc.wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr);
     STAMP(12);
     lds_barrier();
-    load_conv_w();
-    const int how = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + L_MISC));
-    fc1_early = how != 0;
-    fc1_mid = how == 2;
+    load_conv1_w();
   } else {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
-#pragma unroll
-    for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
     consume(bias_c1);
-    consume(bias_c2);
+    consume_conv2_w();
   }
   STAMP(11);
   // fc1: 94 wave-instructions x 1 KB = 96,256 B (fc1 + the head of fc1.bias, all in-arena);
   // 12 per wave with the index clamped (a duplicate copies identical bytes).  Issued here, or
-  // (PIPE) once the MLP reduction is ready, at the start of phase C
+  // (PIPE) per wave once the MLP reduction is ready: during or right after phase B
   auto stream_fc1 = [&]() {
     const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
@@ -686,34 +638,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if constexpr (!PIPE) {
     stream_fc1();
     lds_barrier();
-  } else if (fc1_mid) {
-    // (streamed after phase B's first MFMA round, below: its fragments have landed by then)
-  } else if (fc1_early && (pc.flags & 8)) {
-    // (flags & 8: wave 7 alone streams the whole of fc1 - 94 wave-instructions - once its own conv
-    // fragments have landed; the other waves start phase B without waiting for theirs here)
-    if (wave == 7) {
-#pragma unroll
-      for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
-#pragma unroll
-      for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
-      consume(bias_c1);
-      consume(bias_c2);
-      const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
-      const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
-      for (int i = 0; i < 94; ++i) dma16_sc1(f1src + i * 64 + lane, base + (uint32_t)i * 1024u);
-    }
-  } else if (fc1_early) {
-    // (the MLP weights were ready when the conv weights were: the sc1 stream, as above; the conv
-    // fragments are waited for first - vmcnt counts in issue order, so a fragment wait after the
-    // DMA would wait for the whole 96 KB)
-#pragma unroll
-    for (int sk = 0; sk < 4; ++sk) consume(bw1[sk]);
-#pragma unroll
-    for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
-    consume(bias_c1);
-    consume(bias_c2);
-    stream_fc1();
   }
+  bool fc1_out = !PIPE;  // PIPE: this wave has issued its part of the fc1 stream
   STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
@@ -769,26 +695,36 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       epilogue(t1, acc1);
       epilogue(t2, acc2);
       if (four) epilogue(48, acc3);
-      if (PIPE && fc1_mid && r == 0) {
-        // the MLP weights were ready when the conv weights were: stream fc1 now, behind this
-        // round's MFMAs (which waited for bw1); bw2 / the biases are waited for first (issued with
-        // bw1, so already in) - vmcnt counts in issue order, a later wait would drain the DMA
-#pragma unroll
-        for (int sk = 0; sk < 8; ++sk) consume(bw2[sk]);
-        consume(bias_c1);
-        consume(bias_c2);
-        stream_fc1();
+      if (PIPE && r == 0) {
+        // conv2's group: lane 0 of each wave waits (the wave's other lanes with it) - with the MLP
+        // flag in the same poll round.  If the MLP group is complete too, the wave's part of the
+        // fc1 stream goes out first (the conv2 fragments after it: phase C's first use of them
+        // then waits for both, issued a whole round earlier); else the fragments alone, consumed
+        // before the stream is issued after phase B (vmcnt counts in issue order)
+        int mlp = 0;
+        if (lane == 0) {
+          bool m = false;
+          if (pc.wait) pipe_wait(pc, PG_C2, b, batch, nullptr, (pc.flags & 1) ? -1 : PG_MLP, &m);
+          else m = true;  // (no reduction in this launch: every weight is the previous kernel's)
+          mlp = m && !(pc.flags & 1);
+        }
+        if (__builtin_amdgcn_readfirstlane(mlp)) {
+          stream_fc1();
+          fc1_out = true;
+        }
+        load_conv2_w();
       }
     }
   }
   if constexpr (PIPE) {
-    if (!fc1_early && tid == 0) pipe_wait(pc, 1, PIPE_MLP_BLOCKS, nullptr, nullptr, b, batch);  // (released by the barrier)
+    if (!fc1_out) {  // the MLP group was not complete mid-phase B: this wave waits for it here
+      if (lane == 0 && pc.wait) pipe_wait(pc, PG_MLP, b, batch);
+      consume_conv2_w();
+      stream_fc1();
+    }
     STAMP(13);
   }
   lds_barrier();
-  if constexpr (PIPE) {
-    if (!fc1_early) stream_fc1();  // first, so the fragment loads below are waited for after it
-  }
 
   STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============
@@ -1362,8 +1298,10 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
   init_kernels();
   // the shapes the kernel assumes: every reduction block of a full launch (conv first), or the
   // bookkeeping alone; staged images; a ready wait only behind a full reduction
-  if (stage == nullptr || next_ids == nullptr || pc.bvalid == nullptr || pc.ctr == nullptr || pc.err == nullptr)
-    throw std::runtime_error("fused_train_pipe: needs the stage, its next_ids / bvalid slot, the counters and error word");
+  if (stage == nullptr || next_ids == nullptr || pc.bvalid == nullptr || pc.ctr == nullptr || pc.err == nullptr ||
+      pc.flg == nullptr)
+    throw std::runtime_error(
+        "fused_train_pipe: needs the stage, its next_ids / bvalid slot, the counters, flags and error word");
   if (!(pc.nred == PIPE_BLOCKS || pc.nred == 1) || (pc.wait && pc.nred != PIPE_BLOCKS) || (pc.par & ~1))
     throw std::runtime_error("fused_train_pipe: nred must be the whole reduction or the bookkeeping alone");
   if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || red.rg != nullptr || !red.fuse_sgd)

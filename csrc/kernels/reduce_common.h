@@ -17,10 +17,13 @@ __device__ __forceinline__ void st_wt(bf16* p, bf16 v) {
   __hip_atomic_store(reinterpret_cast<unsigned short*>(p), __builtin_bit_cast(unsigned short, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// write_shadow (common.h) with write-through stores: the same positions, the same values
+// write_shadow (common.h) with write-through stores where the samples of the same launch read
+// the bytes: the kernel-ready images and the fc3 rows.  The row-major conv copy and every bias
+// copy are read by later launches only (the samples take the biases from the fp32 master): plain.
 __device__ __forceinline__ void write_shadow_wt(bf16* __restrict__ sh, int e, float p) {
   const bf16 v = (bf16)p;
-  st_wt(sh + e, v);
+  if (e >= OFF_F3W && e < OFF_F3W + 840) st_wt(sh + e, v);
+  else sh[e] = v;
   if (e >= OFF_C1W && e < OFF_C1W + 450) {
     const int r = e - OFF_C1W, n = r / 75, rem = r - 75 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
     st_wt(sh + SH_W1F + ((c * 5 + ky) * 16 + n) * 8 + kx, v);

@@ -297,18 +297,19 @@ class HipEngine(Engine):
             self._rg_buffers()  # (allocated up front: never inside a graph capture)
         if self.pipeline:
             # the second parity's per-sample rows (the first is a0 .. correct above), the second
-            # {bvalid, next_ids} bookkeeping slot (bvalid in state[2]), the ready counters
-            # [parity][conv, mlp] and the sticky wait-timeout word
+            # {bvalid, next_ids} bookkeeping slot (bvalid in state[2]), the ready counters and
+            # flags and the sticky wait-timeout word
             self._rows2 = dict(a0=torch.zeros_like(self.a0), h1=torch.zeros_like(self.h1),
                                h2=torch.zeros_like(self.h2), z1=torch.zeros_like(self.z1),
                                z2=torch.zeros_like(self.z2), z3=torch.zeros_like(self.z3),
                                slab=torch.zeros_like(self.slab), loss=torch.zeros_like(self.loss),
                                correct=torch.zeros_like(self.correct))
             self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
-            # (uncached memory: every poll reads memory, lenet_fused.hip pipe_wait)
-            self._pipe_ctr_ptr = self.ext.uncached_alloc(4 * 128)
-            # broadcast flags [parity][conv, mlp][sample], a 128-B line each (PIPE_FLAGS & 64)
-            self._pipe_flg_ptr = self.ext.uncached_alloc(4 * B * 128) if self.pipe_flags & 64 else 0
+            # arrival counters [parity][group] and ready flags [parity][group][sample], a 128-B line
+            # each, in uncached memory: every poll reads memory (lenet_fused.hip pipe_wait)
+            ng = self.ext.pipe_groups()
+            self._pipe_ctr_ptr = self.ext.uncached_alloc(2 * ng * 128)
+            self._pipe_flg_ptr = self.ext.uncached_alloc(2 * ng * B * 128)
             self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -411,10 +412,8 @@ class HipEngine(Engine):
 
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
-    # lenet_fused.hip PipeCtl.flags: & 3 the ready-poll form, & 4 / 8 / 16 early fc1 streams, & 64 the
-    # last-arriver broadcast to per-sample flags (default: 17.9 vs 18.9 us/step with counter polls,
-    # profiles/r4/pipe_v7)
-    pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "64"))
+    # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
+    pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "0"))
 
     def _rows(self, par: int) -> dict:
         if par == 0:

@@ -11,6 +11,8 @@
 #   tests:<expr>     GPU tests selected by -k <expr>
 #   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
 #   k20f32           the same, --dtype fp32
+#   envk20:VAR=val   k20 with one environment setting
+#   winfit           bench --steps 10..160 with --diag-windows (wall vs event time per window)
 #   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32    bench.py default window (5000 / 500), bf16 / fp32
@@ -40,6 +42,13 @@ for s in "$@"; do
     longpipe) DNN_PIPELINE=1 timeout -k 10 300 python bench.py > "$O/$s.json" 2> "$O/$s.err" ;;
     k20serial) DNN_PIPELINE=0 timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     longserial) DNN_PIPELINE=0 timeout -k 10 300 python bench.py > "$O/$s.json" 2> "$O/$s.err" ;;
+    envk20:*)  # the driver's window under one runtime env setting: envk20:VAR=value
+      kv="${s#envk20:}"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/k20_$n.json" 2> "$O/k20_$n.err" ;;
+    winfit)  # the window's fixed cost: bench at several step counts, wall vs GPU events per window
+      for k in 10 20 40 80 160; do
+        timeout -k 10 150 python bench.py --steps $k --warmup 5 --diag-windows 3 > "$O/winfit_k$k.json" 2> "$O/winfit_k$k.err"
+      done ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;

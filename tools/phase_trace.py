@@ -24,8 +24,8 @@ PHASES = ["A ingest+staging", "B conv1 fwd", "C conv2 fwd", "D MLP fwd+CE", "D' 
 
 def pipe_main(reps: int = 50, batch: int = 64):
     """--pipe: the pipelined step's merged launch (lenet_fused.hip PIPE): reduction workgroups
-    (start / end), the samples' ready waits (conv: before phase B, MLP: before phase C) and the
-    sample phases, medians over repeats of 1-step chunks (launch 1 = reduction + samples)."""
+    (start / end), the samples' ready waits (conv1: before phase B; conv2 + MLP: mid-phase B, the
+    MLP again after phase B if it was not complete then) and the sample phases, medians over repeats of 1-step chunks (launch 1 = reduction + samples)."""
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True)
     eng.attach(tr)
@@ -53,7 +53,9 @@ def pipe_main(reps: int = 50, batch: int = 64):
                          img=(s[9] - t0) * 0.01, end0=(s[7] - t0) * 0.01))
     rr = recs[5:]
     med = lambda f: float(np.median([f(x) for x in rr]))  # noqa: E731
-    # reduction WG order: conv blocks 0..44 (WGs 0..22), bookkeeping (WG 22 half 1), MLP (WGs 23..56)
+    # reduction WG order: conv1 group blocks 0..7 (WGs 0..3), conv2 blocks 8..44 (WGs 4..22),
+    # bookkeeping (WG 22 half 1), MLP (WGs 23..56)
+    print(f"  conv1 WGs (0-3) add performed med {med(lambda x: np.median(x['red_add'][:4])):.2f} max {med(lambda x: x['red_add'][:4].max()):.2f}")
     print(f"reduction WGs start med {med(lambda x: np.median(x['red_start'])):.2f} max {med(lambda x: x['red_start'].max()):.2f} us")
     print(f"  conv WGs (0-22) end med {med(lambda x: np.median(x['red_end'][:23])):.2f} max {med(lambda x: x['red_end'][:23].max()):.2f}")
     print(f"  MLP WGs (23-56) end med {med(lambda x: np.median(x['red_end'][23:])):.2f} max {med(lambda x: x['red_end'][23:].max()):.2f}")
@@ -68,6 +70,7 @@ def pipe_main(reps: int = 50, batch: int = 64):
     print("  last rep: conv adds performed (sorted):", " ".join(f"{x:.2f}" for x in sorted(last["red_add"][:23])))
     print("  last rep: conv polls (t us, count):", " ".join(f"({t:.2f},{v})" for t, v in zip(last["poll_t"], last["poll_v"])
                                                         if t is not None))
+    # conv_ready: thread 0 saw conv1's flag; mlp_ready: wave 0 past its end-of-phase-B MLP check
     for k in ("img", "conv_ready", "a_done", "b_done", "mlp_ready", "c_done", "end0"):
         print(f"  sample block 0 {k:10s} {med(lambda x: x[k]):8.2f} us")
 
