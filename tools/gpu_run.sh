@@ -18,6 +18,7 @@
 #   long | long32    bench.py default window (5000 / 500), bf16 / fp32
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
+#   pmcserial:<..>   the same with the pipelined step off
 #   phase | phase32 | phasepipe  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
@@ -45,9 +46,14 @@ for s in "$@"; do
     envk20:*)  # the driver's window under one runtime env setting: envk20:VAR=value
       kv="${s#envk20:}"; n=$(echo "$kv" | tr '=/' '__')
       env "$kv" timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/k20_$n.json" 2> "$O/k20_$n.err" ;;
-    winfit)  # the window's fixed cost: bench at several step counts, wall vs GPU events per window
-      for k in 10 20 40 80 160; do
-        timeout -k 10 150 python bench.py --steps $k --warmup 5 --diag-windows 3 > "$O/winfit_k$k.json" 2> "$O/winfit_k$k.err"
+    winfit|winfit:*)  # the window's fixed cost: bench at several step counts, wall vs GPU events per
+      # window (winfit:VAR=val[,k1,k2..]: under one env setting, for the given step counts)
+      spec="${s#winfit}"; spec="${spec#:}"; kv="${spec%%,*}"; ks="10 20 40 80 160"
+      [ "$spec" != "$kv" ] && ks=$(echo "${spec#*,}" | tr ',' ' ')
+      [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
+      for k in $ks; do
+        env "$kv" timeout -k 10 150 python bench.py --steps $k --warmup 5 --diag-windows 3 \
+          > "$O/winfit_${n}_k$k.json" 2> "$O/winfit_${n}_k$k.err"
       done ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
@@ -61,10 +67,12 @@ for s in "$@"; do
       db=$(find "$O/$s" -name '*.db' | head -n 1 || true)
       [ -n "$db" ] && python tools/kstats.py "$db" --steps 2200 > "$O/${s}_kernel_stats.txt" 2>&1 || true
       unset DNN_PIPELINE ;;
-    pmc:*)
-      c="${s#pmc:}"; n=$(echo "$c" | tr ',' '_' | cut -c1-60)
-      timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- \
-        python3 bench.py --steps 200 --warmup 20 --no-epoch > "$O/pmc_$n.log" 2>&1 ;;
+    pmc:*|pmcserial:*)
+      c="${s#*:}"; n=$(echo "$c" | tr ',' '_' | cut -c1-60); pre=pmc
+      [ "${s%%:*}" = pmcserial ] && { export DNN_PIPELINE=0; pre=pmcserial; }
+      timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } --kernel-trace --output-format csv -d "$O/${pre}_$n" -o run -- \
+        python3 bench.py --steps 200 --warmup 20 --no-epoch > "$O/${pre}_$n.log" 2>&1
+      unset DNN_PIPELINE ;;
     phase) timeout -k 10 300 python tools/phase_trace.py > "$O/phase.txt" 2>&1 ;;
     phasepipe) timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe.txt" 2>&1 ;;
     pipeflags:*)  # the pipelined step's variants: phase trace + 2000-step bench per DNN_PIPE_FLAGS value
@@ -75,6 +83,11 @@ for s in "$@"; do
       done
       DNN_PIPELINE=0 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k_serial.json" \
         2> "$O/b2k_serial.err" ;;
+    b2kenv:*)  # phase trace + 2000-step bench of the pipelined step under one env setting (VAR=val)
+      kv="${s#b2kenv:}"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe_$n.txt" 2>&1
+      env "$kv" DNN_PIPELINE=1 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch \
+        > "$O/b2k_$n.json" 2> "$O/b2k_$n.err" ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;
