@@ -198,9 +198,13 @@ def main():
     cur.run(args.warmup)
     if getattr(engine, "pipeline", False) and engine._pipe_ok():
         torch.cuda.synchronize(device)
-        if engine.pipe_failed():  # a ready wait timed out (never seen): time the serial step instead
-            stamp(comm.rank, "pipelined step: a ready wait timed out in the warmup; using the serial step")
-            engine.pipeline = False
+        if engine.pipe_failed():  # a wait timed out (never seen): fall back one level and time that
+            if engine.persist:
+                stamp(comm.rank, "persistent launch: a wait timed out in the warmup; using one launch per step")
+                engine.persist = False
+            else:
+                stamp(comm.rank, "pipelined step: a ready wait timed out in the warmup; using the serial step")
+                engine.pipeline = False
             engine.pipe_err.zero_()
             cur.left = 0
             cur._next_epoch()
@@ -308,6 +312,8 @@ def main():
                           "early_mlp": getattr(engine, "early_mlp", False) or "off",
                           # pipelined step: step k's reduction + SGD in step k+1's launch (lenet_fused.hip PIPE)
                           "pipelined_step": bool(getattr(engine, "_pipe_ok", lambda: False)()),
+                          # persistent launch: the whole timed window's steps in one launch (lenet_fused.hip PERS)
+                          "persistent_launch": bool(getattr(engine, "_pers_ok", lambda: False)()),
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",

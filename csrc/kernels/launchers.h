@@ -83,6 +83,16 @@ struct PipeCtl {
   unsigned* flg = nullptr;          // ready flags (uncached, [2][3][batch] x 128 B): see pipe_reduce
   long long timeout_ticks = 0;      // bound of one ready wait (s_memrealtime ticks, 100 MHz)
   int flags = 0;                    // & 1: no mid-phase-B fc1 stream (measurement)
+  // Persistent launch (lenet_fused.hip PERS; nsteps > 0): ONE launch runs nsteps steps.  The
+  // reduction workgroups loop over the steps (each waits for the samples' per-step arrival
+  // flags), the sample workgroups loop too (each waits for the previous step's ready flags).
+  // Counters and flags carry step tags (monotonic inside the launch) and are zeroed by the last
+  // reduction workgroup to leave (exit counter), so the next launch starts from zero.
+  int nsteps = 0;
+  int32_t* bv_slot[2] = {nullptr, nullptr};   // bookkeeping slots {bvalid} (written in-launch)
+  int32_t* nid_slot[2] = {nullptr, nullptr};  //   and {next_ids}
+  unsigned* arrive = nullptr;                 // [reduction workgroup][PERS_AROW] per-sample arrival tags
+  unsigned* exitc = nullptr;                  // exit counter of the reduction workgroups
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,
@@ -99,6 +109,14 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
                              float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
                              const int32_t* next_ids, unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc,
                              hipStream_t stream);
+// The persistent launch: pc.nsteps steps in one launch (rows: two parities, contiguous - parity
+// 1 of each row kind right after parity 0); see PipeCtl.
+void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                                const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
+                                float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
+                                unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc, hipStream_t stream);
+int persist_max_batch();   // largest batch whose persistent grid is co-resident on this device
+int persist_ctl_bytes(int batch);  // control memory of a persistent launch (uncached)
 int pipe_reduce_blocks();  // reduction blocks of a full PIPE launch (2 per workgroup)
 int pipe_groups();         // ready groups (counters / flags per parity)
 void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32_t* order, int n, int base,

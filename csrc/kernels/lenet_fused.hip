@@ -34,6 +34,9 @@
 //    barriers (s_waitcnt lgkmcnt(0); s_barrier) that leave vmcnt alone.
 //  * Every MFMA loop issues all of a tile's operand loads before its MFMA chain
 //    (sched_barrier), so LDS latency is paid once per batch, not once per K-step.
+#include <algorithm>
+#include <string>
+
 #include "reduce_device.h"
 
 namespace dnn {
@@ -340,8 +343,9 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
 // first), its value at the round that ended the wait returned in *also_set - no extra round trip.
 // Bounded: past the timeout it sets the sticky error word and returns (the step then runs on
 // stale weights and the host raises at the next check) - never a hang.
+// tgt: the tag the flag must reach (PIPE: 1; PERS: the step whose weights are awaited).
 __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int batch, long long* diag = nullptr,
-                                          int also = -1, bool* also_set = nullptr) {
+                                          int also = -1, bool* also_set = nullptr, unsigned tgt = 1u) {
   const unsigned* f = pc.flg + pipe_flag_index(pc.par, grp, b, batch);
   const unsigned* g = pc.flg + pipe_flag_index(pc.par, also < 0 ? grp : also, b, batch);
   if (__hip_atomic_load(pc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // failed before: no wait
@@ -355,8 +359,8 @@ __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int
       diag[4082 + 2 * polls] = (long long)__builtin_amdgcn_s_memrealtime();
       diag[4083 + 2 * polls] = v;
     }
-    if (v != 0u) {
-      if (also_set != nullptr) *also_set = w != 0u;
+    if (v >= tgt) {
+      if (also_set != nullptr) *also_set = w >= tgt;
       break;
     }
     ++polls;
@@ -365,6 +369,166 @@ __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int
     if (wall_clock64() - t0 > pc.timeout_ticks) {
       __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
+    }
+  }
+}
+
+// ---- the persistent launch (PERS) -------------------------------------------------------------
+// ONE launch runs pc.nsteps steps: the PIPE grid (reduction workgroups first, then one workgroup
+// per sample), every workgroup looping over the steps.  Sample step s waits for the ready flags
+// of the reduction of step s - 1 exactly as a PIPE launch waits for its own reduction (tags s
+// instead of 1); the reduction of step t waits for its rows: every sample stores an arrival tag
+// t + 1 into one word per reduction workgroup of the kind that reads its rows - MLP (after phase
+// D': the MLP reduction overlaps the conv backward) and conv (after phase F) - written through,
+// after its row / slab stores drained (the PIPE weight hand-off, run the other way).  Each word
+// has one writer and one poller (a wave of the workgroup polls its batch of words in one load
+// per 64 samples): no counter shared by many pollers.  Rows alternate between two parities; a
+// sample writes parity s & 1 only after the waits of step s, which imply that every reduction
+// block finished step s - 2 (blocks run their steps in order; each one is in a ready group).
+// No kernel boundary, launch ramp or tail sits between two steps.
+constexpr int PERS_WG = (PIPE_BLOCKS + 1) / 2;                // reduction workgroups
+constexpr int PERS_CONV_WG = (PIPE_CONV_BLOCKS + 1 + 1) / 2;  // conv blocks + the bookkeeping block
+constexpr int PERS_AROW = 256;                                // arrival words per workgroup (max batch)
+static_assert((PIPE_CONV_BLOCKS + 1) % 2 == 0, "conv + bookkeeping blocks fill whole workgroups");
+// control memory: [3 group counters | exit counter] 128 B apart, [3][batch] ready flags 128 B
+// apart, [PERS_WG][PERS_AROW] arrival words
+constexpr long PERS_FLG_OFF = 4 * 128;
+__host__ __device__ constexpr long pers_arrive_off(int batch) { return (PERS_FLG_OFF + 3L * batch * 128 + 1023) / 1024 * 1024; }
+int persist_ctl_bytes(int batch) { return (int)(pers_arrive_off(batch) + (long)PERS_WG * PERS_AROW * 4); }
+
+__device__ __forceinline__ unsigned ld_tag(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_tag(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1(const int32_t* p) {
+  return (int)__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt_i(int32_t* p, int v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), (unsigned)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A sample's arrival at step tag - 1: kind 0 = the conv workgroups (slab, loss / correct read by
+// the bookkeeping), 1 = the MLP workgroups.  One store per lane (lane = workgroup), by ONE wave,
+// after every wave of the sample drained its stores and met a barrier.
+__device__ __forceinline__ void pers_arrive(const PipeCtl& pc, int kind, int b, unsigned tag, int lane) {
+  const int w0 = kind ? PERS_CONV_WG : 0, nw = kind ? PERS_WG - PERS_CONV_WG : PERS_CONV_WG;
+  if (lane < nw) st_tag(pc.arrive + (long)(w0 + lane) * PERS_AROW + b, tag);
+}
+
+// One wave of a reduction workgroup waits until every sample's arrival word reached tgt
+// (bounded: the sticky error word, then no more waits anywhere - never a hang).
+__device__ __forceinline__ void pers_wait_rows(const PipeCtl& pc, const unsigned* row, int batch, unsigned tgt,
+                                               int lane) {
+  if (ld_tag(pc.err) != 0u) return;
+  const long long t0 = wall_clock64();
+  while (true) {
+    bool ok = true;
+    for (int b = lane; b < batch; b += 64) ok &= ld_tag(row + b) >= tgt;
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > pc.timeout_ticks) {
+      __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+// The bookkeeping of the persistent launch, the same sequence of publications as a PIPE chunk
+// of nsteps launches + its closing grad_reduce (engine.py _launch_steps_pipe):
+//   t = -1 (launch start, no statistics): cursor + 1, publish slot 1 (step 1's bvalid, step 2's ids);
+//   t = 0 .. n - 2 (step t reduced): statistics of step t (bvalid from slot t & 1), cursor + 1,
+//     publish slot t & 1 (step t + 2's);
+//   t = n - 1: statistics of step n - 1, cursor unchanged, publish slot 0 (the next launch's).
+// Loads of anything written inside the launch are sc1 and every store the samples read is
+// written through.  One wave.
+__device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const PipeCtl& pc, int lane, int t) {
+  const int n = pc.nsteps;
+  const bool stats = t >= 0;
+  const int adv = t == n - 1 ? 0 : 1;
+  const int sin = t < 0 ? 1 : (t & 1);
+  const int sout = t < 0 ? 1 : (t == n - 1 ? 0 : (t & 1));
+  const int bv = ld_sc1(pc.bv_slot[sin]);  // (before anything is published: sin may be sout)
+  float ls = 0.f;
+  int cs = 0;
+  if (stats) {
+    const long r = (long)(t & 1) * a.batch;
+    for (int b = lane; b < a.batch; b += 64) {
+      ls += ldrow<true>(a.loss + r + b);
+      cs += ld_sc1(a.correct + r + b);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
+  const int next = ld_sc1(a.state + ST_CURSOR) + adv;
+  if (lane == 0 && bv > 0 && stats) {
+    a.stats[STAT_LOSS] += (double)ls / (double)bv;
+    a.stats[STAT_BATCHES] += 1.0;
+    a.stats[STAT_CORRECT] += (double)cs;
+    a.stats[STAT_SAMPLES] += (double)bv;
+  }
+  const long base = (long)next * a.batch;
+  for (int b = lane; b < a.batch; b += 64) {
+    const long g = base + b;
+    a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
+    const long g2 = base + a.batch + b;
+    st_wt_i(pc.nid_slot[sout] + b, g2 < a.order_len ? a.order[g2] : -1);
+  }
+  const long rem = (long)a.order_len - base;
+  const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
+  if (lane == 0) {
+    st_wt_i(a.state + ST_CURSOR, next);
+    st_wt_i(pc.bv_slot[sout], nbv);
+  }
+}
+
+// Reduction workgroup `wg` of a persistent launch: blocks 2 wg, 2 wg + 1 (pipe_reduce's map),
+// every step in order: wait for the rows, reduce + SGD (write-through), signal the ready group.
+// The bookkeeping block is in the conv2 group (samples read its slots after that wait).  The last
+// workgroup to leave zeroes every counter, flag and arrival word for the next launch.
+__device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg) {
+  const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
+  const bool bk = m == PIPE_CONV_BLOCKS;
+  int grp, rblk = 0;
+  if (m < PIPE_CONV_BLOCKS) { rblk = PIPE_MLP_BLOCKS + m; grp = m < PIPE_C1_BLOCKS ? PG_C1 : PG_C2; }
+  else if (bk) grp = PG_C2;
+  else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = PG_MLP; }
+  const unsigned gsize = grp == PG_C2 ? PIPE_C2_BLOCKS + 1 : pipe_group_blocks(grp);
+  if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
+  const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
+  for (int t = 0; t < pc.nsteps; ++t) {
+    if (threadIdx.x < 64) pers_wait_rows(pc, arr, a.batch, (unsigned)t + 1u, lane);
+    __syncthreads();
+    if (bk) {
+      if (rtid < 64) bookkeeping_pers(a, pc, lane, t);
+    } else {
+      WtSink sk;
+      grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid, 0, false, t & 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+    __syncthreads();
+    if ((rtid >> 6) == 0) {  // wave 0 of the block: the group's monotonic counter, the last block's flags
+      unsigned old = 0;
+      if (rtid == 0) old = __hip_atomic_fetch_add(pc.ctr + pipe_ctr_index(0, grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old == (unsigned)(t + 1) * gsize - 1u)
+        for (int b = rtid; b < a.batch; b += 64) st_tag(pc.flg + pipe_flag_index(0, grp, b, a.batch), (unsigned)t + 1u);
+    }
+  }
+  // exit: the reduction workgroups leave after every sample's last control access (the conv
+  // workgroups' last wait saw each sample's final arrival); the last one resets the control words
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(pc.exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old == (unsigned)PERS_WG - 1u) {
+      if (lane < PIPE_GROUPS) st_tag(pc.ctr + pipe_ctr_index(0, lane), 0u);
+      for (int i = lane; i < PIPE_GROUPS * a.batch; i += 64)
+        st_tag(pc.flg + pipe_flag_index(0, i / a.batch, i % a.batch, a.batch), 0u);
+      for (int i = lane; i < PERS_WG * a.batch; i += 64) st_tag(pc.arrive + (long)(i / a.batch) * PERS_AROW + i % a.batch, 0u);
+      if (lane == 0) st_tag(pc.exitc, 0u);
     }
   }
 }
@@ -411,7 +575,8 @@ __device__ __forceinline__ void dma_w(const void* gsrc, uint32_t lds_base) {
 
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
 // PIPE (TRAIN + STAGED only): the pipelined step's merged launch (above)
-template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false>
+// PERS (PIPE only): the persistent launch - pc.nsteps steps, rows of both parities (above)
+template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false, bool PERS = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -432,6 +597,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const ReduceArgs ra, const ReduceArgs rc,  //   and the in-launch reduction: MLP (ra), conv + bookkeeping (rc)
     const PipeCtl pc) {                     // PIPE: ra = the previous step's reduction, pc its control
   static_assert(!PIPE || (TRAIN && STAGED && RNR == 0), "the pipelined step is a staged training launch");
+  static_assert(!PERS || PIPE, "the persistent launch is a PIPE grid");
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
@@ -448,7 +614,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int nrw = PIPE ? (pc.nred + 1) / 2 : 0;
   if constexpr (PIPE) {
     if ((int)blockIdx.x < nrw) {
-      pipe_reduce(ra, pc, blockIdx.x, stamps);
+      if constexpr (PERS) pers_reduce(ra, pc, blockIdx.x);
+      else pipe_reduce(ra, pc, blockIdx.x, stamps);
       if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
       return;
     }
@@ -466,17 +633,43 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       return;
     }
   }
-  // diagnostic phase timeline (sample block 0, thread 0): s_memrealtime ticks (100 MHz)
-  const bool stamp = stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0;
-#define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
-  STAMP(0);
-  const int tid = threadIdx.x;
+  const int b = (int)blockIdx.x - nrw;
+  const WeightRd<PIPE> wr(shadow, master);
+  // PERS: the next step's image + label, loaded by waves 5-7 in phase F (register carry: the
+  // same threads store it to LDS in the next step's phase A - no global round trip in-launch)
+  uint4 carry_im = make_uint4(0, 0, 0, 0);
+  int carry_lab = 0;
+  const int nsteps = PERS ? pc.nsteps : 1;
+  int s = 0;  // (a do-while: without PERS the body is straight-line code, no loop at all)
+  do {
+  // the lane's indices are re-derived in every step from an opaque copy of threadIdx.x: the
+  // per-lane address math of every phase then stays inside the step instead of being hoisted
+  // out of the loop and kept live across it (that spilled ~1 KB per lane)
+  int tid_opaque = threadIdx.x;
+  if constexpr (PERS) asm volatile("" : "+v"(tid_opaque));
+  const int tid = tid_opaque;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int fr = lane & 15;   // MFMA fragment row/col within the 16-tile
   const int fg = lane >> 4;   // MFMA k-group (0..3)
-  const int b = (int)blockIdx.x - nrw;
-  const WeightRd<PIPE> wr(shadow, master);
+  // PERS: this step's rows are parity s & 1 (parity 1 of each row kind follows parity 0)
+  const long rsh = PERS ? (long)(s & 1) * batch : 0;
+  float* const a0_s = a0_out + rsh * A0_LD;
+  float* const h1_s = h1_out + rsh * H1_LD;
+  float* const h2_s = h2_out + rsh * H2_LD;
+  float* const z1_s = z1_out + rsh * Z1_LD;
+  float* const z2_s = z2_out + rsh * Z2_LD;
+  float* const z3_s = z3_out + rsh * Z3_LD;
+  float* const slab_s = slab_out + rsh * SLAB;
+  float* const loss_s = loss_out + rsh;
+  int32_t* const correct_s = correct_out + rsh;
+  // PERS: waits from step 1 on (step 0's weights are the previous launch's), tag = the step
+  const int do_wait = PERS ? (s > 0 ? 1 : 0) : pc.wait;
+  const unsigned wtgt = PERS ? (unsigned)s : 1u;
+  // diagnostic phase timeline (sample block 0, thread 0; PERS: the last step): s_memrealtime ticks
+  const bool stamp = stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0 && (!PERS || s == nsteps - 1);
+#define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+  STAMP(0);
 
   // TRAIN: the sample ids and valid count of this step were published by the previous
   // step's reduce kernel (begin_epoch for the first step): one dependent load level less
@@ -490,12 +683,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   constexpr bool staged = TRAIN && STAGED;
   if (TRAIN) {
     if constexpr (staged) {  // issued first: independent of every other load of the kernel
-      st_im = stage_im[(size_t)b * (IMG / 16) + min(tid, IMG / 16 - 1)];
-      st_label = stage_lab[b];
+      if (!PERS || s == 0) {
+        st_im = stage_im[(size_t)b * (IMG / 16) + min(tid, IMG / 16 - 1)];
+        st_label = stage_lab[b];
+      }
     } else {
       sample = order[b];  // `order` = the published batch ids [batch]
     }
-    bvalid = PIPE ? *pc.bvalid : state[ST_BVALID];  // (PIPE: this launch's bookkeeping slot)
+    // (PIPE: this launch's bookkeeping slot.  PERS: step 0's is the previous launch's; from step
+    // 1 on the slot is read after the conv2 wait and checked after phase B - until then valid)
+    if constexpr (PERS) bvalid = s == 0 ? *pc.bv_slot[0] : batch;
+    else bvalid = PIPE ? *pc.bvalid : state[ST_BVALID];
     valid = b < bvalid;
   } else {
     const long gidx = (long)base_index + b;
@@ -509,6 +707,40 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const bool conv_g = TRAIN && RNR > 0 && rc.rg != nullptr;
   float my_loss = 0.f;
   int my_correct = 0;
+  // a row element: plain, or (PERS) written through - the reduction of the same launch reads it
+  auto put_row = [&](float* p, float v) {
+    if constexpr (PERS) st_wt(p, v);
+    else *p = v;
+  };
+  // PERS: every wave drained its stores (rows, slab, image stage) -> barrier -> one wave stores
+  // this sample's arrival tags for the conv workgroups (kind 0) or the MLP workgroups (kind 1)
+  auto pers_arrive_kind = [&](int kind) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) pers_arrive(pc, kind, b, (unsigned)s + 1u, lane);
+  };
+  // an invalid sample (past the batch's valid count): zero rows, and (PERS) both arrivals
+  auto invalid_sample = [&]() {
+    for (int i = tid; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, 0.f);
+    for (int i = tid; i < H1_LD; i += NT) {
+      put_row(h1_s + (size_t)b * H1_LD + i, 0.f);
+      put_row(z1_s + (size_t)b * Z1_LD + i, 0.f);
+    }
+    for (int i = tid; i < H2_LD; i += NT) {
+      put_row(h2_s + (size_t)b * H2_LD + i, 0.f);
+      put_row(z2_s + (size_t)b * Z2_LD + i, 0.f);
+    }
+    for (int i = tid; i < Z3_LD; i += NT) put_row(z3_s + (size_t)b * Z3_LD + i, 0.f);
+    for (int i = tid; i < SLAB; i += NT) put_row(slab_s + (size_t)b * SLAB + i, 0.f);
+    if (tid == 0) {
+      put_row(loss_s + b, 0.f);
+      put_row(reinterpret_cast<float*>(correct_s + b), 0.f);
+    }
+    if constexpr (PERS) {
+      pers_arrive_kind(1);
+      pers_arrive_kind(0);
+    }
+  };
   if (!valid) {
     if (TRAIN && rowg != nullptr) {
       put_row_granules(rowg, batch, b, row_tag, tid, NT, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
@@ -524,21 +756,26 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         }
       }
     }
-    if (TRAIN) {
-      for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
-      for (int i = tid; i < H1_LD; i += NT) {
-        h1_out[(size_t)b * H1_LD + i] = 0.f;
-        z1_out[(size_t)b * Z1_LD + i] = 0.f;
+    if constexpr (PERS) {
+      invalid_sample();
+      continue;
+    } else {
+      if (TRAIN) {
+        for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
+        for (int i = tid; i < H1_LD; i += NT) {
+          h1_out[(size_t)b * H1_LD + i] = 0.f;
+          z1_out[(size_t)b * Z1_LD + i] = 0.f;
+        }
+        for (int i = tid; i < H2_LD; i += NT) {
+          h2_out[(size_t)b * H2_LD + i] = 0.f;
+          z2_out[(size_t)b * Z2_LD + i] = 0.f;
+        }
+        for (int i = tid; i < Z3_LD; i += NT) z3_out[(size_t)b * Z3_LD + i] = 0.f;
+        for (int i = tid; i < SLAB; i += NT) slab_out[(size_t)b * SLAB + i] = 0.f;
+        if (tid == 0) { loss_out[b] = 0.f; correct_out[b] = 0; }
       }
-      for (int i = tid; i < H2_LD; i += NT) {
-        h2_out[(size_t)b * H2_LD + i] = 0.f;
-        z2_out[(size_t)b * Z2_LD + i] = 0.f;
-      }
-      for (int i = tid; i < Z3_LD; i += NT) z3_out[(size_t)b * Z3_LD + i] = 0.f;
-      for (int i = tid; i < SLAB; i += NT) slab_out[(size_t)b * SLAB + i] = 0.f;
-      if (tid == 0) { loss_out[b] = 0.f; correct_out[b] = 0; }
+      return;
     }
-    return;
   }
   int label;
   const uint8_t* img = images + (size_t)sample * IMG;
@@ -604,15 +841,21 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else if (tid < 58) DZ3B[10 + tid - 36] = (bf16)0.f;
   else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
   else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
-  if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  if (PERS && s > 0) {  // the image + label this wave group staged in the previous step's phase F
+    if (tid >= 320) reinterpret_cast<uint4*>(IMGS)[tid - 320] = carry_im;
+    if (tid == 320) *reinterpret_cast<int*>(smem + L_MISC) = carry_lab;
+  } else if (tid < 192) {
+    reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  }
   lds_barrier();
+  if (PERS && s > 0) label = *reinterpret_cast<const int*>(smem + L_MISC);
   STAMP(9);
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
   if constexpr (PIPE) {
     // conv1's weights are the previous step's reduction's: one lane waits for its group (the
     // image and its records need none of it, so they are done first); the barrier releases the
     // other waves, then every wave loads its fragments (sc1) - waited for at phase B's first MFMA
-    if (tid == 0 && pc.wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr);
+    if (tid == 0 && do_wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr, -1, nullptr, wtgt);
     STAMP(12);
     lds_barrier();
     load_conv1_w();
@@ -640,6 +883,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     lds_barrier();
   }
   bool fc1_out = !PIPE;  // PIPE: this wave has issued its part of the fc1 stream
+  int bv_late = batch;   // PERS: this step's valid count (from step 1 on)
   STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
@@ -704,10 +948,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         int mlp = 0;
         if (lane == 0) {
           bool m = false;
-          if (pc.wait) pipe_wait(pc, PG_C2, b, batch, nullptr, (pc.flags & 1) ? -1 : PG_MLP, &m);
+          if (do_wait) pipe_wait(pc, PG_C2, b, batch, nullptr, (pc.flags & 1) ? -1 : PG_MLP, &m, wtgt);
           else m = true;  // (no reduction in this launch: every weight is the previous kernel's)
           mlp = m && !(pc.flags & 1);
         }
+        // PERS: this step's valid count (published by the bookkeeping, a conv2-group block),
+        // consumed after phase B
+        if (PERS && s > 0) bv_late = ld_sc1(pc.bv_slot[s & 1]);
         if (__builtin_amdgcn_readfirstlane(mlp)) {
           stream_fc1();
           fc1_out = true;
@@ -718,13 +965,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   }
   if constexpr (PIPE) {
     if (!fc1_out) {  // the MLP group was not complete mid-phase B: this wave waits for it here
-      if (lane == 0 && pc.wait) pipe_wait(pc, PG_MLP, b, batch);
+      if (lane == 0 && do_wait) pipe_wait(pc, PG_MLP, b, batch, nullptr, -1, nullptr, wtgt);
       consume_conv2_w();
       stream_fc1();
     }
     STAMP(13);
   }
   lds_barrier();
+  if constexpr (PERS) {
+    if (s > 0) {
+      bvalid = bv_late;
+      valid = b < bvalid;
+      if (!valid) {  // (block-uniform) past the epoch's end: no phases C-F for this sample
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fc1 stream has landed before LDS is reused
+        invalid_sample();
+        continue;
+      }
+    }
+  }
 
   STAMP(2);
   // ============ phase C: conv2 (6->16, 5x5) + bias + ReLU + maxpool, MFMA ===============
@@ -869,8 +1127,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
-      loss_out[b] = lse - ll;
-      correct_out[b] = pred == label ? 1 : 0;
+      put_row(loss_s + b, lse - ll);
+      put_row(reinterpret_cast<float*>(correct_s + b), __int_as_float(pred == label ? 1 : 0));
       my_loss = lse - ll;  // (thread 0: also the in-launch bookkeeping's granule)
       my_correct = pred == label ? 1 : 0;
     }
@@ -940,10 +1198,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     put_row_granules(rowg, batch, b, row_tag, tid, NT, A0, H1, H2, DZ1, DZ2, DZ3);
     if (tid == 0) rowg_ctr[b] = row_tag;  // (every thread read the counter at the kernel start)
   } else {
-    for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = A0[i];
-    if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = H1[tid]; z1_out[(size_t)b * Z1_LD + tid] = DZ1[tid]; }
-    if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = H2[tid]; z2_out[(size_t)b * Z2_LD + tid] = DZ2[tid]; }
-    if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = DZ3[tid];
+    for (int i = tid; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, A0[i]);
+    if (tid < H1_LD) { put_row(h1_s + (size_t)b * H1_LD + tid, H1[tid]); put_row(z1_s + (size_t)b * Z1_LD + tid, DZ1[tid]); }
+    if (tid < H2_LD) { put_row(h2_s + (size_t)b * H2_LD + tid, H2[tid]); put_row(z2_s + (size_t)b * Z2_LD + tid, DZ2[tid]); }
+    if (tid < Z3_LD) put_row(z3_s + (size_t)b * Z3_LD + tid, DZ3[tid]);
   }
   lds_barrier();
 
@@ -956,13 +1214,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   //    padding rows are skipped by the consumer, never stored): A operand of
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
   //    flipped kernel WF - no col2im scratch, no gather pass.
-  float* slab = slab_out + (size_t)b * SLAB;
+  float* slab = slab_s + (size_t)b * SLAB;
   // the conv gradient slab: plain rows, or (in-launch reduction) {value, step} granules
   unsigned long long* const slab_g = conv_g ? rowg + rg_off(RG_SLAB, batch) + (long long)b * SLAB : nullptr;
 #define SLAB_PUT(i, v)                                   \
   do {                                                   \
     if (slab_g != nullptr) rg_put(slab_g, (i), row_tag, (v)); \
-    else slab[i] = (v);                                  \
+    else put_row(slab + (i), (v));                       \
   } while (0)
   bf16x8* R3 = reinterpret_cast<bf16x8*>(smem + L_REGA + A_R3);
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
@@ -1026,6 +1284,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (LDS-DMA, issued in phase D) landed
   lds_barrier();
   STAMP(8);
+  // PERS: every wave's row stores (phase D') drained before that barrier: the MLP workgroups go
+  if (PERS && wave == 7) pers_arrive(pc, 1, b, (unsigned)s + 1u, lane);
   if (wave == 3) {  // conv2 bias gradient: 4 lanes per channel over its 10 row sums
     const int o = lane >> 2, part = lane & 3;
     float t = 0.f;
@@ -1159,9 +1419,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (tid < 768 - 2 * (NT - 168)) build_r1_half(IMGS, R1, 2 * (NT - 168) + tid);
   } else {
     if (staged && wave >= 5) {  // a vector load: the lgkmcnt(0) of the barriers does not wait for it
-      const int32_t* p = next_ids + b;
+      const int32_t* p = (PERS ? pc.nid_slot[s & 1] : next_ids) + b;
       asm volatile("" : "+v"(p));
-      ns_next = *p;
+      ns_next = PERS ? ld_sc1(p) : *p;
     }
     build_r1_half(IMGS, R1, tid - 168);
     build_r1_half(IMGS, R1, tid - 168 + (NT - 168));
@@ -1174,6 +1434,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const int lab = t == 0 ? labels[ns_next] : 0;
     stage_im[(size_t)b * (IMG / 16) + t] = v;
     if (t == 0) stage_lab[b] = lab;
+    if constexpr (PERS) {
+      carry_im = v;
+      carry_lab = lab;
+    }
   }
   if (wave == 7) {  // conv1 bias gradient: 8 lanes per channel over its 28 row sums
     const int c = min(lane >> 3, 5), part = lane & 7;
@@ -1225,13 +1489,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int i = tid; i < CODES_PER_SAMPLE; i += NT)
       codes_out[(size_t)b * CODES_PER_SAMPLE + i] = i < 6 * 196 ? CODE1[i] : CODE2[i - 6 * 196];
   }
-  if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);
     STAMP(7);
   }
+  if constexpr (PERS) pers_arrive_kind(0);  // slab + loss / correct drained: the conv workgroups go
 #undef STAMP
 #undef SLAB_PUT
+  } while (PERS && ++s < nsteps);  // steps
+  if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace dnn
@@ -1245,7 +1511,8 @@ void init_kernels() {
   const void* kerns[] = {(const void*)lenet_fused_kernel<true, false, 0>, (const void*)lenet_fused_kernel<true, true, 0>,
                          (const void*)lenet_fused_kernel<true, false, 1>, (const void*)lenet_fused_kernel<true, true, 1>,
                          (const void*)lenet_fused_kernel<true, false, 8>, (const void*)lenet_fused_kernel<true, true, 8>,
-                         (const void*)lenet_fused_kernel<false, false, 0>, (const void*)lenet_fused_kernel<true, true, 0, true>};
+                         (const void*)lenet_fused_kernel<false, false, 0>, (const void*)lenet_fused_kernel<true, true, 0, true>,
+                         (const void*)lenet_fused_kernel<true, true, 0, true, true>};
   for (const void* k : kerns) HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   init_kernels_f32();
   done = true;
@@ -1313,6 +1580,53 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
   hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true>), dim3(nrw + batch), dim3(NT), LDS_TOTAL, stream, images,
                      labels, nullptr, order_len, batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab,
                      loss, correct, stamps, nullptr, next_ids, stage, nullptr, nullptr, red, ReduceArgs{}, pc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// Largest batch whose persistent grid (PERS_WG reduction + batch sample workgroups, one per CU:
+// each holds LDS_TOTAL of LDS) is co-resident on this device - a condition of every in-launch wait.
+int persist_max_batch() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return std::min(cus - PERS_WG, PERS_AROW);
+}
+
+void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                                const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
+                                float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
+                                unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc_in,
+                                hipStream_t stream) {
+  init_kernels();
+  // the shapes the kernel assumes (checked here: a mismatch would fault or hang on the device)
+  if (batch < 1 || batch > persist_max_batch())
+    throw std::runtime_error("fused_train_persist: batch must be 1.." + std::to_string(persist_max_batch()) +
+                             " (the whole grid co-resident)");
+  if (pc_in.nsteps < 1 || pc_in.nsteps > (1 << 20)) throw std::runtime_error("fused_train_persist: nsteps out of range");
+  if (stage == nullptr || pc_in.ctr == nullptr || pc_in.err == nullptr || !pc_in.bv_slot[0] || !pc_in.bv_slot[1] ||
+      !pc_in.nid_slot[0] || !pc_in.nid_slot[1])
+    throw std::runtime_error("fused_train_persist: needs the stage, the control block, the error word and both slots");
+  if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || red.rg != nullptr || !red.fuse_sgd ||
+      red.lo != 0 || red.hi < ARENA)
+    throw std::runtime_error("fused_train_persist: a local whole-arena fused-SGD reduction with bookkeeping");
+  if (red.a0 != a0 || red.h1 != h1 || red.h2 != h2 || red.z1 != z1 || red.z2 != z2 || red.z3 != z3 ||
+      red.slab != slab || red.loss != loss || red.correct != correct)
+    throw std::runtime_error("fused_train_persist: the reduction reads the rows the samples write");
+  PipeCtl pc = pc_in;  // control block layout (one uncached allocation of persist_ctl_bytes)
+  unsigned char* base = reinterpret_cast<unsigned char*>(pc_in.ctr);
+  pc.par = 0;
+  pc.wait = 0;
+  pc.nred = PIPE_BLOCKS;
+  pc.exitc = reinterpret_cast<unsigned*>(base + 3 * 128);
+  pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
+  pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
+  hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true, true>), dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL,
+                     stream, images, labels, nullptr, order_len, batch, 0, red.state, master, shadow, a0, h1, h2, z1,
+                     z2, z3, slab, loss, correct, stamps, nullptr, pc.nid_slot[0], stage, nullptr, nullptr, red,
+                     ReduceArgs{}, pc);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -247,12 +247,24 @@ __device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N]
   }
 }
 
+// A per-sample row element: plain, or (SC: the persistent launch, lenet_fused.hip PERS) an sc1
+// load of a row the sample workgroups of the same launch stored write-through
+template <bool SC>
+__device__ __forceinline__ float ldrow(const float* p) {
+  if constexpr (SC)
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+  else return *p;
+}
+
 // GR: rtag = this reduction block's row tag, rfail = an earlier wait failed (skip the waits)
-template <int LAYER, bool GR, class Sink>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
+// SC / rp (the persistent launch): sc1 row loads, rows of parity rp (rp * batch rows further on)
+template <int LAYER, bool GR, class Sink, bool SC = false>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
+                                        int rp = 0) {
   using L = Fc<LAYER>;
-  const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
-  const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
+  const float* z = (LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3)) + (long)rp * a.batch * L::ZLD;
+  const float* x = (LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2)) + (long)rp * a.batch * L::XLD;
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, kq = lane >> 4;
   const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
@@ -296,8 +308,8 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int b = min(b0 + 4 * s + kq, a.batch - 1);
-        av[s] = z[b * L::ZLD + omc];
-        bv[s] = x[b * L::XLD + inc];
+        av[s] = ldrow<SC>(z + b * L::ZLD + omc);
+        bv[s] = ldrow<SC>(x + b * L::XLD + inc);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -332,7 +344,7 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
 // instead of 64, 4x the threads in flight.
 constexpr int SPLIT = 4;
 // GR (early-MLP overlap): src is a row-granule offset into a.rg instead of a float pointer
-template <bool GR = false>
+template <bool GR = false, bool SC = false>
 __device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q,
                                                   const ReduceArgs* ga = nullptr, int gbase = 0, unsigned rtag = 0,
                                                   bool rfail = false) {
@@ -346,7 +358,7 @@ __device__ __forceinline__ float column_sum_split(const float* src, int ld, int 
       rg_poll<16>(*ga, off, rtag, rfail, v);
     } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = src[min(b0 + 16 * q + k, batch - 1) * ld + col];
+      for (int k = 0; k < 16; ++k) v[k] = ldrow<SC>(src + min(b0 + 16 * q + k, batch - 1) * ld + col);
     }
     __builtin_amdgcn_sched_barrier(0);  // all 16 loads in flight before the first wait
 #pragma unroll
@@ -363,8 +375,9 @@ __device__ __forceinline__ float column_sum_split(const float* src, int ld, int 
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
-template <bool GR, class Sink>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
+template <bool GR, class Sink, bool SC = false>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
+                                         int rp = 0) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
@@ -374,10 +387,11 @@ __device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, u
   else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; kind = 4; }
   else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; kind = 5; }
   const float* src = zp;
+  if constexpr (SC) src += (long)rp * a.batch * ld;  // (the persistent launch's row parity)
   const int cc = min(col, n - 1);  // padding lanes recompute a real column (no divergence)
   const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split<GR>(src, ld, cc, a.batch, q, &a, GR ? (int)rg_off(kind, a.batch) : 0, rtag,
+  const float g = column_sum_split<GR, SC>(src, ld, cc, a.batch, q, &a, GR ? (int)rg_off(kind, a.batch) : 0, rtag,
                                        rfail);  // every lane shuffles: no early exit
   if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
@@ -390,13 +404,14 @@ __device__ __forceinline__ int conv_dst(int e) {
   if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
   return OFF_C2B + (e - SLAB_C2B);
 }
-template <bool GR, class Sink>
-__device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false) {
-  const float* src = a.slab;
+template <bool GR, class Sink, bool SC = false>
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
+                                          int rp = 0) {
+  const float* src = a.slab + (long)rp * a.batch * SLAB;
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split<GR>(src, SLAB, e, a.batch, q, &a, GR ? (int)rg_off(RG_SLAB, a.batch) : 0, rtag,
+  const float g = column_sum_split<GR, SC>(src, SLAB, e, a.batch, q, &a, GR ? (int)rg_off(RG_SLAB, a.batch) : 0, rtag,
                                       rfail);
   if (t < CONV_SLOTS && q == 0) sk.put(0, dst, g, pv, mv, a);
 }

@@ -15,32 +15,32 @@ static_assert(RT % SPLIT == 0, "split column lanes stay inside a wave");
 // Returns true (block-uniform) when this block reduced arena elements.
 // rblk / rtid: the reduction block and its thread (grad_reduce_kernel: blockIdx / threadIdx;
 // the fused kernel's in-launch MLP reduction: two 256-thread reduction blocks per workgroup).
-// GR: rtag / rfail as fc_tile's.
-template <bool GR, class Sink>
+// GR: rtag / rfail as fc_tile's.  SC / rp: fc_tile's (the persistent launch).
+template <bool GR, class Sink, bool SC = false>
 __device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk, int rblk, int rtid, unsigned rtag = 0,
-                                                 bool rfail = false) {
+                                                 bool rfail = false, int rp = 0) {
   const bool mlp = a.hi > OFF_F1W;
   const bool conv = a.lo < OFF_F1W;
   int blk = rblk;
   if (mlp) {
     if (blk < TILE_BLOCKS) {
       const int t = blk * 4 + (rtid >> 6);
-      if (t < FC_T0) fc_tile<0, GR>(t, a, sk, rtag, rfail);
-      else if (t < FC_T0 + FC_T1) fc_tile<1, GR>(t - FC_T0, a, sk, rtag, rfail);
-      else if (t < FC_TILES) fc_tile<2, GR>(t - FC_T0 - FC_T1, a, sk, rtag, rfail);
+      if (t < FC_T0) fc_tile<0, GR, Sink, SC>(t, a, sk, rtag, rfail, rp);
+      else if (t < FC_T0 + FC_T1) fc_tile<1, GR, Sink, SC>(t - FC_T0, a, sk, rtag, rfail, rp);
+      else if (t < FC_TILES) fc_tile<2, GR, Sink, SC>(t - FC_T0 - FC_T1, a, sk, rtag, rfail, rp);
       return true;
     }
     blk -= TILE_BLOCKS;
     constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
     if (blk < FB) {
-      fcb_task<GR>(blk * RT + rtid, a, sk, rtag, rfail);
+      fcb_task<GR, Sink, SC>(blk * RT + rtid, a, sk, rtag, rfail, rp);
       return true;
     }
     blk -= FB;
   }
   if (conv) {
     constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
-    if (blk < CB) { conv_task<GR>(blk * RT + rtid, a, sk, rtag, rfail); return true; }
+    if (blk < CB) { conv_task<GR, Sink, SC>(blk * RT + rtid, a, sk, rtag, rfail, rp); return true; }
     blk -= CB;
   }
   if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping<GR>(a, rtid, rtag, rfail);

@@ -211,7 +211,8 @@ class HipEngine(Engine):
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
                  use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None,
-                 dtype: str = "bf16", early_mlp: bool | None = None, pipeline: bool | None = None) -> None:
+                 dtype: str = "bf16", early_mlp: bool | None = None, pipeline: bool | None = None,
+                 persist: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if dtype not in ("bf16", "fp32"):
             raise ValueError(f"HipEngine dtype must be bf16 or fp32, not {dtype!r}")
@@ -296,14 +297,17 @@ class HipEngine(Engine):
         if dtype == "bf16":
             self._rg_buffers()  # (allocated up front: never inside a graph capture)
         if self.pipeline:
-            # the second parity's per-sample rows (the first is a0 .. correct above), the second
-            # {bvalid, next_ids} bookkeeping slot (bvalid in state[2]), the ready counters and
-            # flags and the sticky wait-timeout word
-            self._rows2 = dict(a0=torch.zeros_like(self.a0), h1=torch.zeros_like(self.h1),
-                               h2=torch.zeros_like(self.h2), z1=torch.zeros_like(self.z1),
-                               z2=torch.zeros_like(self.z2), z3=torch.zeros_like(self.z3),
-                               slab=torch.zeros_like(self.slab), loss=torch.zeros_like(self.loss),
-                               correct=torch.zeros_like(self.correct))
+            # the second parity's per-sample rows (the first is a0 .. correct above) - each row
+            # kind as ONE [2][B][...] buffer, parity 1 right after parity 0 (the persistent
+            # launch addresses both from one pointer) -, the second {bvalid, next_ids}
+            # bookkeeping slot (bvalid in state[2]), the ready counters and flags and the sticky
+            # wait-timeout word
+            self._rows2 = {}
+            for k in ("a0", "h1", "h2", "z1", "z2", "z3", "slab", "loss", "correct"):
+                t = getattr(self, k)
+                both = torch.zeros((2,) + tuple(t.shape), device=dev, dtype=t.dtype)
+                setattr(self, k, both[0])
+                self._rows2[k] = both[1]
             self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
             # arrival counters [parity][group] and ready flags [parity][group][sample], a 128-B line
             # each, in uncached memory: every poll reads memory (lenet_fused.hip pipe_wait)
@@ -311,6 +315,14 @@ class HipEngine(Engine):
             self._pipe_ctr_ptr = self.ext.uncached_alloc(2 * ng * 128)
             self._pipe_flg_ptr = self.ext.uncached_alloc(2 * ng * B * 128)
             self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
+        # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step): a chunk of n steps
+        # is ONE launch - the reduction and sample workgroups loop over the steps and hand off
+        # through in-launch arrival / ready flags, so no kernel boundary sits between two steps.
+        # Needs the whole grid co-resident (batch <= persist_max_batch()); DNN_PERSIST=0 turns it off.
+        if persist is None:
+            persist = os.environ.get("DNN_PERSIST", "0") != "0"
+        self.persist = bool(persist) and self.pipeline and B <= self.ext.persist_max_batch()
+        self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.params_changed()
@@ -463,8 +475,36 @@ class HipEngine(Engine):
                                       stamps=0 if first else self._pipe_stamps, flags=self.pipe_flags,
                                       flg=self._pipe_flg_ptr)
 
+    def _pers_ok(self) -> bool:
+        """The persistent launch runs: the pipelined step's conditions, and persist."""
+        return self.persist and self._pipe_ok()
+
+    def _launch_steps_pers(self, n: int) -> None:
+        """n steps as ONE launch (lenet_fused.hip PERS): the same reduction, bookkeeping slots and
+        publication sequence as _launch_steps_pipe's n + 1 launches, with the reduction of step
+        n - 1 inside the launch too (it re-publishes slot 0 for the next chunk)."""
+        s = self._stream()
+        sp = self._p(self.state)
+        r = self._rows(0)
+        self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
+                             self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
+                             self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
+                             self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
+                             self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
+                             self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids))
+        self.ext.fused_train_persist(self._p(self.train.images), self._p(self.train.labels), self.order_len,
+                                     self.batch, self._p(self.master), self._p(self.shadow), self._p(r["a0"]),
+                                     self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]),
+                                     self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
+                                     self._p(self.stage), self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
+                                     self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
+                                     stamps=self._pipe_stamps, flags=self.pipe_flags)
+
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
+        if self._pers_ok():
+            self._launch_steps_pers(n)
+            return
         if self._pipe_ok():
             self._launch_steps_pipe(n)
             return
@@ -475,6 +515,7 @@ class HipEngine(Engine):
         rg = getattr(self, "_rg", None)
         pc = getattr(self, "_pipe_ctr_ptr", None)
         pf = getattr(self, "_pipe_flg_ptr", None)
+        pp = getattr(self, "_pers_ctl", 0)
         if rg is not None or pc is not None:
             try:
                 torch.cuda.synchronize(self.device)
@@ -484,6 +525,8 @@ class HipEngine(Engine):
                     self.ext.xgmi_free(pc)
                 if pf:
                     self.ext.xgmi_free(pf)
+                if pp:
+                    self.ext.xgmi_free(pp)
             except Exception:
                 pass
 
@@ -646,7 +689,8 @@ class HipEngine(Engine):
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
         key = (nsteps, id(self.grad_sync), self.overlap, self.early_mlp, self.order_len,
                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
-               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok())
+               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
+               self._pers_ok())
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.  The wait before it is
@@ -687,7 +731,7 @@ class HipEngine(Engine):
                 if self._pipe_ok():
                     if poll is not None:
                         poll()
-                    self._launch_steps_pipe(n)
+                    self._launch_steps(n)
                     return
                 for _ in range(n):
                     if poll is not None:

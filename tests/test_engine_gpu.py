@@ -212,26 +212,28 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
     rng = np.random.default_rng(3)
     orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
     res = []
-    for pipe in (False, True):
-        eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe)
+    # serial, pipelined (one launch per step), persistent (one launch per chunk / run_steps call)
+    for pipe, pers in ((False, False), (True, False), (True, True)):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe, persist=pers)
         eng.attach(data)
         stats = []
         for ep, order in enumerate(orders):
             eng.begin_epoch(order)
             if ep == 0:
-                assert eng._pipe_ok() == pipe
+                assert eng._pipe_ok() == pipe and eng._pers_ok() == pers
             eng.run_steps(5)
             eng.run_steps(12 if ep != 1 else 13)  # epoch 1 runs a step past its end (a no-op)
             stats.append(eng.epoch_stats())
         torch.cuda.synchronize()
         assert not (pipe and eng.pipe_failed())
         res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
-    (m0, mo0, sh0, st0), (m1, mo1, sh1, st1) = res
-    assert torch.equal(m0, m1), f"master differs at {int((m0 != m1).sum())} elements"
-    assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1)
-    assert [(x.loss_sum, x.samples, x.correct, x.batches) for x in st0] == \
-        [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1]
-    assert all(x.samples == 1000 and x.batches == 16 for x in st1)
+    m0, mo0, sh0, st0 = res[0]
+    for m1, mo1, sh1, st1 in res[1:]:
+        assert torch.equal(m0, m1), f"master differs at {int((m0 != m1).sum())} elements"
+        assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1)
+        assert [(x.loss_sum, x.samples, x.correct, x.batches) for x in st0] == \
+            [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1]
+        assert all(x.samples == 1000 and x.batches == 16 for x in st1)
 
 
 def test_pipelined_long_run_under_load():
@@ -241,8 +243,8 @@ def test_pipelined_long_run_under_load():
     a = init_arena(seed=6)
     order = np.random.default_rng(4).permutation(4096).astype(np.int32)
     res = []
-    for pipe in (False, True):
-        eng = HipEngine(batch=64, arena=a, graph_chunk=32, pipeline=pipe)
+    for pipe, pers in ((False, False), (True, False), (True, True)):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=32, pipeline=pipe, persist=pers)
         eng.attach(data)
         side = torch.cuda.Stream()
         x = torch.randn(2048, 2048, device="cuda")
@@ -255,5 +257,6 @@ def test_pipelined_long_run_under_load():
         torch.cuda.synchronize()
         assert not (pipe and eng.pipe_failed())
         res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats()))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
-    assert res[0][2].loss_sum == res[1][2].loss_sum
+    for r in res[1:]:
+        assert torch.equal(res[0][0], r[0]) and torch.equal(res[0][1], r[1])
+        assert res[0][2].loss_sum == r[2].loss_sum
