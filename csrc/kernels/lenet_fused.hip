@@ -389,11 +389,19 @@ __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int
 constexpr int PERS_WG = (PIPE_BLOCKS + 1) / 2;                // reduction workgroups
 constexpr int PERS_CONV_WG = (PIPE_CONV_BLOCKS + 1 + 1) / 2;  // conv blocks + the bookkeeping block
 constexpr int PERS_AROW = 256;                                // arrival words per workgroup (max batch)
+constexpr int PERS_C1_WG = PIPE_C1_BLOCKS / 2;                // ready groups = workgroup ranges:
+constexpr int PERS_RROW = 64;                                 //   C1 [0, 4), C2 + bookkeeping [4, 23), MLP [23, 57)
 static_assert((PIPE_CONV_BLOCKS + 1) % 2 == 0, "conv + bookkeeping blocks fill whole workgroups");
-// control memory: [3 group counters | exit counter] 128 B apart, [3][batch] ready flags 128 B
-// apart, [PERS_WG][PERS_AROW] arrival words
+static_assert(PIPE_C1_BLOCKS % 2 == 0, "the conv1 group is whole workgroups");
+static_assert(PERS_WG <= PERS_RROW, "one ready word per reduction workgroup in a sample's row");
+// Ready hand-off: every reduction workgroup stores its step tag into ONE word of every sample's
+// ready row [batch][PERS_RROW] (no counter, no atomic round trip, no last-block broadcast); a
+// sample polls its whole row with one wave-wide load (lane = workgroup) and checks the lanes of
+// the group it waits for.
+// control memory: [exit counter] 128 B, [batch][PERS_RROW] ready rows, [PERS_WG][PERS_AROW]
+// arrival words
 constexpr long PERS_FLG_OFF = 4 * 128;
-__host__ __device__ constexpr long pers_arrive_off(int batch) { return (PERS_FLG_OFF + 3L * batch * 128 + 1023) / 1024 * 1024; }
+__host__ __device__ constexpr long pers_arrive_off(int batch) { return (PERS_FLG_OFF + 4L * batch * PERS_RROW + 1023) / 1024 * 1024; }
 int persist_ctl_bytes(int batch) { return (int)(pers_arrive_off(batch) + (long)PERS_WG * PERS_AROW * 4); }
 
 __device__ __forceinline__ unsigned ld_tag(const unsigned* p) {
@@ -415,6 +423,33 @@ __device__ __forceinline__ void st_wt_i(int32_t* p, int v) {
 __device__ __forceinline__ void pers_arrive(const PipeCtl& pc, int kind, int b, unsigned tag, int lane) {
   const int w0 = kind ? PERS_CONV_WG : 0, nw = kind ? PERS_WG - PERS_CONV_WG : PERS_CONV_WG;
   if (lane < nw) st_tag(pc.arrive + (long)(w0 + lane) * PERS_AROW + b, tag);
+}
+
+// A sample's wave waits until the ready words of workgroups [lo, hi) in its row reach tgt (every
+// lane loads one word: lane = workgroup).  also_lo < also_hi: the same round also reports whether
+// workgroups [also_lo, also_hi) are ready (*also_set, wave-uniform).  Bounded like pipe_wait.
+__device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo, int hi, unsigned tgt, int lane,
+                                                int also_lo = 0, int also_hi = 0, bool* also_set = nullptr,
+                                                long long* diag = nullptr) {
+  if (ld_tag(pc.err) != 0u) return;
+  const unsigned* row = pc.flg + (long)b * PERS_RROW + min(lane, PERS_WG - 1);
+  const long long t0 = wall_clock64();
+  if (diag != nullptr && lane == 0) diag[0] = t0;
+  long long polls = 0;
+  while (true) {
+    const unsigned v = ld_tag(row);
+    if (__all((lane < lo || lane >= hi) || v >= tgt)) {
+      if (also_set != nullptr) *also_set = __all((lane < also_lo || lane >= also_hi) || v >= tgt);
+      break;
+    }
+    ++polls;
+    if (diag != nullptr && lane == 0) diag[1] = polls;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > pc.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
 }
 
 // One wave of a reduction workgroup waits until every sample's arrival word reached tgt
@@ -490,11 +525,9 @@ __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const Pipe
 __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
   const bool bk = m == PIPE_CONV_BLOCKS;
-  int grp, rblk = 0;
-  if (m < PIPE_CONV_BLOCKS) { rblk = PIPE_MLP_BLOCKS + m; grp = m < PIPE_C1_BLOCKS ? PG_C1 : PG_C2; }
-  else if (bk) grp = PG_C2;
-  else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = PG_MLP; }
-  const unsigned gsize = grp == PG_C2 ? PIPE_C2_BLOCKS + 1 : pipe_group_blocks(grp);
+  int rblk = 0;
+  if (m < PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + m;
+  else if (!bk) rblk = m - PIPE_CONV_BLOCKS - 1;
   if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
   for (int t = 0; t < pc.nsteps; ++t) {
@@ -508,13 +541,8 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
     __syncthreads();
-    if ((rtid >> 6) == 0) {  // wave 0 of the block: the group's monotonic counter, the last block's flags
-      unsigned old = 0;
-      if (rtid == 0) old = __hip_atomic_fetch_add(pc.ctr + pipe_ctr_index(0, grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (old == (unsigned)(t + 1) * gsize - 1u)
-        for (int b = rtid; b < a.batch; b += 64) st_tag(pc.flg + pipe_flag_index(0, grp, b, a.batch), (unsigned)t + 1u);
-    }
+    if (threadIdx.x < 64)  // both blocks done: this workgroup's word in every sample's ready row
+      for (int b = lane; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, (unsigned)t + 1u);
   }
   // exit: the reduction workgroups leave after every sample's last control access (the conv
   // workgroups' last wait saw each sample's final arrival); the last one resets the control words
@@ -524,9 +552,7 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
     if (lane == 0) old = __hip_atomic_fetch_add(pc.exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
     if (old == (unsigned)PERS_WG - 1u) {
-      if (lane < PIPE_GROUPS) st_tag(pc.ctr + pipe_ctr_index(0, lane), 0u);
-      for (int i = lane; i < PIPE_GROUPS * a.batch; i += 64)
-        st_tag(pc.flg + pipe_flag_index(0, i / a.batch, i % a.batch, a.batch), 0u);
+      for (int i = lane; i < PERS_RROW * a.batch; i += 64) st_tag(pc.flg + i, 0u);
       for (int i = lane; i < PERS_WG * a.batch; i += 64) st_tag(pc.arrive + (long)(i / a.batch) * PERS_AROW + i % a.batch, 0u);
       if (lane == 0) st_tag(pc.exitc, 0u);
     }
@@ -598,6 +624,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const PipeCtl pc) {                     // PIPE: ra = the previous step's reduction, pc its control
   static_assert(!PIPE || (TRAIN && STAGED && RNR == 0), "the pipelined step is a staged training launch");
   static_assert(!PERS || PIPE, "the persistent launch is a PIPE grid");
+  if constexpr (PIPE) {  // (no early-MLP granules in a PIPE / PERS launch: their code is dead here)
+    rowg = nullptr;
+    rowg_ctr = nullptr;
+  }
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
@@ -721,18 +751,22 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   };
   // an invalid sample (past the batch's valid count): zero rows, and (PERS) both arrivals
   auto invalid_sample = [&]() {
-    for (int i = tid; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, 0.f);
-    for (int i = tid; i < H1_LD; i += NT) {
+    // (an opaque thread index: these addresses must not be shared with phase D''s row stores -
+    // a shared computation stays live across the whole step)
+    int ti = threadIdx.x;
+    asm volatile("" : "+v"(ti));
+    for (int i = ti; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, 0.f);
+    for (int i = ti; i < H1_LD; i += NT) {
       put_row(h1_s + (size_t)b * H1_LD + i, 0.f);
       put_row(z1_s + (size_t)b * Z1_LD + i, 0.f);
     }
-    for (int i = tid; i < H2_LD; i += NT) {
+    for (int i = ti; i < H2_LD; i += NT) {
       put_row(h2_s + (size_t)b * H2_LD + i, 0.f);
       put_row(z2_s + (size_t)b * Z2_LD + i, 0.f);
     }
-    for (int i = tid; i < Z3_LD; i += NT) put_row(z3_s + (size_t)b * Z3_LD + i, 0.f);
-    for (int i = tid; i < SLAB; i += NT) put_row(slab_s + (size_t)b * SLAB + i, 0.f);
-    if (tid == 0) {
+    for (int i = ti; i < Z3_LD; i += NT) put_row(z3_s + (size_t)b * Z3_LD + i, 0.f);
+    for (int i = ti; i < SLAB; i += NT) put_row(slab_s + (size_t)b * SLAB + i, 0.f);
+    if (ti == 0) {
       put_row(loss_s + b, 0.f);
       put_row(reinterpret_cast<float*>(correct_s + b), 0.f);
     }
@@ -855,7 +889,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     // conv1's weights are the previous step's reduction's: one lane waits for its group (the
     // image and its records need none of it, so they are done first); the barrier releases the
     // other waves, then every wave loads its fragments (sc1) - waited for at phase B's first MFMA
-    if (tid == 0 && do_wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr, -1, nullptr, wtgt);
+    if constexpr (PERS) {
+      if (wave == 0 && do_wait) pers_wait_ready(pc, b, 0, PERS_C1_WG, wtgt, lane, 0, 0, nullptr, stamp ? stamps + 14 : nullptr);
+    } else {
+      if (tid == 0 && do_wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr, -1, nullptr, wtgt);
+    }
     STAMP(12);
     lds_barrier();
     load_conv1_w();
@@ -946,7 +984,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         // then waits for both, issued a whole round earlier); else the fragments alone, consumed
         // before the stream is issued after phase B (vmcnt counts in issue order)
         int mlp = 0;
-        if (lane == 0) {
+        if constexpr (PERS) {  // the whole wave polls its sample's ready row (C2 + bookkeeping, MLP)
+          bool m = true;
+          if (do_wait) pers_wait_ready(pc, b, PERS_C1_WG, PERS_CONV_WG, wtgt, lane, PERS_CONV_WG, PERS_WG, &m);
+          mlp = m && !(pc.flags & 1);
+        } else if (lane == 0) {
           bool m = false;
           if (do_wait) pipe_wait(pc, PG_C2, b, batch, nullptr, (pc.flags & 1) ? -1 : PG_MLP, &m, wtgt);
           else m = true;  // (no reduction in this launch: every weight is the previous kernel's)
@@ -965,7 +1007,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   }
   if constexpr (PIPE) {
     if (!fc1_out) {  // the MLP group was not complete mid-phase B: this wave waits for it here
-      if (lane == 0 && do_wait) pipe_wait(pc, PG_MLP, b, batch, nullptr, -1, nullptr, wtgt);
+      if constexpr (PERS) {
+        if (do_wait) pers_wait_ready(pc, b, PERS_CONV_WG, PERS_WG, wtgt, lane);
+      } else {
+        if (lane == 0 && do_wait) pipe_wait(pc, PG_MLP, b, batch, nullptr, -1, nullptr, wtgt);
+      }
       consume_conv2_w();
       stream_fc1();
     }
@@ -1206,7 +1252,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   lds_barrier();
 
   STAMP(5);
-  if (btrace) stamps[16 + 4 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (!PERS && btrace) stamps[16 + 4 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   // ============ phase E: conv2 backward =================================================
   // dY2 = unpool(dA0) masked by ReLU is materialised by rows, branch-free, twice:
   //  * DY2 [16][10][16]: A operand of the conv2 weight gradient (8 pixels per lane),
@@ -1620,7 +1666,7 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   pc.par = 0;
   pc.wait = 0;
   pc.nred = PIPE_BLOCKS;
-  pc.exitc = reinterpret_cast<unsigned*>(base + 3 * 128);
+  pc.exitc = reinterpret_cast<unsigned*>(base);
   pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
   pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
   hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true, true>), dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL,

@@ -263,8 +263,12 @@ template <int LAYER, bool GR, class Sink, bool SC = false>
 __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
                                         int rp = 0) {
   using L = Fc<LAYER>;
-  const float* z = (LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3)) + (long)rp * a.batch * L::ZLD;
-  const float* x = (LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2)) + (long)rp * a.batch * L::XLD;
+  const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
+  const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
+  if constexpr (SC) {  // (the persistent launch's row parity)
+    z += (long)rp * a.batch * L::ZLD;
+    x += (long)rp * a.batch * L::XLD;
+  }
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, kq = lane >> 4;
   const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
@@ -381,18 +385,23 @@ __device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, u
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
-  const float* zp;
-  int ld, col, n, off, kind;
-  if (grp < 8) { zp = a.z1; ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; kind = 3; }
-  else if (grp < 14) { zp = a.z2; ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; kind = 4; }
-  else { zp = a.z3; ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; kind = 5; }
-  const float* src = zp;
-  if constexpr (SC) src += (long)rp * a.batch * ld;  // (the persistent launch's row parity)
+  // each source has its own column-sum call: a select of the three row pointers was folded into a
+  // dynamic index into the by-value argument block, which the compiler copied to scratch
+  int ld, col, n, off;
+  if (grp < 8) { ld = Z1_LD; col = colp; n = 120; off = OFF_F1B; }
+  else if (grp < 14) { ld = Z2_LD; col = colp - 128; n = 84; off = OFF_F2B; }
+  else { ld = Z3_LD; col = colp - 224; n = 10; off = OFF_F3B; }
   const int cc = min(col, n - 1);  // padding lanes recompute a real column (no divergence)
   const int dst = off + cc;
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split<GR, SC>(src, ld, cc, a.batch, q, &a, GR ? (int)rg_off(kind, a.batch) : 0, rtag,
-                                       rfail);  // every lane shuffles: no early exit
+  const long rb = SC ? (long)rp * a.batch : 0;  // (the persistent launch's row parity)
+  float g;  // every lane shuffles: no early exit
+  if (grp < 8)
+    g = column_sum_split<GR, SC>(a.z1 + rb * Z1_LD, Z1_LD, cc, a.batch, q, &a, GR ? (int)rg_off(3, a.batch) : 0, rtag, rfail);
+  else if (grp < 14)
+    g = column_sum_split<GR, SC>(a.z2 + rb * Z2_LD, Z2_LD, cc, a.batch, q, &a, GR ? (int)rg_off(4, a.batch) : 0, rtag, rfail);
+  else
+    g = column_sum_split<GR, SC>(a.z3 + rb * Z3_LD, Z3_LD, cc, a.batch, q, &a, GR ? (int)rg_off(5, a.batch) : 0, rtag, rfail);
   if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
 
@@ -407,7 +416,8 @@ __device__ __forceinline__ int conv_dst(int e) {
 template <bool GR, class Sink, bool SC = false>
 __device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
                                           int rp = 0) {
-  const float* src = a.slab + (long)rp * a.batch * SLAB;
+  const float* src = a.slab;
+  if constexpr (SC) src += (long)rp * a.batch * SLAB;
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)

@@ -318,7 +318,7 @@ class HipEngine(Engine):
         # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step): a chunk of n steps
         # is ONE launch - the reduction and sample workgroups loop over the steps and hand off
         # through in-launch arrival / ready flags, so no kernel boundary sits between two steps.
-        # Needs the whole grid co-resident (batch <= persist_max_batch()); DNN_PERSIST=0 turns it off.
+        # Needs the whole grid co-resident (batch <= persist_max_batch()); DNN_PERSIST=1 turns it on.
         if persist is None:
             persist = os.environ.get("DNN_PERSIST", "0") != "0"
         self.persist = bool(persist) and self.pipeline and B <= self.ext.persist_max_batch()

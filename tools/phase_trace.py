@@ -75,6 +75,43 @@ def pipe_main(reps: int = 50, batch: int = 64):
         print(f"  sample block 0 {k:10s} {med(lambda x: x[k]):8.2f} us")
 
 
+def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
+    """--pers: the persistent launch (lenet_fused.hip PERS): sample block 0's phase stamps of the
+    LAST step of an n-step launch, relative to that step's start (= the end of its previous step),
+    and the launch's wall time per step for n = 8 and n = 64 (event timing; the difference is the
+    steady-state step)."""
+    tr = synthetic(8192, 0)
+    eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True, persist=True)
+    eng.attach(tr)
+    assert eng.persist, "persistent launch unavailable"
+    stamps = torch.zeros(4096 + 64, dtype=torch.int64, device=eng.device)
+    keys = dict(img=9, conv_ready=12, a_done=1, b_done=2, mlp_ready=13, c_done=3, d_done=4, dp_done=5,
+                e1_done=8, e_done=6, f1_done=10, end=7)
+    recs, walls = [], {steps: [], 64: []}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(reps):
+        for n in (steps, 64):
+            eng.begin_epoch(np.roll(np.arange(8192, dtype=np.int32), -64 * (r % 60)))
+            eng._pipe_stamps = stamps.data_ptr() if n == steps else 0
+            stamps.zero_()
+            torch.cuda.synchronize()
+            ev0.record()
+            eng.run_steps(n)
+            ev1.record()
+            torch.cuda.synchronize()
+            walls[n].append(1e3 * ev0.elapsed_time(ev1))
+            if n == steps:
+                s = stamps.cpu().numpy().astype(np.float64)
+                recs.append({k: (s[i] - s[0]) * 0.01 for k, i in keys.items()})
+    assert not eng.pipe_failed(), "a persistent-launch wait timed out"
+    rr = recs[3:]
+    for k in keys:
+        print(f"  sample block 0, last step: {k:10s} {float(np.median([x[k] for x in rr])):8.2f} us")
+    w8, w64 = float(np.median(walls[steps][3:])), float(np.median(walls[64][3:]))
+    print(f"launch wall (events): {steps} steps {w8:.2f} us, 64 steps {w64:.2f} us -> steady step "
+          f"{(w64 - w8) / (64 - steps):.3f} us")
+
+
 def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
     tr = synthetic(4096, 0)
     eng = HipEngine(batch=batch, seed=0, use_graphs=False, early_mlp="full" if inlaunch else False)
@@ -145,7 +182,9 @@ def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
 
 
 if __name__ == "__main__":
-    if "--pipe" in sys.argv:
+    if "--pers" in sys.argv:
+        pers_main()
+    elif "--pipe" in sys.argv:
         pipe_main()
     else:
         main(inlaunch="--inlaunch" in sys.argv)
