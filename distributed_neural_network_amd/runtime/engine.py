@@ -77,6 +77,25 @@ def eval_metrics(loss: torch.Tensor, correct: torch.Tensor, batch_size: int) -> 
     return float((sums / counts).mean()), 100.0 * float(correct.sum()) / max(n, 1)
 
 
+def gpu_shared_by_ranks() -> bool:
+    """Do other ranks of this job run on this process's GPU (more local ranks than visible
+    devices: the one-GPU rehearsals, ``tools/fault_bench.py --share-gpu``)?  The local rank
+    count comes from the launcher's environment (torchrun, OpenMPI, MPICH / Intel MPI, Slurm);
+    without one, the world size is taken as local (conservative)."""
+    n = None
+    for k in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE"):
+        v = os.environ.get(k)
+        if v:
+            try:
+                n = int(v.split("(")[0])
+                break
+            except ValueError:
+                pass
+    if n is None:
+        n = int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", "1")) or 1)
+    return n > max(1, torch.cuda.device_count())
+
+
 class Engine:
     device: torch.device
     batch: int
@@ -318,9 +337,12 @@ class HipEngine(Engine):
         # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step): a chunk of n steps
         # is ONE launch - the reduction and sample workgroups loop over the steps and hand off
         # through in-launch arrival / ready flags, so no kernel boundary sits between two steps.
-        # Needs the whole grid co-resident (batch <= persist_max_batch()); DNN_PERSIST=1 turns it on.
+        # Its reduction and sample workgroups wait on each other, so the whole grid must be
+        # co-resident: batch <= persist_max_batch() (one workgroup per CU), and no other rank's
+        # persistent grid on the same GPU (ranks time-sharing a device would each hold part of
+        # the CUs); DNN_PERSIST=0 turns it off.
         if persist is None:
-            persist = os.environ.get("DNN_PERSIST", "0") != "0"
+            persist = os.environ.get("DNN_PERSIST", "1") != "0" and not gpu_shared_by_ranks()
         self.persist = bool(persist) and self.pipeline and B <= self.ext.persist_max_batch()
         self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
         self.stream = torch.cuda.Stream(dev)

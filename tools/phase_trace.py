@@ -27,7 +27,7 @@ def pipe_main(reps: int = 50, batch: int = 64):
     (start / end), the samples' ready waits (conv1: before phase B; conv2 + MLP: mid-phase B, the
     MLP again after phase B if it was not complete then) and the sample phases, medians over repeats of 1-step chunks (launch 1 = reduction + samples)."""
     tr = synthetic(4096, 0)
-    eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True)
+    eng = HipEngine(batch=batch, seed=0, use_graphs=False, pipeline=True, persist=False)
     eng.attach(tr)
     stamps = torch.zeros(4096 + 64, dtype=torch.int64, device=eng.device)
     eng._pipe_stamps = stamps.data_ptr()
