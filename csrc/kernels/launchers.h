@@ -86,13 +86,12 @@ struct PipeCtl {
   // Persistent launch (lenet_fused.hip PERS; nsteps > 0): ONE launch runs nsteps steps.  The
   // reduction workgroups loop over the steps (each waits for the samples' per-step arrival
   // flags), the sample workgroups loop too (each waits for the previous step's ready flags).
-  // Counters and flags carry step tags (monotonic inside the launch) and are zeroed by the last
-  // reduction workgroup to leave (exit counter), so the next launch starts from zero.
+  // Ready / arrival words carry generation-relative step tags (never reset; lenet_fused.hip).
   int nsteps = 0;
   int32_t* bv_slot[2] = {nullptr, nullptr};   // bookkeeping slots {bvalid} (written in-launch)
   int32_t* nid_slot[2] = {nullptr, nullptr};  //   and {next_ids}
   unsigned* arrive = nullptr;                 // [reduction workgroup][PERS_AROW] per-sample arrival tags
-  unsigned* exitc = nullptr;                  // exit counter of the reduction workgroups
+  unsigned* gen = nullptr;                    // per-workgroup generation words (steps run so far)
 };
 
 void launch_fused_train(const uint8_t* images, const int32_t* labels, const int32_t* order, int order_len,

@@ -394,13 +394,18 @@ constexpr int PERS_RROW = 64;                                 //   C1 [0, 4), C2
 static_assert((PIPE_CONV_BLOCKS + 1) % 2 == 0, "conv + bookkeeping blocks fill whole workgroups");
 static_assert(PIPE_C1_BLOCKS % 2 == 0, "the conv1 group is whole workgroups");
 static_assert(PERS_WG <= PERS_RROW, "one ready word per reduction workgroup in a sample's row");
+// Step tags are generation-relative: every workgroup keeps its own generation word (the steps run
+// by earlier launches; all equal, as every launch adds its nsteps to each), reads it at its start
+// and adds nsteps at its end.  Tags of this launch are gen + t + 1 and compare wrap-safe, so no
+// control word is ever reset: no exit counter, no reset pass before the kernel can retire.
 // Ready hand-off: every reduction workgroup stores its step tag into ONE word of every sample's
 // ready row [batch][PERS_RROW] (no counter, no atomic round trip, no last-block broadcast); a
 // sample polls its whole row with one wave-wide load (lane = workgroup) and checks the lanes of
 // the group it waits for.
-// control memory: [exit counter] 128 B, [batch][PERS_RROW] ready rows, [PERS_WG][PERS_AROW]
+// control memory: [256 generation words], [batch][PERS_RROW] ready rows, [PERS_WG][PERS_AROW]
 // arrival words
-constexpr long PERS_FLG_OFF = 4 * 128;
+constexpr int PERS_MAX_GRID = 256;
+constexpr long PERS_FLG_OFF = PERS_MAX_GRID * 4;
 __host__ __device__ constexpr long pers_arrive_off(int batch) { return (PERS_FLG_OFF + 4L * batch * PERS_RROW + 1023) / 1024 * 1024; }
 int persist_ctl_bytes(int batch) { return (int)(pers_arrive_off(batch) + (long)PERS_WG * PERS_AROW * 4); }
 
@@ -410,6 +415,7 @@ __device__ __forceinline__ unsigned ld_tag(const unsigned* p) {
 __device__ __forceinline__ void st_tag(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ bool tag_ge(unsigned v, unsigned tgt) { return (int)(v - tgt) >= 0; }  // wrap-safe
 __device__ __forceinline__ int ld_sc1(const int32_t* p) {
   return (int)__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -438,8 +444,8 @@ __device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo
   long long polls = 0;
   while (true) {
     const unsigned v = ld_tag(row);
-    if (__all((lane < lo || lane >= hi) || v >= tgt)) {
-      if (also_set != nullptr) *also_set = __all((lane < also_lo || lane >= also_hi) || v >= tgt);
+    if (__all((lane < lo || lane >= hi) || tag_ge(v, tgt))) {
+      if (also_set != nullptr) *also_set = __all((lane < also_lo || lane >= also_hi) || tag_ge(v, tgt));
       break;
     }
     ++polls;
@@ -460,7 +466,7 @@ __device__ __forceinline__ void pers_wait_rows(const PipeCtl& pc, const unsigned
   const long long t0 = wall_clock64();
   while (true) {
     bool ok = true;
-    for (int b = lane; b < batch; b += 64) ok &= ld_tag(row + b) >= tgt;
+    for (int b = lane; b < batch; b += 64) ok &= tag_ge(ld_tag(row + b), tgt);
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > pc.timeout_ticks) {
@@ -528,10 +534,11 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
   int rblk = 0;
   if (m < PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + m;
   else if (!bk) rblk = m - PIPE_CONV_BLOCKS - 1;
+  const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));  // this workgroup's generation
   if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
   for (int t = 0; t < pc.nsteps; ++t) {
-    if (threadIdx.x < 64) pers_wait_rows(pc, arr, a.batch, (unsigned)t + 1u, lane);
+    if (threadIdx.x < 64) pers_wait_rows(pc, arr, a.batch, g0 + (unsigned)t + 1u, lane);
     __syncthreads();
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane, t);
@@ -542,21 +549,9 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
     __syncthreads();
     if (threadIdx.x < 64)  // both blocks done: this workgroup's word in every sample's ready row
-      for (int b = lane; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, (unsigned)t + 1u);
+      for (int b = lane; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, g0 + (unsigned)t + 1u);
   }
-  // exit: the reduction workgroups leave after every sample's last control access (the conv
-  // workgroups' last wait saw each sample's final arrival); the last one resets the control words
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    unsigned old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(pc.exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old == (unsigned)PERS_WG - 1u) {
-      for (int i = lane; i < PERS_RROW * a.batch; i += 64) st_tag(pc.flg + i, 0u);
-      for (int i = lane; i < PERS_WG * a.batch; i += 64) st_tag(pc.arrive + (long)(i / a.batch) * PERS_AROW + i % a.batch, 0u);
-      if (lane == 0) st_tag(pc.exitc, 0u);
-    }
-  }
+  if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
 }
 
 // Weight loads: plain, or (WT: the pipelined step) sc1 buffer loads of the write-through bytes
@@ -670,6 +665,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   uint4 carry_im = make_uint4(0, 0, 0, 0);
   int carry_lab = 0;
   const int nsteps = PERS ? pc.nsteps : 1;
+  const unsigned g0 = PERS ? __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x)) : 0u;  // (PERS) generation
   int s = 0;  // (a do-while: without PERS the body is straight-line code, no loop at all)
   do {
   // the lane's indices are re-derived in every step from an opaque copy of threadIdx.x: the
@@ -695,9 +691,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   int32_t* const correct_s = correct_out + rsh;
   // PERS: waits from step 1 on (step 0's weights are the previous launch's), tag = the step
   const int do_wait = PERS ? (s > 0 ? 1 : 0) : pc.wait;
-  const unsigned wtgt = PERS ? (unsigned)s : 1u;
+  const unsigned wtgt = PERS ? g0 + (unsigned)s : 1u;
   // diagnostic phase timeline (sample block 0, thread 0; PERS: the last step): s_memrealtime ticks
   const bool stamp = stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0 && (!PERS || s == nsteps - 1);
+  if (PERS && stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0 && s < 1024)  // per-step starts
+    stamps[2048 + s] = (long long)__builtin_amdgcn_s_memrealtime();
 #define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
   STAMP(0);
 
@@ -747,7 +745,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   auto pers_arrive_kind = [&](int kind) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (wave == 0) pers_arrive(pc, kind, b, (unsigned)s + 1u, lane);
+    if (wave == 0) pers_arrive(pc, kind, b, g0 + (unsigned)s + 1u, lane);
   };
   // an invalid sample (past the batch's valid count): zero rows, and (PERS) both arrivals
   auto invalid_sample = [&]() {
@@ -878,11 +876,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (PERS && s > 0) {  // the image + label this wave group staged in the previous step's phase F
     if (tid >= 320) reinterpret_cast<uint4*>(IMGS)[tid - 320] = carry_im;
     if (tid == 320) *reinterpret_cast<int*>(smem + L_MISC) = carry_lab;
-  } else if (tid < 192) {
-    reinterpret_cast<uint4*>(IMGS)[tid] = im;
+  } else {
+    if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = im;
+    if (PERS && tid == 0) *reinterpret_cast<int*>(smem + L_MISC) = label;
   }
   lds_barrier();
-  if (PERS && s > 0) label = *reinterpret_cast<const int*>(smem + L_MISC);
+  if (PERS) label = *reinterpret_cast<const int*>(smem + L_MISC);  // (one path for every step)
   STAMP(9);
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
   if constexpr (PIPE) {
@@ -1171,7 +1170,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const float sum = sum16(e);
     const int pred = min16((act && lg == mx) ? lane : 64);  // first max wins (torch.argmax)
     const float lse = mx + logf(sum);
-    const float ll = __shfl(lg, label & 15, 16);
+    // (= __shfl(lg, label & 15, 16); ds_bpermute on the step's lane index - __shfl derives its own
+    // lane id, which the persistent loop kept live across every step)
+    const float ll = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane & 48) | (label & 15)) << 2, __float_as_int(lg)));
     if (lane == 0) {
       put_row(loss_s + b, lse - ll);
       put_row(reinterpret_cast<float*>(correct_s + b), __int_as_float(pred == label ? 1 : 0));
@@ -1331,7 +1332,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   lds_barrier();
   STAMP(8);
   // PERS: every wave's row stores (phase D') drained before that barrier: the MLP workgroups go
-  if (PERS && wave == 7) pers_arrive(pc, 1, b, (unsigned)s + 1u, lane);
+  if (PERS && wave == 7) pers_arrive(pc, 1, b, g0 + (unsigned)s + 1u, lane);
   if (wave == 3) {  // conv2 bias gradient: 4 lanes per channel over its 10 row sums
     const int o = lane >> 2, part = lane & 3;
     float t = 0.f;
@@ -1543,6 +1544,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #undef STAMP
 #undef SLAB_PUT
   } while (PERS && ++s < nsteps);  // steps
+  if (PERS && threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)nsteps);
   if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
@@ -1648,7 +1650,7 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
                                 hipStream_t stream) {
   init_kernels();
   // the shapes the kernel assumes (checked here: a mismatch would fault or hang on the device)
-  if (batch < 1 || batch > persist_max_batch())
+  if (batch < 1 || batch > persist_max_batch() || PERS_WG + batch > PERS_MAX_GRID)
     throw std::runtime_error("fused_train_persist: batch must be 1.." + std::to_string(persist_max_batch()) +
                              " (the whole grid co-resident)");
   if (pc_in.nsteps < 1 || pc_in.nsteps > (1 << 20)) throw std::runtime_error("fused_train_persist: nsteps out of range");
@@ -1666,7 +1668,7 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   pc.par = 0;
   pc.wait = 0;
   pc.nred = PIPE_BLOCKS;
-  pc.exitc = reinterpret_cast<unsigned*>(base);
+  pc.gen = reinterpret_cast<unsigned*>(base);
   pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
   pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
   hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true, true>), dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL,

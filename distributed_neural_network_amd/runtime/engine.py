@@ -444,6 +444,7 @@ class HipEngine(Engine):
         and no in-launch reduction."""
         return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
 
+    pers_eager = os.environ.get("DNN_PERS_EAGER", "0") == "1"
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
     # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
@@ -759,6 +760,14 @@ class HipEngine(Engine):
                     if poll is not None:
                         poll()
                     self._launch_step()
+            return
+        if self.pers_eager and self._pers_ok():
+            # (diagnostic, DNN_PERS_EAGER=1) the persistent launch is ONE kernel: launched
+            # directly instead of as a one-node graph replay
+            if poll is not None:
+                poll()
+            with torch.cuda.device(self.device):
+                self._launch_steps(n)
             return
         if n in getattr(self, "_exact", ()):
             if poll is not None:

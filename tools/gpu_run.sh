@@ -19,6 +19,7 @@
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
+#   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
 #   phase | phase32 | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
@@ -76,6 +77,9 @@ for s in "$@"; do
     phase) timeout -k 10 300 python tools/phase_trace.py > "$O/phase.txt" 2>&1 ;;
     phasepipe) timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe.txt" 2>&1 ;;
     phasepers) timeout -k 10 300 python tools/phase_trace.py --pers > "$O/phasepers.txt" 2>&1 ;;
+    hostprobe|hostprobe:*)  # host-side cost of the timed window (tools/window_host_probe.py); hostprobe:VAR=val
+      kv="${s#hostprobe}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 200 python tools/window_host_probe.py > "$O/hostprobe_$n.json" 2> "$O/hostprobe_$n.err" ;;
     pipeflags:*)  # the pipelined step's variants: phase trace + 2000-step bench per DNN_PIPE_FLAGS value
       for f in $(echo "${s#pipeflags:}" | tr ',' ' '); do
         DNN_PIPE_FLAGS=$f timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe_f$f.txt" 2>&1

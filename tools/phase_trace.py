@@ -87,7 +87,7 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     stamps = torch.zeros(4096 + 64, dtype=torch.int64, device=eng.device)
     keys = dict(img=9, conv_ready=12, a_done=1, b_done=2, mlp_ready=13, c_done=3, d_done=4, dp_done=5,
                 e1_done=8, e_done=6, f1_done=10, end=7)
-    recs, walls = [], {steps: [], 64: []}
+    recs, walls, tl = [], {steps: [], 64: []}, []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(reps):
         for n in (steps, 64):
@@ -103,10 +103,23 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
             if n == steps:
                 s = stamps.cpu().numpy().astype(np.float64)
                 recs.append({k: (s[i] - s[0]) * 0.01 for k, i in keys.items()})
+                nrw = (eng.ext.pipe_reduce_blocks() + 1) // 2
+                bl = s[16:16 + 4 * (nrw + batch)].reshape(nrw + batch, 4)
+                t0 = bl[:, 0].min()
+                tl.append(dict(steps=(s[2048:2048 + steps] - t0) * 0.01, smp_start=(bl[nrw:, 0] - t0) * 0.01,
+                               red_start=(bl[:nrw, 0] - t0) * 0.01, smp_end=(bl[nrw:, 2] - t0) * 0.01,
+                               red_end=(bl[:nrw, 2] - t0) * 0.01))
     assert not eng.pipe_failed(), "a persistent-launch wait timed out"
     rr = recs[3:]
     for k in keys:
         print(f"  sample block 0, last step: {k:10s} {float(np.median([x[k] for x in rr])):8.2f} us")
+    med = lambda f: float(np.median([f(x) for x in tl[3:]]))  # noqa: E731
+    print("launch timeline (us from the first workgroup's start, medians):")
+    print(f"  workgroup starts: reduction max {med(lambda x: x['red_start'].max()):.2f}, samples max "
+          f"{med(lambda x: x['smp_start'].max()):.2f}")
+    print("  sample block 0 step starts: " + " ".join(f"{med(lambda x, k=k: x['steps'][k]):.2f}" for k in range(steps)))
+    print(f"  samples end max {med(lambda x: x['smp_end'].max()):.2f}, reduction end med "
+          f"{med(lambda x: np.median(x['red_end'])):.2f} max {med(lambda x: x['red_end'].max()):.2f}")
     w8, w64 = float(np.median(walls[steps][3:])), float(np.median(walls[64][3:]))
     print(f"launch wall (events): {steps} steps {w8:.2f} us, 64 steps {w64:.2f} us -> steady step "
           f"{(w64 - w8) / (64 - steps):.3f} us")

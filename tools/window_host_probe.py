@@ -1,0 +1,80 @@
+"""Host-side cost of the bench's timed window (diagnostic).
+
+The persistent launch runs a 20-step window as ONE kernel, so whatever the window measures beyond
+the kernel is host work: the Python dispatch, the graph (or kernel) launch, and the wake-up of the
+final synchronize.  For each way of launching the window this prints, in microseconds (medians over
+repeats): ``submit`` (host time until the launch call returns), ``wall`` (launch + synchronize, as
+the bench times it), ``gpu`` (events around the launch) and ``wall - gpu``.
+
+    python tools/window_host_probe.py [steps]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_neural_network_amd.data import synthetic  # noqa: E402
+from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
+
+
+def main(steps: int = 20, reps: int = 40) -> None:
+    tr = synthetic(50000, 0)
+    eng = HipEngine(batch=64, seed=0)
+    eng.attach(tr)
+    spe = 50000 // 64
+    eng.begin_epoch(np.arange(50000, dtype=np.int32))
+    eng.prepare_graphs(exact=(steps,))
+    left = spe
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def graph_replay():
+        eng.run_steps(steps)
+
+    g = eng._graph(steps)
+
+    def raw_replay():
+        g.replay()
+
+    def eager():
+        with torch.cuda.device(eng.device):
+            eng._launch_steps(steps)
+
+    res = {"persistent": bool(eng._pers_ok()), "steps": steps}
+    for name, fn, sync in (("run_steps", graph_replay, "device"), ("graph.replay", raw_replay, "device"),
+                           ("eager", eager, "device"), ("graph.replay+event", raw_replay, "event"),
+                           ("graph.replay+spin", raw_replay, "spin")):
+        sub, wall, gpu = [], [], []
+        for r in range(reps):
+            if left < steps + 1:
+                eng.begin_epoch(np.arange(50000, dtype=np.int32))
+                left = spe
+            torch.cuda.synchronize()
+            ev0.record()
+            t0 = time.perf_counter()
+            fn()
+            t1 = time.perf_counter()
+            ev1.record()
+            if sync == "device":
+                torch.cuda.synchronize()
+            elif sync == "event":
+                ev1.synchronize()
+            else:
+                while not ev1.query():
+                    pass
+            t2 = time.perf_counter()
+            left -= steps
+            sub.append(1e6 * (t1 - t0))
+            wall.append(1e6 * (t2 - t0))
+            gpu.append(1e3 * ev0.elapsed_time(ev1))
+        m = lambda v: round(float(np.median(v[5:])), 2)  # noqa: E731
+        res[name] = {"submit": m(sub), "wall": m(wall), "gpu": m(gpu),
+                     "wall_minus_gpu": round(m(wall) - m(gpu), 2)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 20)
