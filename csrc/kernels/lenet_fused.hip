@@ -528,7 +528,7 @@ __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const Pipe
 // every step in order: wait for the rows, reduce + SGD (write-through), signal the ready group.
 // The bookkeeping block is in the conv2 group (samples read its slots after that wait).  The last
 // workgroup to leave zeroes every counter, flag and arrival word for the next launch.
-__device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg) {
+__device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
   const bool bk = m == PIPE_CONV_BLOCKS;
   int rblk = 0;
@@ -539,6 +539,9 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
   for (int t = 0; t < pc.nsteps; ++t) {
     if (threadIdx.x < 64) pers_wait_rows(pc, arr, a.batch, g0 + (unsigned)t + 1u, lane);
+    // diagnostic (stamps): the last step's rows seen / body done / ready stored, per workgroup
+    const bool st = stamps != nullptr && threadIdx.x == 0 && t == pc.nsteps - 1;
+    if (st) stamps[2400 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane, t);
@@ -546,8 +549,10 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
       WtSink sk;
       grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid, 0, false, t & 1);
     }
+    if (st) stamps[2401 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
     __syncthreads();
+    if (st) stamps[2402 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     if (threadIdx.x < 64)  // both blocks done: this workgroup's word in every sample's ready row
       for (int b = lane; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, g0 + (unsigned)t + 1u);
   }
@@ -639,7 +644,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int nrw = PIPE ? (pc.nred + 1) / 2 : 0;
   if constexpr (PIPE) {
     if ((int)blockIdx.x < nrw) {
-      if constexpr (PERS) pers_reduce(ra, pc, blockIdx.x);
+      if constexpr (PERS) pers_reduce(ra, pc, blockIdx.x, stamps);
       else pipe_reduce(ra, pc, blockIdx.x, stamps);
       if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
       return;
@@ -1540,7 +1545,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     __builtin_amdgcn_s_waitcnt(0);
     STAMP(7);
   }
-  if constexpr (PERS) pers_arrive_kind(0);  // slab + loss / correct drained: the conv workgroups go
+  if constexpr (PERS) {
+    pers_arrive_kind(0);  // slab + loss / correct drained: the conv workgroups go
+    if (stamp) stamps[2398] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
 #undef STAMP
 #undef SLAB_PUT
   } while (PERS && ++s < nsteps);  // steps

@@ -106,7 +106,11 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
                 nrw = (eng.ext.pipe_reduce_blocks() + 1) // 2
                 bl = s[16:16 + 4 * (nrw + batch)].reshape(nrw + batch, 4)
                 t0 = bl[:, 0].min()
-                tl.append(dict(steps=(s[2048:2048 + steps] - t0) * 0.01, smp_start=(bl[nrw:, 0] - t0) * 0.01,
+                last = s[2048 + steps - 1]  # the last step's start (sample block 0)
+                rw = s[2400:2400 + 4 * nrw].reshape(nrw, 4)
+                tl.append(dict(red_seen=(rw[:, 0] - last) * 0.01, red_body=(rw[:, 1] - last) * 0.01,
+                               red_ready=(rw[:, 2] - last) * 0.01, arrive0=(s[2398] - last) * 0.01,
+                               steps=(s[2048:2048 + steps] - t0) * 0.01, smp_start=(bl[nrw:, 0] - t0) * 0.01,
                                red_start=(bl[:nrw, 0] - t0) * 0.01, smp_end=(bl[nrw:, 2] - t0) * 0.01,
                                red_end=(bl[:nrw, 2] - t0) * 0.01))
     assert not eng.pipe_failed(), "a persistent-launch wait timed out"
@@ -120,6 +124,13 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     print("  sample block 0 step starts: " + " ".join(f"{med(lambda x, k=k: x['steps'][k]):.2f}" for k in range(steps)))
     print(f"  samples end max {med(lambda x: x['smp_end'].max()):.2f}, reduction end med "
           f"{med(lambda x: np.median(x['red_end'])):.2f} max {med(lambda x: x['red_end'].max()):.2f}")
+    print("last step's reduction (us from that step's start; sample block 0 stored its end-of-step "
+          f"arrival at {med(lambda x: x['arrive0']):.2f}):")
+    for name, sl in (("conv1 WGs 0-3", slice(0, 4)), ("conv2 WGs 4-22", slice(4, 23)), ("MLP WGs 23-56", slice(23, 57))):
+        print(f"  {name:15s} rows seen med/max {med(lambda x: np.median(x['red_seen'][sl])):.2f}/"
+              f"{med(lambda x: x['red_seen'][sl].max()):.2f}  body done {med(lambda x: np.median(x['red_body'][sl])):.2f}/"
+              f"{med(lambda x: x['red_body'][sl].max()):.2f}  ready stored {med(lambda x: np.median(x['red_ready'][sl])):.2f}/"
+              f"{med(lambda x: x['red_ready'][sl].max()):.2f}")
     w8, w64 = float(np.median(walls[steps][3:])), float(np.median(walls[64][3:]))
     print(f"launch wall (events): {steps} steps {w8:.2f} us, 64 steps {w64:.2f} us -> steady step "
           f"{(w64 - w8) / (64 - steps):.3f} us")
