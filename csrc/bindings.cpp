@@ -54,6 +54,17 @@ static bool g_pending_mlp_set = false, g_pending_conv_set = false;
 // fused_train_pipe launch
 static dnn::ReduceArgs g_pending_pipe{};
 static bool g_pending_pipe_set = false;
+// the last cached persistent launch (fused_train_persist(cache=1)), relaunched by persist_relaunch
+struct PersCache {
+  const uint8_t* images; const int32_t* labels; int order_len, batch;
+  const float* master; const bf16* shadow;
+  float *a0, *h1, *h2, *z1, *z2, *z3, *slab, *loss;
+  int32_t* correct; long long* stamps; unsigned char* stage;
+  dnn::ReduceArgs red; dnn::PipeCtl pc;
+};
+static PersCache g_pers_cache{};
+static bool g_pers_cache_set = false;
+static long long g_pers_cache_handle = 0;  // the caller's key of the cached launch
 
 PYBIND11_MODULE(_dnn_hip, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
@@ -217,7 +228,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   // last grad_reduce(defer=2) call's (rows of parity 0, parity 1 right after them)
   m.def("fused_train_persist", [](u images, u labels, int order_len, int batch, u master, u shadow, u a0, u h1, u h2,
                                   u z1, u z2, u z3, u slab, u loss, u correct, u stage, u ctl, int nsteps, u bv0,
-                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags) {
+                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags,
+                                  long long cache) {
     if (!g_pending_pipe_set) throw std::runtime_error("fused_train_persist needs a grad_reduce(defer=2) call first");
     g_pending_pipe_set = false;
     dnn::PipeCtl pc;
@@ -230,16 +242,38 @@ PYBIND11_MODULE(_dnn_hip, m) {
     pc.err = P<unsigned>(err);
     pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
     pc.flags = flags;
-    dnn::launch_fused_train_persist(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
-                                    P<const float>(master), P<const bf16>(shadow), P<float>(a0), P<float>(h1),
-                                    P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
-                                    P<float>(loss), P<int32_t>(correct), P<long long>(stamps), P<unsigned char>(stage),
-                                    g_pending_pipe, pc, S(stream));
+    PersCache c{P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch, P<const float>(master),
+                P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1), P<float>(z2),
+                P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct), P<long long>(stamps),
+                P<unsigned char>(stage), g_pending_pipe, pc};
+    dnn::launch_fused_train_persist(c.images, c.labels, c.order_len, c.batch, c.master, c.shadow, c.a0, c.h1, c.h2,
+                                    c.z1, c.z2, c.z3, c.slab, c.loss, c.correct, c.stamps, c.stage, c.red, pc,
+                                    S(stream));
+    if (cache) {  // (after a launch that passed every argument check) - cache = the caller's handle
+      g_pers_cache = c;
+      g_pers_cache_set = true;
+      g_pers_cache_handle = cache;
+    }
   }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"),
      py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
      py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("stage"), py::arg("ctl"), py::arg("nsteps"),
      py::arg("bv0"), py::arg("bv1"), py::arg("nid0"), py::arg("nid1"), py::arg("err"), py::arg("timeout_s"),
-     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0);
+     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0, py::arg("cache") = 0);
+  // Cached persistent launch: fused_train_persist(cache=1) keeps its whole argument block here;
+  // persist_relaunch(nsteps, stream) launches it again with another step count - ONE kernel, so a
+  // chunk needs no graph (a graph replay costs ~8 us of host submit, this ~3-4 us; measured in
+  // tools/window_host_probe.py)
+  m.def("persist_relaunch", [](long long handle, int nsteps, u stream) {
+    if (!g_pers_cache_set || handle != g_pers_cache_handle)
+      throw std::runtime_error("persist_relaunch: the cached launch is not this handle's");
+    dnn::PipeCtl pc = g_pers_cache.pc;
+    pc.nsteps = nsteps;
+    const auto& c = g_pers_cache;
+    dnn::launch_fused_train_persist(c.images, c.labels, c.order_len, c.batch, c.master, c.shadow, c.a0, c.h1, c.h2,
+                                    c.z1, c.z2, c.z3, c.slab, c.loss, c.correct, c.stamps, c.stage, c.red, pc,
+                                    S(stream));
+  });
+  m.def("persist_cached", [](long long handle) { return g_pers_cache_set && handle == g_pers_cache_handle; });
   m.def("persist_max_batch", []() { return dnn::persist_max_batch(); });
   m.def("persist_ctl_bytes", [](int batch) { return dnn::persist_ctl_bytes(batch); });
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });

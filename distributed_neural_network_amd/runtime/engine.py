@@ -368,6 +368,7 @@ class HipEngine(Engine):
 
     def invalidate_graphs(self) -> None:
         self._graphs.clear()
+        self._pers_gen += 1
 
     # -- data ---------------------------------------------------------------------------
     def attach(self, train: Split) -> None:
@@ -444,7 +445,9 @@ class HipEngine(Engine):
         and no in-launch reduction."""
         return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
 
-    pers_eager = os.environ.get("DNN_PERS_EAGER", "0") == "1"
+    # persistent launches go out directly from the extension's cached argument block, not as graph
+    # replays (DNN_PERS_DIRECT=0: graph replays, as every other step form)
+    pers_direct = os.environ.get("DNN_PERS_DIRECT", "1") != "0"
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
     # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
@@ -502,7 +505,16 @@ class HipEngine(Engine):
         """The persistent launch runs: the pipelined step's conditions, and persist."""
         return self.persist and self._pipe_ok()
 
-    def _launch_steps_pers(self, n: int) -> None:
+    def _pers_handle(self) -> int:
+        """Key of this engine's persistent launch as cached in the extension (persist_relaunch):
+        everything its argument block depends on that can change between launches."""
+        key = (id(self), self.order_len, self._p(self.order), self._p(self.train.images), self._staged,
+               self._pipe_stamps, self.pipe_flags, self._pers_gen)
+        return (hash(key) & 0x3fffffffffffffff) | 1
+
+    _pers_gen = 0  # bumped by invalidate_graphs: a new argument block must be cached
+
+    def _launch_steps_pers(self, n: int, cache: int = 0) -> None:
         """n steps as ONE launch (lenet_fused.hip PERS): the same reduction, bookkeeping slots and
         publication sequence as _launch_steps_pipe's n + 1 launches, with the reduction of step
         n - 1 inside the launch too (it re-publishes slot 0 for the next chunk)."""
@@ -521,7 +533,7 @@ class HipEngine(Engine):
                                      self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
                                      self._p(self.stage), self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
                                      self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                     stamps=self._pipe_stamps, flags=self.pipe_flags)
+                                     stamps=self._pipe_stamps, flags=self.pipe_flags, cache=cache)
 
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
@@ -761,13 +773,18 @@ class HipEngine(Engine):
                         poll()
                     self._launch_step()
             return
-        if self.pers_eager and self._pers_ok():
-            # (diagnostic, DNN_PERS_EAGER=1) the persistent launch is ONE kernel: launched
-            # directly instead of as a one-node graph replay
+        if self._pers_ok() and self.pers_direct:
+            # the persistent launch is ONE kernel whatever n is: no graph - the extension keeps its
+            # argument block and relaunches it (one pybind call, ~3-4 us of host submit against
+            # ~8 us for a graph replay; tools/window_host_probe.py, profiles/r4/pers_handoff)
             if poll is not None:
                 poll()
+            h = self._pers_handle()
             with torch.cuda.device(self.device):
-                self._launch_steps(n)
+                if self.ext.persist_cached(h):
+                    self.ext.persist_relaunch(h, n, self._stream())
+                else:
+                    self._launch_steps_pers(n, cache=h)
             return
         if n in getattr(self, "_exact", ()):
             if poll is not None:

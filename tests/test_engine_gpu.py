@@ -212,9 +212,11 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
     rng = np.random.default_rng(3)
     orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
     res = []
-    # serial, pipelined (one launch per step), persistent (one launch per chunk / run_steps call)
-    for pipe, pers in ((False, False), (True, False), (True, True)):
+    # serial, pipelined (one launch per step), persistent (one launch per run_steps call: direct
+    # relaunches of the cached argument block, and as chunk-graph replays)
+    for pipe, pers, direct in ((False, False, True), (True, False, True), (True, True, True), (True, True, False)):
         eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe, persist=pers)
+        eng.pers_direct = direct
         eng.attach(data)
         stats = []
         for ep, order in enumerate(orders):
