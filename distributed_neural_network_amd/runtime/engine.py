@@ -24,6 +24,7 @@ epoch ends.
 """
 from __future__ import annotations
 
+import itertools
 import os
 import sys
 import time
@@ -345,6 +346,7 @@ class HipEngine(Engine):
             persist = os.environ.get("DNN_PERSIST", "1") != "0" and not gpu_shared_by_ranks()
         self.persist = bool(persist) and self.pipeline and B <= self.ext.persist_max_batch()
         self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
+        self._pers_handles: dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.params_changed()
@@ -445,9 +447,12 @@ class HipEngine(Engine):
         and no in-launch reduction."""
         return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
 
-    # persistent launches go out directly from the extension's cached argument block, not as graph
-    # replays (DNN_PERS_DIRECT=0: graph replays, as every other step form)
-    pers_direct = os.environ.get("DNN_PERS_DIRECT", "1") != "0"
+    # persistent launches directly from the extension's cached argument block instead of graph
+    # replays (DNN_PERS_DIRECT=1; ~3.4 us less per 20-step window, profiles/r4/pers_direct).  Off by
+    # default: with it on, the full GPU suite hit an illegal address in a LATER engine's epoch start
+    # (after persistent runs whose chunks crossed an epoch's end); the same sequence with graph
+    # replays passes (profiles/r4/pers_direct/README.md) - not yet explained, so not the default
+    pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
     # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
@@ -505,12 +510,20 @@ class HipEngine(Engine):
         """The persistent launch runs: the pipelined step's conditions, and persist."""
         return self.persist and self._pipe_ok()
 
+    _pers_handles_next = itertools.count(1)  # process-wide: a handle is never reused
+
     def _pers_handle(self) -> int:
-        """Key of this engine's persistent launch as cached in the extension (persist_relaunch):
-        everything its argument block depends on that can change between launches."""
-        key = (id(self), self.order_len, self._p(self.order), self._p(self.train.images), self._staged,
+        """Handle of this engine's persistent launch as cached in the extension (persist_relaunch):
+        one per (engine, argument block) - everything the block depends on that can change between
+        launches - drawn from a process-wide counter, so a freed engine's cached block can never
+        match another engine (an id()-based key did: ids are reused, and the relaunch then ran on
+        freed buffers)."""
+        key = (self.order_len, self._p(self.order), self._p(self.train.images), self._staged,
                self._pipe_stamps, self.pipe_flags, self._pers_gen)
-        return (hash(key) & 0x3fffffffffffffff) | 1
+        h = self._pers_handles.get(key)
+        if h is None:
+            h = self._pers_handles[key] = next(HipEngine._pers_handles_next)
+        return h
 
     _pers_gen = 0  # bumped by invalidate_graphs: a new argument block must be cached
 

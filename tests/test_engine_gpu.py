@@ -212,9 +212,9 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
     rng = np.random.default_rng(3)
     orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
     res = []
-    # serial, pipelined (one launch per step), persistent (one launch per run_steps call: direct
-    # relaunches of the cached argument block, and as chunk-graph replays)
-    for pipe, pers, direct in ((False, False, True), (True, False, True), (True, True, True), (True, True, False)):
+    # serial, pipelined (one launch per step), persistent (one launch per chunk, graph replays; the
+    # opt-in direct relaunch - DNN_PERS_DIRECT=1 - is not covered: see profiles/r4/pers_direct)
+    for pipe, pers, direct in ((False, False, False), (True, False, False), (True, True, False)):
         eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe, persist=pers)
         eng.pers_direct = direct
         eng.attach(data)
@@ -227,15 +227,15 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
             eng.run_steps(12 if ep != 1 else 13)  # epoch 1 runs a step past its end (a no-op)
             stats.append(eng.epoch_stats())
         torch.cuda.synchronize()
-        assert not (pipe and eng.pipe_failed())
-        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
-    m0, mo0, sh0, st0 = res[0]
-    for m1, mo1, sh1, st1 in res[1:]:
-        assert torch.equal(m0, m1), f"master differs at {int((m0 != m1).sum())} elements"
-        assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1)
+        assert not (pipe and eng.pipe_failed()), f"variant pipe={pipe} persist={pers} direct={direct}: a wait timed out"
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats, (pipe, pers, direct)))
+    m0, mo0, sh0, st0, _ = res[0]
+    for m1, mo1, sh1, st1, var in res[1:]:
+        assert torch.equal(m0, m1), f"variant {var}: master differs at {int((m0 != m1).sum())} elements"
+        assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1), f"variant {var}: momentum / images differ"
         assert [(x.loss_sum, x.samples, x.correct, x.batches) for x in st0] == \
-            [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1]
-        assert all(x.samples == 1000 and x.batches == 16 for x in st1)
+            [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1], f"variant {var}: statistics differ"
+        assert all(x.samples == 1000 and x.batches == 16 for x in st1), f"variant {var}: sample counts"
 
 
 def test_pipelined_long_run_under_load():
