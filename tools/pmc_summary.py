@@ -8,6 +8,9 @@ import sys
 # counter pass, each with the CSV output (run_counter_collection.csv) or the rocpd database
 # (run_results.db) that rocprofv3 writes
 root, pattern = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "lenet_fused_kernelILb1"
+# --per-step N: the persistent launch runs many steps per dispatch - print each counter summed over
+# every matching dispatch, divided by the N steps the run executed, instead of per-dispatch medians
+per_step = int(sys.argv[sys.argv.index("--per-step") + 1]) if "--per-step" in sys.argv else 0
 agg = collections.defaultdict(list)
 for f in glob.glob(f"{root}/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
@@ -23,9 +26,11 @@ for f in glob.glob(f"{root}/*/run_results.db"):
             per[(disp, cname)] += float(val)
     for (_, cname), v in per.items():
         agg[cname].append(v)
-med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
+med = {k: (sum(v) / per_step if per_step else sorted(v)[len(v) // 2]) for k, v in agg.items()}
+if per_step:
+    print(f"(each counter summed over its {len(next(iter(agg.values()), []))} dispatches / {per_step} steps)")
 for k in sorted(med):
-    print(f"{k:28s} median {med[k]:12.4g}  (n={len(agg[k])})")
+    print(f"{k:28s} {'per step' if per_step else 'median'} {med[k]:12.4g}  (n={len(agg[k])})")
 g = med.get
 if g("SQ_WAVE_CYCLES"):
     wc = g("SQ_WAVE_CYCLES")
