@@ -449,10 +449,12 @@ class HipEngine(Engine):
 
     # persistent launches directly from the extension's cached argument block instead of graph
     # replays (DNN_PERS_DIRECT=1; ~3.4 us less per 20-step window, profiles/r4/pers_direct).  Off by
-    # default: with it on, the full GPU suite hit an illegal address in a LATER engine's epoch start
-    # (after persistent runs whose chunks crossed an epoch's end); the same sequence with graph
-    # replays passes (profiles/r4/pers_direct/README.md) - not yet explained, so not the default
+    # default: with it on, a LATER pipelined engine in the same process hits an illegal address that
+    # surfaces between two syncs with no launch in between (runtime-owned memory corrupted - not
+    # found yet); the same sequence with graph replays passes (profiles/r4/pers_direct/README.md,
+    # tools/repro_direct.py).  DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after every relaunch
     pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
+    pers_direct_sync = os.environ.get("DNN_PERS_DIRECT_SYNC", "0") == "1"
     PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
     # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
@@ -798,6 +800,8 @@ class HipEngine(Engine):
                     self.ext.persist_relaunch(h, n, self._stream())
                 else:
                     self._launch_steps_pers(n, cache=h)
+                if self.pers_direct_sync:  # (diagnostic) no host launch while a persistent kernel runs
+                    torch.cuda.synchronize(self.device)
             return
         if n in getattr(self, "_exact", ()):
             if poll is not None:
