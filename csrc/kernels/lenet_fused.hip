@@ -526,8 +526,9 @@ __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const Pipe
 
 // Reduction workgroup `wg` of a persistent launch: blocks 2 wg, 2 wg + 1 (pipe_reduce's map),
 // every step in order: wait for the rows, reduce + SGD (write-through), signal the ready group.
-// The bookkeeping block is in the conv2 group (samples read its slots after that wait).  The last
-// workgroup to leave zeroes every counter, flag and arrival word for the next launch.
+// The bookkeeping block is in the conv2 group (samples read its slots after that wait).  Nothing
+// is reset between launches: every ready / arrival tag is relative to the workgroup's generation
+// word (all of them start at 0 and each launch advances every one by nsteps, as this one does last).
 __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
   const bool bk = m == PIPE_CONV_BLOCKS;
