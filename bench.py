@@ -49,7 +49,7 @@ from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa:
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
 from distributed_neural_network_amd.parallel import selflaunch  # noqa: E402
-from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, allreduce_ab  # noqa: E402
+from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, OVL_PATHS, allreduce_ab, default_candidates  # noqa: E402,E501
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
-    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + BF16_PATHS + ("default",),
+    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + OVL_PATHS + BF16_PATHS + ("default",),
                     help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
                          "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
@@ -125,6 +125,7 @@ def main():
         # no launcher: become one (nothing has touched the GPU yet; children, never an exec)
         sys.exit(selflaunch.run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
                                 out_fd=out_fd))
+    selflaunch.die_with_parent()  # (a self-launched rank: dies with its launcher; no-op otherwise)
     os.environ.setdefault("DNN_STARTUP_TRACE", "1")
     env = detect()
     if env.world != args.gpus:
@@ -155,7 +156,7 @@ def main():
     policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
     policy.record_waits = True  # per-step exchange wait stamps (one store per wave and step)
     policy.grad_comm = args.grad_comm
-    if args.allreduce in ORDER + BF16_PATHS:
+    if args.allreduce in ORDER + OVL_PATHS + BF16_PATHS:
         policy.path = args.allreduce
     stamp(comm.rank, f"engine {type(engine).__name__} ready; installing the all-reduce path")
     policy.attach(engine)
@@ -175,7 +176,7 @@ def main():
     if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
         ab_steps = args.ab_steps or min(args.steps, 256)
         ab = allreduce_ab(policy, engine, cur, steps=ab_steps, warmup=args.warmup, reps=args.ab_reps,
-                          candidates=ORDER + (BF16_PATHS if args.grad_comm == "bf16" else ()),
+                          candidates=default_candidates(args.grad_comm),
                           log=lambda m: stamp(comm.rank, m) if comm.rank == 0 else None)
         stamp(comm.rank, f"all-reduce A/B (us/step, max over ranks): {ab}")
         cur.left = 0  # the timed run starts on a fresh epoch
@@ -198,14 +199,9 @@ def main():
     cur.run(args.warmup)
     if getattr(engine, "pipeline", False) and engine._pipe_ok():
         torch.cuda.synchronize(device)
-        if engine.pipe_failed():  # a wait timed out (never seen): fall back one level and time that
-            if engine.persist:
-                stamp(comm.rank, "persistent launch: a wait timed out in the warmup; using one launch per step")
-                engine.persist = False
-            else:
-                stamp(comm.rank, "pipelined step: a ready wait timed out in the warmup; using the serial step")
-                engine.pipeline = False
-            engine.pipe_err.zero_()
+        if engine.step_wait_failed():  # a wait timed out (never seen): fall back one level and time that
+            level = engine.degrade()
+            stamp(comm.rank, f"an in-launch step wait timed out in the warmup; using the {level} step")
             cur.left = 0
             cur._next_epoch()
             engine.prepare_graphs(exact=(args.steps,) if args.steps <= min(512, cur.left - args.warmup) else ())
@@ -326,6 +322,8 @@ def main():
             out["local_step_us"] = ab["local_us_per_step"]  # same steps with no all-reduce (A/B baseline)
             # the reported window's us/step next to the A/B's number for the same path (same shape)
             out["chosen_timed_us"] = round(1000.0 * ms_per_step, 3)
+            out["ab_wall_s"] = ab["ab_wall_s"]
+            out["allreduce_ab_variant"] = ab["variant"]
         if comm.distributed and args.sync == "step-allreduce":
             out["exchange_wait_us"] = waits
         os.write(out_fd, (json.dumps(out) + "\n").encode())

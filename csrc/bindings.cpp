@@ -275,6 +275,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("persist_cached", [](long long handle) { return g_pers_cache_set && handle == g_pers_cache_handle; });
   m.def("persist_max_batch", []() { return dnn::persist_max_batch(); });
+  m.def("persist_resident_workgroups", []() { return dnn::persist_resident_workgroups(); });
   m.def("persist_ctl_bytes", [](int batch) { return dnn::persist_ctl_bytes(batch); });
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });
   m.def("pipe_groups", []() { return dnn::pipe_groups(); });

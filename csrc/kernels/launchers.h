@@ -115,6 +115,7 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
                                 float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
                                 unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc, hipStream_t stream);
 int persist_max_batch();   // largest batch whose persistent grid is co-resident on this device
+int persist_resident_workgroups();  // workgroups of the persistent kernel resident at once (occupancy x CUs)
 int persist_ctl_bytes(int batch);  // control memory of a persistent launch (uncached)
 int pipe_reduce_blocks();  // reduction blocks of a full PIPE launch (2 per workgroup)
 int pipe_groups();         // ready groups (counters / flags per parity)

@@ -749,6 +749,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // PERS: every wave drained its stores (rows, slab, image stage) -> barrier -> one wave stores
   // this sample's arrival tags for the conv workgroups (kind 0) or the MLP workgroups (kind 1)
   auto pers_arrive_kind = [&](int kind) {
+    // fault injection (flags & 256, tests only): sample 0 arrives for the conv workgroups of step 1
+    // only 3 wait timeouts late - the reduction's bounded wait then fails, sets the sticky error
+    // word, and every later wait returns at once (the host steps down to a slower step form)
+    if (PERS && (pc.flags & 256) && b == 0 && s == 1 && kind == 0 && tid == 0) {
+      const long long t0 = wall_clock64();
+      while (wall_clock64() - t0 < 3 * pc.timeout_ticks) __builtin_amdgcn_s_sleep(64);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave == 0) pers_arrive(pc, kind, b, g0 + (unsigned)s + 1u, lane);
@@ -1642,14 +1649,26 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
 
 // Largest batch whose persistent grid (PERS_WG reduction + batch sample workgroups, one per CU:
 // each holds LDS_TOTAL of LDS) is co-resident on this device - a condition of every in-launch wait.
-int persist_max_batch() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
+// The count comes from the runtime's occupancy calculator for THIS kernel at its launch shape
+// (NT threads, LDS_TOTAL dynamic LDS: one workgroup per CU) times the CU count - not from an
+// assumption - and keeps PERS_MARGIN CUs free for other work on the device (an RCCL kernel, the
+// eval launch of another stream), so the grid stays co-resident next to them.
+constexpr int PERS_MARGIN = 8;
+int persist_resident_workgroups() {
+  static int resident = -1;
+  if (resident < 0) {
+    init_kernels();
+    int dev = 0, cus = 0, per_cu = 0;
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, 0, true, true>), NT, LDS_TOTAL));
+    resident = per_cu * cus;
   }
-  return std::min(cus - PERS_WG, PERS_AROW);
+  return resident;
+}
+int persist_max_batch() {
+  return std::max(0, std::min(persist_resident_workgroups() - PERS_WG - PERS_MARGIN, PERS_AROW));
 }
 
 void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,

@@ -39,11 +39,33 @@ from typing import Callable, Optional
 
 import torch
 
-ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl")
+ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+# opt-in (DNN_AB_OVL=1): the in-launch (-ovl) forms - they lost 3x to the one-launch exchange in the
+# 2-rank rehearsal (profiles/r4/ab_rehearsal: 134 / 143 vs 43.5 us), so by default they cost no
+# 8-GPU start-up time
+OVL_PATHS = ("xgmi-pull-ovl", "xgmi-rsag-ovl")
 # opt-in (--grad-comm bf16): the xGMI exchanges with bf16 gradient granules - half the link
 # bytes, lower-precision gradients, so never a candidate unless asked for
 BF16_PATHS = ("xgmi-pull-bf16", "xgmi-rsag-bf16")
-RANK = ORDER + BF16_PATHS  # tie-break order
+RANK = ORDER + OVL_PATHS + BF16_PATHS  # tie-break order
+
+
+def default_candidates(grad_comm: str = "fp32") -> tuple[str, ...]:
+    """The A/B's candidate list: ORDER, + OVL_PATHS with DNN_AB_OVL=1, + BF16_PATHS when bf16
+    gradient communication was asked for."""
+    c = ORDER
+    if os.environ.get("DNN_AB_OVL", "0") == "1":
+        c = c + OVL_PATHS
+    if grad_comm == "bf16":
+        c = c + BF16_PATHS
+    return c
+
+
+def budget_default() -> float:
+    """Wall budget of the whole A/B (DNN_AB_BUDGET_S, default 240 s): candidates not started
+    within it are skipped (and reported failed with that reason), and a candidate's RCCL init
+    timeout never exceeds what is left of it."""
+    return float(os.environ.get("DNN_AB_BUDGET_S", "240"))
 
 
 def choose(results: dict[str, dict]) -> str | None:
@@ -119,12 +141,23 @@ def _agree(comm, ok: bool) -> bool:
 
 def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: int = 2, reps: int = 3,
                  candidates: tuple[str, ...] = ORDER, log: Optional[Callable[[str], None]] = None,
-                 rccl_init_timeout_s: float = 60.0, spin: int = 200) -> dict:
+                 rccl_init_timeout_s: float = 60.0, spin: int = 200, budget_s: float | None = None,
+                 rccl_init_after_xgmi_s: float = 15.0) -> dict:
     """Collective (every rank calls it with the same arguments).  ``cur`` is the run's
     ``EpochCursor``.  Times every candidate, installs the winner on ``engine`` (``policy.path``
     pins it for later re-attaches) and returns {"allreduce_ab": {path: us_per_step | None},
-    "allreduce": winner, "local_us_per_step": ..., "failed": [...], "why": {path: reason}}."""
+    "allreduce": winner, "local_us_per_step": ..., "failed": [...], "why": {path: reason},
+    "ab_wall_s": seconds, "variant": {path: step form it was timed with}}.
+
+    Bounded: the whole A/B has a wall budget (``budget_s``, default
+    ``budget_default()``); a candidate is started only while the budget lasts (decided from the
+    max elapsed time over ranks, so every rank skips the same ones), a candidate whose install +
+    timing ran past it is marked failed, and the RCCL init timeout of a candidate is capped by
+    the budget left - and by ``rccl_init_after_xgmi_s`` once an xGMI path has passed (RCCL can
+    then only win by being fast, and a slow init says it will not)."""
     comm = policy.comm
+    budget = budget_default() if budget_s is None else float(budget_s)
+    t_start = time.perf_counter()
     say = log or (lambda s: None)
     snap = (engine.master.detach().clone(), engine.mom.detach().clone())
 
@@ -140,13 +173,26 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
     lazy = getattr(policy, "lazy_check", False)
     policy.lazy_check = True  # an xGMI wait failure is voted per candidate below, not at an epoch end
     tmo = os.environ.get("DNN_RCCL_INIT_TIMEOUT_S")
-    os.environ["DNN_RCCL_INIT_TIMEOUT_S"] = str(min(float(tmo or 1e9), rccl_init_timeout_s))
+    variant: dict[str, str] = {}
     try:
         for rnd in range(rounds):
             seq = names if rnd % 2 == 0 else tuple(reversed(names))
             for name in seq:
                 if results.get(name, {}).get("ok") is False:
                     continue  # failed once: not tried again
+                left = budget - comm.reduce_scalar(time.perf_counter() - t_start, "max")
+                if left <= 0:
+                    if name not in results:
+                        results[name] = {"ok": False, "us_per_step": None, "why": f"skipped: A/B wall budget "
+                                                                                   f"({budget:.0f} s) spent"}
+                        say(f"A/B {name}: skipped (budget spent)")
+                    continue
+                xgmi_ok = any(v.get("ok") for k, v in results.items() if k.startswith("xgmi"))
+                cap = min(float(tmo or 1e9), rccl_init_timeout_s, max(1.0, left))
+                if xgmi_ok:
+                    cap = min(cap, rccl_init_after_xgmi_s)
+                os.environ["DNN_RCCL_INIT_TIMEOUT_S"] = str(cap)
+                policy.ab_deadline = time.time() + left  # (candidates may bound their own set-up by it)
                 t0 = time.perf_counter()
                 why = ""
                 try:
@@ -176,6 +222,15 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
                     _drop(policy, engine, name)
                     say(f"A/B {name}: FAILED ({results[name]['why']})")
                     continue
+                spent = comm.reduce_scalar(time.perf_counter() - t0, "max")
+                if spent > left:  # ran past the whole A/B's budget: not selectable
+                    results[name] = {"ok": False, "us_per_step": None,
+                                     "why": f"over the A/B wall budget ({spent:.1f} s for this candidate, "
+                                            f"{left:.1f} s left)"}
+                    _drop(policy, engine, name)
+                    say(f"A/B {name}: FAILED ({results[name]['why']})")
+                    continue
+                variant[name] = step_variant(engine)
                 prev = results.get(name, {}).get("us_per_step")
                 results[name] = {"ok": True, "us_per_step": us if prev is None else min(prev, us)}
                 say(f"A/B {name}: {us:.3f} us/step (round {rnd}, {time.perf_counter() - t0:.2f}s incl. install)")
@@ -197,6 +252,7 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
         restore()
     finally:
         policy.lazy_check = lazy
+        policy.ab_deadline = None
         if tmo is None:
             os.environ.pop("DNN_RCCL_INIT_TIMEOUT_S", None)
         else:
@@ -207,7 +263,22 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
                                   if results.get("local", {}).get("us_per_step") is not None else None),
             "allreduce": policy.installed(engine),
             "failed": sorted(k for k, v in results.items() if not v.get("ok")),
-            "why": {k: v["why"] for k, v in results.items() if not v.get("ok")}}
+            "why": {k: v["why"] for k, v in results.items() if not v.get("ok")},
+            "ab_wall_s": round(comm.reduce_scalar(time.perf_counter() - t_start, "max"), 3),
+            "variant": variant}
+
+
+def step_variant(engine) -> str:
+    """The step form a candidate was timed with (the no-all-reduce baseline may run
+    the persistent step while a candidate runs the serial one): persistent / pipelined /
+    early-mlp / serial."""
+    if getattr(engine, "_pers_ok", lambda: False)():
+        return "persistent"
+    if getattr(engine, "_pipe_ok", lambda: False)():
+        return "pipelined"
+    if getattr(engine, "_early_ok", lambda: False)():
+        return "early-mlp"
+    return "serial"
 
 
 def _drop(policy, engine, name: str) -> None:
@@ -228,4 +299,5 @@ def _drop(policy, engine, name: str) -> None:
             policy.comm.native = None
 
 
-__all__ = ["BF16_PATHS", "ORDER", "allreduce_ab", "choose", "prepare_window", "window"]
+__all__ = ["BF16_PATHS", "ORDER", "OVL_PATHS", "allreduce_ab", "budget_default", "choose", "default_candidates",
+           "prepare_window", "step_variant", "window"]

@@ -115,6 +115,15 @@ class Communicator:
             self.store = dist.TCPStore(self.env.master_addr, self.env.master_port, self.env.world,
                                        is_master=self.env.rank == 0, timeout=self.timeout,
                                        wait_for_workers=False)
+        # process identity (host:pid): the stand-alone store stays up while a rank of this host is
+        # alive and exits once they are all gone (parallel/store_server.py); the heartbeat
+        # watchdog reads it too (a gone local pid is a dead rank, fault.Heartbeat)
+        try:
+            import socket
+
+            self.store.set(f"dnn/pid/{self.orig_rank}", f"{socket.gethostname()}:{os.getpid()}")
+        except Exception:
+            pass
 
     STALE_BEAT_S = 30.0
 

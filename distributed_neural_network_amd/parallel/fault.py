@@ -100,6 +100,7 @@ class Heartbeat:
         self._gaps: list[float] = []  # recent gaps between a peer's consecutive beat stamps (s)
         self._last_val: dict[int, float] = {}
         self.dead: set[int] = set()
+        self.done: set[int] = set()  # peers that checked out (finished normally; never flagged)
         self.detected_at: dict[int, float] = {}  # rank -> time.time() when the watchdog flagged it
         # rank -> time its flag was cleared by a recovery agreement: staleness counts from here,
         # so a rank that was only late gets a full timeout to beat again before a new flag
@@ -168,6 +169,24 @@ class Heartbeat:
             return False
         return self._local_pid_gone(rank)
 
+    def check_out(self) -> None:
+        """This rank finished its run normally (``Trainer._finish``, after the final barrier):
+        peers must never take its exit for a death.  Written BEFORE the process exits, so a peer
+        that sees the pid gone (or the launcher's notice) and THEN reads this key always finds it
+        (``_run`` tests in that order)."""
+        self.store.set(f"dnn/done/{self.comm.orig_rank}", repr(time.time()))
+
+    def checked_out(self, rank: int) -> bool:
+        if rank in self.done:
+            return True
+        try:
+            if self.store.check([f"dnn/done/{rank}"]):
+                self.done.add(rank)
+                return True
+        except Exception:
+            pass
+        return False
+
     def _local_pid_gone(self, rank: int) -> bool:
         if rank not in self._pids:
             pid = None
@@ -205,9 +224,15 @@ class Heartbeat:
             try:
                 self._beat()
                 for r in list(self.comm.members):
-                    if r == self.comm.orig_rank or r in self.dead:
+                    if r == self.comm.orig_rank or r in self.dead or r in self.done:
                         continue
-                    if self.reported_dead(r):
+                    # order matters: liveness first, then the check-out - a rank writes its
+                    # check-out before it exits, so a gone process whose key is not there yet
+                    # cannot be a normal exit
+                    gone = self.reported_dead(r)
+                    if self.checked_out(r):
+                        continue  # finished its run: its exit and its silence are not a death
+                    if gone:
                         self._flag(r, "process exited (reported by the launcher)")
                     elif self.stale(r):
                         self._flag(r, f"heartbeat stale > {self.timeout}s")
@@ -340,6 +365,19 @@ def stall_process(kind: str, seconds: float) -> None:
         return
     subprocess.Popen(["/bin/sh", "-c", f"sleep {seconds}; kill -CONT {os.getpid()}"], start_new_session=True)
     os.kill(os.getpid(), signal.SIGSTOP)
+
+
+def end_skew_injection(orig_rank: int, where: str = "before") -> float:
+    """Fault injection for tests (``DNN_INJECT_END_SKEW=rank:seconds[:after]``): that rank idles
+    this long after the last epoch's last collective - before the final barrier (default: its
+    peers wait in the barrier), or ``after`` it (its peers check out and exit first, while its
+    watchdog still runs).  Returns the delay for the point ``where`` (0: none)."""
+    spec = os.environ.get("DNN_INJECT_END_SKEW", "")
+    if not spec:
+        return 0.0
+    parts = spec.split(":")
+    at = parts[2] if len(parts) > 2 else "before"
+    return float(parts[1]) if int(parts[0]) == orig_rank and at == where else 0.0
 
 
 def beat_pause_injection(orig_rank: int, epoch: int) -> float:

@@ -7,7 +7,8 @@ run_training.sh:1-3).  ``bench.py --gpus N`` must produce its number whether a l
 environment it becomes its own launcher:
 
 * it runs BEFORE anything touches the GPU (no HIP call, no ``torch.cuda.is_available()``): the
-  parent only counts devices, hosts the rendezvous TCPStore (so any rank may die and the others
+  parent only counts devices (KFD topology in sysfs + the visibility variables, never a HIP
+  call), hosts the rendezvous TCPStore (so any rank may die and the others
   still see it: ``dnn/dead/<rank>`` is published the moment a child fails, as in
   parallel/launch.py) and starts N children with ``subprocess`` - never an exec;
 * every child gets RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR=127.0.0.1 / MASTER_PORT and
@@ -48,25 +49,72 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def visible_devices() -> int:
-    """GPUs this process could use, counted without initialising the GPU runtime."""
+def _kfd_gpu_nodes(root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPU nodes of the KFD topology (sysfs: a node with a non-zero ``gfx_target_version`` is a
+    GPU, the others are CPU nodes).  -1 if the topology cannot be read."""
     try:
-        import torch
+        names = os.listdir(root)
+    except OSError:
+        return -1
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version":
+                        n += int(v.strip() or 0) != 0
+                        break
+        except (OSError, ValueError):
+            continue
+    return n
 
-        return int(torch.cuda.device_count())
+
+def _visible_list(n_nodes: int) -> int:
+    """Apply the runtime's visibility masks (ROCR_, then HIP_ / CUDA_VISIBLE_DEVICES) to n_nodes."""
+    n = n_nodes
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(k)
+        if v is None:
+            continue
+        ids = [x for x in v.split(",") if x.strip() != ""]
+        n = min(n, len(ids)) if n >= 0 else len(ids)
+    return n
+
+
+def visible_devices() -> int:
+    """GPUs this process could use, counted WITHOUT any HIP call in this process (the launcher
+    must not initialise the GPU runtime: its children are started from it).  Reads the KFD
+    topology in sysfs and the visibility variables; if sysfs is unreadable, a short-lived child
+    process asks torch (whatever that initialises dies with the child)."""
+    n = _kfd_gpu_nodes()
+    if n >= 0:
+        return max(0, _visible_list(n))
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1])
     except Exception:
         return 0
 
 
-def _die_with_parent() -> None:
-    """preexec_fn of every rank: SIGKILL it when the launcher dies (a driver timeout that kills
-    the launcher must not leave ranks holding GPUs in their own sessions)."""
+def die_with_parent() -> None:
+    """Called by a self-launched rank (``DNN_SELF_LAUNCHED=1``) at its start: SIGKILL it when the
+    launcher dies (a driver timeout that kills the launcher must not leave ranks holding GPUs in
+    their own sessions).  The rank sets this itself - the launcher passes no preexec_fn, which
+    would force fork + exec in a copy of a multi-threaded parent.  If the launcher is already gone
+    (it died before this call), the rank exits at once."""
+    if os.environ.get("DNN_SELF_LAUNCHED") != "1":
+        return
     try:
         import ctypes
 
         ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG
     except Exception:
-        pass
+        return
+    want = os.environ.get("DNN_LAUNCHER_PID")
+    if want and os.getppid() != int(want):
+        os._exit(1)
 
 
 class _Child:
@@ -121,17 +169,18 @@ def run(cmd: Sequence[str], nproc: int, out_fd: int | None = None, extra_env: Op
         env = dict(base)
         env.update(RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(nproc),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_STORE_EXTERNAL="1",
-                   DNN_SELF_LAUNCHED="1", PYTHONUNBUFFERED="1")
+                   DNN_SELF_LAUNCHED="1", DNN_LAUNCHER_PID=str(os.getpid()), PYTHONUNBUFFERED="1")
         p = subprocess.Popen(list(cmd), env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                             bufsize=1, start_new_session=True, stdin=subprocess.DEVNULL,
-                             preexec_fn=_die_with_parent)
-        c = _Child(r, p, tail_lines)
+                             bufsize=1, start_new_session=True, stdin=subprocess.DEVNULL)
+        children.append(_Child(r, p, tail_lines))
+    # the relay threads start only once every child exists (no child is spawned while they run)
+    for c in children:
+        r, p = c.rank, c.proc
         c.threads = [threading.Thread(target=_pump, args=(p.stderr, _prefixed(r, err), c.err_tail.append), daemon=True),
                      threading.Thread(target=_pump, args=(p.stdout, None if r == 0 else _prefixed(r, err),
                                                           c.out.append), daemon=True)]
         for t in c.threads:
             t.start()
-        children.append(c)
     print(f"[launch +{time.time() - t0:.3f}s] store on 127.0.0.1:{port}, {nproc} ranks started", file=err, flush=True)
 
     def _forward(signum, frame):  # the launcher is being stopped: stop the ranks first
@@ -217,4 +266,4 @@ def _kill_group(p: subprocess.Popen, sig: int) -> None:
             pass
 
 
-__all__ = ["launcher_present", "run", "visible_devices"]
+__all__ = ["die_with_parent", "launcher_present", "run", "visible_devices"]

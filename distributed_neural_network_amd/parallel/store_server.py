@@ -11,7 +11,11 @@ single rank.
 It exits when every rank of the job has checked out (``dnn/closed`` counter, incremented by
 ``Communicator.close``; a rank the recovery dropped counts through ``dnn/dropped``), when every
 heartbeat it has seen is older than ``--stale`` seconds (the ranks are gone without checking
-out: a crash, Ctrl-C, SIGKILL), or when nothing at all has changed for ``--idle`` seconds.  It
+out: a crash, Ctrl-C, SIGKILL), when every rank process registered on this host
+(``dnn/pid/<r>`` = host:pid, written by every rank at connect) is gone, or when nothing at all
+has changed for ``--idle`` seconds - the idle exit only while no registered rank of this host
+is alive: a live job that makes no store writes for a while (a bench without a heartbeat) keeps
+its store.  It
 publishes ``dnn/store_server`` = ``--token`` (rank 0's job token), so rank 0 can tell its own
 server from one an earlier job left on the port (Communicator._check_fresh_store).
 
@@ -21,8 +25,24 @@ usage (started by Communicator; not by hand):
 from __future__ import annotations
 
 import argparse
+import os
+import socket
 import sys
 import time
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except OSError:
+        return True
 
 
 def main(argv=None) -> int:
@@ -41,6 +61,8 @@ def main(argv=None) -> int:
                           timeout=__import__("datetime").timedelta(seconds=30))
     store.set("dnn/store_server", a.token)
     last_change, last_sig = time.time(), None
+    host = socket.gethostname()
+    pids: dict[int, int] = {}  # registered ranks of this host
     while True:
         time.sleep(0.2)
         try:
@@ -66,9 +88,23 @@ def main(argv=None) -> int:
         if seen and time.time() - max(seen) > a.stale:
             print(f"[store] no heartbeat for {a.stale:.0f} s: the job is gone, exiting", file=sys.stderr, flush=True)
             return 0
+        for r in range(a.world):
+            if r not in pids:
+                try:
+                    k = f"dnn/pid/{r}"
+                    if store.check([k]):
+                        h, _, p = store.get(k).decode().rpartition(":")
+                        pids[r] = int(p) if h == host else -1
+                except Exception:
+                    pass
+        local = [p for p in pids.values() if p > 0]
+        alive = [p for p in local if _pid_alive(p)]
+        if local and not alive and len(pids) == a.world:
+            print("[store] every rank process of this host is gone: exiting", file=sys.stderr, flush=True)
+            return 0
         if sig != last_sig:
             last_sig, last_change = sig, time.time()
-        elif time.time() - last_change > a.idle:
+        elif time.time() - last_change > a.idle and not alive:
             print(f"[store] no activity for {a.idle:.0f} s: exiting", file=sys.stderr, flush=True)
             return 0
 

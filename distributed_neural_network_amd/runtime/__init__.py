@@ -1,5 +1,5 @@
-from .engine import ENGINES, CpuEngine, Engine, HipEngine, StepStats, eval_metrics, make_engine
+from .engine import ENGINES, CpuEngine, Engine, HipEngine, StepStats, StepWaitTimeout, eval_metrics, make_engine
 from .layer_engine import LayerEngine
 
-__all__ = ["ENGINES", "CpuEngine", "Engine", "HipEngine", "LayerEngine", "StepStats", "eval_metrics",
+__all__ = ["ENGINES", "CpuEngine", "Engine", "HipEngine", "LayerEngine", "StepStats", "StepWaitTimeout", "eval_metrics",
            "make_engine"]

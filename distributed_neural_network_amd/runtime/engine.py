@@ -40,6 +40,13 @@ from ..models.network import LAYOUT, arena_state_dict, init_arena, load_state_di
 from ..ops import native, reference
 
 
+class StepWaitTimeout(RuntimeError):
+    """A bounded in-launch wait of the pipelined / persistent step (or the early-MLP row wait)
+    timed out: the epoch's parameters are not trustworthy.  ``Trainer.run`` restores the epoch's
+    snapshot, steps the engine down (``HipEngine.degrade``: persistent -> pipelined -> serial)
+    and redoes the epoch; nothing else is lost."""
+
+
 class GradSync(Protocol):
     """Per-step gradient synchronisation (the step-allreduce policy implements it)."""
 
@@ -455,7 +462,9 @@ class HipEngine(Engine):
     # tools/repro_direct.py).  DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after every relaunch
     pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
     pers_direct_sync = os.environ.get("DNN_PERS_DIRECT_SYNC", "0") == "1"
-    PIPE_TIMEOUT_S = 10.0  # bound of one ready wait (then a sticky error word, raised at epoch_stats)
+    # bound of one ready wait (then a sticky error word, raised at epoch_stats); DNN_PIPE_TIMEOUT_S
+    # overrides it (tests force a timeout with a tiny bound + an injected delay, DNN_PIPE_FLAGS=256)
+    PIPE_TIMEOUT_S = float(os.environ.get("DNN_PIPE_TIMEOUT_S", "10.0"))
     _pipe_stamps = 0  # diagnostic (tools/phase_trace.py --pipe): stamp buffer of the merged launches
     # lenet_fused.hip PipeCtl.flags (measurement switches): & 1 no mid-phase-B fc1 stream
     pipe_flags = int(os.environ.get("DNN_PIPE_FLAGS", "0"))
@@ -818,14 +827,41 @@ class HipEngine(Engine):
                         poll()
                     g.replay()
 
+    def step_wait_failed(self) -> bool:
+        """Did an in-launch wait of this engine's step time out (sticky error words)?"""
+        return self.early_failed() or self.pipe_failed()
+
+    def degrade(self) -> str | None:
+        """Step down one level after a StepWaitTimeout: persistent -> pipelined -> serial (each
+        bit-identical to the next).  Clears the sticky error words and the cached graphs; returns
+        the new level, or None if the engine already runs the serial step (nothing to step down
+        to: the caller re-raises)."""
+        if self.persist:
+            self.persist = False
+            level = "pipelined"
+        elif self.pipeline:
+            self.pipeline = False
+            level = "serial"
+        elif self.early_mlp:
+            self.early_mlp = False
+            level = "serial (no in-launch reduction)"
+        else:
+            return None
+        if hasattr(self, "pipe_err"):
+            self.pipe_err.zero_()
+        if self._rg is not None:
+            self._rg["err"].zero_()
+        self.invalidate_graphs()
+        return level
+
     def epoch_stats(self, reset: bool = True) -> StepStats:
         v = self.stats.cpu().tolist()
         if self.early_failed():
-            raise RuntimeError("early-MLP overlap: a row-granule wait timed out (the MLP reduction of a step "
-                               "did not see the fused kernel's rows); rerun with DNN_EARLY_MLP=0")
+            raise StepWaitTimeout("early-MLP overlap: a row-granule wait timed out (the MLP reduction of a step "
+                                  "did not see the fused kernel's rows)")
         if self.pipe_failed():
-            raise RuntimeError("pipelined step: a ready wait timed out (the samples did not see their launch's "
-                               "reduction finish); rerun with DNN_PIPELINE=0")
+            raise StepWaitTimeout("pipelined / persistent step: a ready or arrival wait timed out (a reduction or "
+                                  "sample workgroup did not see its hand-off in time)")
         if reset:
             self.stats.zero_()
         return StepStats(v[0], int(round(v[1])), int(round(v[2])), int(round(v[3])))

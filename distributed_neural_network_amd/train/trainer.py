@@ -26,8 +26,8 @@ import torch
 from ..data import EpochSampler, get_splits
 from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
 from ..parallel.fault import (DropInjector, Heartbeat, agree_survivors, announce_alive, beat_pause_injection,
-                              simulate_failure, stall_injection, stall_process)
-from ..runtime import eval_metrics, make_engine
+                              end_skew_injection, simulate_failure, stall_injection, stall_process)
+from ..runtime import StepWaitTimeout, eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
 from ..utils.metrics import Run
 from ..utils.timers import PhaseTimers
@@ -134,6 +134,24 @@ class Trainer:
         self.engine.run_steps(n)
         self.comm.wait_device()  # interruptible: raises CommError if a peer is declared dead
 
+    def _check_step_waits(self, epoch: int) -> None:
+        """Raise StepWaitTimeout if a bounded in-launch wait timed out this epoch.  With a per-step
+        all-reduce installed every rank votes (one tiny collective per epoch), so all ranks step
+        down and redo the epoch together and their exchange step counters stay in step; without
+        one (one rank, epoch-avg) the ranks train independently within an epoch and each decides
+        alone (a rank that redoes its epoch only arrives later at the epoch-end average)."""
+        failed = getattr(self.engine, "step_wait_failed", None)
+        if failed is None:
+            return
+        bad = bool(failed())
+        if self.comm.distributed and self.engine.grad_sync is not None:
+            votes = self.comm.gather_scalars(1.0 if bad else 0.0)
+            ranks = [i for i, v in enumerate(votes) if v != 0.0]
+            if ranks:
+                raise StepWaitTimeout(f"an in-launch step wait timed out on rank(s) {ranks} in epoch {epoch}")
+        elif bad:
+            raise StepWaitTimeout(f"an in-launch step wait timed out in epoch {epoch}")
+
     def _recover(self, epoch: int, snap: tuple[torch.Tensor, torch.Tensor], err: Exception) -> None:
         """Survivor side of a failure: every stage is timed (wall clock, so the stamps compare
         across the ranks of one host) and recorded: detect (the watchdog flagged a peer, or the
@@ -236,11 +254,11 @@ class Trainer:
         self.allreduce_ab = None
         if c.allreduce == "ab" and self.comm.distributed and hasattr(self.policy, "PATHS"):
             # start-up A/B of the per-step all-reduce on this node (parameters restored after)
-            from ..parallel.autotune import BF16_PATHS, ORDER, allreduce_ab
+            from ..parallel.autotune import allreduce_ab, default_candidates
             from ..runtime.cursor import EpochCursor
 
             cur = EpochCursor(self.engine, self.sampler, self.policy, c.batch_size)
-            cands = ORDER + (BF16_PATHS if self.policy.grad_comm == "bf16" else ())
+            cands = default_candidates(self.policy.grad_comm)
             self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur, steps=64, warmup=16, candidates=cands)
             self._say(f"[allreduce] start-up A/B (us/step, max over ranks): {self.allreduce_ab['allreduce_ab']}; "
                       f"using {self.allreduce_ab['allreduce']}")
@@ -295,6 +313,7 @@ class Trainer:
                 if self.policy.trains():
                     with self.timers.phase(PhaseTimers.TRAIN):
                         self._train_epoch(epoch)
+                self._check_step_waits(epoch)
                 stats = self.engine.epoch_stats(reset=True)
                 t0 = time.perf_counter()
                 self.policy.epoch_end(self.engine, epoch)
@@ -314,6 +333,32 @@ class Trainer:
                 # peer too); the lines are printed below in the reference's order
                 with self.timers.phase(PhaseTimers.EVAL):
                     val_loss, val_acc = self._evaluate()
+                if epoch == c.epochs - 1 and self.comm.distributed:
+                    skew = end_skew_injection(self.comm.orig_rank)
+                    if skew:
+                        print(f"[fault] injected end skew: rank {self.comm.orig_rank} idles {skew} s after the last "
+                              f"collective", flush=True)
+                        time.sleep(skew)
+                    # nobody leaves before every rank is done with the last collective (a fast rank's
+                    # exit must not reach a slow peer's watchdog while that peer still waits on it);
+                    # inside the recovery scope: a real death here still re-forms and redoes the epoch
+                    self.comm.barrier()
+            except StepWaitTimeout as e:
+                # an in-launch wait of the pipelined / persistent step timed out (e.g. the grid
+                # lost co-residency to other work on the device): restore the epoch's snapshot,
+                # step the engine down one level and redo the epoch - the job goes on
+                level = self.engine.degrade() if hasattr(self.engine, "degrade") else None
+                if level is None:
+                    raise
+                print(f"[engine] rank {self.comm.orig_rank}: {e}; stepping down to the {level} step and redoing "
+                      f"epoch {epoch} from its start", flush=True)
+                self.run_log.record(event="step_degraded", epoch=epoch, level=level, rank=self.comm.orig_rank)
+                with torch.no_grad():
+                    self.engine.master.copy_(snap[0])
+                    self.engine.mom.copy_(snap[1])
+                self.engine.params_changed()
+                self.engine.epoch_stats(reset=True)
+                continue
             except CommError as e:
                 if not self.comm.distributed or self.hb is None:
                     raise
@@ -392,7 +437,17 @@ class Trainer:
                 if c.write_logs:
                     logfiles.write_log(c.log_dir, logfiles.log_name(c.batch_size, c.epochs, c.nb_proc, "children"),
                                        logfiles.children_lines(T[PhaseTimers.DATA], T[PhaseTimers.TRAIN], comm_c))
+        skew = end_skew_injection(self.comm.orig_rank, "after") if self.comm.distributed else 0.0
+        if skew:
+            print(f"[fault] injected end skew: rank {self.comm.orig_rank} idles {skew} s after the final barrier",
+                  flush=True)
+            time.sleep(skew)
         if self.hb is not None:
+            # check out before the beat stops and the process exits: peers never flag this exit
+            try:
+                self.hb.check_out()
+            except Exception:
+                pass
             self.hb.stop()
         self.run_log.stop()
         self.comm.close()

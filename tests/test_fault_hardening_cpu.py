@@ -174,3 +174,60 @@ def test_store_server_exits_when_heartbeats_go_stale():
     finally:
         if srv.poll() is None:
             srv.kill()
+
+
+def test_checked_out_peer_is_never_flagged():
+    """A peer that finished its run (``dnn/done/<r>``, written before it exits) is not dead when
+    its pid is gone or its heartbeat goes stale (a fast rank's normal exit
+    was taken for a death and the last epoch was redone without it)."""
+    store = dist.TCPStore("127.0.0.1", 0, 1, is_master=True, wait_for_workers=False)
+    c = Communicator(DistEnv(0, 1, 0, "127.0.0.1", store.port), "cpu")
+    c.members = [0, 1]
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    p.wait()
+    store.set("dnn/pid/1", f"{socket.gethostname()}:{p.pid}")  # exited
+    store.set("dnn/hb/1", repr(time.time() - 60.0))             # and silent
+    store.set("dnn/done/1", repr(time.time()))                  # but checked out first
+    hb = Heartbeat(c, period_s=0.02, timeout_s=0.1)
+    try:
+        time.sleep(0.5)
+        assert 1 not in hb.dead and hb.checked_out(1) and c.lost() == []
+    finally:
+        hb.stop()
+
+
+@pytest.mark.parametrize("where", ["before", "after"])
+def test_normal_exit_of_fast_rank_is_not_a_drop(tmp_path, where):
+    """Rank 0 idles 0.5 s after the last epoch's last collective (``before``: the final barrier
+    holds its peers; ``after``: its peers pass the barrier, check out and EXIT while rank 0's
+    watchdog still runs): no flag, no recovery, every epoch reported once."""
+    env = {"DNN_INJECT_END_SKEW": f"0:0.5:{where}", "DNN_HEARTBEAT_TIMEOUT": "1.0"}
+    r = _launch_env(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2", "--batch-size", "32",
+                        "--sync", "step-allreduce", "--nb-proc", "3"] + SMALL, tmp_path, env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "injected end skew: rank 0" in r.stdout
+    assert "[fault] watchdog" not in r.stdout and "dropped in epoch" not in r.stdout, r.stdout
+    assert "re-created" not in r.stdout, r.stdout
+    assert r.stdout.count("Validation loss of updated master model:") == 2
+
+
+def test_store_server_outlives_idle_while_a_local_rank_lives():
+    """No heartbeat, no store writes (a bench rank): the idle exit waits while a registered rank
+    process of this host is alive, and the server exits once every registered rank is gone
+    (the idle exit could pull the store from under a live job)."""
+    port = _free_port()
+    srv = _server(port, 2, "tok2", "--idle", "0.5")
+    live = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        st = _wait_up(port, "tok2")
+        st.set("dnn/pid/0", f"{socket.gethostname()}:{live.pid}")
+        st.set("dnn/pid/1", f"{socket.gethostname()}:{os.getpid() + 10 ** 7}")  # never a live pid
+        time.sleep(2.5)
+        assert srv.poll() is None, "store exited under a live rank"
+        live.kill()
+        live.wait()
+        assert srv.wait(timeout=20) == 0
+    finally:
+        for p in (srv, live):
+            if p.poll() is None:
+                p.kill()

@@ -253,3 +253,63 @@ def test_bench_refuses_nothing_without_launcher(n):
     i_launch = src.index("selflaunch.run(")
     i_gpu = src.index("torch.cuda.set_device")
     assert i_launch < i_gpu  # children are spawned before the first GPU call
+
+
+def test_device_count_reads_sysfs_not_hip(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the KFD topology + visibility variables (a
+    torch.cuda.device_count() fallback could initialise HIP in the launcher)."""
+    for i, gfx in enumerate([0, 90500, 90500, 0, 90500]):  # 2 CPU nodes, 3 GPU nodes
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {gfx}\nsimd_count 1024\n")
+    assert selflaunch._kfd_gpu_nodes(str(tmp_path)) == 3
+    assert selflaunch._kfd_gpu_nodes(str(tmp_path / "missing")) == -1
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    assert selflaunch._visible_list(3) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert selflaunch._visible_list(3) == 2
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")
+    assert selflaunch._visible_list(3) == 0
+    # the module never imports the GPU runtime's device query at launch time
+    src = open(selflaunch.__file__).read()
+    body = src[src.index("def visible_devices"):src.index("def die_with_parent")]
+    assert "torch.cuda" not in body.split("subprocess.run")[0]
+
+
+def test_ab_wall_budget_bounds_the_start_up(monkeypatch):
+    """a candidate whose set-up sleeps past the A/B's wall budget is marked
+    failed, the candidates after it are skipped, RCCL's init timeout is capped by the budget left
+    (and after an xGMI pass), and the JSON carries ab_wall_s + the step variant per path."""
+    from distributed_neural_network_amd.parallel import rccl
+
+    seen_tmo = []
+
+    class Slow:
+        def __init__(self, comm):
+            seen_tmo.append(float(os.environ["DNN_RCCL_INIT_TIMEOUT_S"]))
+            time.sleep(1.6)  # ignores every deadline
+            raise CommError("init too slow")
+
+    monkeypatch.setattr(rccl, "RcclComm", Slow)
+    eng, pol = _Engine(), _Policy(_Comm())
+    t0 = time.perf_counter()
+    res, _ = _ab(pol, eng, candidates=("xgmi-pull", "rccl", "rccl-overlap", "xgmi-rsag"), budget_s=1.0,
+                 rounds=1)
+    wall = time.perf_counter() - t0
+    assert res["allreduce"] == "xgmi-pull", res
+    assert "rccl" in res["failed"] and "rccl-overlap" in res["failed"] and "xgmi-rsag" in res["failed"], res
+    assert "skipped" in res["why"]["xgmi-rsag"] and "budget" in res["why"]["xgmi-rsag"], res
+    assert seen_tmo and seen_tmo[0] <= 15.0, seen_tmo  # capped after the xGMI pass
+    assert wall < 1.0 + 1.6 + 1.0 and res["ab_wall_s"] <= wall + 0.01, (wall, res)
+    assert res["variant"]["xgmi-pull"] in ("persistent", "pipelined", "early-mlp", "serial")
+    assert pol.ab_deadline is None
+
+
+def test_ab_default_candidates_drop_the_losing_ovl_forms(monkeypatch):
+    monkeypatch.delenv("DNN_AB_OVL", raising=False)
+    c = autotune.default_candidates()
+    assert not set(autotune.OVL_PATHS) & set(c) and not set(autotune.BF16_PATHS) & set(c)
+    monkeypatch.setenv("DNN_AB_OVL", "1")
+    assert set(autotune.OVL_PATHS) <= set(autotune.default_candidates("bf16"))
+    assert set(autotune.BF16_PATHS) <= set(autotune.default_candidates("bf16"))
