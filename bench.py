@@ -197,7 +197,7 @@ def main():
         comm.allreduce_(wl2, "sum")
         eval_metrics(wl + wl2, wc.float() + wc2, B)
     cur.run(args.warmup)
-    if getattr(engine, "pipeline", False) and engine._pipe_ok():
+    if getattr(engine, "pipeline", False) and (engine._pipe_ok() or engine._pers_ok()):
         torch.cuda.synchronize(device)
         if engine.step_wait_failed():  # a wait timed out (never seen): fall back one level and time that
             level = engine.degrade()

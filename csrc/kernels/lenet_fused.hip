@@ -529,13 +529,27 @@ __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const Pipe
 // The bookkeeping block is in the conv2 group (samples read its slots after that wait).  Nothing
 // is reset between launches: every ready / arrival tag is relative to the workgroup's generation
 // word (all of them start at 0 and each launch advances every one by nsteps, as this one does last).
+// XNR > 1 (the per-step all-reduce inside the persistent launch, up to XNR ranks): each block
+// reduces its elements as above, then exchanges them over xGMI exactly as the serial one-launch
+// exchange does (reduce_device.h xp_exchange / xp_exchange_rsag: the same per-lane granule
+// protocol, block -> counter map, two-hop owner map and rank-order sum, so the parameters are
+// bit-identical to it), and applies SGD with write-through stores before the workgroup signals
+// its ready group.  The step tag of block gb in step t is xp_ctr[gb] + t + 1 (the counter the
+// serial exchange keeps); the launch advances every counter by nsteps at its end.
+template <int XNR>
 __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
-  const int half = threadIdx.x >> 8, m = 2 * wg + half, rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
+  // (block-level indices are wave-uniform: readfirstlane keeps them - and the exchange's step tag
+  // and slot pointers derived from them - in scalar registers)
+  const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), m = 2 * wg + half, rtid = threadIdx.x & 255,
+            lane = threadIdx.x & 63;
   const bool bk = m == PIPE_CONV_BLOCKS;
   int rblk = 0;
   if (m < PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + m;
   else if (!bk) rblk = m - PIPE_CONV_BLOCKS - 1;
   const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));  // this workgroup's generation
+  // (XNR) this block's exchange counter: the grad_reduce block index (bookkeeping: the last one)
+  const int gb = bk ? PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS : rblk;
+  const unsigned xc0 = XNR > 1 ? __builtin_amdgcn_readfirstlane(a.xp_ctr[gb]) : 0u;
   if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
   for (int t = 0; t < pc.nsteps; ++t) {
@@ -544,11 +558,34 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
     const bool st = stamps != nullptr && threadIdx.x == 0 && t == pc.nsteps - 1;
     if (st) stamps[2400 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    // the lane's indices are re-derived in every step from an opaque copy of threadIdx.x, so the
+    // per-lane address math of the reduction paths stays inside the step instead of being hoisted
+    // out of the loop and kept live across it (the sample loop's trick: ~130 VGPRs held otherwise)
+    int tid_o = threadIdx.x;
+    asm volatile("" : "+v"(tid_o));
+    const int rtid_s = tid_o & 255;
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane, t);
+    } else if constexpr (XNR > 1) {
+      const unsigned step = xc0 + (unsigned)t + 1u;
+      const bool failed = __hip_atomic_load(a.xp_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+      XpSinkT<false, true> sk;
+      sk.tag = (unsigned long long)step << 32;
+      sk.stash = tid_o;  // (8 x NT floats of the otherwise unused LDS)
+      sk.stride = NT;
+      // pull: every lane's granules go to this rank's slot; two-hop: only non-owners' (the
+      // owner publishes the SUM in its ag slot instead)
+      const bool publish = (a.xp_mode & 2) == 0 || gb % a.xp_nranks != a.xp_rank;
+      sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                               (step & 1u) * a.xp_gslot_bytes)
+                       : nullptr;
+      if (grad_reduce_body<false, XpSinkT<false, true>, true>(a, sk, rblk, rtid_s, 0, false, t & 1)) {
+        if ((a.xp_mode & 2) == 0) xp_exchange<XNR, false, true>(a, sk, step, failed, rblk, rtid_s);
+        else xp_exchange_rsag<XNR, false, true>(a, sk, step, failed, rblk, rtid_s);
+      }
     } else {
       WtSink sk;
-      grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid, 0, false, t & 1);
+      grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid_s, 0, false, t & 1);
     }
     if (st) stamps[2401 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
@@ -558,6 +595,9 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
       for (int b = lane; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, g0 + (unsigned)t + 1u);
   }
   if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
+  if constexpr (XNR > 1) {
+    if (rtid == 0) a.xp_ctr[gb] = xc0 + (unsigned)pc.nsteps;  // (the next launch reads it: kernel boundary)
+  }
 }
 
 // Weight loads: plain, or (WT: the pipelined step) sc1 buffer loads of the write-through bytes
@@ -603,7 +643,8 @@ __device__ __forceinline__ void dma_w(const void* gsrc, uint32_t lds_base) {
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
 // PIPE (TRAIN + STAGED only): the pipelined step's merged launch (above)
 // PERS (PIPE only): the persistent launch - pc.nsteps steps, rows of both parities (above)
-template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false, bool PERS = false>
+// XNR (PERS only): the per-step xGMI all-reduce inside the launch for groups of up to XNR ranks (0: none)
+template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false, bool PERS = false, int XNR = 0>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -625,6 +666,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     const PipeCtl pc) {                     // PIPE: ra = the previous step's reduction, pc its control
   static_assert(!PIPE || (TRAIN && STAGED && RNR == 0), "the pipelined step is a staged training launch");
   static_assert(!PERS || PIPE, "the persistent launch is a PIPE grid");
+  static_assert(XNR == 0 || PERS, "the in-launch exchange is a persistent-launch feature");
   if constexpr (PIPE) {  // (no early-MLP granules in a PIPE / PERS launch: their code is dead here)
     rowg = nullptr;
     rowg_ctr = nullptr;
@@ -645,7 +687,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int nrw = PIPE ? (pc.nred + 1) / 2 : 0;
   if constexpr (PIPE) {
     if ((int)blockIdx.x < nrw) {
-      if constexpr (PERS) pers_reduce(ra, pc, blockIdx.x, stamps);
+      if constexpr (PERS) pers_reduce<XNR>(ra, pc, blockIdx.x, XNR > 1 ? nullptr : stamps);  // (XNR: at the register limit)
       else pipe_reduce(ra, pc, blockIdx.x, stamps);
       if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
       return;
@@ -764,22 +806,22 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   auto invalid_sample = [&]() {
     // (an opaque thread index: these addresses must not be shared with phase D''s row stores -
     // a shared computation stays live across the whole step)
-    int ti = threadIdx.x;
-    asm volatile("" : "+v"(ti));
-    for (int i = ti; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, 0.f);
+    int ti = threadIdx.x, bo = b;  // (b too: its row offsets were hoisted into the prologue and spilled)
+    asm volatile("" : "+v"(ti), "+v"(bo));
+    for (int i = ti; i < A0_LD; i += NT) put_row(a0_s + (size_t)bo * A0_LD + i, 0.f);
     for (int i = ti; i < H1_LD; i += NT) {
-      put_row(h1_s + (size_t)b * H1_LD + i, 0.f);
-      put_row(z1_s + (size_t)b * Z1_LD + i, 0.f);
+      put_row(h1_s + (size_t)bo * H1_LD + i, 0.f);
+      put_row(z1_s + (size_t)bo * Z1_LD + i, 0.f);
     }
     for (int i = ti; i < H2_LD; i += NT) {
-      put_row(h2_s + (size_t)b * H2_LD + i, 0.f);
-      put_row(z2_s + (size_t)b * Z2_LD + i, 0.f);
+      put_row(h2_s + (size_t)bo * H2_LD + i, 0.f);
+      put_row(z2_s + (size_t)bo * Z2_LD + i, 0.f);
     }
-    for (int i = ti; i < Z3_LD; i += NT) put_row(z3_s + (size_t)b * Z3_LD + i, 0.f);
-    for (int i = ti; i < SLAB; i += NT) put_row(slab_s + (size_t)b * SLAB + i, 0.f);
+    for (int i = ti; i < Z3_LD; i += NT) put_row(z3_s + (size_t)bo * Z3_LD + i, 0.f);
+    for (int i = ti; i < SLAB; i += NT) put_row(slab_s + (size_t)bo * SLAB + i, 0.f);
     if (ti == 0) {
-      put_row(loss_s + b, 0.f);
-      put_row(reinterpret_cast<float*>(correct_s + b), 0.f);
+      put_row(loss_s + bo, 0.f);
+      put_row(reinterpret_cast<float*>(correct_s + bo), 0.f);
     }
     if constexpr (PERS) {
       pers_arrive_kind(1);
@@ -1576,7 +1618,8 @@ void init_kernels() {
                          (const void*)lenet_fused_kernel<true, false, 1>, (const void*)lenet_fused_kernel<true, true, 1>,
                          (const void*)lenet_fused_kernel<true, false, 8>, (const void*)lenet_fused_kernel<true, true, 8>,
                          (const void*)lenet_fused_kernel<false, false, 0>, (const void*)lenet_fused_kernel<true, true, 0, true>,
-                         (const void*)lenet_fused_kernel<true, true, 0, true, true>};
+                         (const void*)lenet_fused_kernel<true, true, 0, true, true>,
+                         (const void*)lenet_fused_kernel<true, true, 0, true, true, 8>};
   for (const void* k : kerns) HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   init_kernels_f32();
   done = true;
@@ -1663,7 +1706,10 @@ int persist_resident_workgroups() {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, 0, true, true>), NT, LDS_TOTAL));
-    resident = per_cu * cus;
+    int per_cu_x = 0;  // (the exchange instance: its own register count)
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu_x, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, 0, true, true, 8>), NT, LDS_TOTAL));
+    resident = std::min(per_cu, per_cu_x) * cus;
   }
   return resident;
 }
@@ -1685,9 +1731,16 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   if (stage == nullptr || pc_in.ctr == nullptr || pc_in.err == nullptr || !pc_in.bv_slot[0] || !pc_in.bv_slot[1] ||
       !pc_in.nid_slot[0] || !pc_in.nid_slot[1])
     throw std::runtime_error("fused_train_persist: needs the stage, the control block, the error word and both slots");
-  if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || red.rg != nullptr || !red.fuse_sgd ||
-      red.lo != 0 || red.hi < ARENA)
-    throw std::runtime_error("fused_train_persist: a local whole-arena fused-SGD reduction with bookkeeping");
+  if (!red.bookkeeping || red.batch != batch || red.rg != nullptr || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA)
+    throw std::runtime_error("fused_train_persist: a whole-arena fused-SGD reduction with bookkeeping");
+  // the in-launch exchange: the serial one-launch exchange's arguments (whole arena, counters from
+  // block 0, fp32 granules, pull or two-hop); grad_scale 1 (the tile update folds it: reduce_device.h)
+  if (red.xp_nranks != 0 &&
+      (red.xp_nranks < 1 || red.xp_nranks > XG_MAX_RANKS || red.xp_blk_off != 0 || (red.xp_mode & ~2) != 0 ||
+       red.grad_scale != 1.f || red.xp_ctr == nullptr || red.xp_err == nullptr || red.xp_abort == nullptr ||
+       red.xp_rank < 0 || red.xp_rank >= red.xp_nranks))
+    throw std::runtime_error("fused_train_persist: the in-launch exchange takes the whole-arena one-launch exchange "
+                             "(fp32 granules, pull or two-hop, grad_scale 1, counters set)");
   if (red.a0 != a0 || red.h1 != h1 || red.h2 != h2 || red.z1 != z1 || red.z2 != z2 || red.z3 != z3 ||
       red.slab != slab || red.loss != loss || red.correct != correct)
     throw std::runtime_error("fused_train_persist: the reduction reads the rows the samples write");
@@ -1699,10 +1752,11 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   pc.gen = reinterpret_cast<unsigned*>(base);
   pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
   pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
-  hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true, true>), dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL,
-                     stream, images, labels, nullptr, order_len, batch, 0, red.state, master, shadow, a0, h1, h2, z1,
-                     z2, z3, slab, loss, correct, stamps, nullptr, pc.nid_slot[0], stage, nullptr, nullptr, red,
-                     ReduceArgs{}, pc);
+  auto* kern = red.xp_nranks == 0 ? &lenet_fused_kernel<true, true, 0, true, true>
+                                   : &lenet_fused_kernel<true, true, 0, true, true, 8>;
+  hipLaunchKernelGGL(kern, dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL, stream, images, labels, nullptr, order_len,
+                     batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, nullptr,
+                     pc.nid_slot[0], stage, nullptr, nullptr, red, ReduceArgs{}, pc);
   HIP_CHECK(hipGetLastError());
 }
 

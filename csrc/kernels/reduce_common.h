@@ -80,6 +80,7 @@ __device__ __forceinline__ void sgd_finish(int e, float g, float p_old, float m_
 template <bool WT>
 struct DirectSinkT {
   static constexpr bool kTile = WT;  // fc1 / fc2 tiles finish in put_tile (below)
+  static constexpr bool kTileInfo = false;  // (XpSinkT<PK, true> records its fc tile: see there)
   // WT, optional: put_tile's write-through stores wait until *gate >= gate_target (the pipelined
   // step's conv ready counter): the samples' poll of that counter then does not queue behind the
   // MLP tiles' write-through traffic (lenet_fused.hip PIPE flags & 32)
@@ -127,19 +128,17 @@ __device__ __forceinline__ void st_wt8(bf16* p, unsigned lo, unsigned hi) {  // 
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool WT>
+// The write-through SGD + image update of a finished fc1 / fc2 weight-gradient tile (lane (i, kq)
+// holds rows o0 + 4 kq + j of column i0 + i): SGD per element (master / momentum plain: the
+// samples read no fc weight from the fp32 master), then the bf16 images with 8-byte write-through
+// stores - a 4 x 4 transpose inside each lane quad (DPP rotations) gives lane u the 4 consecutive
+// columns of row o0 + 4 kq + u for the row-major copy; the transposed fc2 image [i][o] takes the
+// lane's own 4 consecutive rows as they are.  Every lane of the wave calls it (DPP).
 template <int LAYER>
-__device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, const float (&pv)[4], const float (&mv)[4],
-                                                         const int (&e)[4], int o0, int i0, int lane,
-                                                         const ReduceArgs& a) {
+__device__ __forceinline__ void wt_tile_update(const f32x4& acc, const float (&pv)[4], const float (&mv)[4],
+                                               const int (&e)[4], int o0, int i0, int lane, const ReduceArgs& a) {
   constexpr int O = LAYER == 0 ? 120 : 84, I = LAYER == 0 ? 400 : 120, OFF = LAYER == 0 ? OFF_F1W : OFF_F2W;
   const int i = lane & 15, kq = lane >> 4, u = lane & 3;
-  if (gate != nullptr && lane == 0) {  // bounded: the samples' own wait on this counter has the timeout
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gate_target &&
-           wall_clock64() - t0 < 200000000ll)
-      __builtin_amdgcn_s_sleep(4);
-  }
   const bool iv = i0 + i < I;
   unsigned bv[4];  // this lane's column, rows o0 + 4 kq + j: bf16 bits (0 outside the layer)
 #pragma unroll
@@ -164,11 +163,37 @@ __device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, cons
                                       bv[2] | (bv[3] << 16));
   }
 }
+
+template <bool WT>
+template <int LAYER>
+__device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, const float (&pv)[4], const float (&mv)[4],
+                                                         const int (&e)[4], int o0, int i0, int lane,
+                                                         const ReduceArgs& a) {
+  if (gate != nullptr && lane == 0) {  // bounded: the samples' own wait on this counter has the timeout
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gate_target &&
+           wall_clock64() - t0 < 200000000ll)
+      __builtin_amdgcn_s_sleep(4);
+  }
+  wt_tile_update<LAYER>(acc, pv, mv, e, o0, i0, lane, a);
+}
 //    PK (bf16 granules, xp_mode bit 4): the lane's elements travel in pairs (0, 1) and (2, 3)
 //    as ONE granule {bf16 | bf16, step} each, published by the exchange once both are known.
-template <bool PK>
+//    WT (the persistent launch's in-launch exchange, lenet_fused.hip PERS): the update after the
+//    exchange stores what the samples of the same launch read write-through - an fc1 / fc2 tile
+//    through wt_tile_update (the lane records its tile: tile_info), every other element as
+//    sgd_finish<true> does.
+template <bool PK, bool WT = false>
 struct XpSinkT {
   static constexpr bool kTile = false;
+  static constexpr bool kTileInfo = WT;
+  int tl = -1, to0 = 0, ti0 = 0;  // WT: the fc tile (layer, o0, i0) this lane's elements belong to
+  template <int LAYER>
+  __device__ __forceinline__ void tile_info(int o0, int i0) {
+    tl = LAYER;
+    to0 = o0;
+    ti0 = i0;
+  }
   template <int LAYER>
   __device__ __forceinline__ void put_tile(const f32x4&, const float (&)[4], const float (&)[4], const int (&)[4], int,
                                            int, int, const ReduceArgs&) {}
@@ -177,9 +202,33 @@ struct XpSinkT {
   int e[4] = {0, 0, 0, 0};
   float g[4] = {0.f, 0.f, 0.f, 0.f}, p[4], m[4];
   bool v[4] = {false, false, false, false};
+  // WT: the prefetched master / momentum values wait out the exchange in LDS instead of 8
+  // registers ([8][stride] floats from this thread's slot: p[j] at j * stride, m[j] at (4 + j) *
+  // stride) - the persistent launch's reduction path is at the 256-VGPR limit (its workgroups use
+  // no other LDS).  The stash must be set.
+  int stash = 0, stride = 0;  // this thread's first stash float, floats between its values
+  __device__ __forceinline__ static float* lds() {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    return reinterpret_cast<float*>(smem);
+  }
+  __device__ __forceinline__ float pv(int j) const {
+    if constexpr (WT) return lds()[stash + j * stride];
+    else return p[j];
+  }
+  __device__ __forceinline__ float mv(int j) const {
+    if constexpr (WT) return lds()[stash + (4 + j) * stride];
+    else return m[j];
+  }
   __device__ __forceinline__ void put(int j, int e_, float g_, float p_, float m_, const ReduceArgs& a) {
     g_ *= a.grad_scale;
-    e[j] = e_; g[j] = g_; p[j] = p_; m[j] = m_; v[j] = true;
+    e[j] = e_; g[j] = g_; v[j] = true;
+    if constexpr (WT) {
+      lds()[stash + j * stride] = p_;
+      lds()[stash + (4 + j) * stride] = m_;
+    } else {
+      p[j] = p_;
+      m[j] = m_;
+    }
     if (!PK && own != nullptr)  // (two-hop form: null on the owner of the block's elements)
       __hip_atomic_store(own + e_, tag | __float_as_uint(g_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -330,6 +379,7 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
     }
   }
   acc += acc1;
+  if constexpr (Sink::kTileInfo) sk.template tile_info<LAYER>(o0, i0);
   if constexpr (Sink::kTile && LAYER < 2) {  // the pipelined step: wide write-through image stores
     sk.template put_tile<LAYER>(acc, pv, mv, e, o0, i0, lane, a);
     return;

@@ -105,17 +105,42 @@ __device__ __forceinline__ long long poll_granules(const ReduceArgs& a, const un
   return wall_clock64() - t0;
 }
 
-template <bool PK>
-__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSinkT<PK>& sk, const float (&s)[4]) {
+// WT (the persistent launch): write-through stores of everything the samples of the same launch
+// read - an fc1 / fc2 tile through wt_tile_update (the same SGD arithmetic: grad_scale is 1 there,
+// so acc * grad_scale is s * xp_scale bit for bit), any other element as sgd_finish<true>.
+template <bool PK, bool WT = false>
+__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSinkT<PK, WT>& sk, const float (&s)[4]) {
+  if constexpr (WT) {
+    if (sk.tl == 0 || sk.tl == 1) {  // (wave-uniform: one tile per wave)
+      f32x4 acc;
+      float pv[4], mv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = s[j] * a.xp_scale;
+        pv[j] = sk.v[j] ? sk.pv(j) : 0.f;
+        mv[j] = sk.v[j] ? sk.mv(j) : 0.f;
+      }
+      const int lane = threadIdx.x & 63;
+      if (sk.tl == 0) wt_tile_update<0>(acc, pv, mv, sk.e, sk.to0, sk.ti0, lane, a);
+      else wt_tile_update<1>(acc, pv, mv, sk.e, sk.to0, sk.ti0, lane, a);
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (!sk.v[j]) continue;
     const float gr = s[j] * a.xp_scale;
     float p, m;
-    sgd_update(gr, sk.p[j], sk.m[j], a.lr, a.momentum, p, m);
+    sgd_update(gr, sk.pv(j), sk.mv(j), a.lr, a.momentum, p, m);
     a.mom[sk.e[j]] = m;
-    a.master[sk.e[j]] = p;
-    write_shadow(a.shadow, sk.e[j], p);
+    if constexpr (WT) {
+      if (is_bias(sk.e[j])) st_wt(a.master + sk.e[j], p);
+      else a.master[sk.e[j]] = p;
+      write_shadow_wt(a.shadow, sk.e[j], p);
+    } else {
+      a.master[sk.e[j]] = p;
+      write_shadow(a.shadow, sk.e[j], p);
+    }
   }
 }
 
@@ -170,9 +195,9 @@ __device__ __forceinline__ void unpack_pairs(float (&x)[4], const bool (&valid)[
 // NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
 // group does not pay for 8 ranks' loads in flight.  PK: bf16 granules (half the link bytes;
 // the sum stays fp32 in rank order).
-template <int NR, bool PK>
-__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed, int rblk,
-                                            int rtid) {
+template <int NR, bool PK, bool WT = false>
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK, WT>& sk, unsigned step, bool failed,
+                                            int rblk, int rtid) {
   const int par = step & 1u;
   pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);
   float v[NR][4];
@@ -210,8 +235,8 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK>& sk
 // applies SGD; the other ranks read that slot.  2 E / N granules per link instead of E, one
 // more dependent remote read.  PK: the sum is all-gathered as bf16 too (every rank, the owner
 // included, applies the rounded sum).
-template <int NR, bool PK>
-__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK>& sk, unsigned step, bool failed,
+template <int NR, bool PK, bool WT = false>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK, WT>& sk, unsigned step, bool failed,
                                                  int rblk, int rtid) {
   const int par = step & 1u;
   const int owner = (rblk + a.xp_blk_off) % a.xp_nranks;

@@ -210,3 +210,49 @@ def per_sample_outputs_masked(weights: torch.Tensor, master: torch.Tensor, image
     z3p[:, :10] = z3
     return {"a0": a0, "h1": h1, "h2": h2, "z1": z1, "z2": z2, "z3": z3p, "slab": slab, "loss": loss,
             "logits": logits}
+
+
+def reduce_rows(rows: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """The batch reduction of per-sample rows into the flat gradient arena (fp64 sums, the kernel's
+    grad_reduce contract: fc wgrad = z^T x over the batch, biases and conv slabs = column sums)."""
+    g = torch.zeros(LAYOUT.total, dtype=torch.float64)
+    v = LAYOUT.views(g)
+    r = {k: rows[k].double() for k in ("a0", "h1", "h2", "z1", "z2", "z3", "slab")}
+    v["fc1.weight"].copy_(r["z1"].T @ r["a0"])
+    v["fc1.bias"].copy_(r["z1"].sum(0))
+    v["fc2.weight"].copy_(r["z2"].T @ r["h1"])
+    v["fc2.bias"].copy_(r["z2"].sum(0))
+    v["fc3.weight"].copy_(r["z3"][:, :10].T @ r["h2"])
+    v["fc3.bias"].copy_(r["z3"][:, :10].sum(0))
+    sl = r["slab"].sum(0)
+    v["conv1.weight"].copy_(sl[0:450].view(6, 3, 5, 5))
+    v["conv1.bias"].copy_(sl[450:456])
+    v["conv2.weight"].copy_(sl[456:2856].view(16, 6, 5, 5))
+    v["conv2.bias"].copy_(sl[2856:2872])
+    return g.float()
+
+
+def train_steps_bf16(master: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor, order, batch: int,
+                     steps: int, lr: float, momentum: float, mom: torch.Tensor | None = None):
+    """``steps`` training steps of the bf16 fused engine, emulated on the CPU: every step runs
+    ``per_sample_outputs_bf16`` on the bf16 images of the current fp32 master (the shadow the
+    optimizer packs), reduces the rows over the batch, and applies momentum SGD in fp32 exactly as
+    the kernel does (m = fma(momentum, m, g); p = fma(-lr, m, p)).  Returns (master, momentum,
+    per-step mean losses).  The kernel matches it to accumulation-order noise, step after step."""
+    p = master.detach().float().cpu().clone()
+    m = torch.zeros_like(p) if mom is None else mom.detach().float().cpu().clone()
+    order = torch.as_tensor(order, dtype=torch.int64)
+    losses = []
+    mask = LAYOUT.pad_mask().float()
+    for s in range(steps):
+        idx = order[s * batch:(s + 1) * batch]
+        if idx.numel() == 0:
+            break
+        n = int(idx.numel())
+        rows = per_sample_outputs_bf16(p.bfloat16(), p, images_u8[idx], labels[idx], n)
+        g = reduce_rows(rows) * mask
+        # fp32 fma, as sgd_update: rounding once per operation pair like the kernel's fmaf
+        m = (momentum * m.double() + g.double()).float()
+        p = (-lr * m.double() + p.double()).float()
+        losses.append(float(rows["loss"].double().mean()))
+    return p, m, losses

@@ -39,7 +39,8 @@ from typing import Callable, Optional
 
 import torch
 
-ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+# the persistent-launch forms first: on a tie they win (no kernel boundary between steps)
+ORDER = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
 # opt-in (DNN_AB_OVL=1): the in-launch (-ovl) forms - they lost 3x to the one-launch exchange in the
 # 2-rank rehearsal (profiles/r4/ab_rehearsal: 134 / 143 vs 43.5 us), so by default they cost no
 # 8-GPU start-up time

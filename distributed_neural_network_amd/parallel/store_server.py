@@ -45,6 +45,25 @@ def _pid_alive(pid: int) -> bool:
         return True
 
 
+def decide(world: int, closed: int, dropped: int, beats: list, stale: float, pids: dict, alive: list,
+           idle_for: float, idle: float, now: float) -> str | None:
+    """Why the server should exit now (None: keep serving).  ``beats``: each rank's last heartbeat
+    stamp (None: none seen); ``pids``: registered ranks -> pid on this host (-1: another host);
+    ``alive``: the registered local pids still running; ``idle_for``: seconds since anything in
+    the store last changed."""
+    if closed + dropped >= world:
+        return "every rank checked out"
+    seen = [t for t in beats if t is not None]
+    if seen and now - max(seen) > stale:
+        return f"no heartbeat for {stale:.0f} s: the job is gone"
+    local = [p for p in pids.values() if p > 0]
+    if local and not alive and len(pids) == world:
+        return "every rank process of this host is gone"
+    if idle_for > idle and not alive:
+        return f"no activity for {idle:.0f} s"
+    return None
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default="0.0.0.0")
@@ -75,19 +94,12 @@ def main(argv=None) -> int:
             sig = (closed, dropped, store.num_keys(), tuple(beats))
         except Exception:
             return 1
-        if closed + dropped >= a.world:
-            time.sleep(1.0)  # let the last clients finish their final reads
-            return 0
         stamps = []
         for v in beats:
             try:
                 stamps.append(float(v.decode()) if v else None)
             except ValueError:
                 stamps.append(None)
-        seen = [t for t in stamps if t is not None]
-        if seen and time.time() - max(seen) > a.stale:
-            print(f"[store] no heartbeat for {a.stale:.0f} s: the job is gone, exiting", file=sys.stderr, flush=True)
-            return 0
         for r in range(a.world):
             if r not in pids:
                 try:
@@ -97,15 +109,16 @@ def main(argv=None) -> int:
                         pids[r] = int(p) if h == host else -1
                 except Exception:
                     pass
-        local = [p for p in pids.values() if p > 0]
-        alive = [p for p in local if _pid_alive(p)]
-        if local and not alive and len(pids) == a.world:
-            print("[store] every rank process of this host is gone: exiting", file=sys.stderr, flush=True)
-            return 0
+        alive = [p for p in pids.values() if p > 0 and _pid_alive(p)]
         if sig != last_sig:
             last_sig, last_change = sig, time.time()
-        elif time.time() - last_change > a.idle and not alive:
-            print(f"[store] no activity for {a.idle:.0f} s: exiting", file=sys.stderr, flush=True)
+        why = decide(a.world, closed, dropped, stamps, a.stale, pids, alive, time.time() - last_change, a.idle,
+                     time.time())
+        if why is not None:
+            if closed + dropped >= a.world:
+                time.sleep(1.0)  # let the last clients finish their final reads
+            else:
+                print(f"[store] {why}: exiting", file=sys.stderr, flush=True)
             return 0
 
 

@@ -135,8 +135,12 @@ class StepAllReduce(SyncPolicy):
     # (xgmi-pull-bf16 / xgmi-rsag-bf16: the same exchanges with bf16 gradient granules, opt-in)
     # (xgmi-pull-ovl / xgmi-rsag-ovl: the same exchanges run by the fused launch's in-launch MLP
     # reduction, overlapped with the conv backward - HipEngine early_mlp="mlp"; bit-identical)
-    PATHS = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl", "xgmi-pull-bf16",
-             "xgmi-rsag-bf16")
+    # (xgmi-pull-pers / xgmi-rsag-pers: the same exchanges inside the PERSISTENT launch's reduction
+    # workgroups - the whole window one launch, no kernel boundary between steps, the exchange +
+    # SGD before each step's ready hand-off; lenet_fused.hip XNR; self-tested bit for bit against
+    # the serial one-launch exchange)
+    PATHS = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl",
+             "xgmi-rsag-ovl", "xgmi-pull-bf16", "xgmi-rsag-bf16")
     path: str | None = None
     grad_comm = "fp32"  # "bf16": the default xGMI path uses bf16 gradient granules (--grad-comm)
     record_waits = False  # xGMI paths: record every step's exchange wait (XgmiGroup.wait_stats)
@@ -148,7 +152,9 @@ class StepAllReduce(SyncPolicy):
             return
         name = self.path or self.default_path(engine)
         chain = [name]
-        if name.startswith("xgmi") and name != "xgmi-pull":
+        if name.endswith("-pers"):
+            chain.append(name.removesuffix("-pers"))
+        if name.startswith("xgmi") and "xgmi-pull" not in chain:
             chain.append("xgmi-pull")
         if name.startswith("xgmi"):
             chain.append("rccl" if self.comm.backend == "nccl" else "torch-pg")
@@ -170,7 +176,10 @@ class StepAllReduce(SyncPolicy):
                 if self.comm.backend == "nccl" else "torch-pg"
         if xgmi.wanted(self.comm) and engine.grad.numel() <= self.XGMI_MAX_ELEMS:
             mode = xgmi.exchange_mode() | (4 if self.grad_comm == "bf16" else 0)
-            return "xgmi-" + xgmi.MODE_NAMES[mode]
+            # the persistent form where the engine has one (fp32 granules; falls back to the
+            # serial one-launch exchange if its self-test fails)
+            pers = "-pers" if mode in (0, 2) and getattr(engine, "persist", False) else ""
+            return "xgmi-" + xgmi.MODE_NAMES[mode] + pers
         return "rccl" if self.comm.backend == "nccl" else "torch-pg"
 
     def installed(self, engine) -> str | None:
@@ -184,7 +193,8 @@ class StepAllReduce(SyncPolicy):
 
             form = MODE_NAMES[gs.group.xp_mode]
             ovl = "-ovl" if getattr(engine, "early_mlp", False) and engine._early_ok() else ""
-            return f"xgmi-{form}{ovl}" + ("" if gs.group.one_launch else "-two-launch")
+            pers = "-pers" if getattr(engine, "pers_exchange", False) and engine._pers_xchg() is not None else ""
+            return f"xgmi-{form}{ovl}{pers}" + ("" if gs.group.one_launch else "-two-launch")
         if kind == "NativeGradAllReduce":
             return "rccl-overlap" if gs.overlap else "rccl"
         return "torch-pg"
@@ -211,12 +221,23 @@ class StepAllReduce(SyncPolicy):
             self.install_why = "the in-launch (-ovl) reduction needs the fused engine"
             return False
         engine.grad_sync = None
+        pers = name.endswith("-pers")
+        if hasattr(engine, "pers_exchange"):
+            engine.pers_exchange = False
+        elif pers:
+            self.install_why = "the persistent (-pers) exchange needs the fused engine"
+            return False
         if name == "local":
             return True
         if name.startswith("xgmi"):
             from .xgmi import EXCHANGE_MODES
 
-            return self._install_xgmi(engine, EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-ovl")])
+            mode = EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-ovl").removesuffix("-pers")]
+            if not self._install_xgmi(engine, mode):
+                return False
+            if pers:
+                return self._install_pers(engine, mode)
+            return True
         if name in ("rccl", "rccl-overlap"):
             if self.comm.backend != "nccl":
                 self.install_why = f"RCCL needs the nccl backend (this run's host collectives: {self.comm.backend})"
@@ -278,6 +299,33 @@ class StepAllReduce(SyncPolicy):
                           flush=True)
         if hasattr(engine, "invalidate_graphs"):
             engine.invalidate_graphs()
+        return True
+
+    def _install_pers(self, engine, mode: int) -> bool:
+        """The "-pers" form on top of an installed one-launch exchange: self-tested once per group
+        and form (HipEngine.selftest_pers_exchange: bit for bit against the serial one-launch
+        exchange on every rank), then the engine runs its persistent launch with the exchange
+        inside.  Collective; False (on every rank) leaves nothing installed."""
+        xg = engine.grad_sync.group if engine.grad_sync is not None else None
+        if xg is None or not xg.one_launch or mode not in (0, 2) or not hasattr(engine, "selftest_pers_exchange"):
+            engine.grad_sync = None
+            self.install_why = "the persistent exchange needs the self-tested one-launch exchange (fp32 granules)"
+            return False
+        cache = xg.__dict__.setdefault("selftested_pers", {})
+        if mode not in cache:
+            cache[mode] = engine.selftest_pers_exchange(xg, self.comm)
+            if xg.broken:
+                self._drop_xgmi_group()
+                engine.grad_sync = None
+                self.install_why = f"the persistent exchange self-test raised or timed out ({cache[mode][1]})"
+                return False
+        ok, why = cache[mode]
+        if not ok:
+            engine.grad_sync = None
+            self.install_why = f"the persistent exchange self-test failed: {why or 'on a peer'}"
+            return False
+        engine.pers_exchange = True
+        engine.invalidate_graphs()
         return True
 
     def _drop_xgmi_group(self) -> None:

@@ -85,6 +85,25 @@ def eval_metrics(loss: torch.Tensor, correct: torch.Tensor, batch_size: int) -> 
     return float((sums / counts).mean()), 100.0 * float(correct.sum()) / max(n, 1)
 
 
+def ranks_per_gpu() -> int:
+    """Ranks of this job per visible GPU on this host (1 unless ranks time-share a device: the
+    one-GPU rehearsals).  The local rank count comes from the launcher's environment (torchrun,
+    OpenMPI, MPICH / Intel MPI, Slurm); without one, the world size is taken as local."""
+    n = None
+    for k in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE"):
+        v = os.environ.get(k)
+        if v:
+            try:
+                n = int(v.split("(")[0])
+                break
+            except ValueError:
+                pass
+    if n is None:
+        n = int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", "1")) or 1)
+    d = max(1, torch.cuda.device_count())
+    return max(1, -(-n // d))
+
+
 def gpu_shared_by_ranks() -> bool:
     """Do other ranks of this job run on this process's GPU (more local ranks than visible
     devices: the one-GPU rehearsals, ``tools/fault_bench.py --share-gpu``)?  The local rank
@@ -350,8 +369,17 @@ class HipEngine(Engine):
         # persistent grid on the same GPU (ranks time-sharing a device would each hold part of
         # the CUs); DNN_PERSIST=0 turns it off.
         if persist is None:
-            persist = os.environ.get("DNN_PERSIST", "1") != "0" and not gpu_shared_by_ranks()
-        self.persist = bool(persist) and self.pipeline and B <= self.ext.persist_max_batch()
+            persist = os.environ.get("DNN_PERSIST", "1") != "0"
+        # ranks time-sharing this GPU (one-GPU rehearsals): every rank's grid must be resident at
+        # once - ranks x (reduction + sample workgroups) within the occupancy-derived count
+        share = ranks_per_gpu()
+        fits = B <= self.ext.persist_max_batch() and (
+            share == 1 or share * (self.ext.pipe_reduce_blocks() // 2 + 1 + B)
+            <= self.ext.persist_resident_workgroups() - 8)
+        self.persist = bool(persist) and self.pipeline and fits
+        # the per-step xGMI all-reduce inside the persistent launch (installed by the
+        # step-allreduce policy's "-pers" paths after their self-test; lenet_fused.hip XNR)
+        self.pers_exchange = False
         self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
         self._pers_handles: dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(dev)
@@ -454,6 +482,17 @@ class HipEngine(Engine):
         and no in-launch reduction."""
         return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
 
+    def _pers_xchg(self):
+        """The xGMI group whose one-launch exchange runs inside the persistent launch, or None:
+        installed by a "-pers" path (pers_exchange), self-tested one-launch exchange, fp32
+        granules (pull or two-hop)."""
+        if not self.pers_exchange or self.grad_sync is None or not getattr(self.grad_sync, "fuses_sgd", False):
+            return None
+        grp = getattr(self.grad_sync, "group", None)
+        if grp is None or not grp.one_launch or grp.xp_mode not in (0, 2):
+            return None
+        return grp
+
     # persistent launches directly from the extension's cached argument block instead of graph
     # replays (DNN_PERS_DIRECT=1; ~3.4 us less per 20-step window, profiles/r4/pers_direct).  Off by
     # default: with it on, a LATER pipelined engine in the same process hits an illegal address that
@@ -518,8 +557,11 @@ class HipEngine(Engine):
                                       flg=self._pipe_flg_ptr)
 
     def _pers_ok(self) -> bool:
-        """The persistent launch runs: the pipelined step's conditions, and persist."""
-        return self.persist and self._pipe_ok()
+        """The persistent launch runs: the pipelined step's conditions and persist - or, with a
+        per-step all-reduce, its "-pers" form (the exchange inside the launch's reduction)."""
+        if not (self.persist and self.pipeline and self._staged and not self.early_mlp):
+            return False
+        return self.grad_sync is None or self._pers_xchg() is not None
 
     _pers_handles_next = itertools.count(1)  # process-wide: a handle is never reused
 
@@ -529,8 +571,10 @@ class HipEngine(Engine):
         launches - drawn from a process-wide counter, so a freed engine's cached block can never
         match another engine (an id()-based key did: ids are reused, and the relaunch then ran on
         freed buffers)."""
+        grp = self._pers_xchg()
         key = (self.order_len, self._p(self.order), self._p(self.train.images), self._staged,
-               self._pipe_stamps, self.pipe_flags, self._pers_gen)
+               self._pipe_stamps, self.pipe_flags, self._pers_gen,
+               None if grp is None else (id(grp), grp.xp_mode, grp.generation))
         h = self._pers_handles.get(key)
         if h is None:
             h = self._pers_handles[key] = next(HipEngine._pers_handles_next)
@@ -545,12 +589,14 @@ class HipEngine(Engine):
         s = self._stream()
         sp = self._p(self.state)
         r = self._rows(0)
+        grp = self._pers_xchg()
+        xg = grp.exchange() if grp is not None else {}
         self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
                              self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
                              self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
                              self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
                              self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
-                             self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids))
+                             self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids), **xg)
         self.ext.fused_train_persist(self._p(self.train.images), self._p(self.train.labels), self.order_len,
                                      self.batch, self._p(self.master), self._p(self.shadow), self._p(r["a0"]),
                                      self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]),
@@ -745,11 +791,74 @@ class HipEngine(Engine):
         torch.cuda.synchronize(dev)
         return all(v == 1.0 for v in votes)
 
+    def selftest_pers_exchange(self, grp, comm, steps: int = 3) -> tuple[bool, str]:
+        """Collective: do ``steps`` training steps with the exchange INSIDE the persistent launch
+        give the serial one-launch exchange's parameters, momentum and bf16 images BIT FOR BIT on
+        every rank?  Both runs start from the same parameters and the same sample order (this
+        rank's first ``steps`` batches of the attached split), launched eagerly.  Everything the
+        runs touch - parameters, optimizer state, epoch cursor and order, bookkeeping slots, the
+        image stage, epoch statistics - is restored afterwards, so it can run mid-epoch (the
+        start-up A/B).  Returns (every rank passed, this rank's reason if not)."""
+        avail = self.train is not None and self.persist and self.pipeline and self.stage is not None
+        if not all(v == 1.0 for v in comm.gather_scalars(1.0 if avail else 0.0)):  # (same collectives everywhere)
+            return False, "the persistent launch is not available on " + ("this rank" if not avail else "a peer")
+        dev = self.device
+        keep = [self.master, self.mom, self.shadow, self.state, self.stats, self.batch_ids, self.next_ids,
+                self.next_ids2, self.stage]
+        saved = [t.clone() for t in keep]
+        saved_attrs = (self.order_len, self._staged, self.pers_exchange)
+        saved_order = self.order[:self.order_len].clone()
+        n = min(len(self.train), steps * self.batch)
+        order = np.arange(n, dtype=np.int32)
+        results, why, ok = [], "", True
+        timeout, grp.timeout_s = grp.timeout_s, min(grp.timeout_s, 10.0)
+        for pers in (False, True):
+            err = False
+            try:
+                with torch.cuda.device(dev), torch.no_grad():
+                    self.master.copy_(saved[0])
+                    self.mom.copy_(saved[1])
+                    self.params_changed()
+                    self.pers_exchange = pers
+                    self.invalidate_graphs()
+                    self.begin_epoch(order)
+                    if pers != self._pers_ok():
+                        raise RuntimeError("the persistent exchange form did not engage")
+                    self._launch_steps(steps)
+                    torch.cuda.synchronize(dev)
+                    err = grp.failed() or self.pipe_failed()
+                    why = "a wait failed" if err else why
+                    results.append((self.master.cpu(), self.mom.cpu(), self.shadow.cpu()))
+            except Exception as e:
+                err, why = True, f"{type(e).__name__}: {e}"
+            if any(v != 0.0 for v in comm.gather_scalars(1.0 if err else 0.0)):
+                grp.broken = True
+                ok = False
+                break
+        grp.timeout_s = timeout
+        if ok:
+            same = all(torch.equal(x, y) for x, y in zip(*results))
+            why = "" if same else "mismatch in " + str(
+                [k for k, (x, y) in zip(("master", "mom", "shadow"), zip(*results)) if not torch.equal(x, y)])
+            ok = same
+        votes = comm.gather_scalars(1.0 if ok else 0.0)
+        with torch.no_grad():
+            self.order_len, self._staged, self.pers_exchange = saved_attrs
+            if self.order_len:
+                self.order[:self.order_len].copy_(saved_order)
+            for t, v in zip(keep, saved):
+                t.copy_(v)
+            if hasattr(self, "pipe_err"):
+                self.pipe_err.zero_()
+        self.invalidate_graphs()
+        torch.cuda.synchronize(dev)
+        return all(v == 1.0 for v in votes), why
+
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
         key = (nsteps, id(self.grad_sync), self.overlap, self.early_mlp, self.order_len,
                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
                getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
-               self._pers_ok())
+               self._pers_ok(), self.pers_exchange)
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.  The wait before it is
@@ -787,7 +896,7 @@ class HipEngine(Engine):
         poll = self.poll
         if not self.use_graphs:
             with torch.cuda.device(self.device):
-                if self._pipe_ok():
+                if self._pipe_ok() or self._pers_ok():
                     if poll is not None:
                         poll()
                     self._launch_steps(n)
@@ -838,7 +947,7 @@ class HipEngine(Engine):
         to: the caller re-raises)."""
         if self.persist:
             self.persist = False
-            level = "pipelined"
+            level = "pipelined" if self.grad_sync is None else "serial (one-launch exchange)"
         elif self.pipeline:
             self.pipeline = False
             level = "serial"

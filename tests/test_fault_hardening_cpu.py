@@ -215,14 +215,24 @@ def test_store_server_outlives_idle_while_a_local_rank_lives():
     """No heartbeat, no store writes (a bench rank): the idle exit waits while a registered rank
     process of this host is alive, and the server exits once every registered rank is gone
     (the idle exit could pull the store from under a live job)."""
+    from distributed_neural_network_amd.parallel.store_server import decide
+
+    kw = dict(world=2, closed=0, dropped=0, beats=[None, None], stale=30.0, idle=5.0, now=1000.0)
+    assert decide(pids={0: 11, 1: 12}, alive=[11], idle_for=1e4, **kw) is None  # a live rank: stay
+    assert "gone" in decide(pids={0: 11, 1: 12}, alive=[], idle_for=0.0, **kw)  # all local ranks gone
+    assert decide(pids={0: 11}, alive=[], idle_for=1.0, **kw) is None  # rank 1 not registered yet
+    assert "no activity" in decide(pids={}, alive=[], idle_for=6.0, **kw)  # nothing known: idle exit
+    assert "checked out" in decide(pids={0: 11}, alive=[11], idle_for=0.0, **dict(kw, closed=2))
+    assert "heartbeat" in decide(pids={0: 11}, alive=[11], idle_for=0.0, **dict(kw, beats=[900.0, None]))
+    # the running server applies it: a registered live rank keeps it up past the idle bound
     port = _free_port()
-    srv = _server(port, 2, "tok2", "--idle", "0.5")
+    srv = _server(port, 2, "tok2", "--idle", "5")
     live = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
     try:
         st = _wait_up(port, "tok2")
         st.set("dnn/pid/0", f"{socket.gethostname()}:{live.pid}")
         st.set("dnn/pid/1", f"{socket.gethostname()}:{os.getpid() + 10 ** 7}")  # never a live pid
-        time.sleep(2.5)
+        time.sleep(6.5)
         assert srv.poll() is None, "store exited under a live rank"
         live.kill()
         live.wait()

@@ -119,7 +119,8 @@ if os.environ.get("ENGINE", "fused") == "layers":
     eng = LayerEngine(batch=64, model="lenet-bn", seed=11, device="cuda", graph_chunk=8,
                       use_graphs=os.environ["GRAPHS"] == "1")
 else:
-    eng = HipEngine(batch=64, arena=init_arena(seed=11), graph_chunk=8, use_graphs=os.environ["GRAPHS"] == "1")
+    eng = HipEngine(batch=int(os.environ.get("BATCH", "64")), arena=init_arena(seed=11), graph_chunk=8,
+                    use_graphs=os.environ["GRAPHS"] == "1")
 eng.attach(data)
 pol = make_policy("step-allreduce", comm)
 pol.attach(eng)
@@ -128,26 +129,28 @@ samp = EpochSampler.for_rank(len(data), comm.rank, comm.world, seed=1, mode="sha
 for ep in range(2):
     pol.epoch_start(eng, ep)
     eng.begin_epoch(samp.order(ep))
-    eng.run_steps(samp.steps(64))
+    eng.run_steps(samp.steps(eng.batch))
     eng.synchronize()
     pol.epoch_end(eng, ep)
 kind = type(eng.grad_sync).__name__
 one = bool(getattr(getattr(eng.grad_sync, "group", None), "one_launch", False))
 xp_mode = int(getattr(getattr(eng.grad_sync, "group", None), "xp_mode", -1))
 ar_mode = int(getattr(getattr(eng.grad_sync, "group", None), "ar_mode", -1))
-torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "xp_mode": xp_mode, "ar_mode": ar_mode},
+path = pol.installed(eng)
+torch.save({"master": eng.master.cpu(), "kind": kind, "one_launch": one, "xp_mode": xp_mode, "ar_mode": ar_mode,
+            "path": path, "pers": bool(getattr(eng, "_pers_ok", lambda: False)())},
            os.path.join(os.environ["OUT"], f"r{comm.rank}.pt"))
 comm.close()
 '''
 
 
 def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="auto", engine="fused",
-               early="0"):
-    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{early}"
+               early="0", persist="0", batch=64):
+    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{early}{persist}{batch}{graphs}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
                OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch, DNN_XGMI_EXCHANGE=exchange, ENGINE=engine,
-               DNN_EARLY_MLP=early)
+               DNN_EARLY_MLP=early, DNN_PERSIST=persist, BATCH=str(batch))
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -225,11 +228,12 @@ def test_bench_two_ranks_xgmi(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
-    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag", "xgmi-pull-ovl",
-                                                                   "xgmi-rsag-ovl"), out
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag", "xgmi-pull-pers",
+                                                                   "xgmi-rsag-pers"), out
     ab = out["allreduce_ab"]
-    assert set(ab) == {"xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl", "xgmi-rsag-ovl"}, out
-    assert ab["xgmi-pull-ovl"] is not None, out
+    assert set(ab) == {"xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"}, out
+    assert ab["xgmi-pull-pers"] is not None and out["allreduce_ab_variant"]["xgmi-pull-pers"] == "persistent", out
+    assert out["ab_wall_s"] > 0, out
     assert ab["xgmi-pull"] is not None and ab["rccl"] is None and "rccl" in out["allreduce_failed"], out
     assert out["local_step_us"] > 0, out
     w = out["exchange_wait_us"]
@@ -268,3 +272,63 @@ def test_xgmi_early_mlp_two_ranks(tmp_path):
             r.stderr[-2000:]
         for i in range(2):
             assert torch.equal(res[i]["master"], ref[i]["master"]), (xch, i)
+
+
+@pytest.mark.parametrize("batch", [16, 64])
+def test_xgmi_exchange_inside_persistent_launch_two_ranks(tmp_path, batch):
+    """2 ranks on the box's GPU, the per-step exchange INSIDE the persistent
+    launch (xgmi-pull-pers / xgmi-rsag-pers: the reduction workgroups exchange their elements
+    over xGMI after each step's batch reduction, sum in rank order, apply SGD and only then signal
+    the samples) - installed after its self-test, engaged, and bit-identical on both ranks to the
+    serial one-launch exchange, over 2 epochs with graph replays and eager launches."""
+    import torch
+
+    port = 29701 + (batch // 16) * 10
+    ref, r0 = _two_ranks(tmp_path, "xgmi", "1", port, exchange="pull", batch=batch)
+    assert all(not x["pers"] and x["path"] == "xgmi-pull" for x in ref), r0.stderr[-2000:]
+    for k, (xch, graphs) in enumerate((("pull", "1"), ("rsag", "1"), ("pull", "0"))):
+        res, r = _two_ranks(tmp_path, "xgmi", graphs, port + 2 + 2 * k, exchange=xch, persist="1", batch=batch)
+        assert all(x["pers"] and x["path"] == f"xgmi-{xch}-pers" for x in res), (
+            [(x["path"], x["pers"]) for x in res], r.stdout[-2000:] + r.stderr[-3000:])
+        for i in range(2):
+            assert torch.equal(res[i]["master"], ref[i]["master"]), (xch, graphs, i)
+
+
+def test_xgmi_pers_one_rank_matches_local_sgd():
+    """World size 1 with forced collectives: the persistent launch with the exchange inside
+    (a 1-rank group: every wait is on this rank's own granules) equals the persistent local step."""
+    code = r'''
+import numpy as np, torch
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.parallel import Communicator, make_policy
+torch.cuda.set_device(0)
+comm = Communicator(device=torch.device("cuda", 0))
+data = synthetic(1000, 5)
+a = init_arena(seed=9)
+res = []
+for path in (None, "xgmi-pull-pers", "xgmi-rsag-pers"):
+    eng = HipEngine(batch=64, arena=a, graph_chunk=8)
+    eng.attach(data)
+    pol = make_policy("step-allreduce", comm)
+    pol.path = path
+    pol.attach(eng)
+    if path is None:
+        eng.grad_sync = None
+    else:
+        assert pol.installed(eng) == path, pol.installed(eng)
+    eng.begin_epoch(np.arange(1000, dtype=np.int32))
+    assert eng._pers_ok()
+    eng.run_steps(16)
+    torch.cuda.synchronize()
+    if path is not None:
+        pol.epoch_end(eng, 0)
+    res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), eng.epoch_stats()))
+for m, mo, sh, st in res[1:]:
+    assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo) and torch.equal(res[0][2], sh)
+    assert st.samples == 1000 and st.loss_sum == res[0][3].loss_sum
+comm.close()
+print("OK")
+'''.replace("torch.cuda.set_device(0)", "from distributed_neural_network_amd.runtime import HipEngine\ntorch.cuda.set_device(0)")
+    r = _py(code, {"DNN_FORCE_COLLECTIVES": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29727"})
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

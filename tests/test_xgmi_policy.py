@@ -38,7 +38,8 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
 
     for name in StepAllReduce.PATHS:
         if name.startswith("xgmi-"):
-            base = name.removesuffix("-ovl")  # (-ovl: the same exchange run by the in-launch reduction)
+            # (-ovl: the same exchange run by the in-launch reduction; -pers: inside the persistent launch)
+            base = name.removesuffix("-ovl").removesuffix("-pers")
             mode = xgmi.EXCHANGE_MODES[base[len("xgmi-"):]]
             assert "xgmi-" + xgmi.MODE_NAMES[mode] == base
     assert set(autotune.BF16_PATHS) <= set(StepAllReduce.PATHS)
@@ -51,12 +52,18 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
         overlap = False
         grad = torch.zeros(62006)
 
+    class _PersEng(_Eng):
+        persist = True
+
     pol = StepAllReduce.__new__(StepAllReduce)
     pol.comm, pol.bucket_kb = _Comm(), 0
     monkeypatch.setattr(xgmi, "wanted", lambda comm: True)
     monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
     assert pol.default_path(_Eng()) == "xgmi-pull"
+    # an engine with the persistent launch gets the exchange inside it (fp32 granules only)
+    assert pol.default_path(_PersEng()) == "xgmi-pull-pers"
     pol.grad_comm = "bf16"
+    assert pol.default_path(_PersEng()) == "xgmi-pull-bf16"
     assert pol.default_path(_Eng()) == "xgmi-pull-bf16"
     monkeypatch.setenv("DNN_XGMI_EXCHANGE", "rsag")
     assert pol.default_path(_Eng()) == "xgmi-rsag-bf16"
@@ -89,6 +96,8 @@ def test_choose_never_local_and_skips_failed():
 def test_choose_tie_prefers_order():
     res = {"rccl": _r(20.0), "xgmi-rsag": _r(20.0), "xgmi-pull": _r(20.0)}
     assert autotune.choose(res) == "xgmi-pull"
+    res["xgmi-pull-pers"] = _r(20.0)  # the persistent form is ranked first
+    assert autotune.choose(res) == "xgmi-pull-pers"
 
 
 def test_ab_two_ranks_agree(tmp_path):

@@ -16,6 +16,7 @@
 #   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32    bench.py default window (5000 / 500), bf16 / fp32
+#   b2k              bench.py 2000 / 200 steps, no epoch timing
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
@@ -58,6 +59,7 @@ for s in "$@"; do
       done ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
+    b2k) timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k.json" 2> "$O/b2k.err" ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
     prof|prof32|profserial|profpipe)
       dt=bf16; [ "$s" = prof32 ] && dt=fp32
