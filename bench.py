@@ -230,6 +230,8 @@ def main():
               f"{1e3 * ev[0].elapsed_time(ev[1]) / args.steps:.2f} us/step events", file=sys.stderr)
     if hasattr(engine.grad_sync, "check"):
         engine.grad_sync.check()  # raises if any xGMI wait in the timed window timed out
+    if getattr(engine, "step_wait_failed", lambda: False)():  # an in-launch wait timed out: not a valid number
+        raise RuntimeError("an in-launch step wait timed out inside the timed window")
     # per-step exchange wait inside the kernel over the timed steps (xGMI paths): this rank's
     # median / p99 / max, then the max over ranks
     waits = xg.wait_stats() if xg is not None else None

@@ -27,6 +27,8 @@ void rccl_destroy(uintptr_t comm);
 // one-shot xGMI all-reduce (comm/xgmi_allreduce.hip)
 std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
 uintptr_t uncached_alloc(long long bytes);
+void uncached_free(uintptr_t p);
+std::pair<long long, long long> uncached_pool_stats();
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
 std::string xgmi_device_id();
@@ -532,6 +534,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_device_id", &dnn::xgmi_device_id);
   m.def("xgmi_free", &dnn::xgmi_free);
   m.def("uncached_alloc", &dnn::uncached_alloc);
+  m.def("uncached_free", &dnn::uncached_free);
+  m.def("uncached_pool_stats", &dnn::uncached_pool_stats);
   m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
   m.def("xgmi_set_abort", &dnn::xgmi_set_abort);
   m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);

@@ -33,6 +33,9 @@
 // completes; later launches skip the wait.  The host checks the word at epoch end.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -293,12 +296,53 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity) {
 // Uncached (fine-grained) device memory, zeroed, for on-GPU hand-offs by tagged granules
 // between concurrently running kernels (the early-MLP row granules): every access bypasses
 // the per-XCD L2s, as the xGMI regions' do.  Freed with xgmi_free.
+//
+// Pooled: a block given back with uncached_free is kept for the next request of its size class
+// (zeroed again on reuse), never returned to the driver - an engine's control words, flags and
+// row granules are re-allocated by every engine a process builds (tests, A/B candidates), and
+// each hipFree / hipExtMallocWithFlags pair of fine-grained memory cost a device-wide
+// synchronisation and a page-table update while other engines' kernels were queued.
+namespace {
+std::mutex g_uc_mu;
+std::multimap<long long, void*> g_uc_free;     // size class -> free blocks
+std::map<void*, long long> g_uc_size;          // every pooled block -> its size class
+long long uc_class(long long bytes) { return std::max<long long>(4096, (bytes + 4095) / 4096 * 4096); }
+}  // namespace
+
 uintptr_t uncached_alloc(long long bytes) {
+  const long long cls = uc_class(bytes);
   void* p = nullptr;
-  xcheck(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
-  xcheck(hipMemset(p, 0, bytes), "hipMemset(uncached)");
+  {
+    std::lock_guard<std::mutex> lk(g_uc_mu);
+    auto it = g_uc_free.find(cls);
+    if (it != g_uc_free.end()) {
+      p = it->second;
+      g_uc_free.erase(it);
+    }
+  }
+  if (p == nullptr) {
+    xcheck(hipExtMallocWithFlags(&p, cls, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+    std::lock_guard<std::mutex> lk(g_uc_mu);
+    g_uc_size[p] = cls;
+  }
+  xcheck(hipMemset(p, 0, cls), "hipMemset(uncached)");
   xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   return reinterpret_cast<uintptr_t>(p);
+}
+
+// Give an uncached_alloc block back to the pool (the caller has synchronised: no kernel uses it).
+void uncached_free(uintptr_t p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_uc_mu);
+  auto it = g_uc_size.find(reinterpret_cast<void*>(p));
+  if (it == g_uc_size.end()) throw std::runtime_error("uncached_free: not a pooled uncached block");
+  g_uc_free.emplace(it->second, it->first);
+}
+
+// (diagnostic) pooled blocks: (total, free)
+std::pair<long long, long long> uncached_pool_stats() {
+  std::lock_guard<std::mutex> lk(g_uc_mu);
+  return {(long long)g_uc_size.size(), (long long)g_uc_free.size()};
 }
 
 uintptr_t xgmi_open(const std::string& handle) {

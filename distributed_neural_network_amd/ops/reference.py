@@ -142,8 +142,19 @@ def per_sample_outputs_bf16(shadow: torch.Tensor, master: torch.Tensor, images_u
     slab = torch.cat([dW1.flatten(1), db1, dW2.flatten(1), db2], 1)
     z3p = torch.zeros(B, 16)
     z3p[:, :10] = z3
+    codes = torch.cat([_codes_from_pool(p1, i1, 28), _codes_from_pool(p2, i2, 10)], 1)
     return {"a0": a0, "h1": h1, "h2": h2, "z1": z1, "z2": z2, "z3": z3p, "slab": slab, "loss": loss,
-            "correct": correct, "logits": logits}
+            "correct": correct, "logits": logits, "codes": codes}
+
+
+def _codes_from_pool(pooled: torch.Tensor, idx: torch.Tensor, w: int) -> torch.Tensor:
+    """The fused kernel's 2-bit max-pool code of a ReLU + 2x2 max-pool: the pixel dy * 2 + dx the
+    max came from, 4 where the pooled value is 0 (every input <= 0: no gradient)."""
+    B, C = pooled.shape[:2]
+    y, x = idx // w, idx % w
+    code = (y % 2) * 2 + (x % 2)
+    code = torch.where(pooled > 0, code, torch.full_like(code, 4))
+    return code.reshape(B, -1).to(torch.uint8)
 
 
 CODES_PER_SAMPLE = 6 * 196 + 400  # lenet_fused.hip: CODE1 [6][14*14] | CODE2 [16][5*5]
@@ -256,3 +267,33 @@ def train_steps_bf16(master: torch.Tensor, images_u8: torch.Tensor, labels: torc
         p = (-lr * m.double() + p.double()).float()
         losses.append(float(rows["loss"].double().mean()))
     return p, m, losses
+
+
+def train_steps_fp32_masked(master: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor, order, batch: int,
+                            steps: int, lr: float, momentum: float):
+    """The fp32 reference arithmetic over ``steps`` steps, MASK-AWARE: every step's ReLU / max-pool
+    decisions are those of the bf16 trajectory (``train_steps_bf16``, run alongside from the same
+    start), every operand and accumulator stays fp32 (``per_sample_outputs_masked`` on the fp32
+    master).  A near-tie that bf16 operands flip then cannot turn rounding noise into an O(1)
+    change of one sample's gradient, so the bf16 kernel's trajectory can be held to bf16 precision
+    of fp32 (~1e-2).  Returns (fp32 master, momentum, per-step mean losses)."""
+    pe = master.detach().float().cpu().clone()
+    p32 = pe.clone()
+    me, m32 = torch.zeros_like(pe), torch.zeros_like(pe)
+    order = torch.as_tensor(order, dtype=torch.int64)
+    mask = LAYOUT.pad_mask().float()
+    losses = []
+    for s in range(steps):
+        idx = order[s * batch:(s + 1) * batch]
+        if idx.numel() == 0:
+            break
+        n = int(idx.numel())
+        emu = per_sample_outputs_bf16(pe.bfloat16(), pe, images_u8[idx], labels[idx], n)
+        f32 = per_sample_outputs_masked(p32, p32, images_u8[idx], labels[idx], emu["codes"], emu["h1"] > 0,
+                                        emu["h2"] > 0, n)
+        for p, m, rows in ((pe, me, emu), (p32, m32, f32)):
+            g = reduce_rows(rows) * mask
+            m.copy_((momentum * m.double() + g.double()).float())
+            p.copy_((-lr * m.double() + p.double()).float())
+        losses.append(float(f32["loss"].double().mean()))
+    return p32, m32, losses

@@ -105,22 +105,8 @@ def ranks_per_gpu() -> int:
 
 
 def gpu_shared_by_ranks() -> bool:
-    """Do other ranks of this job run on this process's GPU (more local ranks than visible
-    devices: the one-GPU rehearsals, ``tools/fault_bench.py --share-gpu``)?  The local rank
-    count comes from the launcher's environment (torchrun, OpenMPI, MPICH / Intel MPI, Slurm);
-    without one, the world size is taken as local (conservative)."""
-    n = None
-    for k in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE"):
-        v = os.environ.get(k)
-        if v:
-            try:
-                n = int(v.split("(")[0])
-                break
-            except ValueError:
-                pass
-    if n is None:
-        n = int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", "1")) or 1)
-    return n > max(1, torch.cuda.device_count())
+    """Do other ranks of this job run on this process's GPU (the one-GPU rehearsals)?"""
+    return ranks_per_gpu() > 1
 
 
 class Engine:
@@ -617,21 +603,17 @@ class HipEngine(Engine):
             self._launch_step()
 
     def __del__(self) -> None:
+        """Give the uncached control buffers back to the extension's pool (never to the driver:
+        csrc/comm/xgmi_allreduce.hip uncached_alloc) once this engine's queued work is done."""
         rg = getattr(self, "_rg", None)
-        pc = getattr(self, "_pipe_ctr_ptr", None)
-        pf = getattr(self, "_pipe_flg_ptr", None)
-        pp = getattr(self, "_pers_ctl", 0)
-        if rg is not None or pc is not None:
+        bufs = [getattr(self, "_pipe_ctr_ptr", 0), getattr(self, "_pipe_flg_ptr", 0), getattr(self, "_pers_ctl", 0),
+                rg["ptr"] if rg is not None else 0]
+        if any(bufs):
             try:
                 torch.cuda.synchronize(self.device)
-                if rg is not None:
-                    self.ext.xgmi_free(rg["ptr"])
-                if pc is not None:
-                    self.ext.xgmi_free(pc)
-                if pf:
-                    self.ext.xgmi_free(pf)
-                if pp:
-                    self.ext.xgmi_free(pp)
+                for p in bufs:
+                    if p:
+                        self.ext.uncached_free(p)
             except Exception:
                 pass
 

@@ -143,16 +143,25 @@ def test_train_steps_track_cpu_oracle(form):
     hs, cs = hip.epoch_stats(), cpu.epoch_stats()
     assert hs.batches == cs.batches == 10 and hs.samples == cs.samples == 640
     em, _, el = reference.train_steps_bf16(arena, split.images, split.labels, order, B, 10, hip.lr, hip.momentum)
+    mm, _, ml = reference.train_steps_fp32_masked(arena, split.images, split.labels, order, B, 10, hip.lr,
+                                                  hip.momentum)
     upd = hip.master.cpu() - arena
     r_emu = _rel(upd, em - arena)
     l_emu = abs(hs.mean_loss - float(np.mean(el))) / abs(float(np.mean(el)))
+    r_msk = _rel(upd, mm - arena)
+    l_msk = abs(hs.mean_loss - float(np.mean(ml))) / abs(float(np.mean(ml)))
     r_f32 = _rel(upd, cpu.master - arena)
     l_f32 = abs(hs.mean_loss - cs.mean_loss) / abs(cs.mean_loss)
-    print(f"{form}: update vs bf16 emulation {r_emu:.2e}, loss {l_emu:.2e}; vs fp32 {r_f32:.2e}, loss {l_f32:.2e}")
+    print(f"{form}: update vs bf16 emulation {r_emu:.2e}, loss {l_emu:.2e}; vs mask-aware fp32 {r_msk:.2e}, "
+          f"loss {l_msk:.2e}; vs plain fp32 {r_f32:.2e}, loss {l_f32:.2e}")
     assert r_emu < 1e-3, f"parameter update vs the bf16-emulating trajectory: rel err {r_emu:.3e}"
     assert l_emu < 1e-4, f"epoch loss vs the bf16-emulating trajectory: rel err {l_emu:.3e}"
-    assert r_f32 < 3e-2, f"parameter update vs the fp32 oracle: rel err {r_f32:.3e}"
-    assert l_f32 < 1e-2, f"epoch loss vs the fp32 oracle: rel err {l_f32:.3e}"
+    assert r_msk < 1e-2, f"parameter update vs the mask-aware fp32 trajectory: rel err {r_msk:.3e}"
+    assert l_msk < 1e-3, f"epoch loss vs the mask-aware fp32 trajectory: rel err {l_msk:.3e}"
+    # the plain fp32 engine (its own pool / ReLU decisions): near-ties flipped by bf16 operands move a
+    # few samples' gradients by O(1) - measured 3.4e-2 on this data; a loose guard against drift
+    assert r_f32 < 6e-2, f"parameter update vs the fp32 oracle: rel err {r_f32:.3e}"
+    assert l_f32 < 1e-3, f"epoch loss vs the fp32 oracle: rel err {l_f32:.3e}"
 
 
 def test_eval_matches_oracle():

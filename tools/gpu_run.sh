@@ -22,6 +22,7 @@
 #   pmcserial:<..>   the same with the pipelined step off
 #   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
 #   phase | phase32 | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
+#   reprodirect      tools/repro_direct.py with DNN_PERS_DIRECT=1 (the round-4 direct-relaunch fault)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
@@ -96,6 +97,7 @@ for s in "$@"; do
       env "$kv" DNN_PIPELINE=1 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch \
         > "$O/b2k_$n.json" 2> "$O/b2k_$n.err" ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
+    reprodirect) DNN_PERS_DIRECT=1 timeout -k 10 300 python -u tools/repro_direct.py > "$O/reprodirect.log" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;
     rehearse2diag) DNN_BACKEND=gloo DNN_AB_DEBUG=1 timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
