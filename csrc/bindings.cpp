@@ -28,7 +28,7 @@ void rccl_destroy(uintptr_t comm);
 std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
 uintptr_t uncached_alloc(long long bytes);
 void uncached_free(uintptr_t p);
-std::pair<long long, long long> uncached_pool_stats();
+std::tuple<long long, long long, long long> uncached_pool_stats();
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
 std::string xgmi_device_id();

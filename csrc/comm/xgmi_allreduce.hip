@@ -33,6 +33,10 @@
 // completes; later launches skip the wait.  The host checks the word at epoch end.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <tuple>
 #include <map>
 #include <mutex>
 
@@ -306,7 +310,16 @@ namespace {
 std::mutex g_uc_mu;
 std::multimap<long long, void*> g_uc_free;     // size class -> free blocks
 std::map<void*, long long> g_uc_size;          // every pooled block -> its size class
+long long g_uc_violations = 0;                 // reused blocks whose canary was overwritten while free
 long long uc_class(long long bytes) { return std::max<long long>(4096, (bytes + 4095) / 4096 * 4096); }
+constexpr unsigned char UC_CANARY = 0xA5;
+// A free block holds the canary byte everywhere: a kernel that still wrote to its old owner's
+// control words after that owner was destroyed (a use-after-free) would show up as a broken
+// canary when the block is handed out again (DNN_UNCACHED_CANARY=0 skips the check).
+bool uc_check_canary() {
+  const char* v = std::getenv("DNN_UNCACHED_CANARY");
+  return v == nullptr || v[0] != '0';
+}
 }  // namespace
 
 uintptr_t uncached_alloc(long long bytes) {
@@ -318,6 +331,18 @@ uintptr_t uncached_alloc(long long bytes) {
     if (it != g_uc_free.end()) {
       p = it->second;
       g_uc_free.erase(it);
+    }
+  }
+  if (p != nullptr && uc_check_canary()) {
+    std::vector<unsigned char> h((size_t)cls);
+    xcheck(hipMemcpy(h.data(), p, (size_t)cls, hipMemcpyDeviceToHost), "hipMemcpy(uncached canary)");
+    long long bad = 0;
+    for (unsigned char c : h) bad += c != UC_CANARY;
+    if (bad) {
+      std::lock_guard<std::mutex> lk(g_uc_mu);
+      ++g_uc_violations;
+      std::fprintf(stderr, "[uncached pool] %lld bytes of a free %lld-byte block were written after its free\n", bad,
+                   cls);
     }
   }
   if (p == nullptr) {
@@ -333,16 +358,25 @@ uintptr_t uncached_alloc(long long bytes) {
 // Give an uncached_alloc block back to the pool (the caller has synchronised: no kernel uses it).
 void uncached_free(uintptr_t p) {
   if (!p) return;
+  long long cls = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_uc_mu);
+    auto it = g_uc_size.find(reinterpret_cast<void*>(p));
+    if (it == g_uc_size.end()) throw std::runtime_error("uncached_free: not a pooled uncached block");
+    cls = it->second;
+  }
+  if (uc_check_canary()) {
+    xcheck(hipMemset(reinterpret_cast<void*>(p), UC_CANARY, cls), "hipMemset(uncached canary)");
+    xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
   std::lock_guard<std::mutex> lk(g_uc_mu);
-  auto it = g_uc_size.find(reinterpret_cast<void*>(p));
-  if (it == g_uc_size.end()) throw std::runtime_error("uncached_free: not a pooled uncached block");
-  g_uc_free.emplace(it->second, it->first);
+  g_uc_free.emplace(cls, reinterpret_cast<void*>(p));
 }
 
-// (diagnostic) pooled blocks: (total, free)
-std::pair<long long, long long> uncached_pool_stats() {
+// (diagnostic) pooled blocks: (total, free, canary violations seen on reuse)
+std::tuple<long long, long long, long long> uncached_pool_stats() {
   std::lock_guard<std::mutex> lk(g_uc_mu);
-  return {(long long)g_uc_size.size(), (long long)g_uc_free.size()};
+  return {(long long)g_uc_size.size(), (long long)g_uc_free.size(), g_uc_violations};
 }
 
 uintptr_t xgmi_open(const std::string& handle) {

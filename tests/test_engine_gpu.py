@@ -262,3 +262,17 @@ def test_pipelined_long_run_under_load():
     for r in res[1:]:
         assert torch.equal(res[0][0], r[0]) and torch.equal(res[0][1], r[1])
         assert res[0][2].loss_sum == r[2].loss_sum
+
+
+def test_direct_relaunch_minimal_pair_regression(tmp_path):
+    """Round 4's direct-relaunch fault (profiles/r4/pers_direct): direct persistent relaunches
+    (staged[True]) followed by the early-MLP engines, then serial / pipelined / persistent engines
+    in the same process, faulted with hipErrorIllegalAddress while engines freed their uncached
+    control buffers (hipFree) between them.  The buffers now come from a never-freed pool whose
+    free blocks hold a canary: the sequence must finish AND no freed block may have been written
+    after its free (no kernel touches a destroyed engine's control words)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_PERS_DIRECT="1", REPRO_SKIP="bitwise,staged_F,determ")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "repro_direct.py")], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DONE" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+    assert " 0 canary violations" in r.stdout, r.stdout[-2000:]

@@ -9,6 +9,7 @@
 #   smoke            __graft_entry__.smoke()
 #   tests            the whole GPU suite (pytest -m gpu, per-test timeout)
 #   tests:<expr>     GPU tests selected by -k <expr>
+#   envtests:VAR=val the whole GPU suite under one environment setting
 #   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
 #   k20f32           the same, --dtype fp32
 #   envk20:VAR=val   k20 with one environment setting
@@ -39,6 +40,10 @@ for s in "$@"; do
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
              > "$O/tests.log" 2>&1 ;;
+    envtests:*)  # the whole GPU suite under one env setting: envtests:VAR=value
+      kv="${s#envtests:}"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+             > "$O/tests_$n.log" 2>&1 ;;
     tests:*) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
              -k "${s#tests:}" > "$O/tests_k.log" 2>&1 ;;
     k20|k20b) timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
