@@ -480,11 +480,15 @@ class HipEngine(Engine):
         return grp
 
     # persistent launches directly from the extension's cached argument block instead of graph
-    # replays (DNN_PERS_DIRECT=1; ~3.4 us less per 20-step window, profiles/r4/pers_direct).  Off by
-    # default: with it on, a LATER pipelined engine in the same process hits an illegal address that
-    # surfaces between two syncs with no launch in between (runtime-owned memory corrupted - not
-    # found yet); the same sequence with graph replays passes (profiles/r4/pers_direct/README.md,
-    # tools/repro_direct.py).  DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after every relaunch
+    # replays (DNN_PERS_DIRECT=1).  Round 4 measured ~3.4 us less per 20-step window and saw an
+    # illegal address in a LATER engine of the same process (profiles/r4/pers_direct).  The fault
+    # needed engines freeing their uncached control buffers (hipFree of fine-grained memory) between
+    # direct-mode runs; those buffers now come from a never-freed pool whose free blocks carry a
+    # canary (csrc/comm/xgmi_allreduce.hip uncached_alloc): the minimal pair and the whole GPU suite
+    # pass in direct mode with no canary broken, i.e. no kernel wrote to a destroyed engine's control
+    # words (profiles/r5/direct_pool).  Off by default: on the round-5 box the window measured the
+    # same either way (18.18 vs 18.02-18.07 us).  DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after
+    # every relaunch
     pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
     pers_direct_sync = os.environ.get("DNN_PERS_DIRECT_SYNC", "0") == "1"
     # bound of one ready wait (then a sticky error word, raised at epoch_stats); DNN_PIPE_TIMEOUT_S

@@ -116,3 +116,59 @@ def test_ab_two_ranks_agree(tmp_path):
         assert g["restored"], "parameters not restored after the A/B"
     assert got[0]["res"] == got[1]["res"]  # one decision, from all-reduced numbers only
     assert torch.equal(got[0]["master"], got[1]["master"])
+
+
+def test_pers_install_and_fallback(monkeypatch):
+    """The "-pers" paths: installed on top of the one-launch exchange only after the persistent-
+    exchange self-test passed on every rank (cached per group and form); a failing self-test makes
+    the default chain fall back to the serial one-launch exchange of the same form."""
+    from distributed_neural_network_amd.parallel import sync
+
+    class _Grp:
+        one_launch, xp_mode, broken = True, 0, False
+
+    class _Sync:
+        fuses_sgd = True
+
+        def __init__(self, grp):
+            self.group = grp
+
+    class _Comm:
+        backend, distributed, rank, world = "nccl", True, 0, 2
+
+    class _Eng:
+        overlap = False
+        persist = True
+        grad = torch.zeros(62006)
+
+        def __init__(self, ok):
+            self.ok, self.calls, self.grad_sync, self.pers_exchange = ok, 0, None, False
+
+        def invalidate_graphs(self):
+            pass
+
+        def selftest_pers_exchange(self, grp, comm):
+            self.calls += 1
+            return (self.ok, "" if self.ok else "mismatch in ['master']")
+
+    grp = _Grp()
+
+    def fake_install_xgmi(self, engine, mode):
+        grp.xp_mode = mode
+        engine.grad_sync = _Sync(grp)
+        return True
+
+    monkeypatch.setattr(sync.StepAllReduce, "_install_xgmi", fake_install_xgmi)
+    monkeypatch.setattr(xgmi, "wanted", lambda comm: True)
+    monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
+    pol = sync.StepAllReduce(_Comm())
+    eng = _Eng(True)
+    assert pol.install(eng, "xgmi-rsag-pers") and eng.pers_exchange and grp.xp_mode == 2
+    assert pol.install(eng, "xgmi-rsag-pers") and eng.calls == 1  # cached per group and form
+    assert pol.install(eng, "xgmi-pull") and not eng.pers_exchange  # a plain path clears it
+    bad = _Eng(False)
+    grp.__dict__.pop("selftested_pers", None)
+    assert not pol.install(bad, "xgmi-pull-pers") and "self-test failed" in pol.install_why
+    assert bad.grad_sync is None and not bad.pers_exchange
+    pol.attach(bad)  # default path xgmi-pull-pers -> its self-test fails (cached) -> xgmi-pull
+    assert bad.grad_sync is not None and not bad.pers_exchange and grp.xp_mode == 0
