@@ -250,6 +250,8 @@ class Trainer:
         if c.allreduce not in ("default", "ab") and hasattr(self.policy, "PATHS"):
             self.policy.path = c.allreduce
         self.policy.attach(self.engine)
+        if self.comm.distributed and hasattr(self.policy, "installed"):
+            self._say(f"[allreduce] per-step all-reduce path: {self.policy.installed(self.engine)}")
         self.sampler = self._sampler()
         self.allreduce_ab = None
         if c.allreduce == "ab" and self.comm.distributed and hasattr(self.policy, "PATHS"):
