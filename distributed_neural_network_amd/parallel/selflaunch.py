@@ -49,24 +49,35 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _kfd_gpu_nodes(root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
-    """GPU nodes of the KFD topology (sysfs: a node with a non-zero ``gfx_target_version`` is a
-    GPU, the others are CPU nodes).  -1 if the topology cannot be read."""
+def _kfd_gpu_nodes(root: str = "/sys/class/kfd/kfd/topology/nodes", dri: str = "/dev/dri") -> int:
+    """GPU nodes of the KFD topology that this process can open (sysfs: a node with a non-zero
+    ``gfx_target_version`` is a GPU; it counts only if its render node ``/dev/dri/renderD<minor>``
+    is accessible - a container sees every GPU of the host in the topology but gets only its own
+    render nodes, which is the filter the ROCm runtime applies).  -1 if the topology cannot be read."""
     try:
         names = os.listdir(root)
     except OSError:
         return -1
     n = 0
     for d in names:
+        props = {}
         try:
             with open(os.path.join(root, d, "properties")) as f:
                 for line in f:
                     k, _, v = line.partition(" ")
-                    if k == "gfx_target_version":
-                        n += int(v.strip() or 0) != 0
-                        break
-        except (OSError, ValueError):
+                    props[k] = v.strip()
+        except OSError:
             continue
+        try:
+            if int(props.get("gfx_target_version", "0") or 0) == 0:
+                continue
+        except ValueError:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is not None and os.path.isdir(dri):
+            if not os.access(os.path.join(dri, f"renderD{minor}"), os.R_OK | os.W_OK):
+                continue
+        n += 1
     return n
 
 
@@ -160,6 +171,7 @@ def run(cmd: Sequence[str], nproc: int, out_fd: int | None = None, extra_env: Op
     base = dict(os.environ)
     base.update(extra_env or {})
     ndev = visible_devices()
+    print(f"[launch] {ndev} GPU(s) visible to this job (KFD topology + visibility variables)", file=err, flush=True)
     if nproc > max(ndev, 1) and not base.get("DNN_BACKEND"):
         base["DNN_BACKEND"] = "gloo"
         print(f"[launch] {nproc} ranks on {ndev} visible GPU(s): ranks share devices, host collectives over gloo",

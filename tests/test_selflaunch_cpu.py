@@ -258,11 +258,18 @@ def test_bench_refuses_nothing_without_launcher(n):
 def test_device_count_reads_sysfs_not_hip(tmp_path, monkeypatch):
     """The launcher counts GPUs from the KFD topology + visibility variables (a
     torch.cuda.device_count() fallback could initialise HIP in the launcher)."""
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    topo.mkdir()
+    dri.mkdir()
     for i, gfx in enumerate([0, 90500, 90500, 0, 90500]):  # 2 CPU nodes, 3 GPU nodes
-        d = tmp_path / str(i)
+        d = topo / str(i)
         d.mkdir()
-        (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {gfx}\nsimd_count 1024\n")
-    assert selflaunch._kfd_gpu_nodes(str(tmp_path)) == 3
+        (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {gfx}\nsimd_count 1024\n"
+                                      f"drm_render_minor {128 + i}\n")
+    for i in (1, 2):  # this "container" may open the render nodes of two of the three GPUs
+        (dri / f"renderD{128 + i}").write_text("")
+    assert selflaunch._kfd_gpu_nodes(str(topo), str(dri)) == 2
+    assert selflaunch._kfd_gpu_nodes(str(topo), str(tmp_path / "no-dri")) == 3  # no /dev/dri to check
     assert selflaunch._kfd_gpu_nodes(str(tmp_path / "missing")) == -1
     for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         monkeypatch.delenv(k, raising=False)
