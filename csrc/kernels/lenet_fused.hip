@@ -37,7 +37,7 @@
 #include <algorithm>
 #include <string>
 
-#include "reduce_device.h"
+#include "pers_common.h"
 
 namespace dnn {
 
@@ -278,11 +278,6 @@ __device__ __forceinline__ void dgrad_rows(const unsigned char* r3b, const bf16x
 //   PG_MLP fc weights + biases (phase C: the fc1 LDS stream; phase D fragments): checked in the
 //          same poll round - a wave streams its part of fc1 mid-phase B if the group is
 //          already complete, else after phase B once it is.
-constexpr int PIPE_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
-constexpr int PIPE_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT;
-constexpr int PIPE_C1_BLOCKS = (SLAB_C2W * SPLIT + RT - 1) / RT;  // conv1 W + b: slab [0, SLAB_C2W)
-constexpr int PIPE_C2_BLOCKS = PIPE_CONV_BLOCKS - PIPE_C1_BLOCKS;
-constexpr int PIPE_BLOCKS = PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS + 1;
 constexpr int PG_C1 = 0, PG_C2 = 1, PG_MLP = 2, PIPE_GROUPS = 3;
 constexpr int PIPE_CTR_STRIDE = 32;  // counters and flags 128 B apart, each on a line of its own
 static_assert(PIPE_BLOCKS == GRAD_REDUCE_BLOCKS, "the pipelined launch runs the whole grad_reduce");
@@ -388,9 +383,8 @@ __device__ __forceinline__ void pipe_wait(const PipeCtl& pc, int grp, int b, int
 // No kernel boundary, launch ramp or tail sits between two steps.
 constexpr int PERS_WG = (PIPE_BLOCKS + 1) / 2;                // reduction workgroups
 constexpr int PERS_CONV_WG = (PIPE_CONV_BLOCKS + 1 + 1) / 2;  // conv blocks + the bookkeeping block
-constexpr int PERS_AROW = 256;                                // arrival words per workgroup (max batch)
 constexpr int PERS_C1_WG = PIPE_C1_BLOCKS / 2;                // ready groups = workgroup ranges:
-constexpr int PERS_RROW = 64;                                 //   C1 [0, 4), C2 + bookkeeping [4, 23), MLP [23, 57)
+                                                              //   C1 [0, 4), C2 + bookkeeping [4, 23), MLP [23, 57)
 static_assert((PIPE_CONV_BLOCKS + 1) % 2 == 0, "conv + bookkeeping blocks fill whole workgroups");
 static_assert(PIPE_C1_BLOCKS % 2 == 0, "the conv1 group is whole workgroups");
 static_assert(PERS_WG <= PERS_RROW, "one ready word per reduction workgroup in a sample's row");
@@ -404,24 +398,7 @@ static_assert(PERS_WG <= PERS_RROW, "one ready word per reduction workgroup in a
 // the group it waits for.
 // control memory: [256 generation words], [batch][PERS_RROW] ready rows, [PERS_WG][PERS_AROW]
 // arrival words
-constexpr int PERS_MAX_GRID = 256;
-constexpr long PERS_FLG_OFF = PERS_MAX_GRID * 4;
-__host__ __device__ constexpr long pers_arrive_off(int batch) { return (PERS_FLG_OFF + 4L * batch * PERS_RROW + 1023) / 1024 * 1024; }
 int persist_ctl_bytes(int batch) { return (int)(pers_arrive_off(batch) + (long)PERS_WG * PERS_AROW * 4); }
-
-__device__ __forceinline__ unsigned ld_tag(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_tag(unsigned* p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool tag_ge(unsigned v, unsigned tgt) { return (int)(v - tgt) >= 0; }  // wrap-safe
-__device__ __forceinline__ int ld_sc1(const int32_t* p) {
-  return (int)__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_wt_i(int32_t* p, int v) {
-  __hip_atomic_store(reinterpret_cast<unsigned*>(p), (unsigned)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // A sample's arrival at step tag - 1: kind 0 = the conv workgroups (slab, loss / correct read by
 // the bookkeeping), 1 = the MLP workgroups.  One store per lane (lane = workgroup), by ONE wave,
@@ -455,72 +432,6 @@ __device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo
       if (lane == 0) __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
-  }
-}
-
-// One wave of a reduction workgroup waits until every sample's arrival word reached tgt
-// (bounded: the sticky error word, then no more waits anywhere - never a hang).
-__device__ __forceinline__ void pers_wait_rows(const PipeCtl& pc, const unsigned* row, int batch, unsigned tgt,
-                                               int lane) {
-  if (ld_tag(pc.err) != 0u) return;
-  const long long t0 = wall_clock64();
-  while (true) {
-    bool ok = true;
-    for (int b = lane; b < batch; b += 64) ok &= tag_ge(ld_tag(row + b), tgt);
-    if (__all(ok)) break;
-    __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > pc.timeout_ticks) {
-      __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-  }
-}
-
-// The bookkeeping of the persistent launch, the same sequence of publications as a PIPE chunk
-// of nsteps launches + its closing grad_reduce (engine.py _launch_steps_pipe):
-//   t = -1 (launch start, no statistics): cursor + 1, publish slot 1 (step 1's bvalid, step 2's ids);
-//   t = 0 .. n - 2 (step t reduced): statistics of step t (bvalid from slot t & 1), cursor + 1,
-//     publish slot t & 1 (step t + 2's);
-//   t = n - 1: statistics of step n - 1, cursor unchanged, publish slot 0 (the next launch's).
-// Loads of anything written inside the launch are sc1 and every store the samples read is
-// written through.  One wave.
-__device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const PipeCtl& pc, int lane, int t) {
-  const int n = pc.nsteps;
-  const bool stats = t >= 0;
-  const int adv = t == n - 1 ? 0 : 1;
-  const int sin = t < 0 ? 1 : (t & 1);
-  const int sout = t < 0 ? 1 : (t == n - 1 ? 0 : (t & 1));
-  const int bv = ld_sc1(pc.bv_slot[sin]);  // (before anything is published: sin may be sout)
-  float ls = 0.f;
-  int cs = 0;
-  if (stats) {
-    const long r = (long)(t & 1) * a.batch;
-    for (int b = lane; b < a.batch; b += 64) {
-      ls += ldrow<true>(a.loss + r + b);
-      cs += ld_sc1(a.correct + r + b);
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }
-  const int next = ld_sc1(a.state + ST_CURSOR) + adv;
-  if (lane == 0 && bv > 0 && stats) {
-    a.stats[STAT_LOSS] += (double)ls / (double)bv;
-    a.stats[STAT_BATCHES] += 1.0;
-    a.stats[STAT_CORRECT] += (double)cs;
-    a.stats[STAT_SAMPLES] += (double)bv;
-  }
-  const long base = (long)next * a.batch;
-  for (int b = lane; b < a.batch; b += 64) {
-    const long g = base + b;
-    a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
-    const long g2 = base + a.batch + b;
-    st_wt_i(pc.nid_slot[sout] + b, g2 < a.order_len ? a.order[g2] : -1);
-  }
-  const long rem = (long)a.order_len - base;
-  const int nbv = rem < a.batch ? (rem > 0 ? (int)rem : 0) : a.batch;
-  if (lane == 0) {
-    st_wt_i(a.state + ST_CURSOR, next);
-    st_wt_i(pc.bv_slot[sout], nbv);
   }
 }
 
