@@ -30,9 +30,22 @@ def _launch(n, args, cwd, timeout=240):
 
 
 def _launch_env(n, args, cwd, env_extra, timeout=300):
+    """Run a launched job; on a timeout, kill it and fail WITH its output so far (every rank dumps
+    its thread stacks every 30 s: DNN_FAULTHANDLER_S) - a hang must name where it sits."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", **env_extra)
+    env.setdefault("DNN_FAULTHANDLER_S", "30")
     cmd = [sys.executable, "-m", "distributed_neural_network_amd.parallel.launch", "-n", str(n), "--cpu"] + args
-    return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        import signal
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        raise AssertionError(f"job timed out after {timeout} s\n--- stdout ---\n{out[-6000:]}\n--- stderr ---\n"
+                             f"{err[-12000:]}")
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
 def _run_worker(tmp_path, mode, world, n=192, batch=16, epochs=2):
