@@ -486,9 +486,9 @@ class HipEngine(Engine):
     # direct-mode runs; those buffers now come from a never-freed pool whose free blocks carry a
     # canary (csrc/comm/xgmi_allreduce.hip uncached_alloc): the minimal pair and the whole GPU suite
     # pass in direct mode with no canary broken, i.e. no kernel wrote to a destroyed engine's control
-    # words (profiles/r5/direct_pool).  Off by default: on the round-5 box the window measured the
-    # same either way (18.18 vs 18.02-18.07 us).  DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after
-    # every relaunch
+    # words (profiles/r5/direct_pool).  Off by default: on the round-5 box six alternating 20/5
+    # windows each way measured graph replays FASTER (median 18.07 vs 18.16 us, ab6/).
+    # DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after every relaunch
     pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
     pers_direct_sync = os.environ.get("DNN_PERS_DIRECT_SYNC", "0") == "1"
     # bound of one ready wait (then a sticky error word, raised at epoch_stats); DNN_PIPE_TIMEOUT_S

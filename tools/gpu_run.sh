@@ -18,6 +18,7 @@
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32    bench.py default window (5000 / 500), bf16 / fp32
 #   b2k              bench.py 2000 / 200 steps, no epoch timing
+#   abdirect:N       N alternating 20/5 windows: graph replays vs direct relaunch (DNN_PERS_DIRECT=1)
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
@@ -65,6 +66,12 @@ for s in "$@"; do
       done ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
+    abdirect:*)  # alternating 20/5 windows, graph replays vs direct relaunch, N rounds: abdirect:N
+      for i in $(seq 1 "${s#abdirect:}"); do
+        timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-epoch > "$O/abd_graph_$i.json" 2> "$O/abd_graph_$i.err"
+        DNN_PERS_DIRECT=1 timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-epoch > "$O/abd_direct_$i.json" \
+          2> "$O/abd_direct_$i.err"
+      done ;;
     b2k) timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k.json" 2> "$O/b2k.err" ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
     prof|prof32|profserial|profpipe)
