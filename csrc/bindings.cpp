@@ -276,6 +276,35 @@ PYBIND11_MODULE(_dnn_hip, m) {
                                     S(stream));
   });
   m.def("persist_cached", [](long long handle) { return g_pers_cache_set && handle == g_pers_cache_handle; });
+  // the fp32 kernel's persistent launch (lenet_f32.hip PERS): the reduction is the last
+  // grad_reduce(defer=2) call's (graph replays only: no cached relaunch)
+  m.def("fused_train_persist_f32", [](u images, u labels, int order_len, int batch, u master, u a0, u h1, u h2, u z1,
+                                      u z2, u z3, u slab, u loss, u correct, u ctl, int nsteps, u bv0, u bv1, u nid0,
+                                      u nid1, u err, double timeout_s, u stream, int flags, u stamps) {
+    if (!g_pending_pipe_set) throw std::runtime_error("fused_train_persist_f32 needs a grad_reduce(defer=2) call first");
+    g_pending_pipe_set = false;
+    dnn::PipeCtl pc;
+    pc.ctr = P<unsigned>(ctl);
+    pc.nsteps = nsteps;
+    pc.bv_slot[0] = P<int32_t>(bv0);
+    pc.bv_slot[1] = P<int32_t>(bv1);
+    pc.nid_slot[0] = P<int32_t>(nid0);
+    pc.nid_slot[1] = P<int32_t>(nid1);
+    pc.err = P<unsigned>(err);
+    pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
+    pc.flags = flags;
+    dnn::launch_fused_train_persist_f32(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
+                                        P<const float>(master), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
+                                        P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss),
+                                        P<int32_t>(correct), g_pending_pipe, pc, S(stream), P<long long>(stamps));
+  }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"), py::arg("a0"),
+     py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"),
+     py::arg("correct"), py::arg("ctl"), py::arg("nsteps"), py::arg("bv0"), py::arg("bv1"), py::arg("nid0"),
+     py::arg("nid1"), py::arg("err"), py::arg("timeout_s"), py::arg("stream"), py::arg("flags") = 0,
+     py::arg("stamps") = 0);
+  m.def("persist_max_batch_f32", []() { return dnn::persist_max_batch_f32(); });
+  m.def("persist_resident_workgroups_f32", []() { return dnn::persist_resident_workgroups_f32(); });
+  m.def("persist_wg_f32", []() { return dnn::persist_wg_f32(); });
   m.def("persist_max_batch", []() { return dnn::persist_max_batch(); });
   m.def("persist_resident_workgroups", []() { return dnn::persist_resident_workgroups(); });
   m.def("persist_ctl_bytes", [](int batch) { return dnn::persist_ctl_bytes(batch); });

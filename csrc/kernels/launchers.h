@@ -132,6 +132,16 @@ void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const 
                             hipStream_t stream, long long* stamps = nullptr);
 void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, int base, int count,
                            const float* master, float* loss, int32_t* correct, hipStream_t stream);
+// its persistent launch (lenet_f32.hip PERS): pc.nsteps steps in one launch, the reduction
+// (red: whole arena, fused SGD, bookkeeping) in its first persist_wg_f32() workgroups; rows and
+// control block as launch_fused_train_persist's; red.batch_ids = step 0's sample ids
+void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                                    const float* master, float* a0, float* h1, float* h2, float* z1, float* z2,
+                                    float* z3, float* slab, float* loss, int32_t* correct, const ReduceArgs& red,
+                                    const PipeCtl& pc, hipStream_t stream, long long* stamps = nullptr);
+int persist_max_batch_f32();
+int persist_resident_workgroups_f32();
+int persist_wg_f32();
 
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();

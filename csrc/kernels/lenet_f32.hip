@@ -30,7 +30,7 @@
 //    it runs dense (k = the 100 unpooled pixels) on v_mfma_f32_16x16x4_f32 in 5 waves, beside the
 //    data gradient's VALU work in the other 11;
 //  * fixed summation orders everywhere (no atomics): bitwise reproducible run to run.
-#include "launchers.h"
+#include "pers_common.h"
 
 namespace dnn {
 namespace f32k {
@@ -119,19 +119,169 @@ __device__ __forceinline__ float masked(float v, bool keep) {
   return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
 }
 
-template <bool TRAIN>
-__global__ void __launch_bounds__(NT) lenet_f32_kernel(
-    const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ order,  // TRAIN: this step's sample ids [batch]
-    int order_len, int batch, int base_index, const int32_t* __restrict__ state,
-    const float* __restrict__ master,  // fp32 parameter arena
-    float* __restrict__ a0_out, float* __restrict__ h1_out, float* __restrict__ h2_out,
-    float* __restrict__ z1_out, float* __restrict__ z2_out, float* __restrict__ z3_out,
-    float* __restrict__ slab_out, float* __restrict__ loss_out, int32_t* __restrict__ correct_out,
-    long long* __restrict__ stamps) {  // diagnostic: block 0's phase timeline (s_memrealtime, 100 MHz)
+// ---- the persistent launch (PERS) ------------------------------------------------------------
+// The bf16 kernel's persistent launch (lenet_fused.hip PERS: one launch runs pc.nsteps steps,
+// reduction and sample workgroups hand off through generation-relative arrival / ready tags),
+// for the fp32 kernel's 1024-thread workgroups: a reduction workgroup runs FOUR 256-thread
+// reduction blocks.  Block map m = 4 wg + (thread >> 8): conv blocks [0, 45), the bookkeeping
+// block 45, two idle blocks (so the conv workgroups [0, PF_CONV_WG) wait for the conv arrival
+// only), then the MLP blocks.  Samples wait for every workgroup's ready word before a step (the
+// conv1 group finishes last anyway - the hand-off runs conv1 -> conv1) and load the weights with
+// sc1 loads of the fp32 master, which the reduction stores write-through (WtF32Sink).
+constexpr int PF_CONV_WG = (PIPE_CONV_BLOCKS + 1 + 3) / 4;     // conv + bookkeeping (+ idle) workgroups
+constexpr int PF_WG = PF_CONV_WG + (PIPE_MLP_BLOCKS + 3) / 4;  // reduction workgroups
+static_assert(PF_WG <= PERS_RROW, "one ready word per reduction workgroup in a sample's row");
+
+__device__ __forceinline__ void pf_arrive(const PipeCtl& pc, int kind, int b, unsigned tag, int lane) {
+  const int w0 = kind ? PF_CONV_WG : 0, nw = kind ? PF_WG - PF_CONV_WG : PF_CONV_WG;
+  if (lane < nw) st_tag(pc.arrive + (long)(w0 + lane) * PERS_AROW + b, tag);
+}
+
+// one wave waits until every reduction workgroup's word of this sample's ready row reached tgt
+// (bounded like pers_wait_rows: the sticky error word, never a hang)
+__device__ __forceinline__ void pf_wait_ready(const PipeCtl& pc, int b, unsigned tgt, int lane) {
+  if (ld_tag(pc.err) != 0u) return;
+  const unsigned* row = pc.flg + (long)b * PERS_RROW + min(lane, PF_WG - 1);
+  const long long t0 = wall_clock64();
+  while (true) {
+    if (__all(tag_ge(ld_tag(row), tgt))) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > pc.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+// Reduction workgroup wg: its four blocks, every step in order - wait for the rows (conv
+// workgroups: the conv arrival, which every sample stores after its MLP rows too), reduce + SGD
+// (write-through master), then this workgroup's word in every sample's ready row.
+// stamps (diagnostic, tools/phase_trace_f32.py --pers): the last step's rows seen / body done /
+// ready stored of workgroup wg at stamps[6144 + 4 wg + k]
+__device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), m = 4 * wg + q, rtid = threadIdx.x & 255,
+            lane = threadIdx.x & 63;
+  const bool bk = m == PIPE_CONV_BLOCKS;
+  int rblk = -1;  // (-1: idle)
+  if (m < PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + m;
+  else if (m >= 4 * PF_CONV_WG && m - 4 * PF_CONV_WG < PIPE_MLP_BLOCKS) rblk = m - 4 * PF_CONV_WG;
+  const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));
+  if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
+  const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
+  for (int t = 0; t < pc.nsteps; ++t) {
+    int tid_o = threadIdx.x;  // (opaque: the lane's address math stays inside the step)
+    asm volatile("" : "+v"(tid_o));
+    const int lane_o = tid_o & 63;
+    if (tid_o < 64) pers_wait_rows(pc, arr, a.batch, g0 + (unsigned)t + 1u, lane_o);
+    const bool st = stamps != nullptr && threadIdx.x == 0 && t == pc.nsteps - 1;
+    if (st) stamps[6144 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (bk) {
+      if (rtid < 64) bookkeeping_pers(a, pc, lane_o, t);
+    } else if (rblk >= 0) {
+      WtF32Sink sk;
+      grad_reduce_body<false, WtF32Sink, true>(a, sk, rblk, tid_o & 255, 0, false, t & 1);
+    }
+    if (st) stamps[6145 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+    __syncthreads();
+    if (st) stamps[6146 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (tid_o < 64)
+      for (int b = lane_o; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, g0 + (unsigned)t + 1u);
+  }
+  if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
+}
+
+// Parameter loads: plain, or (WT: the persistent launch) sc1 loads of the write-through master
+template <bool WT>
+struct MasterRd {
+  const float* ms;
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit MasterRd(const float* master) : ms(master) {
+    if constexpr (WT) r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(master), 0, ARENA * 4, 0x00020000);
+  }
+  __device__ __forceinline__ float f(int i) const {
+    if constexpr (WT)
+      return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(ms + i), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT));
+    else return ms[i];
+  }
+  __device__ __forceinline__ f4 v4(int i) const {  // 4 floats at element i (16-B aligned)
+    if constexpr (WT) return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, i * 4, 0, 16));
+    else return *reinterpret_cast<const f4*>(ms + i);
+  }
+};
+
+// The kernel's arguments (one block for both launch forms)
+struct F32Args {
+  const uint8_t* images;
+  const int32_t* labels;
+  const int32_t* order;  // TRAIN: this step's sample ids [batch] (PERS: the first step's)
+  int order_len, batch, base_index;
+  const int32_t* state;
+  const float* master;   // fp32 parameter arena
+  float *a0, *h1, *h2, *z1, *z2, *z3, *slab, *loss;  // per-sample rows (PERS: parity 0; parity 1 follows)
+  int32_t* correct;
+  long long* stamps;     // diagnostic: block 0's phase timeline (s_memrealtime, 100 MHz)
+};
+
+// ONE sample's step (workgroup = sample b).  PERS: step s of the persistent launch - sample is
+// this step's id (-1: none), ns_next receives the next step's (read before the conv arrival).
+template <bool TRAIN, bool PERS>
+__device__ __forceinline__ void f32_step(const F32Args& A, const PipeCtl& pc, int b, int sample, int s, unsigned g0,
+                                         int& ns_next) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
+  // (PERS: the lane's indices come from an opaque copy of threadIdx.x in every step, so their
+  // address math is not hoisted out of the step loop and kept live across it)
+  int tid_o = threadIdx.x;
+  if constexpr (PERS) asm volatile("" : "+v"(tid_o));
+  const int tid = tid_o, lane = tid & 63, wave = tid >> 6;
+  const int batch = A.batch;
+  const uint8_t* const images = A.images;
+  const int32_t* const labels = A.labels;
+  // (PERS: the phase stamps of the last step; per-step stamps of sample 0 at [2048 + k * 1024 + s]:
+  // k = 0 step start, 1 ready wait passed, 2 MLP arrival stored, 3 conv arrival stored)
+  long long* const stamps = PERS ? (s == pc.nsteps - 1 ? A.stamps : nullptr) : A.stamps;
+  const bool pstamp = PERS && A.stamps != nullptr && b == 0 && s < 1024;
+  auto pst = [&](int k, bool who) {
+    if (pstamp && who) A.stamps[2048 + 1024 * k + s] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  pst(0, tid == 0);
+  const MasterRd<PERS> mr(A.master);
+  // PERS: this step's rows are parity s & 1
+  const long rsh = PERS ? (long)(s & 1) * batch : 0;
+  float* const a0_out = A.a0 + rsh * A0_LD;
+  float* const h1_out = A.h1 + rsh * H1_LD;
+  float* const h2_out = A.h2 + rsh * H2_LD;
+  float* const z1_out = A.z1 + rsh * Z1_LD;
+  float* const z2_out = A.z2 + rsh * Z2_LD;
+  float* const z3_out = A.z3 + rsh * Z3_LD;
+  float* const slab_out = A.slab + rsh * SLAB;
+  float* const loss_out = A.loss + rsh;
+  int32_t* const correct_out = A.correct + rsh;
+  // a row element: plain, or (PERS) written through - the reduction of the same launch reads it
+  auto put_row = [&](float* p, float v) {
+    if constexpr (PERS) st_wt(p, v);
+    else *p = v;
+  };
+  // PERS: every wave drained its stores -> barrier -> one wave stores the arrival tags of this
+  // sample for the conv workgroups (kind 0; first the next step's sample id, read before the
+  // bookkeeping of this step can overwrite its slot) or the MLP workgroups (kind 1)
+  auto arrive = [&](int kind) {
+    if (kind == 0) {
+      ns_next = __builtin_amdgcn_readfirstlane(ld_sc1(pc.nid_slot[s & 1] + b));
+      // fault injection (flags & 256, tests only): sample 0 arrives for the conv workgroups of
+      // step 1 three wait timeouts late (lenet_fused.hip's)
+      if ((pc.flags & 256) && b == 0 && s == 1 && tid == 0) {
+        const long long t0 = wall_clock64();
+        while (wall_clock64() - t0 < 3 * pc.timeout_ticks) __builtin_amdgcn_s_sleep(64);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) pf_arrive(pc, kind, b, g0 + (unsigned)s + 1u, lane);
+    if (kind == 0) pst(3, tid == 0);
+  };
   const bool stamp = stamps != nullptr && b == 0 && tid == 0;
 #define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
   // (diagnostic: when lane t of block 0 finished its part of a concurrent phase)
@@ -148,29 +298,54 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     if (stamps != nullptr && b == 0 && lane == 0) stamps[(base) + wave] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
   STAMP(0);
-  int bvalid = 1, sample;
+  float* X = reinterpret_cast<float*>(smem + L_X);
+  // the image ingest: 16 pixels of row (c, y) = tid / 2, columns 16 (tid & 1) .. (tid < 192)
+  auto ingest = [&](int id) {
+    if (tid < 192) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (!PERS || id >= 0) v = reinterpret_cast<const uint4*>(images + (size_t)id * IMG)[tid];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const int row = tid >> 1, c = row >> 5, y = row & 31;
+      float* dst = X + c * X_CH + y * X_RS + 16 * (tid & 1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        reinterpret_cast<f2*>(dst)[k] = f2{u8norm((w[k >> 1] >> (16 * (k & 1))) & 0xffu),
+                                           u8norm((w[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu)};
+    }
+  };
+  int bvalid = 1;
   bool valid;
-  if (TRAIN) {
-    bvalid = state[ST_BVALID];
+  if constexpr (PERS) {
+    // the image first (its sample id was published two steps ahead: no wait needed) - it lands
+    // in LDS while wave 0 waits for the previous step's reduction (from step 1 on); then this
+    // step's valid count from its bookkeeping slot (published with the ready words)
+    ingest(sample);
+    if (s > 0 && wave == 0) pf_wait_ready(pc, b, g0 + (unsigned)s, lane);
+    lds_barrier();
+    pst(1, tid == 0);
+    bvalid = __builtin_amdgcn_readfirstlane(ld_sc1(pc.bv_slot[s & 1]));
     valid = b < bvalid;
-    sample = order[b];
+  } else if (TRAIN) {
+    bvalid = A.state[ST_BVALID];
+    valid = b < bvalid;
   } else {
-    const long g = (long)base_index + b;
-    valid = g < order_len;
-    sample = (int)g;
+    valid = (long)A.base_index + b < A.order_len;
   }
   if (!valid) {  // tail of the last batch: zero rows, the reduction adds nothing
     if (TRAIN) {
-      for (int i = tid; i < A0_LD; i += NT) a0_out[(size_t)b * A0_LD + i] = 0.f;
-      if (tid < H1_LD) { h1_out[(size_t)b * H1_LD + tid] = 0.f; z1_out[(size_t)b * Z1_LD + tid] = 0.f; }
-      if (tid < H2_LD) { h2_out[(size_t)b * H2_LD + tid] = 0.f; z2_out[(size_t)b * Z2_LD + tid] = 0.f; }
-      if (tid < Z3_LD) z3_out[(size_t)b * Z3_LD + tid] = 0.f;
-      for (int i = tid; i < SLAB; i += NT) slab_out[(size_t)b * SLAB + i] = 0.f;
-      if (tid == 0) { loss_out[b] = 0.f; correct_out[b] = 0; }
+      for (int i = tid; i < A0_LD; i += NT) put_row(a0_out + (size_t)b * A0_LD + i, 0.f);
+      if (tid < H1_LD) { put_row(h1_out + (size_t)b * H1_LD + tid, 0.f); put_row(z1_out + (size_t)b * Z1_LD + tid, 0.f); }
+      if (tid < H2_LD) { put_row(h2_out + (size_t)b * H2_LD + tid, 0.f); put_row(z2_out + (size_t)b * Z2_LD + tid, 0.f); }
+      if (tid < Z3_LD) put_row(z3_out + (size_t)b * Z3_LD + tid, 0.f);
+      for (int i = tid; i < SLAB; i += NT) put_row(slab_out + (size_t)b * SLAB + i, 0.f);
+      if (tid == 0) { put_row(loss_out + b, 0.f); put_row(reinterpret_cast<float*>(correct_out + b), 0.f); }
+    }
+    if constexpr (PERS) {
+      arrive(1);
+      arrive(0);
     }
     return;
   }
-  float* X = reinterpret_cast<float*>(smem + L_X);
   float* WT1 = reinterpret_cast<float*>(smem + L_WT1);
   float* WT2 = reinterpret_cast<float*>(smem + L_WT2);
   float* WD = reinterpret_cast<float*>(smem + L_WD);
@@ -197,21 +372,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 
   // ============ phase A: ingest + weight staging ========================================
   {
-    const uint8_t* img = images + (size_t)sample * IMG;
-    if (tid < 192) {  // 16 pixels of row (c, y) = tid / 2, columns 16 (tid & 1) ..
-      const uint4 v = reinterpret_cast<const uint4*>(img)[tid];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      const int row = tid >> 1, c = row >> 5, y = row & 31;
-      float* dst = X + c * X_CH + y * X_RS + 16 * (tid & 1);
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        reinterpret_cast<f2*>(dst)[k] = f2{u8norm((w[k >> 1] >> (16 * (k & 1))) & 0xffu),
-                                           u8norm((w[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu)};
-    }
+    if constexpr (!PERS) ingest(sample);  // (PERS: above, before the wait)
     for (int i = tid; i < 450; i += NT) {
       const int o = i / 75, k = i - 75 * o, c = k / 25;
       const int t = k - 25 * c, ky = t / 5;
-      WT1[((o >> 1) * 3 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = master[OFF_C1W + i];
+      WT1[((o >> 1) * 3 + c) * WP_C + ky * WP_R + 2 * (t - 5 * ky) + (o & 1)] = mr.f(OFF_C1W + i);
     }
     if (tid < 236) {
       int src;
@@ -220,7 +385,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       else if (tid < B_F2) src = OFF_F1B + tid - B_F1;
       else if (tid < B_F3) src = OFF_F2B + tid - B_F2;
       else src = OFF_F3B + tid - B_F3;
-      BIAS[tid] = master[src];
+      BIAS[tid] = mr.f(src);
     }
   }
   // the weights conv1 does not need are loaded into registers now and stored to LDS after the
@@ -228,12 +393,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   f4 lf2[3], lf3;
   float lw2[3];
   {
-    const f4* f2src = reinterpret_cast<const f4*>(master + OFF_F2W);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) lf2[k] = f2src[min(tid + NT * k, 2519)];
-    lf3 = reinterpret_cast<const f4*>(master + OFF_F3W)[min(tid, 209)];
+    for (int k = 0; k < 3; ++k) lf2[k] = mr.v4(OFF_F2W + 4 * min(tid + NT * k, 2519));
+    lf3 = mr.v4(OFF_F3W + 4 * min(tid, 209));
 #pragma unroll
-    for (int k = 0; k < 3; ++k) lw2[k] = master[OFF_C2W + min(tid + NT * k, 2399)];
+    for (int k = 0; k < 3; ++k) lw2[k] = mr.f(OFF_C2W + min(tid + NT * k, 2399));
   }
   lds_barrier();
   STAMP(1);
@@ -301,6 +465,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     }
   }
   if (tid < 210) reinterpret_cast<f4*>(F3)[tid] = lf3;
+  if constexpr (PERS) {  // (PERS: the fc2 weights go in now - their 12 registers would spill under conv2)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (tid + NT * k < 2520) reinterpret_cast<f4*>(F2)[tid + NT * k] = lf2[k];
+  }
   lds_barrier();
   STAMP(2);
 
@@ -312,9 +481,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   // (the first 64 columns of the rows now, the remaining 36 after the conv2 products: register
   // budget)
   f4 r0[8], r1[8];
-  const f4* w1 = reinterpret_cast<const f4*>(master + OFF_F1W);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r0[j] = w1[min(wave + 16 * j, 119) * 100 + lane];
+  for (int j = 0; j < 8; ++j) r0[j] = mr.v4(OFF_F1W + 4 * (min(wave + 16 * j, 119) * 100 + lane));
   f2 cacc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
   // task c_r = (window c_w, channel pair c_pp), pair-minor: a 32-lane read group covers 4
   // windows x 8 pairs, so its 8-B image reads are 4 broadcast addresses and its 16-B weight reads
@@ -364,7 +532,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   // (their patch and weight registers are dead; waves 7-15 have no conv2 work and issue them
   // at once), so they land under the epilogue instead of at the start of phase D
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r1[j] = w1[min(wave + 16 * j, 119) * 100 + 64 + min(lane, 35)];
+  for (int j = 0; j < 8; ++j) r1[j] = mr.v4(OFF_F1W + 4 * (min(wave + 16 * j, 119) * 100 + 64 + min(lane, 35)));
   lds_barrier();
   STAMP(3);
   if (tid < 200) {
@@ -420,9 +588,11 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   }
   // fc1 waits on L2 and leaves the LDS idle: the fc2 weights (in registers since phase A)
   // and the zero padding of dY2 go in now
+  if constexpr (!PERS) {
 #pragma unroll
-  for (int k = 0; k < 3; ++k)
-    if (tid + NT * k < 2520) reinterpret_cast<f4*>(F2)[tid + NT * k] = lf2[k];
+    for (int k = 0; k < 3; ++k)
+      if (tid + NT * k < 2520) reinterpret_cast<f4*>(F2)[tid + NT * k] = lf2[k];
+  }
   if (TRAIN)
     for (int i = tid; i < 16 * DY2_CH; i += NT) DY2[i] = 0.f;  // dY2 padding (phase E fills the argmaxes)
   lds_barrier();
@@ -459,8 +629,8 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     const float lse = mx + logf(sum);
     const float ll = __shfl(lg, label & 15, 16);
     if (lane == 0) {
-      loss_out[b] = lse - ll;
-      correct_out[b] = pred == label ? 1 : 0;
+      put_row(loss_out + b, lse - ll);
+      put_row(reinterpret_cast<float*>(correct_out + b), __int_as_float(pred == label ? 1 : 0));
     }
     if (TRAIN && lane < 16) DZ3[lane] = act ? (e / sum - (lane == label ? 1.f : 0.f)) / (float)bvalid : 0.f;
   } else if (TRAIN && wave <= 6) {
@@ -483,7 +653,9 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       }
       base += __popcll(m);
     }
-    if (lane < 2 * W1_PARTS) T1[c * T1_LD + base + lane] = f2{0.f, 0.f};  // slices round up: zero pad
+    float zf = 0.f;  // (PERS: an opaque zero - a hoisted 64-bit zero constant spilled across the step loop)
+    if constexpr (PERS) asm volatile("" : "+v"(zf));
+    if (lane < 2 * W1_PARTS) T1[c * T1_LD + base + lane] = f2{zf, zf};  // slices round up: zero pad
     if (lane == 0) NACT[c] = base;
   } else if (TRAIN && wave <= 14) {
     // and the conv2 table: channels o = 2 (wave - 7) + (lane >= 32), one per half wave
@@ -543,7 +715,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 #pragma unroll
     for (int w = 1; w < 16; ++w) d += PART[w * 400 + tid];
     DA0[tid] = d;
-    a0_out[(size_t)b * A0_LD + tid] = A0[tid];
+    put_row(a0_out + (size_t)b * A0_LD + tid, A0[tid]);
     // pool2 / ReLU2 backward: dY2 at the argmax pixel (zero-padded copy for the data gradient)
     // and the value of the window's entry in the conv2 weight-gradient table
     const int o = tid / 25, w = tid - 25 * o, wy = w / 5, wx = w - 5 * wy;
@@ -553,15 +725,23 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       reinterpret_cast<float*>(T2 + o * 25 + PS2[tid])[0] = d;
     }
   } else if (tid < 520) {
-    h1_out[(size_t)b * H1_LD + tid - 400] = H1[tid - 400];
-    z1_out[(size_t)b * Z1_LD + tid - 400] = DZ1[tid - 400];
+    put_row(h1_out + (size_t)b * H1_LD + tid - 400, H1[tid - 400]);
+    put_row(z1_out + (size_t)b * Z1_LD + tid - 400, DZ1[tid - 400]);
   } else if (tid < 604) {
-    h2_out[(size_t)b * H2_LD + tid - 520] = H2[tid - 520];
-    z2_out[(size_t)b * Z2_LD + tid - 520] = DZ2[tid - 520];
+    put_row(h2_out + (size_t)b * H2_LD + tid - 520, H2[tid - 520]);
+    put_row(z2_out + (size_t)b * Z2_LD + tid - 520, DZ2[tid - 520]);
   } else if (tid < 620) {
-    z3_out[(size_t)b * Z3_LD + tid - 604] = DZ3[tid - 604];
+    put_row(z3_out + (size_t)b * Z3_LD + tid - 604, DZ3[tid - 604]);
   }
+  // PERS: the MLP rows (and loss / correct) drained before this barrier, then wave 11 (its
+  // phase-E work is the shortest) stores the arrival for the MLP workgroups - their reduction
+  // overlaps the conv backward
+  if constexpr (PERS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
+  if constexpr (PERS) {
+    if (wave == 11) pf_arrive(pc, 1, b, g0 + (unsigned)s + 1u, lane);
+    pst(2, tid == 704);
+  }
   STAMP(11);
 
   // ============ phase E: conv2 backward ===================================================
@@ -671,7 +851,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       const int n = 32 * wv + 16 * t + col;
       if (n < 150) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) slab[SLAB_C2W + (4 * q + r) * 150 + n] = t ? acc1[r] : acc0[r];
+        for (int r = 0; r < 4; ++r) put_row(slab + SLAB_C2W + (4 * q + r) * 150 + n, t ? acc1[r] : acc0[r]);
       }
     }
   }
@@ -683,7 +863,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
       const int n = NACT[6 + o];
 #pragma unroll
       for (int w = 0; w < 25; ++w) sb += masked(T2[o * 25 + w].x, w < n);  // fixed trip: reads in flight
-      slab[SLAB_C2B + o] = sb;
+      put_row(slab + SLAB_C2B + o, sb);
     }
     if (tid < 704) {  // the re-strided image copy for the conv1 weight gradient: 3072 pixels over 704 lanes
       float* XW = reinterpret_cast<float*>(smem + L_F2);
@@ -754,7 +934,7 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
     f4 t = pp[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) t += pp[i];
-    slab[SLAB_C1B + c] = (t.x + t.y) + (t.z + t.w);
+    put_row(slab + SLAB_C1B + c, (t.x + t.y) + (t.z + t.w));
     LANE_STAMP(19, 992);
   }
   const float* XW = reinterpret_cast<const float*>(smem + L_F2);
@@ -785,18 +965,46 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
   lds_barrier();
   STAMP(14);
   if (tid < 450) {
-    float s = PART[tid];
+    float sum = PART[tid];
 #pragma unroll
-    for (int p = 1; p < W1_PARTS; ++p) s += PART[p * 450 + tid];
-    slab[SLAB_C1W + tid] = s;
+    for (int p = 1; p < W1_PARTS; ++p) sum += PART[p * 450 + tid];
+    put_row(slab + SLAB_C1W + tid, sum);
   }
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);
     STAMP(15);
   }
+  if constexpr (PERS) arrive(0);  // slab drained: the conv workgroups go
 #undef STAMP
 #undef LANE_STAMP
 #undef WAVE_STAMP
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(NT) lenet_f32_kernel(const F32Args A) {
+  const int b = blockIdx.x;
+  int sample, unused = 0;
+  if constexpr (TRAIN) sample = A.order[b];
+  else sample = A.base_index + b;
+  f32_step<TRAIN, false>(A, PipeCtl{}, b, sample, 0, 0u, unused);
+}
+
+// The persistent launch: PF_WG reduction workgroups, then one workgroup per sample, every one
+// looping over pc.nsteps steps (lenet_fused.hip PERS's protocol; the rows alternate parities)
+__global__ void __launch_bounds__(NT) lenet_f32_pers_kernel(const F32Args A, const ReduceArgs ra, const PipeCtl pc) {
+  if ((int)blockIdx.x < PF_WG) {
+    pers_reduce_f32(ra, pc, blockIdx.x, A.stamps);
+    return;
+  }
+  const int b = (int)blockIdx.x - PF_WG;
+  const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));
+  int sample = __builtin_amdgcn_readfirstlane(A.order[b]);  // step 0's (the published batch ids)
+  for (int s = 0; s < pc.nsteps; ++s) {
+    int next = -1;
+    f32_step<true, true>(A, pc, b, sample, s, g0, next);
+    sample = next;
+  }
+  if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
 }
 
 }  // namespace f32k
@@ -804,10 +1012,10 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(
 void init_kernels_f32() {
   static bool done = false;
   if (done) return;
-  HIP_CHECK(hipFuncSetAttribute((const void*)f32k::lenet_f32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                f32k::LDS_TOTAL));
-  HIP_CHECK(hipFuncSetAttribute((const void*)f32k::lenet_f32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                f32k::LDS_TOTAL));
+  const void* kerns[] = {(const void*)f32k::lenet_f32_kernel<true>, (const void*)f32k::lenet_f32_kernel<false>,
+                         (const void*)f32k::lenet_f32_pers_kernel};
+  for (const void* k : kerns)
+    HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, f32k::LDS_TOTAL));
   done = true;
 }
 
@@ -816,8 +1024,9 @@ void launch_fused_train_f32(const uint8_t* images, const int32_t* labels, const 
                             float* z1, float* z2, float* z3, float* slab, float* loss, int32_t* correct,
                             hipStream_t stream, long long* stamps) {
   init_kernels_f32();
-  hipLaunchKernelGGL(f32k::lenet_f32_kernel<true>, dim3(batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images, labels,
-                     order, order_len, batch, 0, state, master, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps);
+  const f32k::F32Args A{images, labels, order, order_len, batch, 0, state, master, a0, h1, h2, z1, z2, z3, slab,
+                        loss, correct, stamps};
+  hipLaunchKernelGGL(f32k::lenet_f32_kernel<true>, dim3(batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, A);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -825,9 +1034,63 @@ void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, 
                            const float* master, float* loss, int32_t* correct, hipStream_t stream) {
   init_kernels_f32();
   if (count <= 0) return;
-  hipLaunchKernelGGL(f32k::lenet_f32_kernel<false>, dim3(count), dim3(f32k::NT), f32k::LDS_TOTAL, stream, images,
-                     labels, nullptr, n, count, base, nullptr, master, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, loss, correct, nullptr);
+  const f32k::F32Args A{images, labels, nullptr, n, count, base, nullptr, master, nullptr, nullptr, nullptr,
+                        nullptr, nullptr, nullptr, nullptr, loss, correct, nullptr};
+  hipLaunchKernelGGL(f32k::lenet_f32_kernel<false>, dim3(count), dim3(f32k::NT), f32k::LDS_TOTAL, stream, A);
+  HIP_CHECK(hipGetLastError());
+}
+
+// The fp32 persistent grid's co-residency (lenet_fused.hip persist_resident_workgroups' rule, for
+// this kernel: one 1024-thread workgroup per CU) and the largest batch that keeps PERS_MARGIN_F32
+// CUs free next to it.
+constexpr int PERS_MARGIN_F32 = 8;
+int persist_resident_workgroups_f32() {
+  static int resident = -1;
+  if (resident < 0) {
+    init_kernels_f32();
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(f32k::lenet_f32_pers_kernel), f32k::NT, f32k::LDS_TOTAL));
+    resident = per_cu * cus;
+  }
+  return resident;
+}
+int persist_wg_f32() { return f32k::PF_WG; }
+int persist_max_batch_f32() {
+  return std::max(0, std::min(persist_resident_workgroups_f32() - f32k::PF_WG - PERS_MARGIN_F32, PERS_AROW));
+}
+
+void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                                    const float* master, float* a0, float* h1, float* h2, float* z1, float* z2,
+                                    float* z3, float* slab, float* loss, int32_t* correct, const ReduceArgs& red,
+                                    const PipeCtl& pc_in, hipStream_t stream, long long* stamps) {
+  init_kernels_f32();
+  // the shapes the kernel assumes (checked here: a mismatch would fault or hang on the device)
+  if (batch < 1 || batch > persist_max_batch_f32() || f32k::PF_WG + batch > PERS_MAX_GRID)
+    throw std::runtime_error("fused_train_persist_f32: batch must be 1.." + std::to_string(persist_max_batch_f32()) +
+                             " (the whole grid co-resident)");
+  if (pc_in.nsteps < 1 || pc_in.nsteps > (1 << 20))
+    throw std::runtime_error("fused_train_persist_f32: nsteps out of range");
+  if (pc_in.ctr == nullptr || pc_in.err == nullptr || !pc_in.bv_slot[0] || !pc_in.bv_slot[1] || !pc_in.nid_slot[0] ||
+      !pc_in.nid_slot[1])
+    throw std::runtime_error("fused_train_persist_f32: needs the control block, the error word and both slots");
+  if (!red.bookkeeping || red.batch != batch || red.rg != nullptr || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA ||
+      red.xp_nranks != 0 || red.batch_ids == nullptr || red.master != master)
+    throw std::runtime_error("fused_train_persist_f32: a local whole-arena fused-SGD reduction with bookkeeping");
+  if (red.a0 != a0 || red.h1 != h1 || red.h2 != h2 || red.z1 != z1 || red.z2 != z2 || red.z3 != z3 ||
+      red.slab != slab || red.loss != loss || red.correct != correct)
+    throw std::runtime_error("fused_train_persist_f32: the reduction reads the rows the samples write");
+  PipeCtl pc = pc_in;  // control block layout (one uncached allocation of persist_ctl_bytes)
+  unsigned char* base = reinterpret_cast<unsigned char*>(pc_in.ctr);
+  pc.gen = reinterpret_cast<unsigned*>(base);
+  pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
+  pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
+  const f32k::F32Args A{images, labels, red.batch_ids, order_len, batch, 0, nullptr, master, a0, h1, h2, z1, z2, z3,
+                        slab, loss, correct, stamps};
+  hipLaunchKernelGGL(f32k::lenet_f32_pers_kernel, dim3(f32k::PF_WG + batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream,
+                     A, red, pc);
   HIP_CHECK(hipGetLastError());
 }
 

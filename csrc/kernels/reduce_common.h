@@ -102,6 +102,26 @@ struct DirectSinkT {
 using DirectSink = DirectSinkT<false>;
 using WtSink = DirectSinkT<true>;
 
+// The fp32 engine's persistent launch (lenet_f32.hip PERS): its samples read EVERY weight from
+// the fp32 master, so every new parameter is stored write-through there; the momentum and the
+// bf16 shadow are read by later launches only (plain).  No tile path: the fc tiles finish per
+// element, with DirectSink's arithmetic (bit-identical to the serial fp32 step).
+struct WtF32Sink {
+  static constexpr bool kTile = false;
+  static constexpr bool kTileInfo = false;
+  __device__ __forceinline__ void put(int, int e, float g, float p_old, float m_old, const ReduceArgs& a) {
+    g *= a.grad_scale;
+    float p, m;
+    sgd_update(g, p_old, m_old, a.lr, a.momentum, p, m);
+    a.mom[e] = m;
+    st_wt(a.master + e, p);
+    write_shadow(a.shadow, e, p);
+  }
+  template <int LAYER>
+  __device__ __forceinline__ void put_tile(const f32x4&, const float (&)[4], const float (&)[4], const int (&)[4], int,
+                                           int, int, const ReduceArgs&) {}
+};
+
 // lane u of a quad reads lane (u + R) & 3's value
 template <int R>
 __device__ __forceinline__ unsigned qrot(unsigned v) {
@@ -318,7 +338,10 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
     z += (long)rp * a.batch * L::ZLD;
     x += (long)rp * a.batch * L::XLD;
   }
-  const int lane = threadIdx.x & 63;
+  int lane = threadIdx.x & 63;
+  // (SC: the persistent launches call this once per step - an opaque lane keeps its per-lane
+  // offsets inside the step instead of hoisted out of the step loop and held across it)
+  if constexpr (SC) asm volatile("" : "+v"(lane));
   const int col = lane & 15, kq = lane >> 4;
   const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
   const int om = o0 + col, in = i0 + col;

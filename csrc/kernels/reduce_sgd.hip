@@ -84,9 +84,10 @@ __global__ void __launch_bounds__(RT) epoch_begin_kernel(const int32_t* __restri
         if (k == 0) reinterpret_cast<int32_t*>(stage + (size_t)batch * IMG)[b] = labels[s];
       }
     }
+  }
+  if (next_ids != nullptr)  // (the staged step, and the fp32 persistent launch: step 1's ids)
     for (int b = blockIdx.x * RT + threadIdx.x; b < batch; b += gridDim.x * RT)
       next_ids[b] = batch + b < n ? staged[batch + b] : -1;
-  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     state[ST_CURSOR] = 0;
     state[ST_BVALID] = min(batch, n);

@@ -178,7 +178,8 @@ class StepAllReduce(SyncPolicy):
             mode = xgmi.exchange_mode() | (4 if self.grad_comm == "bf16" else 0)
             # the persistent form where the engine has one (fp32 granules; falls back to the
             # serial one-launch exchange if its self-test fails)
-            pers = "-pers" if mode in (0, 2) and getattr(engine, "persist", False) else ""
+            pers = ("-pers" if mode in (0, 2) and getattr(engine, "persist", False) and getattr(engine, "pipeline", False)
+                    else "")  # (the bf16 persistent launch: the fp32 one has no in-launch exchange)
             return "xgmi-" + xgmi.MODE_NAMES[mode] + pers
         return "rccl" if self.comm.backend == "nccl" else "torch-pg"
 

@@ -294,6 +294,7 @@ class HipEngine(Engine):
         self.stage = torch.zeros(B * (3072 + 4), device=dev, dtype=torch.uint8) if stage_images else None
         self.next_ids = torch.full((B,), -1, device=dev, dtype=torch.int32)  # ids two steps ahead
         self._staged = False  # stage holds this epoch's step-0 batch (set by begin_epoch)
+        self._ahead = False  # (fp32 persistent) next_ids holds this epoch's step-1 ids (set by begin_epoch)
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
@@ -328,26 +329,8 @@ class HipEngine(Engine):
         self._rg: dict | None = None
         if dtype == "bf16":
             self._rg_buffers()  # (allocated up front: never inside a graph capture)
-        if self.pipeline:
-            # the second parity's per-sample rows (the first is a0 .. correct above) - each row
-            # kind as ONE [2][B][...] buffer, parity 1 right after parity 0 (the persistent
-            # launch addresses both from one pointer) -, the second {bvalid, next_ids}
-            # bookkeeping slot (bvalid in state[2]), the ready counters and flags and the sticky
-            # wait-timeout word
-            self._rows2 = {}
-            for k in ("a0", "h1", "h2", "z1", "z2", "z3", "slab", "loss", "correct"):
-                t = getattr(self, k)
-                both = torch.zeros((2,) + tuple(t.shape), device=dev, dtype=t.dtype)
-                setattr(self, k, both[0])
-                self._rows2[k] = both[1]
-            self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
-            # arrival counters [parity][group] and ready flags [parity][group][sample], a 128-B line
-            # each, in uncached memory: every poll reads memory (lenet_fused.hip pipe_wait)
-            ng = self.ext.pipe_groups()
-            self._pipe_ctr_ptr = self.ext.uncached_alloc(2 * ng * 128)
-            self._pipe_flg_ptr = self.ext.uncached_alloc(2 * ng * B * 128)
-            self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
-        # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step): a chunk of n steps
+        # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step - or, fp32,
+        # lenet_f32.hip PERS on its own: the fp32 kernel has no pipelined form): a chunk of n steps
         # is ONE launch - the reduction and sample workgroups loop over the steps and hand off
         # through in-launch arrival / ready flags, so no kernel boundary sits between two steps.
         # Its reduction and sample workgroups wait on each other, so the whole grid must be
@@ -359,10 +342,34 @@ class HipEngine(Engine):
         # ranks time-sharing this GPU (one-GPU rehearsals): every rank's grid must be resident at
         # once - ranks x (reduction + sample workgroups) within the occupancy-derived count
         share = ranks_per_gpu()
-        fits = B <= self.ext.persist_max_batch() and (
-            share == 1 or share * (self.ext.pipe_reduce_blocks() // 2 + 1 + B)
-            <= self.ext.persist_resident_workgroups() - 8)
-        self.persist = bool(persist) and self.pipeline and fits
+        if dtype == "fp32":
+            fits = B <= self.ext.persist_max_batch_f32() and (
+                share == 1 or share * (self.ext.persist_wg_f32() + B)
+                <= self.ext.persist_resident_workgroups_f32() - 8)
+        else:
+            fits = B <= self.ext.persist_max_batch() and (
+                share == 1 or share * (self.ext.pipe_reduce_blocks() // 2 + 1 + B)
+                <= self.ext.persist_resident_workgroups() - 8)
+        self.persist = bool(persist) and (self.pipeline or dtype == "fp32") and fits
+        if self.pipeline or self.persist:
+            # the second parity's per-sample rows (the first is a0 .. correct above) - each row
+            # kind as ONE [2][B][...] buffer, parity 1 right after parity 0 (the persistent
+            # launch addresses both from one pointer) -, the second {bvalid, next_ids}
+            # bookkeeping slot (bvalid in state[2]) and the sticky wait-timeout word
+            self._rows2 = {}
+            for k in ("a0", "h1", "h2", "z1", "z2", "z3", "slab", "loss", "correct"):
+                t = getattr(self, k)
+                both = torch.zeros((2,) + tuple(t.shape), device=dev, dtype=t.dtype)
+                setattr(self, k, both[0])
+                self._rows2[k] = both[1]
+            self.next_ids2 = torch.full((B,), -1, device=dev, dtype=torch.int32)
+            self.pipe_err = torch.zeros(1, device=dev, dtype=torch.int32)
+        if self.pipeline:
+            # arrival counters [parity][group] and ready flags [parity][group][sample], a 128-B line
+            # each, in uncached memory: every poll reads memory (lenet_fused.hip pipe_wait)
+            ng = self.ext.pipe_groups()
+            self._pipe_ctr_ptr = self.ext.uncached_alloc(2 * ng * 128)
+            self._pipe_flg_ptr = self.ext.uncached_alloc(2 * ng * B * 128)
         # the per-step xGMI all-reduce inside the persistent launch (installed by the
         # step-allreduce policy's "-pers" paths after their self-test; lenet_fused.hip XNR)
         self.pers_exchange = False
@@ -429,8 +436,15 @@ class HipEngine(Engine):
         if staged != self._staged:
             self.invalidate_graphs()  # the stage pointer is a baked kernel argument
         self._staged = staged
+        # the fp32 persistent launch reads the next step's ids from the bookkeeping slots (no stage)
+        ahead = self.dtype == "fp32" and self.persist and self.train is not None and n > 0
+        if ahead != self._ahead:
+            self.invalidate_graphs()  # next_ids is a baked reduction argument
+        self._ahead = ahead
         st = dict(images=self._p(self.train.images), labels=self._p(self.train.labels),
                   next_ids=self._p(self.next_ids), stage=self._p(self.stage)) if staged else {}
+        if ahead:
+            st = dict(next_ids=self._p(self.next_ids))
         with torch.cuda.device(self.device):
             self.ext.epoch_begin(self._p(self.staged), self._p(self.order), n, self._p(self.state),
                                  self._p(self.batch_ids), self.batch, main.cuda_stream, **st)
@@ -443,7 +457,7 @@ class HipEngine(Engine):
                              self._p(self.mom), self._p(self.shadow), self._p(self.state), self._p(self.stats),
                              self.lr, self.momentum, 1.0, fuse_sgd, lo, hi, bookkeeping, self._p(self.order),
                              self.order_len, self._p(self.batch_ids), s,
-                             next_ids=self._p(self.next_ids) if self._staged else 0, **xg)
+                             next_ids=self._p(self.next_ids) if self._staged or self._ahead else 0, **xg)
 
     RG_TIMEOUT_S = 10.0  # bound of one early-MLP row wait (then a sticky error word, raised at epoch_stats)
 
@@ -461,7 +475,7 @@ class HipEngine(Engine):
         return self._rg is not None and int(self._rg["err"].item()) != 0
 
     def pipe_failed(self) -> bool:
-        return self.pipeline and int(self.pipe_err.item()) != 0
+        return hasattr(self, "pipe_err") and int(self.pipe_err.item()) != 0
 
     def _pipe_ok(self) -> bool:
         """The pipelined step runs: bf16 with staged images, no all-reduce installed (one rank)
@@ -548,7 +562,10 @@ class HipEngine(Engine):
 
     def _pers_ok(self) -> bool:
         """The persistent launch runs: the pipelined step's conditions and persist - or, with a
-        per-step all-reduce, its "-pers" form (the exchange inside the launch's reduction)."""
+        per-step all-reduce, its "-pers" form (the exchange inside the launch's reduction).
+        fp32: lenet_f32.hip's persistent launch, local steps only."""
+        if self.dtype == "fp32":
+            return self.persist and self._ahead and self.grad_sync is None
         if not (self.persist and self.pipeline and self._staged and not self.early_mlp):
             return False
         return self.grad_sync is None or self._pers_xchg() is not None
@@ -579,6 +596,21 @@ class HipEngine(Engine):
         s = self._stream()
         sp = self._p(self.state)
         r = self._rows(0)
+        if self.dtype == "fp32":
+            self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
+                                 self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
+                                 self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
+                                 self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
+                                 self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
+                                 self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids))
+            self.ext.fused_train_persist_f32(self._p(self.train.images), self._p(self.train.labels), self.order_len,
+                                             self.batch, self._p(self.master), self._p(r["a0"]), self._p(r["h1"]),
+                                             self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]), self._p(r["z3"]),
+                                             self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
+                                             self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
+                                             self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
+                                             flags=self.pipe_flags, stamps=self._pipe_stamps)
+            return
         grp = self._pers_xchg()
         xg = grp.exchange() if grp is not None else {}
         self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
@@ -892,7 +924,7 @@ class HipEngine(Engine):
                         poll()
                     self._launch_step()
             return
-        if self._pers_ok() and self.pers_direct:
+        if self._pers_ok() and self.pers_direct and self.dtype == "bf16":
             # the persistent launch is ONE kernel whatever n is: no graph - the extension keeps its
             # argument block and relaunches it (one pybind call, ~3-4 us of host submit against
             # ~8 us for a graph replay; tools/window_host_probe.py, profiles/r4/pers_handoff)
@@ -933,7 +965,8 @@ class HipEngine(Engine):
         to: the caller re-raises)."""
         if self.persist:
             self.persist = False
-            level = "pipelined" if self.grad_sync is None else "serial (one-launch exchange)"
+            level = ("pipelined" if self.grad_sync is None and self.pipeline
+                     else "serial (one-launch exchange)" if self.grad_sync is not None else "serial")
         elif self.pipeline:
             self.pipeline = False
             level = "serial"

@@ -19,22 +19,24 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(tmp_path, name, env_extra):
+def _train(tmp_path, name, env_extra, dtype="bf16"):
     d = tmp_path / name
     d.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "2",
                         "--batch-size", "64", "--train-samples", "1024", "--test-samples", "256", "--lr", "0.01",
-                        "--seed", "3", "--save", "ck.pt", "--device", "cuda"], cwd=d, env=env, capture_output=True,
-                       text=True, timeout=300)
+                        "--seed", "3", "--save", "ck.pt", "--device", "cuda", "--dtype", dtype], cwd=d, env=env,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return torch.load(d / "ck.pt", weights_only=True), r
 
 
-def test_forced_persistent_timeout_steps_down_and_matches_serial(tmp_path):
-    sd, r = _train(tmp_path, "forced", {"DNN_PIPE_FLAGS": "256", "DNN_PIPE_TIMEOUT_S": "0.002"})
-    assert "stepping down to the pipelined step" in r.stdout, r.stdout[-3000:]
+@pytest.mark.parametrize("dtype,level", [("bf16", "pipelined"), ("fp32", "serial")])
+def test_forced_persistent_timeout_steps_down_and_matches_serial(tmp_path, dtype, level):
+    # (fp32: lenet_f32.hip's persistent launch, same injected delay; it steps down to the serial step)
+    sd, r = _train(tmp_path, "forced", {"DNN_PIPE_FLAGS": "256", "DNN_PIPE_TIMEOUT_S": "0.002"}, dtype)
+    assert f"stepping down to the {level} step" in r.stdout, r.stdout[-3000:]
     assert r.stdout.count("Validation loss of updated master model:") == 2
-    ref, _ = _train(tmp_path, "serial", {"DNN_PERSIST": "0", "DNN_PIPELINE": "0"})
+    ref, _ = _train(tmp_path, "serial", {"DNN_PERSIST": "0", "DNN_PIPELINE": "0"}, dtype)
     for k in ref:
         assert torch.equal(sd[k], ref[k]), k

@@ -238,6 +238,41 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
         assert all(x.samples == 1000 and x.batches == 16 for x in st1), f"variant {var}: sample counts"
 
 
+@pytest.mark.parametrize("graphs,chunk", [(True, 8), (True, 1), (False, 4), (True, 64)])
+def test_fp32_persistent_matches_serial_step(graphs, chunk):
+    """The fp32 kernel's persistent launch (lenet_f32.hip PERS: 4 reduction blocks per 1024-thread
+    workgroup, write-through fp32 master, sc1 weight loads, rows of two parities) gives the serial
+    fp32 step's parameters, momentum, bf16 images and epoch statistics BIT FOR BIT - shuffled
+    epochs with a tail batch, a step past an epoch's end, chunk graphs of 1 / 8 / 64 steps and
+    eager launches - and no wait times out."""
+    data = synthetic(1000, 11)  # 15 full batches + a tail of 40
+    a = init_arena(seed=5)
+    rng = np.random.default_rng(3)
+    orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
+    res = []
+    for pers in (False, True):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, dtype="fp32", persist=pers)
+        assert eng.persist == pers
+        eng.attach(data)
+        stats = []
+        for ep, order in enumerate(orders):
+            eng.begin_epoch(order)
+            if ep == 0:
+                assert eng._pers_ok() == pers
+            eng.run_steps(5)
+            eng.run_steps(12 if ep != 1 else 13)
+            stats.append(eng.epoch_stats())
+        torch.cuda.synchronize()
+        assert not eng.pipe_failed(), f"persist={pers}: a wait timed out"
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
+    (m0, mo0, sh0, st0), (m1, mo1, sh1, st1) = res
+    assert torch.equal(m0, m1), f"master differs at {int((m0 != m1).sum())} elements"
+    assert torch.equal(mo0, mo1) and torch.equal(sh0, sh1), "momentum / images differ"
+    assert [(x.loss_sum, x.samples, x.correct, x.batches) for x in st0] == \
+        [(x.loss_sum, x.samples, x.correct, x.batches) for x in st1], "statistics differ"
+    assert all(x.samples == 1000 and x.batches == 16 for x in st1)
+
+
 def test_pipelined_long_run_under_load():
     """600 pipelined steps next to a second stream of GPU work (uneven load on the CUs the
     hand-off crosses) against the serial step, bit for bit."""
@@ -245,8 +280,10 @@ def test_pipelined_long_run_under_load():
     a = init_arena(seed=6)
     order = np.random.default_rng(4).permutation(4096).astype(np.int32)
     res = []
-    for pipe, pers in ((False, False), (True, False), (True, True)):
-        eng = HipEngine(batch=64, arena=a, graph_chunk=32, pipeline=pipe, persist=pers)
+    for pipe, pers, dt in ((False, False, "bf16"), (True, False, "bf16"), (True, True, "bf16"), (False, False, "fp32"),
+                           (False, True, "fp32")):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=32, pipeline=pipe, persist=pers, dtype=dt)
+        assert eng.persist == pers
         eng.attach(data)
         side = torch.cuda.Stream()
         x = torch.randn(2048, 2048, device="cuda")
@@ -257,11 +294,12 @@ def test_pipelined_long_run_under_load():
                     x = torch.tanh(x @ x * 1e-3)
             eng.run_steps(60)
         torch.cuda.synchronize()
-        assert not (pipe and eng.pipe_failed())
+        assert not eng.pipe_failed()
         res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats()))
-    for r in res[1:]:
-        assert torch.equal(res[0][0], r[0]) and torch.equal(res[0][1], r[1])
-        assert res[0][2].loss_sum == r[2].loss_sum
+    for r in res[1:3] + res[4:]:  # (bf16 variants against bf16 serial, fp32 persistent against fp32 serial)
+        r0 = res[0] if r is not res[4] else res[3]
+        assert torch.equal(r0[0], r[0]) and torch.equal(r0[1], r[1])
+        assert r0[2].loss_sum == r[2].loss_sum
 
 
 def test_direct_relaunch_minimal_pair_regression(tmp_path):

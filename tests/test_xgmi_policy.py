@@ -54,6 +54,11 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
 
     class _PersEng(_Eng):
         persist = True
+        pipeline = True
+
+    class _PersF32Eng(_Eng):  # (the fp32 persistent launch has no in-launch exchange)
+        persist = True
+        pipeline = False
 
     pol = StepAllReduce.__new__(StepAllReduce)
     pol.comm, pol.bucket_kb = _Comm(), 0
@@ -62,6 +67,7 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
     assert pol.default_path(_Eng()) == "xgmi-pull"
     # an engine with the persistent launch gets the exchange inside it (fp32 granules only)
     assert pol.default_path(_PersEng()) == "xgmi-pull-pers"
+    assert pol.default_path(_PersF32Eng()) == "xgmi-pull"
     pol.grad_comm = "bf16"
     assert pol.default_path(_PersEng()) == "xgmi-pull-bf16"
     assert pol.default_path(_Eng()) == "xgmi-pull-bf16"
@@ -138,7 +144,7 @@ def test_pers_install_and_fallback(monkeypatch):
 
     class _Eng:
         overlap = False
-        persist = True
+        persist = pipeline = True
         grad = torch.zeros(62006)
 
         def __init__(self, ok):

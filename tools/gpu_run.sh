@@ -12,18 +12,19 @@
 #   envtests:VAR=val the whole GPU suite under one environment setting
 #   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
 #   k20f32           the same, --dtype fp32
+#   k20f32serial     the same with the fp32 persistent launch off (DNN_PERSIST=0)
 #   envk20:VAR=val   k20 with one environment setting
 #   winfit           bench --steps 10..160 with --diag-windows (wall vs event time per window)
 #   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
-#   long | long32    bench.py default window (5000 / 500), bf16 / fp32
+#   long | long32 | long32serial   bench.py default window (5000 / 500), bf16 / fp32 / fp32 without PERS
 #   b2k              bench.py 2000 / 200 steps, no epoch timing
 #   abdirect:N       N alternating 20/5 windows: graph replays vs direct relaunch (DNN_PERS_DIRECT=1)
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
 #   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
-#   phase | phase32 | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
+#   phase | phase32 | phase32pers | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   reprodirect      tools/repro_direct.py with DNN_PERS_DIRECT=1 (the round-4 direct-relaunch fault)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
@@ -65,6 +66,8 @@ for s in "$@"; do
           > "$O/winfit_${n}_k$k.json" 2> "$O/winfit_${n}_k$k.err"
       done ;;
     k20f32) timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
+    k20f32serial) DNN_PERSIST=0 timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" \
+                    2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
     abdirect:*)  # alternating 20/5 windows, graph replays vs direct relaunch, N rounds: abdirect:N
       for i in $(seq 1 "${s#abdirect:}"); do
@@ -74,6 +77,7 @@ for s in "$@"; do
       done ;;
     b2k) timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k.json" 2> "$O/b2k.err" ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
+    long32serial) DNN_PERSIST=0 timeout -k 10 300 python bench.py --dtype fp32 > "$O/$s.json" 2> "$O/$s.err" ;;
     prof|prof32|profserial|profpipe)
       dt=bf16; [ "$s" = prof32 ] && dt=fp32
       [ "$s" = profserial ] && export DNN_PIPELINE=0
@@ -109,6 +113,7 @@ for s in "$@"; do
       env "$kv" DNN_PIPELINE=1 timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch \
         > "$O/b2k_$n.json" 2> "$O/b2k_$n.err" ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
+    phase32pers) timeout -k 10 300 python tools/phase_trace_f32.py --pers > "$O/phase32pers.txt" 2>&1 ;;
     reprodirect) DNN_PERS_DIRECT=1 timeout -k 10 300 python -u tools/repro_direct.py > "$O/reprodirect.log" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;

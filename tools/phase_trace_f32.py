@@ -55,5 +55,65 @@ def main(reps: int = 50, batch: int = 64):
     print(f"{'kernel wall (event)':30s} {np.median(walls[5:]):8.2f} us")
 
 
+def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
+    """--pers: the fp32 persistent launch (lenet_f32.hip PERS): sample block 0's phases of the LAST
+    step of an n-step launch (relative to that step's start), its per-step hand-off stamps, the
+    reduction workgroups' last step, and the wall time per step for n = 8 and n = 64."""
+    tr = synthetic(8192, 0)
+    eng = HipEngine(batch=batch, seed=0, use_graphs=False, dtype="fp32", persist=True)
+    eng.attach(tr)
+    assert eng.persist, "persistent launch unavailable"
+    nwg = eng.ext.persist_wg_f32()
+    stamps = torch.zeros(8192, dtype=torch.int64, device=eng.device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    walls, rows, hand, red = {steps: [], 64: []}, [], [], []
+    for r in range(reps):
+        for n in (steps, 64):
+            eng.begin_epoch(np.roll(np.arange(8192, dtype=np.int32), -64 * (r % 60)))
+            eng._pipe_stamps = stamps.data_ptr() if n == steps else 0
+            stamps.zero_()
+            torch.cuda.synchronize()
+            ev0.record()
+            eng.run_steps(n)
+            ev1.record()
+            torch.cuda.synchronize()
+            walls[n].append(1e3 * ev0.elapsed_time(ev1))
+            if n != steps:
+                continue
+            st = stamps.cpu().numpy().astype(np.float64)
+            start = st[2048:2048 + steps]
+            rows.append(np.diff(st[:16]) * 0.01)
+            # per step s >= 1: wait (start -> ready passed), MLP / conv arrival after the start
+            hand.append(np.stack([(st[3072:3072 + steps] - start), (st[4096:4096 + steps] - start),
+                                  (st[5120:5120 + steps] - start), np.r_[np.diff(start), np.nan]]) * 0.01)
+            last = start[-1]
+            rw = st[6144:6144 + 4 * nwg].reshape(nwg, 4)
+            red.append(dict(seen=(rw[:, 0] - last) * 0.01, body=(rw[:, 1] - last) * 0.01,
+                            ready=(rw[:, 2] - last) * 0.01, arrive=(st[5120 + steps - 1] - last) * 0.01))
+    assert not eng.pipe_failed(), "a persistent-launch wait timed out"
+    med = np.median(np.array(rows[3:]), axis=0)
+    print("sample block 0, last step (us per phase):")
+    for name, v in zip(NAMES, med):
+        print(f"  {name:30s} {v:8.2f}")
+    h = np.nanmedian(np.array(hand[3:]), axis=0)  # [4][steps]
+    print("sample block 0 per step (us from the step's start; medians): ready passed / MLP arrival / "
+          "conv arrival / step length")
+    for s in range(steps):
+        print(f"  step {s}: " + " ".join(f"{h[k][s]:7.2f}" for k in range(4)))
+    m = lambda f: float(np.median([f(x) for x in red[3:]]))  # noqa: E731
+    print(f"last step's reduction (us from that step's start; sample 0 stored its conv arrival at "
+          f"{m(lambda x: x['arrive']):.2f}):")
+    for name, sl in (("conv WGs 0-11", slice(0, 12)), ("MLP WGs 12-", slice(12, nwg))):
+        print(f"  {name:14s} rows seen med/max {m(lambda x: np.median(x['seen'][sl])):.2f}/"
+              f"{m(lambda x: x['seen'][sl].max()):.2f}, body done {m(lambda x: np.median(x['body'][sl])):.2f}/"
+              f"{m(lambda x: x['body'][sl].max()):.2f}, ready stored {m(lambda x: np.median(x['ready'][sl])):.2f}/"
+              f"{m(lambda x: x['ready'][sl].max()):.2f}")
+    w8, w64 = np.median(walls[steps][3:]), np.median(walls[64][3:])
+    print(f"wall: {steps} steps {w8:.1f} us, 64 steps {w64:.1f} us -> steady step {(w64 - w8) / (64 - steps):.2f} us")
+
+
 if __name__ == "__main__":
-    main()
+    if "--pers" in sys.argv:
+        pers_main()
+    else:
+        main()
