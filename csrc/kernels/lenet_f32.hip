@@ -176,10 +176,10 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     const bool st = stamps != nullptr && threadIdx.x == 0 && t == pc.nsteps - 1;
     if (st) stamps[6144 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    WtF32Sink sk;
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane_o, t);
     } else if (rblk >= 0) {
-      WtF32Sink sk;
       grad_reduce_body<false, WtF32Sink, true>(a, sk, rblk, tid_o & 255, 0, false, t & 1);
     }
     if (st) stamps[6145 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -188,6 +188,7 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     if (st) stamps[6146 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     if (tid_o < 64)
       for (int b = lane_o; b < a.batch; b += 64) st_tag(pc.flg + (long)b * PERS_RROW + wg, g0 + (unsigned)t + 1u);
+    sk.flush(a);  // momentum + bf16 shadow: off the hand-off's critical path (drained by the next step's wait)
   }
   if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
 }

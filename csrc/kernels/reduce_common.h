@@ -81,6 +81,7 @@ template <bool WT>
 struct DirectSinkT {
   static constexpr bool kTile = WT;  // fc1 / fc2 tiles finish in put_tile (below)
   static constexpr bool kTileInfo = false;  // (XpSinkT<PK, true> records its fc tile: see there)
+  static constexpr bool kOpaqueLane = false;
   // WT, optional: put_tile's write-through stores wait until *gate >= gate_target (the pipelined
   // step's conv ready counter): the samples' poll of that counter then does not queue behind the
   // MLP tiles' write-through traffic (lenet_fused.hip PIPE flags & 32)
@@ -103,19 +104,32 @@ using DirectSink = DirectSinkT<false>;
 using WtSink = DirectSinkT<true>;
 
 // The fp32 engine's persistent launch (lenet_f32.hip PERS): its samples read EVERY weight from
-// the fp32 master, so every new parameter is stored write-through there; the momentum and the
-// bf16 shadow are read by later launches only (plain).  No tile path: the fc tiles finish per
-// element, with DirectSink's arithmetic (bit-identical to the serial fp32 step).
+// the fp32 master, so every new parameter is stored write-through there at once; the momentum and
+// the bf16 shadow are read by later steps of the same block / later launches only, so their
+// stores are held back (up to 4 per lane) and issued by flush() after the block signalled ready -
+// the drain before the ready word then waits for the master stores alone.  No tile path: the fc
+// tiles finish per element, with DirectSink's arithmetic (bit-identical to the serial fp32 step).
 struct WtF32Sink {
   static constexpr bool kTile = false;
   static constexpr bool kTileInfo = false;
-  __device__ __forceinline__ void put(int, int e, float g, float p_old, float m_old, const ReduceArgs& a) {
+  static constexpr bool kOpaqueLane = true;
+  int e[4];
+  float p[4], m[4];
+  bool v[4] = {false, false, false, false};
+  __device__ __forceinline__ void put(int j, int e_, float g, float p_old, float m_old, const ReduceArgs& a) {
     g *= a.grad_scale;
-    float p, m;
-    sgd_update(g, p_old, m_old, a.lr, a.momentum, p, m);
-    a.mom[e] = m;
-    st_wt(a.master + e, p);
-    write_shadow(a.shadow, e, p);
+    sgd_update(g, p_old, m_old, a.lr, a.momentum, p[j], m[j]);
+    e[j] = e_;
+    v[j] = true;
+    st_wt(a.master + e_, p[j]);
+  }
+  __device__ __forceinline__ void flush(const ReduceArgs& a) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (v[j]) {
+        a.mom[e[j]] = m[j];
+        write_shadow(a.shadow, e[j], p[j]);
+      }
   }
   template <int LAYER>
   __device__ __forceinline__ void put_tile(const f32x4&, const float (&)[4], const float (&)[4], const int (&)[4], int,
@@ -207,6 +221,7 @@ template <bool PK, bool WT = false>
 struct XpSinkT {
   static constexpr bool kTile = false;
   static constexpr bool kTileInfo = WT;
+  static constexpr bool kOpaqueLane = false;
   int tl = -1, to0 = 0, ti0 = 0;  // WT: the fc tile (layer, o0, i0) this lane's elements belong to
   template <int LAYER>
   __device__ __forceinline__ void tile_info(int o0, int i0) {
@@ -339,9 +354,9 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
     x += (long)rp * a.batch * L::XLD;
   }
   int lane = threadIdx.x & 63;
-  // (SC: the persistent launches call this once per step - an opaque lane keeps its per-lane
-  // offsets inside the step instead of hoisted out of the step loop and held across it)
-  if constexpr (SC) asm volatile("" : "+v"(lane));
+  // (kOpaqueLane: the fp32 persistent launch calls this once per step at 128 VGPRs - an opaque
+  // lane keeps its per-lane offsets inside the step instead of hoisted out of the step loop)
+  if constexpr (Sink::kOpaqueLane) asm volatile("" : "+v"(lane));
   const int col = lane & 15, kq = lane >> 4;
   const int o0 = (t / L::IT) * 16, i0 = (t % L::IT) * 16;
   const int om = o0 + col, in = i0 + col;

@@ -338,7 +338,10 @@ class HipEngine(Engine):
         # persistent grid on the same GPU (ranks time-sharing a device would each hold part of
         # the CUs); DNN_PERSIST=0 turns it off.
         if persist is None:
-            persist = os.environ.get("DNN_PERSIST", "1") != "0"
+            # (fp32: opt-in, DNN_PERSIST_F32=1 - its hand-off measured slower than the serial fp32
+            # step's kernel boundary: 27.96 vs 26.40 us per step over 5000 steps, profiles/r5/fp32_pers)
+            persist = (os.environ.get("DNN_PERSIST", "1") != "0" if dtype == "bf16"
+                       else os.environ.get("DNN_PERSIST_F32", "0") == "1")
         # ranks time-sharing this GPU (one-GPU rehearsals): every rank's grid must be resident at
         # once - ranks x (reduction + sample workgroups) within the occupancy-derived count
         share = ranks_per_gpu()

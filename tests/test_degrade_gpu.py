@@ -34,7 +34,8 @@ def _train(tmp_path, name, env_extra, dtype="bf16"):
 @pytest.mark.parametrize("dtype,level", [("bf16", "pipelined"), ("fp32", "serial")])
 def test_forced_persistent_timeout_steps_down_and_matches_serial(tmp_path, dtype, level):
     # (fp32: lenet_f32.hip's persistent launch, same injected delay; it steps down to the serial step)
-    sd, r = _train(tmp_path, "forced", {"DNN_PIPE_FLAGS": "256", "DNN_PIPE_TIMEOUT_S": "0.002"}, dtype)
+    forced = {"DNN_PIPE_FLAGS": "256", "DNN_PIPE_TIMEOUT_S": "0.002", "DNN_PERSIST_F32": "1"}  # (fp32's is opt-in)
+    sd, r = _train(tmp_path, "forced", forced, dtype)
     assert f"stepping down to the {level} step" in r.stdout, r.stdout[-3000:]
     assert r.stdout.count("Validation loss of updated master model:") == 2
     ref, _ = _train(tmp_path, "serial", {"DNN_PERSIST": "0", "DNN_PIPELINE": "0"}, dtype)

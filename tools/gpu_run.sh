@@ -18,7 +18,7 @@
 #   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32 | long32serial   bench.py default window (5000 / 500), bf16 / fp32 / fp32 without PERS
-#   b2k              bench.py 2000 / 200 steps, no epoch timing
+#   b2k              bench.py 2000 / 200 steps, no epoch timing (envb2k:VAR=val: under one env setting)
 #   abdirect:N       N alternating 20/5 windows: graph replays vs direct relaunch (DNN_PERS_DIRECT=1)
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
@@ -76,6 +76,12 @@ for s in "$@"; do
           2> "$O/abd_direct_$i.err"
       done ;;
     b2k) timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k.json" 2> "$O/b2k.err" ;;
+    envb2k:*)  # b2k under one runtime env setting: envb2k:VAR=value
+      kv="${s#envb2k:}"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k_$n.json" 2> "$O/b2k_$n.err" ;;
+    envphasepers:*)  # phasepers under one runtime env setting
+      kv="${s#envphasepers:}"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" timeout -k 10 300 python tools/phase_trace.py --pers > "$O/phasepers_$n.txt" 2>&1 ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
     long32serial) DNN_PERSIST=0 timeout -k 10 300 python bench.py --dtype fp32 > "$O/$s.json" 2> "$O/$s.err" ;;
     prof|prof32|profserial|profpipe)
