@@ -411,16 +411,28 @@ __device__ __forceinline__ void pers_arrive(const PipeCtl& pc, int kind, int b, 
 // A sample's wave waits until the ready words of workgroups [lo, hi) in its row reach tgt (every
 // lane loads one word: lane = workgroup).  also_lo < also_hi: the same round also reports whether
 // workgroups [also_lo, also_hi) are ready (*also_set, wave-uniform).  Bounded like pipe_wait.
+// pre (optional): the error word and this lane's ready word, loaded by the caller earlier (their
+// round trip overlapped with other work); otherwise both are loaded here in ONE round trip.
+struct PersPoll {
+  unsigned err, v;
+};
+__device__ __forceinline__ const unsigned* pers_ready_word(const PipeCtl& pc, int b, int lane) {
+  return pc.flg + (long)b * PERS_RROW + min(lane, PERS_WG - 1);
+}
+__device__ __forceinline__ PersPoll pers_poll_issue(const PipeCtl& pc, int b, int lane) {
+  return PersPoll{ld_tag(pc.err), ld_tag(pers_ready_word(pc, b, lane))};
+}
 __device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo, int hi, unsigned tgt, int lane,
                                                 int also_lo = 0, int also_hi = 0, bool* also_set = nullptr,
-                                                long long* diag = nullptr) {
-  if (ld_tag(pc.err) != 0u) return;
-  const unsigned* row = pc.flg + (long)b * PERS_RROW + min(lane, PERS_WG - 1);
+                                                long long* diag = nullptr, const PersPoll* pre = nullptr) {
+  const unsigned* row = pers_ready_word(pc, b, lane);
+  const PersPoll first = pre != nullptr ? *pre : pers_poll_issue(pc, b, lane);
+  if (first.err != 0u) return;
   const long long t0 = wall_clock64();
   if (diag != nullptr && lane == 0) diag[0] = t0;
   long long polls = 0;
+  unsigned v = first.v;
   while (true) {
-    const unsigned v = ld_tag(row);
     if (__all((lane < lo || lane >= hi) || tag_ge(v, tgt))) {
       if (also_set != nullptr) *also_set = __all((lane < also_lo || lane >= also_hi) || tag_ge(v, tgt));
       break;
@@ -432,7 +444,38 @@ __device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo
       if (lane == 0) __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
+    v = ld_tag(row);
   }
+}
+
+// Wave 0 at a persistent step's start: wait for the conv1 group's ready words (as pers_wait_ready).
+// If the MLP group's words show ready first - the MLP reduction overlaps the previous step's conv
+// backward, so it usually is - the wave streams the whole fc1 image into LDS meanwhile (every
+// chunk: the other waves are at the barrier), in the idle time before conv1's weights instead of
+// mid-phase B on every wave.  Returns whether it did (the caller skips the mid-phase-B stream).
+template <class F>
+__device__ __forceinline__ bool pers_wait_c1_early_fc1(const PipeCtl& pc, int b, unsigned tgt, int lane,
+                                                       F&& stream_all) {
+  const unsigned* row = pers_ready_word(pc, b, lane);
+  const PersPoll first = pers_poll_issue(pc, b, lane);
+  if (first.err != 0u) return false;
+  const long long t0 = wall_clock64();
+  bool streamed = false;
+  unsigned v = first.v;
+  while (true) {
+    if (__all(lane >= PERS_C1_WG || tag_ge(v, tgt))) break;
+    if (!streamed && __all(lane < PERS_CONV_WG || tag_ge(v, tgt))) {
+      stream_all();
+      streamed = true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > pc.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store(pc.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    v = ld_tag(row);
+  }
+  return streamed;
 }
 
 // Reduction workgroup `wg` of a persistent launch: blocks 2 wg, 2 wg + 1 (pipe_reduce's map),
@@ -855,7 +898,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     // image and its records need none of it, so they are done first); the barrier releases the
     // other waves, then every wave loads its fragments (sc1) - waited for at phase B's first MFMA
     if constexpr (PERS) {
-      if (wave == 0 && do_wait) pers_wait_ready(pc, b, 0, PERS_C1_WG, wtgt, lane, 0, 0, nullptr, stamp ? stamps + 14 : nullptr);
+      if (wave == 0) {
+        bool early = false;
+        if (do_wait && !(pc.flags & 3)) {  // (flags & 2, measurement: no early stream)
+          early = pers_wait_c1_early_fc1(pc, b, wtgt, lane, [&]() {  // all 94 fc1 chunks (1 KB each)
+            const uint4* f1src = reinterpret_cast<const uint4*>(shadow + OFF_F1W);
+            const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGA));
+            for (int i = 0; i < 94; ++i) dma_w<PIPE>(f1src + i * 64 + lane, base + (uint32_t)i * 1024u);
+          });
+        } else if (do_wait) {
+          pers_wait_ready(pc, b, 0, PERS_C1_WG, wtgt, lane, 0, 0, nullptr, stamp ? stamps + 14 : nullptr);
+        }
+        if (lane == 0) reinterpret_cast<int*>(smem + L_MISC)[1] = early ? 1 : 0;
+      }
     } else {
       if (tid == 0 && do_wait) pipe_wait(pc, PG_C1, b, batch, stamp ? stamps + 14 : nullptr, -1, nullptr, wtgt);
     }
@@ -885,11 +940,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     stream_fc1();
     lds_barrier();
   }
-  bool fc1_out = !PIPE;  // PIPE: this wave has issued its part of the fc1 stream
+  // PIPE: this wave has issued its part of the fc1 stream (PERS: or wave 0 streamed all of it
+  // while waiting for conv1's weights)
+  bool fc1_out = !PIPE;
+  if constexpr (PERS) fc1_out = reinterpret_cast<const int*>(smem + L_MISC)[1] != 0;
   int bv_late = batch;   // PERS: this step's valid count (from step 1 on)
   STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
+  // PERS: the mid-phase-B poll's first round (error word + ready row) and, from step 2 on, this
+  // step's valid count are loaded NOW - their round trips fly under the first MFMA round instead
+  // of following it.  (The valid count of step s was published by the bookkeeping of step s - 2,
+  // which the conv2-group wait of step s - 1 already ordered before this load; step 1's slot is
+  // the launch start's publication, ordered only by this step's conv2-group wait: read after it.)
+  PersPoll c2_pre{0u, 0u};
+  if constexpr (PERS) {
+    if (do_wait) c2_pre = pers_poll_issue(pc, b, lane);
+    if (s > 1) bv_late = ld_sc1(pc.bv_slot[s & 1]);
+  }
   {
     const float bias = fr < 6 ? bias_c1 : 0.f;
     const int wi = fr >> 2, pi = fr & 3;  // A-operand row -> (window, pixel)
@@ -942,6 +1010,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       epilogue(t1, acc1);
       epilogue(t2, acc2);
       if (four) epilogue(48, acc3);
+      STAMP(1000 + 3 * r);  // (diagnostic: phase B round r's epilogue issued)
       if (PIPE && r == 0) {
         // conv2's group: lane 0 of each wave waits (the wave's other lanes with it) - with the MLP
         // flag in the same poll round.  If the MLP group is complete too, the wave's part of the
@@ -951,7 +1020,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         int mlp = 0;
         if constexpr (PERS) {  // the whole wave polls its sample's ready row (C2 + bookkeeping, MLP)
           bool m = true;
-          if (do_wait) pers_wait_ready(pc, b, PERS_C1_WG, PERS_CONV_WG, wtgt, lane, PERS_CONV_WG, PERS_WG, &m);
+          if (do_wait) pers_wait_ready(pc, b, PERS_C1_WG, PERS_CONV_WG, wtgt, lane, PERS_CONV_WG, PERS_WG, &m, nullptr, &c2_pre);
           mlp = m && !(pc.flags & 1);
         } else if (lane == 0) {
           bool m = false;
@@ -961,12 +1030,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         }
         // PERS: this step's valid count (published by the bookkeeping, a conv2-group block),
         // consumed after phase B
-        if (PERS && s > 0) bv_late = ld_sc1(pc.bv_slot[s & 1]);
-        if (__builtin_amdgcn_readfirstlane(mlp)) {
+        if (PERS && s == 1) bv_late = ld_sc1(pc.bv_slot[s & 1]);
+        STAMP(1001);  // (diagnostic: the mid-phase-B wait returned)
+        if (!fc1_out && __builtin_amdgcn_readfirstlane(mlp)) {
           stream_fc1();
           fc1_out = true;
         }
         load_conv2_w();
+        STAMP(1002);  // (diagnostic: the fc1 stream + conv2 fragment loads issued)
       }
     }
   }

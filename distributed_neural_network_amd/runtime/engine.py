@@ -376,7 +376,15 @@ class HipEngine(Engine):
         # the per-step xGMI all-reduce inside the persistent launch (installed by the
         # step-allreduce policy's "-pers" paths after their self-test; lenet_fused.hip XNR)
         self.pers_exchange = False
-        self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
+        # control words of the persistent launch (generation, ready and arrival words): uncached
+        # (fine-grained) memory, or (DNN_PERS_CTL=coarse, measurement) an ordinary device buffer -
+        # every access to them is an sc1 load / store either way
+        self._pers_ctl_t = None
+        if self.persist and os.environ.get("DNN_PERS_CTL", "uncached") == "coarse":
+            self._pers_ctl_t = torch.zeros(self.ext.persist_ctl_bytes(B) // 4 + 64, device=dev, dtype=torch.int32)
+            self._pers_ctl = self._pers_ctl_t.data_ptr()
+        else:
+            self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
         self._pers_handles: dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -645,7 +653,8 @@ class HipEngine(Engine):
         """Give the uncached control buffers back to the extension's pool (never to the driver:
         csrc/comm/xgmi_allreduce.hip uncached_alloc) once this engine's queued work is done."""
         rg = getattr(self, "_rg", None)
-        bufs = [getattr(self, "_pipe_ctr_ptr", 0), getattr(self, "_pipe_flg_ptr", 0), getattr(self, "_pers_ctl", 0),
+        bufs = [getattr(self, "_pipe_ctr_ptr", 0), getattr(self, "_pipe_flg_ptr", 0),
+                getattr(self, "_pers_ctl", 0) if getattr(self, "_pers_ctl_t", None) is None else 0,
                 rg["ptr"] if rg is not None else 0]
         if any(bufs):
             try:

@@ -85,8 +85,8 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     eng.attach(tr)
     assert eng.persist, "persistent launch unavailable"
     stamps = torch.zeros(4096 + 64, dtype=torch.int64, device=eng.device)
-    keys = dict(img=9, conv_ready=12, a_done=1, b_done=2, mlp_ready=13, c_done=3, d_done=4, dp_done=5,
-                e1_done=8, e_done=6, f1_done=10, end=7)
+    keys = dict(img=9, conv_ready=12, a_done=1, b_r0=1000, b_wait=1001, b_issue=1002, b_r1=1003, mlp_ready=13,
+                b_done=2, c_done=3, d_done=4, dp_done=5, e1_done=8, e_done=6, f1_done=10, end=7)
     recs, walls, tl = [], {steps: [], 64: []}, []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(reps):
