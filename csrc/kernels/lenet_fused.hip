@@ -542,7 +542,11 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
       grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid_s, 0, false, t & 1);
     }
     if (st) stamps[2401 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
+    // (diagnostic: the last step's per-wave body done / drain done of the conv1 workgroups)
+    const bool wst = stamps != nullptr && (threadIdx.x & 63) == 0 && t == pc.nsteps - 1 && wg < PERS_C1_WG;
+    if (wst) stamps[2640 + 16 * wg + 2 * (threadIdx.x >> 6)] = (long long)__builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+    if (wst) stamps[2641 + 16 * wg + 2 * (threadIdx.x >> 6)] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (st) stamps[2402 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     if (threadIdx.x < 64)  // both blocks done: this workgroup's word in every sample's ready row

@@ -108,7 +108,9 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
                 t0 = bl[:, 0].min()
                 last = s[2048 + steps - 1]  # the last step's start (sample block 0)
                 rw = s[2400:2400 + 4 * nrw].reshape(nrw, 4)
-                tl.append(dict(red_seen=(rw[:, 0] - last) * 0.01, red_body=(rw[:, 1] - last) * 0.01,
+                cw = s[2640:2640 + 16 * 4].reshape(4, 8, 2)  # conv1 WGs x waves x (body done, drained)
+                tl.append(dict(c1_body=(cw[:, :, 0] - last) * 0.01, c1_drain=(cw[:, :, 1] - last) * 0.01,
+                               red_seen=(rw[:, 0] - last) * 0.01, red_body=(rw[:, 1] - last) * 0.01,
                                red_ready=(rw[:, 2] - last) * 0.01, arrive0=(s[2398] - last) * 0.01,
                                steps=(s[2048:2048 + steps] - t0) * 0.01, smp_start=(bl[nrw:, 0] - t0) * 0.01,
                                red_start=(bl[:nrw, 0] - t0) * 0.01, smp_end=(bl[nrw:, 2] - t0) * 0.01,
@@ -131,6 +133,10 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
               f"{med(lambda x: x['red_seen'][sl].max()):.2f}  body done {med(lambda x: np.median(x['red_body'][sl])):.2f}/"
               f"{med(lambda x: x['red_body'][sl].max()):.2f}  ready stored {med(lambda x: np.median(x['red_ready'][sl])):.2f}/"
               f"{med(lambda x: x['red_ready'][sl].max()):.2f}")
+    print("  conv1 WGs per wave (us from the step's start; medians): body done / vmcnt drained")
+    for w in range(4):
+        print(f"    WG {w}: " + "  ".join(f"{med(lambda x, w=w, v=v: x['c1_body'][w][v]):.2f}/"
+                                         f"{med(lambda x, w=w, v=v: x['c1_drain'][w][v]):.2f}" for v in range(8)))
     w8, w64 = float(np.median(walls[steps][3:])), float(np.median(walls[64][3:]))
     print(f"launch wall (events): {steps} steps {w8:.2f} us, 64 steps {w64:.2f} us -> steady step "
           f"{(w64 - w8) / (64 - steps):.3f} us")
