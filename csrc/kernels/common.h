@@ -88,7 +88,7 @@ constexpr int IMG = 3 * 32 * 32;
 // Written by the optimizer kernels right after each update (one owner thread per
 // parameter writes its bf16 value to every position it occupies), so the fused kernel
 // loads MFMA fragments with one 16-B load each instead of re-arranging weights per sample.
-constexpr int SH_W1F = ARENA;               // conv1 fwd B frags  [16 pairs (c,ky)][16 n][8 kx]
+constexpr int SH_W1F = ARENA;               // conv1 fwd B frags  [16 pairs (c,ky)][16 n' = 2 o + s][8 j]: W[o][c][ky][j - s]
 constexpr int SH_W2F = SH_W1F + 16 * 16 * 8;  // conv2 fwd B frags  [32 pairs (c,ky)][16 n][8 kx]
 constexpr int SH_WF = SH_W2F + 32 * 16 * 8;   // conv2 dgrad B frags (flipped) [80 (ky',o)][16 c][8 kx']
 constexpr int SH_W2T = SH_WF + 80 * 16 * 8;   // fc2 transposed [120 i][96 o]
@@ -109,7 +109,8 @@ __device__ __forceinline__ void write_shadow(bf16* __restrict__ sh, int e, float
   sh[e] = v;
   if (e >= OFF_C1W && e < OFF_C1W + 450) {
     const int r = e - OFF_C1W, n = r / 75, rem = r - 75 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
-    sh[SH_W1F + ((c * 5 + ky) * 16 + n) * 8 + kx] = v;
+    sh[SH_W1F + ((c * 5 + ky) * 16 + 2 * n) * 8 + kx] = v;  // shift 0 (lenet_fused.hip phase B: pixel pairs)
+    sh[SH_W1F + ((c * 5 + ky) * 16 + 2 * n + 1) * 8 + kx + 1] = v;  // shift 1
   } else if (e >= OFF_C2W && e < OFF_C2W + 2400) {
     const int r = e - OFF_C2W, n = r / 150, rem = r - 150 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
     sh[SH_W2F + ((c * 5 + ky) * 16 + n) * 8 + kx] = v;

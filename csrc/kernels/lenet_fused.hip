@@ -411,8 +411,9 @@ __device__ __forceinline__ void pers_arrive(const PipeCtl& pc, int kind, int b, 
 // A sample's wave waits until the ready words of workgroups [lo, hi) in its row reach tgt (every
 // lane loads one word: lane = workgroup).  also_lo < also_hi: the same round also reports whether
 // workgroups [also_lo, also_hi) are ready (*also_set, wave-uniform).  Bounded like pipe_wait.
-// pre (optional): the error word and this lane's ready word, loaded by the caller earlier (their
-// round trip overlapped with other work); otherwise both are loaded here in ONE round trip.
+// has_pre: the error word and this lane's ready word were loaded by the caller earlier (pre_err,
+// pre_v: their round trip overlapped with other work); otherwise both are loaded here in ONE
+// round trip.
 struct PersPoll {
   unsigned err, v;
 };
@@ -424,14 +425,19 @@ __device__ __forceinline__ PersPoll pers_poll_issue(const PipeCtl& pc, int b, in
 }
 __device__ __forceinline__ void pers_wait_ready(const PipeCtl& pc, int b, int lo, int hi, unsigned tgt, int lane,
                                                 int also_lo = 0, int also_hi = 0, bool* also_set = nullptr,
-                                                long long* diag = nullptr, const PersPoll* pre = nullptr) {
+                                                long long* diag = nullptr, bool has_pre = false, unsigned pre_err = 0u,
+                                                unsigned pre_v = 0u) {
   const unsigned* row = pers_ready_word(pc, b, lane);
-  const PersPoll first = pre != nullptr ? *pre : pers_poll_issue(pc, b, lane);
-  if (first.err != 0u) return;
+  unsigned ferr = pre_err, v = pre_v;
+  if (!has_pre) {
+    const PersPoll first = pers_poll_issue(pc, b, lane);
+    ferr = first.err;
+    v = first.v;
+  }
+  if (ferr != 0u) return;
   const long long t0 = wall_clock64();
   if (diag != nullptr && lane == 0) diag[0] = t0;
   long long polls = 0;
-  unsigned v = first.v;
   while (true) {
     if (__all((lane < lo || lane >= hi) || tag_ge(v, tgt))) {
       if (also_set != nullptr) *also_set = __all((lane < also_lo || lane >= also_hi) || tag_ge(v, tgt));
@@ -703,6 +709,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (PERS && stamps != nullptr && (int)blockIdx.x == nrw && threadIdx.x == 0 && s < 1024)  // per-step starts
     stamps[2048 + s] = (long long)__builtin_amdgcn_s_memrealtime();
 #define STAMP(i) do { if (stamp) stamps[i] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+  // (diagnostic: lane 0 of EVERY wave of the stamped block, stamps[base + wave])
+  const bool wstamp = stamps != nullptr && (int)blockIdx.x == nrw && (threadIdx.x & 63) == 0 && (!PERS || s == nsteps - 1);
+#define WSTAMP(base) do { if (wstamp) stamps[(base) + (threadIdx.x >> 6)] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
   STAMP(0);
 
   // TRAIN: the sample ids and valid count of this step were published by the previous
@@ -863,7 +872,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   auto load_conv1_w = [&]() {
 #pragma unroll
     for (int sk = 0; sk < 4; ++sk) bw1[sk] = wr.w8(SH_W1F + ((4 * sk + fg) * 16 + fr) * 8);
-    bias_c1 = wr.f(OFF_C1B + min(fr, 5));
+    bias_c1 = wr.f(OFF_C1B + min(fr >> 1, 5));  // (column fr = 2 o + s: channel o)
   };
   auto load_conv2_w = [&]() {
 #pragma unroll
@@ -897,6 +906,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (PERS) label = *reinterpret_cast<const int*>(smem + L_MISC);  // (one path for every step)
   STAMP(9);
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
+  unsigned c2_err = 0u, c2_v = 0u;  // (PERS, below)
+  int bv_pre = batch;
   if constexpr (PIPE) {
     // conv1's weights are the previous step's reduction's: one lane waits for its group (the
     // image and its records need none of it, so they are done first); the barrier releases the
@@ -920,6 +931,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     STAMP(12);
     lds_barrier();
+    // PERS: the mid-phase-B poll's first round (error word + ready row) and, from step 2 on, this
+    // step's valid count are loaded NOW, just before conv1's fragments - their round trips fly
+    // with those loads and under phase B's first MFMA round instead of following it.  (The valid
+    // count of step s was published by the bookkeeping of step s - 2, which the conv2-group wait
+    // of step s - 1 already ordered before this load; step 1's slot is the launch start's
+    // publication, ordered only by this step's conv2-group wait: read after it.)
+    if constexpr (PERS) {
+      if (do_wait) {
+        const PersPoll p = pers_poll_issue(pc, b, lane);
+        c2_err = p.err;
+        c2_v = p.v;
+      }
+      if (s > 1) bv_pre = ld_sc1(pc.bv_slot[s & 1]);
+    }
     load_conv1_w();
   } else {
 #pragma unroll
@@ -948,73 +973,81 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // while waiting for conv1's weights)
   bool fc1_out = !PIPE;
   if constexpr (PERS) fc1_out = reinterpret_cast<const int*>(smem + L_MISC)[1] != 0;
-  int bv_late = batch;   // PERS: this step's valid count (from step 1 on)
+  int bv_late = bv_pre;  // PERS: this step's valid count (from step 1 on)
   STAMP(1);
 
   // ============ phase B: conv1 (3->6, 5x5) + bias + ReLU + maxpool, MFMA ================
-  // PERS: the mid-phase-B poll's first round (error word + ready row) and, from step 2 on, this
-  // step's valid count are loaded NOW - their round trips fly under the first MFMA round instead
-  // of following it.  (The valid count of step s was published by the bookkeeping of step s - 2,
-  // which the conv2-group wait of step s - 1 already ordered before this load; step 1's slot is
-  // the launch start's publication, ordered only by this step's conv2-group wait: read after it.)
-  PersPoll c2_pre{0u, 0u};
-  if constexpr (PERS) {
-    if (do_wait) c2_pre = pers_poll_issue(pc, b, lane);
-    if (s > 1) bv_late = ld_sc1(pc.bv_slot[s & 1]);
-  }
   {
-    const float bias = fr < 6 ? bias_c1 : 0.f;
-    const int wi = fr >> 2, pi = fr & 3;  // A-operand row -> (window, pixel)
+    // conv1 as a GEMM over output PIXEL PAIRS: row = (pool window q, output row dy) of the two
+    // horizontally adjacent outputs x, x + 1; column n' = 2 o + s = output channel o at shift s
+    // (12 of 16 used); K = (c, ky) pairs x the 8 pixels j of an R1 record, against the B image
+    // W1F[(c, ky)][2 o + s][j] = W[o][c][ky][j - s] (common.h write_shadow).  One 8-pixel record
+    // feeds both outputs of a pair, so 25 tiles x 4 K-steps instead of 49 x 4 (one pixel per
+    // row, 6 of 16 columns): half the MFMAs and half the A-operand LDS reads.
+    float bias = 0.f;  // (set after round 0's MFMAs: see there)
+    const int wl = fr >> 1, dy = fr & 1;  // A-operand row -> (window of the tile, output row)
     auto a_index = [&](int t, int sk) {  // R1 record of (tile t, K-step sk) for this lane
-      const int q = 4 * t + wi;
-      const int y = 2 * (q / 14) + (pi >> 1), x = 2 * (q % 14) + (pi & 1);
+      const int q = min(8 * t + wl, 195);  // (tile 24's rows past window 195: clamped, discarded)
+      const int y = 2 * (q / 14) + dy, x = 2 * (q % 14);
       const int pr = min(4 * sk + fg, 14);  // pair 15 is K padding: real data x zero weights
       return (pr / 5 * 32 + y + pr % 5) * 29 + x;
     };
     auto epilogue = [&](int t, f32x4 acc) {
-      if (fr < 6) {  // lane holds window fg of tile t for channel fr
-        const int qo = 4 * t + fg;
-        float best = acc[0] + bias;
-        int arg = 0;
+      // lane (fr = 2 o + s, fg) holds rows 4 fg + i = (window 2 fg + (i >> 1), dy = i & 1) at
+      // shift s; its neighbour lane fr ^ 1 (DPP quad swap, every lane) holds the other shift
+      float nb[4];
 #pragma unroll
-        for (int i = 1; i < 4; ++i) {
-          const float v = acc[i] + bias;
-          if (v > best) { best = v; arg = i; }
+      for (int i = 0; i < 4; ++i)
+        nb[i] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[i]), 0xB1, 0xf, 0xf, false));
+      if (fr < 12 && dy == 0) {  // (fr even: s = 0) channel o = fr / 2, windows 2 fg, 2 fg + 1
+        const int o = fr >> 1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int qo = 8 * t + 2 * fg + h;
+          if (qo < 196) {
+            // the window's pixels in torch's order (first max wins): (y, x), (y, x + 1), (y + 1, x), (y + 1, x + 1)
+            float best = acc[2 * h] + bias;
+            int arg = 0;
+            const float v1 = nb[2 * h] + bias, v2 = acc[2 * h + 1] + bias, v3 = nb[2 * h + 1] + bias;
+            if (v1 > best) { best = v1; arg = 1; }
+            if (v2 > best) { best = v2; arg = 2; }
+            if (v3 > best) { best = v3; arg = 3; }
+            P1[(o * 14 + qo / 14) * 20 + qo % 14] = (bf16)fmaxf(best, 0.f);
+            CODE1[o * 196 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
+          }
         }
-        P1[(fr * 14 + qo / 14) * 20 + qo % 14] = (bf16)fmaxf(best, 0.f);
-        CODE1[fr * 196 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
       }
     };
-    // 49 tiles = 6 per wave + 1: two rounds of three tiles (12 loads in flight) on every wave;
-    // the 49th tile rides along as a fourth in wave 0's second round (a third round of its own
-    // put one more LDS round trip + MFMA chain on wave 0, the phase's critical path)
+    // 25 tiles: round 0 = tiles wave, wave + 8; round 1 = tile wave + 16 (+ tile 24 on wave 0)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int t0 = wave + 24 * r, t1 = t0 + 8, t2 = t0 + 16;
-      const bool four = wave == 0 && r == 1;  // wave-uniform
-      bf16x8 a0[4], a1[4], a2[4], a3[4];
+      const int t0 = r == 0 ? wave : wave + 16, t1 = r == 0 ? wave + 8 : 24;
+      const bool two = r == 0 || wave == 0;  // wave-uniform
+      bf16x8 a0[4], a1[4];
 #pragma unroll
       for (int sk = 0; sk < 4; ++sk) {
         a0[sk] = R1[a_index(t0, sk)];
-        a1[sk] = R1[a_index(t1, sk)];
-        a2[sk] = R1[a_index(t2, sk)];
-        if (four) a3[sk] = R1[a_index(48, sk)];
+        if (two) a1[sk] = R1[a_index(t1, sk)];
       }
       __builtin_amdgcn_sched_barrier(0);
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
-      f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int sk = 0; sk < 4; ++sk) {
         acc0 = mfma32(a0[sk], bw1[sk], acc0);
-        acc1 = mfma32(a1[sk], bw1[sk], acc1);
-        acc2 = mfma32(a2[sk], bw1[sk], acc2);
-        if (four) acc3 = mfma32(a3[sk], bw1[sk], acc3);
+        if (two) acc1 = mfma32(a1[sk], bw1[sk], acc1);
+      }
+      // the bias is waited for HERE, on every lane (its load came with the B fragments the MFMAs
+      // just waited for): first used inside the epilogue's divergent branch, hipcc otherwise keeps
+      // it "pending" past that branch and waits again in round 1 with a vmcnt that also drains
+      // the fc1 LDS-DMA issued in between (it does not count asm DMA)
+      if (r == 0) {
+        asm volatile("" : "+v"(bias_c1));
+        bias = fr < 12 ? bias_c1 : 0.f;
       }
       epilogue(t0, acc0);
-      epilogue(t1, acc1);
-      epilogue(t2, acc2);
-      if (four) epilogue(48, acc3);
+      if (two) epilogue(t1, acc1);
       STAMP(1000 + 3 * r);  // (diagnostic: phase B round r's epilogue issued)
+      WSTAMP(1010 + 10 * r);
       if (PIPE && r == 0) {
         // conv2's group: lane 0 of each wave waits (the wave's other lanes with it) - with the MLP
         // flag in the same poll round.  If the MLP group is complete too, the wave's part of the
@@ -1024,7 +1057,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         int mlp = 0;
         if constexpr (PERS) {  // the whole wave polls its sample's ready row (C2 + bookkeeping, MLP)
           bool m = true;
-          if (do_wait) pers_wait_ready(pc, b, PERS_C1_WG, PERS_CONV_WG, wtgt, lane, PERS_CONV_WG, PERS_WG, &m, nullptr, &c2_pre);
+          // (the pre-issued round's values become "defined" only here, after round 0's MFMAs - hipcc
+          // would otherwise hoist the error check to the loads and wait for their round trip there)
+          unsigned c2e = c2_err, c2v = c2_v;
+          asm volatile("" : "+v"(c2e), "+v"(c2v) : "v"(acc0[0]));
+          if (do_wait) pers_wait_ready(pc, b, PERS_C1_WG, PERS_CONV_WG, wtgt, lane, PERS_CONV_WG, PERS_WG, &m, nullptr, true,
+                                       c2e, c2v);
           mlp = m && !(pc.flags & 1);
         } else if (lane == 0) {
           bool m = false;
@@ -1036,6 +1074,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         // consumed after phase B
         if (PERS && s == 1) bv_late = ld_sc1(pc.bv_slot[s & 1]);
         STAMP(1001);  // (diagnostic: the mid-phase-B wait returned)
+        WSTAMP(1040);
         if (!fc1_out && __builtin_amdgcn_readfirstlane(mlp)) {
           stream_fc1();
           fc1_out = true;
@@ -1057,6 +1096,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
     STAMP(13);
   }
+  WSTAMP(1050);  // (diagnostic: each wave at phase B's closing barrier)
   lds_barrier();
   if constexpr (PERS) {
     if (s > 0) {
@@ -1586,6 +1626,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (stamp) stamps[2398] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 #undef STAMP
+#undef WSTAMP
 #undef SLAB_PUT
   } while (PERS && ++s < nsteps);  // steps
   if (PERS && threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)nsteps);

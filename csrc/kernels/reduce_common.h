@@ -26,7 +26,8 @@ __device__ __forceinline__ void write_shadow_wt(bf16* __restrict__ sh, int e, fl
   else sh[e] = v;
   if (e >= OFF_C1W && e < OFF_C1W + 450) {
     const int r = e - OFF_C1W, n = r / 75, rem = r - 75 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
-    st_wt(sh + SH_W1F + ((c * 5 + ky) * 16 + n) * 8 + kx, v);
+    st_wt(sh + SH_W1F + ((c * 5 + ky) * 16 + 2 * n) * 8 + kx, v);  // (common.h write_shadow: both shifts)
+    st_wt(sh + SH_W1F + ((c * 5 + ky) * 16 + 2 * n + 1) * 8 + kx + 1, v);
   } else if (e >= OFF_C2W && e < OFF_C2W + 2400) {
     const int r = e - OFF_C2W, n = r / 150, rem = r - 150 * n, c = rem / 25, ky = (rem % 25) / 5, kx = rem % 5;
     st_wt(sh + SH_W2F + ((c * 5 + ky) * 16 + n) * 8 + kx, v);

@@ -103,6 +103,8 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
             if n == steps:
                 s = stamps.cpu().numpy().astype(np.float64)
                 recs.append({k: (s[i] - s[0]) * 0.01 for k, i in keys.items()})
+                for nm, base in (("w_r0", 1010), ("w_r1", 1020), ("w_wait", 1040), ("w_bar", 1050)):
+                    recs[-1][nm] = (s[base:base + 8] - s[0]) * 0.01
                 nrw = (eng.ext.pipe_reduce_blocks() + 1) // 2
                 bl = s[16:16 + 4 * (nrw + batch)].reshape(nrw + batch, 4)
                 t0 = bl[:, 0].min()
@@ -119,6 +121,8 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     rr = recs[3:]
     for k in keys:
         print(f"  sample block 0, last step: {k:10s} {float(np.median([x[k] for x in rr])):8.2f} us")
+    for nm in ("w_r0", "w_wait", "w_r1", "w_bar"):
+        print(f"  phase B per wave {nm:6s}: " + " ".join(f"{v:6.2f}" for v in np.median([x[nm] for x in rr], axis=0)))
     med = lambda f: float(np.median([f(x) for x in tl[3:]]))  # noqa: E731
     print("launch timeline (us from the first workgroup's start, medians):")
     print(f"  workgroup starts: reduction max {med(lambda x: x['red_start'].max()):.2f}, samples max "
