@@ -238,6 +238,31 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
         assert all(x.samples == 1000 and x.batches == 16 for x in st1), f"variant {var}: sample counts"
 
 
+@pytest.mark.parametrize("flags", [1, 2])
+def test_persistent_fc1_stream_forms_match_serial(flags):
+    """The persistent step's three fc1-stream placements give the same bits: by default wave 0
+    streams fc1 during the conv1 wait once the MLP group is ready; DNN_PIPE_FLAGS=2 streams it
+    mid-phase B (every wave its part, after the conv2-group poll); =1 after phase B (the late
+    path, with the conv2 fragments consumed first)."""
+    data = synthetic(1000, 11)
+    a = init_arena(seed=5)
+    order = np.random.default_rng(3).permutation(1000).astype(np.int32)
+    res = []
+    for pers, fl in ((False, 0), (True, 0), (True, flags)):
+        eng = HipEngine(batch=64, arena=a, graph_chunk=8, pipeline=pers, persist=pers)
+        eng.pipe_flags = fl
+        eng.attach(data)
+        for _ in range(2):
+            eng.begin_epoch(order)
+            eng.run_steps(16)
+        st = eng.epoch_stats()
+        torch.cuda.synchronize()
+        assert not eng.pipe_failed()
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), st.loss_sum))
+    for r in res[1:]:
+        assert all(torch.equal(x, y) for x, y in zip(res[0][:3], r[:3])) and res[0][3] == r[3]
+
+
 @pytest.mark.parametrize("graphs,chunk", [(True, 8), (True, 1), (False, 4), (True, 64)])
 def test_fp32_persistent_matches_serial_step(graphs, chunk):
     """The fp32 kernel's persistent launch (lenet_f32.hip PERS: 4 reduction blocks per 1024-thread
