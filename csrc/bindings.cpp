@@ -305,6 +305,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("persist_max_batch_f32", []() { return dnn::persist_max_batch_f32(); });
   m.def("persist_resident_workgroups_f32", []() { return dnn::persist_resident_workgroups_f32(); });
   m.def("persist_wg_f32", []() { return dnn::persist_wg_f32(); });
+  m.def("persist_conv_wg_f32", []() { return dnn::persist_conv_wg_f32(); });
+  m.def("persist_ctl_bytes_f32", [](int batch) { return dnn::persist_ctl_bytes_f32(batch); });
   m.def("persist_max_batch", []() { return dnn::persist_max_batch(); });
   m.def("persist_resident_workgroups", []() { return dnn::persist_resident_workgroups(); });
   m.def("persist_ctl_bytes", [](int batch) { return dnn::persist_ctl_bytes(batch); });

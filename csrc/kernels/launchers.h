@@ -142,6 +142,8 @@ void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels
 int persist_max_batch_f32();
 int persist_resident_workgroups_f32();
 int persist_wg_f32();
+int persist_conv_wg_f32();
+int persist_ctl_bytes_f32(int batch);
 
 // one-time kernel attribute setup (must run before any hipGraph capture)
 void init_kernels();

@@ -122,13 +122,17 @@ __device__ __forceinline__ float masked(float v, bool keep) {
 // ---- the persistent launch (PERS) ------------------------------------------------------------
 // The bf16 kernel's persistent launch (lenet_fused.hip PERS: one launch runs pc.nsteps steps,
 // reduction and sample workgroups hand off through generation-relative arrival / ready tags),
-// for the fp32 kernel's 1024-thread workgroups: a reduction workgroup runs FOUR 256-thread
-// reduction blocks.  Block map m = 4 wg + (thread >> 8): conv blocks [0, 45), the bookkeeping
-// block 45, two idle blocks (so the conv workgroups [0, PF_CONV_WG) wait for the conv arrival
-// only), then the MLP blocks.  Samples wait for every workgroup's ready word before a step (the
-// conv1 group finishes last anyway - the hand-off runs conv1 -> conv1) and load the weights with
-// sc1 loads of the fp32 master, which the reduction stores write-through (WtF32Sink).
-constexpr int PF_CONV_WG = (PIPE_CONV_BLOCKS + 1 + 3) / 4;     // conv + bookkeeping (+ idle) workgroups
+// for the fp32 kernel's 1024-thread workgroups.  A conv reduction block (or the bookkeeping) gets
+// a workgroup of its own (the other three quarters idle): four 256-thread blocks on one CU
+// finished their slab reductions ~0.6 us apart each - their 16-deep dword load chains queue at
+// the CU's texture path - so the last block of a 4-block workgroup set the conv hand-off ~1.8 us
+// after the first (profiles/r5/fp32_pers).  The MLP blocks, off the critical path, run four per
+// workgroup.  Map: workgroup wg < PF_CONV_WG: conv block wg (45 = the bookkeeping); then MLP
+// blocks 4 (wg - PF_CONV_WG) + quarter.  Samples wait for every workgroup's ready word before a
+// step (the conv1 group finishes last anyway - the hand-off runs conv1 -> conv1) and load the
+// weights with sc1 loads of the fp32 master, which the reduction stores write-through
+// (WtF32Sink).
+constexpr int PF_CONV_WG = PIPE_CONV_BLOCKS + 1;                // conv + bookkeeping workgroups
 constexpr int PF_WG = PF_CONV_WG + (PIPE_MLP_BLOCKS + 3) / 4;  // reduction workgroups
 static_assert(PF_WG <= PERS_RROW, "one ready word per reduction workgroup in a sample's row");
 
@@ -159,12 +163,15 @@ __device__ __forceinline__ void pf_wait_ready(const PipeCtl& pc, int b, unsigned
 // stamps (diagnostic, tools/phase_trace_f32.py --pers): the last step's rows seen / body done /
 // ready stored of workgroup wg at stamps[6144 + 4 wg + k]
 __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), m = 4 * wg + q, rtid = threadIdx.x & 255,
-            lane = threadIdx.x & 63;
-  const bool bk = m == PIPE_CONV_BLOCKS;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
+  const bool bk = wg == PIPE_CONV_BLOCKS && q == 0;
   int rblk = -1;  // (-1: idle)
-  if (m < PIPE_CONV_BLOCKS) rblk = PIPE_MLP_BLOCKS + m;
-  else if (m >= 4 * PF_CONV_WG && m - 4 * PF_CONV_WG < PIPE_MLP_BLOCKS) rblk = m - 4 * PF_CONV_WG;
+  if (wg < PIPE_CONV_BLOCKS) {
+    if (q == 0) rblk = PIPE_MLP_BLOCKS + wg;
+  } else if (wg >= PF_CONV_WG) {
+    const int mm = 4 * (wg - PF_CONV_WG) + q;
+    if (mm < PIPE_MLP_BLOCKS) rblk = mm;
+  }
   const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));
   if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
@@ -183,7 +190,11 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
       grad_reduce_body<false, WtF32Sink, true>(a, sk, rblk, tid_o & 255, 0, false, t & 1);
     }
     if (st) stamps[6145 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
+    // (diagnostic: the last step's per-wave body done / drained, stamps[6400 + 32 wg + 2 wave + k])
+    const bool wst = stamps != nullptr && (threadIdx.x & 63) == 0 && t == pc.nsteps - 1;
+    if (wst) stamps[6400 + 32 * wg + 2 * (threadIdx.x >> 6)] = (long long)__builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+    if (wst) stamps[6401 + 32 * wg + 2 * (threadIdx.x >> 6)] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (st) stamps[6146 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     if (tid_o < 64)
@@ -1059,6 +1070,8 @@ int persist_resident_workgroups_f32() {
   return resident;
 }
 int persist_wg_f32() { return f32k::PF_WG; }
+int persist_conv_wg_f32() { return f32k::PF_CONV_WG; }
+int persist_ctl_bytes_f32(int batch) { return (int)(pers_arrive_off(batch) + (long)f32k::PF_WG * PERS_AROW * 4); }
 int persist_max_batch_f32() {
   return std::max(0, std::min(persist_resident_workgroups_f32() - f32k::PF_WG - PERS_MARGIN_F32, PERS_AROW));
 }

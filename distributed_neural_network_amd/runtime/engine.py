@@ -338,10 +338,11 @@ class HipEngine(Engine):
         # persistent grid on the same GPU (ranks time-sharing a device would each hold part of
         # the CUs); DNN_PERSIST=0 turns it off.
         if persist is None:
-            # (fp32: opt-in, DNN_PERSIST_F32=1 - its hand-off measured slower than the serial fp32
-            # step's kernel boundary: 27.96 vs 26.40 us per step over 5000 steps, profiles/r5/fp32_pers)
+            # (fp32: DNN_PERSIST_F32=0 turns it off - with one conv reduction block per workgroup
+            # it matches the serial fp32 step over 5000 steps, 26.46 vs 26.43 us, and beats it in
+            # the 20/5 window, 27.61 vs 28.07 us: profiles/r5/fp32_pers)
             persist = (os.environ.get("DNN_PERSIST", "1") != "0" if dtype == "bf16"
-                       else os.environ.get("DNN_PERSIST_F32", "0") == "1")
+                       else os.environ.get("DNN_PERSIST_F32", "1") != "0" and os.environ.get("DNN_PERSIST", "1") != "0")
         # ranks time-sharing this GPU (one-GPU rehearsals): every rank's grid must be resident at
         # once - ranks x (reduction + sample workgroups) within the occupancy-derived count
         share = ranks_per_gpu()
@@ -381,10 +382,12 @@ class HipEngine(Engine):
         # every access to them is an sc1 load / store either way
         self._pers_ctl_t = None
         if self.persist and os.environ.get("DNN_PERS_CTL", "uncached") == "coarse":
-            self._pers_ctl_t = torch.zeros(self.ext.persist_ctl_bytes(B) // 4 + 64, device=dev, dtype=torch.int32)
+            self._pers_ctl_t = torch.zeros(max(self.ext.persist_ctl_bytes(B), self.ext.persist_ctl_bytes_f32(B)) // 4 + 64,
+                                           device=dev, dtype=torch.int32)
             self._pers_ctl = self._pers_ctl_t.data_ptr()
         else:
-            self._pers_ctl = self.ext.uncached_alloc(self.ext.persist_ctl_bytes(B)) if self.persist else 0
+            ctl_bytes = self.ext.persist_ctl_bytes_f32(B) if dtype == "fp32" else self.ext.persist_ctl_bytes(B)
+            self._pers_ctl = self.ext.uncached_alloc(ctl_bytes) if self.persist else 0
         self._pers_handles: dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}

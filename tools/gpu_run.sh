@@ -84,6 +84,9 @@ for s in "$@"; do
       env "$kv" timeout -k 10 300 python tools/phase_trace.py --pers > "$O/phasepers_$n.txt" 2>&1 ;;
     long32) timeout -k 10 300 python bench.py --dtype fp32 > "$O/long32.json" 2> "$O/long32.err" ;;
     long32serial) DNN_PERSIST=0 timeout -k 10 300 python bench.py --dtype fp32 > "$O/$s.json" 2> "$O/$s.err" ;;
+    long32pers) DNN_PERSIST_F32=1 timeout -k 10 300 python bench.py --dtype fp32 > "$O/$s.json" 2> "$O/$s.err" ;;
+    k20f32pers) DNN_PERSIST_F32=1 timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" \
+                  2> "$O/$s.err" ;;
     prof|prof32|profserial|profpipe)
       dt=bf16; [ "$s" = prof32 ] && dt=fp32
       [ "$s" = profserial ] && export DNN_PIPELINE=0

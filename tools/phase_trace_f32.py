@@ -64,7 +64,7 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     eng.attach(tr)
     assert eng.persist, "persistent launch unavailable"
     nwg = eng.ext.persist_wg_f32()
-    stamps = torch.zeros(8192, dtype=torch.int64, device=eng.device)
+    stamps = torch.zeros(6400 + 32 * nwg + 64, dtype=torch.int64, device=eng.device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     walls, rows, hand, red = {steps: [], 64: []}, [], [], []
     for r in range(reps):
@@ -88,7 +88,9 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
                                   (st[5120:5120 + steps] - start), np.r_[np.diff(start), np.nan]]) * 0.01)
             last = start[-1]
             rw = st[6144:6144 + 4 * nwg].reshape(nwg, 4)
-            red.append(dict(seen=(rw[:, 0] - last) * 0.01, body=(rw[:, 1] - last) * 0.01,
+            pw = st[6400:6400 + 32 * nwg].reshape(nwg, 16, 2)
+            red.append(dict(wbody=(pw[:, :, 0] - last) * 0.01, wdrain=(pw[:, :, 1] - last) * 0.01,
+                            seen=(rw[:, 0] - last) * 0.01, body=(rw[:, 1] - last) * 0.01,
                             ready=(rw[:, 2] - last) * 0.01, arrive=(st[5120 + steps - 1] - last) * 0.01))
     assert not eng.pipe_failed(), "a persistent-launch wait timed out"
     med = np.median(np.array(rows[3:]), axis=0)
@@ -103,11 +105,16 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
     m = lambda f: float(np.median([f(x) for x in red[3:]]))  # noqa: E731
     print(f"last step's reduction (us from that step's start; sample 0 stored its conv arrival at "
           f"{m(lambda x: x['arrive']):.2f}):")
-    for name, sl in (("conv WGs 0-11", slice(0, 12)), ("MLP WGs 12-", slice(12, nwg))):
+    cw = eng.ext.persist_conv_wg_f32()
+    for name, sl in ((f"conv WGs 0-{cw - 1}", slice(0, cw)), (f"MLP WGs {cw}-", slice(cw, nwg))):
         print(f"  {name:14s} rows seen med/max {m(lambda x: np.median(x['seen'][sl])):.2f}/"
               f"{m(lambda x: x['seen'][sl].max()):.2f}, body done {m(lambda x: np.median(x['body'][sl])):.2f}/"
               f"{m(lambda x: x['body'][sl].max()):.2f}, ready stored {m(lambda x: np.median(x['ready'][sl])):.2f}/"
               f"{m(lambda x: x['ready'][sl].max()):.2f}")
+    print("per workgroup, the slowest wave (us from the last step's start): body done / drained")
+    for w in range(nwg):
+        print(f"  WG {w:2d}: {m(lambda x, w=w: x['wbody'][w].max()):6.2f} / {m(lambda x, w=w: x['wdrain'][w].max()):6.2f}"
+              f"   (waves: " + " ".join(f"{m(lambda x, w=w, v=v: x['wbody'][w][v]):.2f}" for v in range(16)) + ")")
     w8, w64 = np.median(walls[steps][3:]), np.median(walls[64][3:])
     print(f"wall: {steps} steps {w8:.1f} us, 64 steps {w64:.1f} us -> steady step {(w64 - w8) / (64 - steps):.2f} us")
 
