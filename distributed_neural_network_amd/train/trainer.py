@@ -152,6 +152,8 @@ class Trainer:
         elif bad:
             raise StepWaitTimeout(f"an in-launch step wait timed out in epoch {epoch}")
 
+    RECOVERY_ATTEMPTS = 3  # recoveries of one failure (a CommError inside _recover starts it over)
+
     def _recover(self, epoch: int, snap: tuple[torch.Tensor, torch.Tensor], err: Exception) -> None:
         """Survivor side of a failure: every stage is timed (wall clock, so the stamps compare
         across the ranks of one host) and recorded: detect (the watchdog flagged a peer, or the
@@ -364,7 +366,19 @@ class Trainer:
             except CommError as e:
                 if not self.comm.distributed or self.hb is None:
                     raise
-                self._recover(epoch, snap, e)
+                # a failure DURING the recovery (e.g. a survivor flagged stale under load while
+                # the re-formed group's barrier runs) starts the recovery over: agree, re-form
+                err: Exception = e
+                for _ in range(self.RECOVERY_ATTEMPTS):
+                    try:
+                        self._recover(epoch, snap, err)
+                        break
+                    except CommError as e2:
+                        print(f"[fault] rank {self.comm.orig_rank}: recovery interrupted ({e2}); recovering again",
+                              flush=True)
+                        err = e2
+                else:
+                    raise err
                 continue
             loss_sum, batches, correct, samples = [float(x) for x in tot.tolist()]
             trainers = self.policy.trainer_count()
