@@ -380,6 +380,24 @@ def end_skew_injection(orig_rank: int, where: str = "before") -> float:
     return float(parts[1]) if int(parts[0]) == orig_rank and at == where else 0.0
 
 
+_RECOVERY_FAULTS_DONE: set = set()
+
+
+def recovery_fault_injection(orig_rank: int, generation: int) -> bool:
+    """Fault injection for tests (``DNN_INJECT_RECOVERY_FAIL=rank:generation``): that rank's
+    recovery fails ONCE right after it re-formed the group into that generation, before the new
+    group's barrier (as if a survivor were flagged mid-recovery) - the trainer must start the
+    recovery over instead of dying.  Returns whether to fail now."""
+    spec = os.environ.get("DNN_INJECT_RECOVERY_FAIL", "")
+    if not spec:
+        return False
+    r, g = (int(x) for x in spec.split(":"))
+    if r != orig_rank or g != generation or (r, g) in _RECOVERY_FAULTS_DONE:
+        return False
+    _RECOVERY_FAULTS_DONE.add((r, g))
+    return True
+
+
 def beat_pause_injection(orig_rank: int, epoch: int) -> float:
     """Fault injection for tests (``DNN_INJECT_BEAT_PAUSE=rank:epoch:seconds``): this rank's
     heartbeat thread stops beating for that long at the start of that epoch while the rank itself

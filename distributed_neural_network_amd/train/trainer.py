@@ -26,7 +26,8 @@ import torch
 from ..data import EpochSampler, get_splits
 from ..parallel import CommError, Communicator, assert_replicas_identical, detect, make_policy
 from ..parallel.fault import (DropInjector, Heartbeat, agree_survivors, announce_alive, beat_pause_injection,
-                              end_skew_injection, simulate_failure, stall_injection, stall_process)
+                              end_skew_injection, recovery_fault_injection, simulate_failure, stall_injection,
+                              stall_process)
 from ..runtime import StepWaitTimeout, eval_metrics, make_engine
 from ..utils import checkpoint, logfiles
 from ..utils.metrics import Run
@@ -190,6 +191,8 @@ class Trainer:
         dead = [r for r in old if r not in members]
         self.comm.reform(dead)
         stage("reform")
+        if recovery_fault_injection(self.comm.orig_rank, self.comm.generation):
+            raise CommError(f"injected recovery failure (generation {self.comm.generation})")
         if dead and self.comm.rank == 0:
             try:  # the dropped ranks will never check out of the store (parallel/store_server.py)
                 self.comm.store.add("dnn/dropped", len(dead))

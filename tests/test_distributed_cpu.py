@@ -196,6 +196,21 @@ def test_rank_drop_reforms_and_finishes(tmp_path, sync):
     assert side["epoch"] == 2 and side["world"] == 2
 
 
+def test_failure_during_recovery_recovers_again(tmp_path):
+    """A CommError INSIDE a recovery (DNN_INJECT_RECOVERY_FAIL: rank 0 fails once right after it
+    re-formed generation 1, before the new group's barrier) starts the recovery over - rank 2's
+    barrier fails with it and both agree again - instead of escaping the recovery scope: the run
+    finishes on the two survivors."""
+    r = _launch_env(3, [os.path.join(ROOT, "data_parallelism_train.py"), "--epochs", "3", "--batch-size", "32",
+                        "--sync", "step-allreduce", "--drop-rank", "1", "--drop-at-epoch", "1", "--drop-at-step", "2",
+                        "--save", "ck.pt", "--nb-proc", "3"] + SMALL, tmp_path, {"DNN_INJECT_RECOVERY_FAIL": "0:1"})
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "recovery interrupted (injected recovery failure (generation 1))" in r.stdout, r.stdout[-4000:]
+    assert r.stdout.count("Validation loss of updated master model:") == 3
+    sd, side = checkpoint.load(str(tmp_path / "ck.pt"))
+    assert side["epoch"] == 2 and side["world"] == 2
+
+
 def test_survivor_agreement_counts_early_announcements():
     """A survivor that announced itself before tearing its group down (announce_alive) is in
     the next generation even if it has not reached agree_survivors yet; a stale rank is not."""
