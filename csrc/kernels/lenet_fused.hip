@@ -1115,27 +1115,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   // The MLP B fragments each lane needs in phase D are loaded now so conv2 hides their
   // latency; lane roles in the MLP: wave w owns output columns 16w + fr.
   const int ncol = 16 * wave + fr;
-  bf16x8 w2f[4], w2t[3], w3t, w3f[3];
-  {
-    const int r2 = OFF_F2W + min(ncol, 83) * 120;             // fc2 row (forward)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) w2f[ks] = wr.w8(r2 + 32 * ks + 8 * fg);
-    const int t2 = SH_W2T + min(ncol, 119) * 96;               // fc2^T row (dgrad)
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) w2t[ks] = wr.w8(t2 + 32 * ks + 8 * fg);
-    w3t = wr.w8(SH_W3T + min(ncol, 83) * 16 + 8 * fg);         // fc3^T (dgrad)
-    const int r3 = OFF_F3W + min(fr, 9) * 84;                  // fc3 row (forward; 8-B aligned)
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
-      const bf16x4 lo = wr.w4(r3 + 32 * ks + 8 * fg);
-      const bf16x4 hi = wr.w4(r3 + 32 * ks + 8 * fg + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { w3f[ks][j] = lo[j]; w3f[ks][4 + j] = hi[j]; }
-    }
-  }
-  float bias_f1 = wr.f(OFF_F1B + min(ncol, 119));
-  float bias_f2 = wr.f(OFF_F2B + min(ncol, 83));
-  float bias_f3 = wr.f(OFF_F3B + min(fr, 9));
   if (tid < 168) {  // window records of P1 rows (overwrite R1: dead until phase F); 2 threads per row
     const int row = tid >> 1, h = tid & 1;  // row = c*14 + y; half h builds records 7h .. 7h+6 (< 13)
     bf16 v[14];
@@ -1151,6 +1130,33 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       }
     }
   }
+  bf16x8 w2f[4], w2t[3], w3t, w3f[3];
+  // Only the waves that use a fragment load it (fc2, fc3^T: waves 0-5; fc3: wave 0), and fc2^T's
+  // (the MLP dgrad's) are loaded in phase D: the CU's vector-memory path is the bound here (a
+  // wave stalls at issue while it is backed up, ~25 cycles per 1-KB wave load), and the record
+  // builders go first so their LDS work overlaps the other waves' loads
+  {
+    const int r2 = OFF_F2W + min(ncol, 83) * 120;             // fc2 row (forward)
+    if (wave < 6) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) w2f[ks] = wr.w8(r2 + 32 * ks + 8 * fg);
+      w3t = wr.w8(SH_W3T + min(ncol, 83) * 16 + 8 * fg);       // fc3^T (dgrad)
+    }
+    if (wave == 0) {
+      const int r3 = OFF_F3W + min(fr, 9) * 84;                // fc3 row (forward; 8-B aligned)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x4 lo = wr.w4(r3 + 32 * ks + 8 * fg);
+        const bf16x4 hi = wr.w4(r3 + 32 * ks + 8 * fg + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { w3f[ks][j] = lo[j]; w3f[ks][4 + j] = hi[j]; }
+      }
+    }
+  }
+  float bias_f1 = wr.f(OFF_F1B + min(ncol, 119));
+  float bias_f2 = 0.f, bias_f3 = 0.f;
+  if (wave < 6) bias_f2 = wr.f(OFF_F2B + min(ncol, 83));
+  if (wave == 0) bias_f3 = wr.f(OFF_F3B + min(fr, 9));
   lds_barrier();
   if (wave < 7) {
     const int t = wave;
@@ -1187,7 +1193,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) consume(w2f[ks]);
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) { consume(w2t[ks]); consume(w3f[ks]); }
+  for (int ks = 0; ks < 3; ++ks) consume(w3f[ks]);
   consume(w3t);
   consume(bias_f1);
   consume(bias_f2);
@@ -1214,6 +1220,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int ks = 0; ks < 13; ++ks) {
       bv[ks] = *reinterpret_cast<const bf16x8*>(wrow + 32 * ks + 8 * fg);
       av[ks] = row0(A0B, 32 * ks + 8 * fg, fr);
+    }
+    if (TRAIN) {  // fc2^T fragments (the MLP dgrad's), behind this wave's LDS reads
+      const int t2 = SH_W2T + min(ncol, 119) * 96;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) w2t[ks] = wr.w8(t2 + 32 * ks + 8 * fg);
     }
     __builtin_amdgcn_sched_barrier(0);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
