@@ -60,7 +60,11 @@ __device__ __forceinline__ void pers_wait_rows(const PipeCtl& pc, const unsigned
 //     publish slot t & 1 (step t + 2's);
 //   t = n - 1: statistics of step n - 1, cursor unchanged, publish slot 0 (the next launch's).
 // Loads of anything written inside the launch are sc1 and every store the samples read is
-// written through.  One wave.
+// written through.  batch_ids (the serial layout's "this step's ids") is written at t = n - 1
+// only: the fp32 persistent launch's samples read their step-0 ids from it at their start, and a
+// launch-start write of step 1's ids there raced with late-starting samples (one in three
+// back-to-back launch sequences under load trained on wrong ids: tools/race_hunt.py,
+// profiles/r5/fp32_pers_race).  One wave.
 __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const PipeCtl& pc, int lane, int t) {
   const int n = pc.nsteps;
   const bool stats = t >= 0;
@@ -89,7 +93,7 @@ __device__ __forceinline__ void bookkeeping_pers(const ReduceArgs& a, const Pipe
   const long base = (long)next * a.batch;
   for (int b = lane; b < a.batch; b += 64) {
     const long g = base + b;
-    a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
+    if (t == n - 1) a.batch_ids[b] = g < a.order_len ? a.order[g] : 0;
     const long g2 = base + a.batch + b;
     st_wt_i(pc.nid_slot[sout] + b, g2 < a.order_len ? a.order[g2] : -1);
   }

@@ -321,10 +321,44 @@ def test_pipelined_long_run_under_load():
         torch.cuda.synchronize()
         assert not eng.pipe_failed()
         res.append((eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats()))
-    for r in res[1:3] + res[4:]:  # (bf16 variants against bf16 serial, fp32 persistent against fp32 serial)
-        r0 = res[0] if r is not res[4] else res[3]
-        assert torch.equal(r0[0], r[0]) and torch.equal(r0[1], r[1])
-        assert r0[2].loss_sum == r[2].loss_sum
+    names = ("bf16 serial", "bf16 pipelined", "bf16 persistent", "fp32 serial", "fp32 persistent")
+    for i in (1, 2, 4):  # (bf16 variants against bf16 serial, fp32 persistent against fp32 serial)
+        r, r0 = res[i], res[0] if i < 3 else res[3]
+        bad = (r0[0] != r[0]).nonzero().flatten()
+        assert torch.equal(r0[0], r[0]) and torch.equal(r0[1], r[1]), \
+            f"{names[i]}: {bad.numel()} master values differ, first at {bad[:8].tolist()}"
+        assert r0[2].loss_sum == r[2].loss_sum, names[i]
+
+
+def test_fp32_persistent_back_to_back_launches_race_regression():
+    """Round 5's fp32 persistent race (profiles/r5/fp32_pers_race): the launch-start bookkeeping
+    overwrote the batch ids that late-starting sample workgroups still had to read as their step-0
+    ids, so ~1 in 3 back-to-back chunk sequences (run_steps(60) = graphs of 32 + 16 + 8 + 4 steps)
+    next to a side stream trained on wrong samples.  15 such runs, each bit for bit against the
+    serial fp32 step (before the fix: P(no mismatch) ~ 0.65^15 < 0.2 %)."""
+    data = synthetic(4096, 12)
+    order = np.random.default_rng(4).permutation(4096).astype(np.int32)
+
+    def run(pers, seed):
+        eng = HipEngine(batch=64, arena=init_arena(seed=6), graph_chunk=32, pipeline=False, persist=pers, dtype="fp32")
+        assert eng.persist == pers
+        eng.attach(data)
+        side = torch.cuda.Stream()
+        x = torch.randn(2048, 2048, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed))
+        for _ in range(10):
+            eng.begin_epoch(order)
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    x = torch.tanh(x @ x * 1e-3)
+            eng.run_steps(60)
+        torch.cuda.synchronize()
+        assert not eng.pipe_failed()
+        return eng.master.cpu(), eng.mom.cpu(), eng.epoch_stats().loss_sum
+
+    ref = run(False, 0)
+    for r in range(15):
+        got = run(True, r + 1)
+        assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]) and ref[2] == got[2], f"run {r}"
 
 
 def test_direct_relaunch_minimal_pair_regression(tmp_path):

@@ -29,6 +29,7 @@
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
+#   racehunt:N[:variants[:VAR=val[:extra args]]]  tools/race_hunt.py (long run under load vs serial, per variant)
 #   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B)
 #   vgg              layer engine, cifar-vgg bf16 / fp32, split-K fc1 forward on / off
 set -e
@@ -140,6 +141,10 @@ for s in "$@"; do
         timeout -k 10 200 python bench.py --batch-size "$b" --steps 2000 --warmup 200 --no-epoch \
           > "$O/sweep_b$b.json" 2> "$O/sweep_b$b.err"
       done ;;
+    racehunt:*)  # racehunt:N[:variants[:VAR=val]] tools/race_hunt.py: the long-run-under-load comparison per variant
+      IFS=: read -r _ n vs kv xa <<< "$s"; [ -z "$vs" ] && vs=bf16-pipe,bf16-pers,fp32-pers; [ -z "$kv" ] && kv="DNN_NOTHING=0"
+      tag=$(echo "${vs}_${kv}_$xa" | tr ',=/ ' '-___')
+      env "$kv" timeout -k 10 500 python tools/race_hunt.py --rounds "$n" --variants "$vs" $xa > "$O/racehunt_$tag.txt" 2>&1 ;;
     useso:*)  # A/B of kernel builds in one call: copy ops/variants/NAME.so over the live extension
       cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" \
         distributed_neural_network_amd/ops/_dnn_hip.cpython-310-x86_64-linux-gnu.so ;;
