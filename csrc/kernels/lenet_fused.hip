@@ -1131,6 +1131,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   }
   bf16x8 w2f[4], w2t[3], w3t, w3f[3];
+  float bias_f1 = wr.f(OFF_F1B + min(ncol, 119));  // (first: waited for right after the R2 barrier, below)
   // Only the waves that use a fragment load it (fc2, fc3^T: waves 0-5; fc3: wave 0), and fc2^T's
   // (the MLP dgrad's) are loaded in phase D: the CU's vector-memory path is the bound here (a
   // wave stalls at issue while it is backed up, ~25 cycles per 1-KB wave load), and the record
@@ -1153,11 +1154,22 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       }
     }
   }
-  float bias_f1 = wr.f(OFF_F1B + min(ncol, 119));
   float bias_f2 = 0.f, bias_f3 = 0.f;
   if (wave < 6) bias_f2 = wr.f(OFF_F2B + min(ncol, 83));
   if (wave == 0) bias_f3 = wr.f(OFF_F3B + min(fr, 9));
   lds_barrier();
+  // Wave 7 has no conv2 tile: it streams the flipped conv2 kernel (20,480 B) for phase E now -
+  // LDS-DMA into REGB behind R2 (R1 is dead) - instead of every wave queueing three chunks at
+  // phase D's start.  bias_f1 is waited for first on every wave (it is the oldest MLP load, so
+  // only it): hipcc does not count the DMA, and a later wait of its own for a value this wave
+  // loaded before the stream would drain the stream with it.
+  consume(bias_f1);
+  if (TRAIN && wave == 7) {
+    const uint4* src = reinterpret_cast<const uint4*>(shadow + SH_WF);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGB + B_WF));
+#pragma unroll
+    for (int i = 0; i < 20; ++i) dma_w<PIPE>(src + i * 64 + lane, base + (uint32_t)i * 1024u);
+  }
   if (wave < 7) {
     const int t = wave;
     const int wi = fr >> 2, pi = fr & 3;
@@ -1189,30 +1201,25 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       CODE2[fr * 25 + qo] = best > 0.f ? (uint8_t)arg : (uint8_t)4;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // fc1 LDS-DMA and the MLP fragments landed
+  // fc1 LDS-DMA and the MLP fragments landed (wave 7: all but its 20 WF chunks, the newest -
+  // waited for at phase E's start); each fragment consumed only where it was loaded
+  if (TRAIN && wave == 7) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wave < 6) {
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) consume(w2f[ks]);
+    for (int ks = 0; ks < 4; ++ks) consume(w2f[ks]);
+    consume(w3t);
+    consume(bias_f2);
+  }
+  if (wave == 0) {
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) consume(w3f[ks]);
-  consume(w3t);
-  consume(bias_f1);
-  consume(bias_f2);
-  consume(bias_f3);
+    for (int ks = 0; ks < 3; ++ks) consume(w3f[ks]);
+    consume(bias_f3);
+  }
   lds_barrier();
 
   STAMP(3);
   // ============ phase D: MLP forward, cross-entropy, MLP data-backward ==================
-  if (TRAIN) {
-    // flipped conv2 kernel (20,480 B) for phase E: LDS-DMA into REGB behind R2 (W2 images
-    // and R1 are dead), in flight during the whole MLP
-    const uint4* src = reinterpret_cast<const uint4*>(shadow + SH_WF);
-    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_REGB + B_WF));
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int i = min(wave + 8 * k, 19);
-      dma_w<PIPE>(src + i * 64 + lane, base + (uint32_t)__builtin_amdgcn_readfirstlane(i) * 1024u);
-    }
-  }
   {  // fc1: h1 = relu(W1 a0 + b1), 120 x 400; wave w -> output tile w
     const bf16* wrow = fc1s + min(ncol, 119) * 400;
     bf16x8 av[13], bv[13];
@@ -1420,7 +1427,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (LDS-DMA, issued in phase D) landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // WF (wave 7's LDS-DMA, issued in phase C) landed
   lds_barrier();
   STAMP(8);
   // PERS: every wave's row stores (phase D') drained before that barrier: the MLP workgroups go
