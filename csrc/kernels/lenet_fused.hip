@@ -69,7 +69,8 @@ constexpr int L_DZ1B = L_DZ1 + 512;         // bf16 [128]
 constexpr int L_DA0 = L_DZ1B + 256;         // f32 [400]
 constexpr int L_IMG = L_DA0 + 1600;         // u8 [3][32][32] raw image (re-used by phase F)
 constexpr int L_MISC = L_IMG + 3072;
-constexpr int LDS_TOTAL = L_MISC + 64;      // 156,304 B
+constexpr int L_F1C = L_MISC + 64;          // u8 [80] phase F's conv1-wgrad column table (kF1Col)
+constexpr int LDS_TOTAL = L_F1C + 128;      // 156,432 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
@@ -604,6 +605,14 @@ __device__ __forceinline__ void dma_w(const void* gsrc, uint32_t lds_base) {
   else dma16(gsrc, lds_base);
 }
 
+// Phase F's conv1 weight gradient: which of the 75 columns (c, ky, kx) lane fr of wave w (< 5)
+// computes, kF1Col[16 w + fr] (bit 7: a padding lane - it reads that column, its result is
+// discarded).  The B fragments are R1 records at (c * 32 + ky) * 29 + 8 fg + kx: in column order
+// the 16 lanes of a ds_read_b128 lane group hit 8 of the 16 bank quads twice (2 LDS cycles per group
+// instead of 1, 140 reads per step: tools/lds_banks.py).  This assignment (a search over the
+// guide's lane groups) leaves 16 of the 20 (wave, group) pairs conflict-free.
+__constant__ unsigned char kF1Col[80] = {73, 39, 201, 19, 35, 65, 56, 42, 30, 27, 59, 33, 38, 3, 25, 62, 74, 20, 17, 0, 57, 23, 72, 36, 13, 53, 10, 4, 22, 202, 18, 34, 54, 182, 67, 41, 68, 28, 2, 71, 31, 11, 55, 15, 40, 6, 9, 58, 49, 51, 37, 177, 43, 44, 12, 63, 21, 26, 24, 14, 60, 61, 48, 64, 50, 7, 70, 47, 46, 69, 45, 1, 8, 16, 32, 5, 66, 29, 178, 52};
+
 // STAGED (TRAIN only): the image + label come from the stage buffer (see `stage` below)
 // PIPE (TRAIN + STAGED only): the pipelined step's merged launch (above)
 // PERS (PIPE only): the persistent launch - pc.nsteps steps, rows of both parities (above)
@@ -678,6 +687,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   int carry_lab = 0;
   const int nsteps = PERS ? pc.nsteps : 1;
   const unsigned g0 = PERS ? __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x)) : 0u;  // (PERS) generation
+  if (TRAIN && threadIdx.x < 80) smem[L_F1C + threadIdx.x] = kF1Col[threadIdx.x];  // (read in phase F)
   int s = 0;  // (a do-while: without PERS the body is straight-line code, no loop at all)
   do {
   // the lane's indices are re-derived in every step from an opaque copy of threadIdx.x: the
@@ -1594,7 +1604,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if (part == 0 && lane < 48) SLAB_PUT(SLAB_C1B + c, t);
   }
   if (wave < 5) {  // dW1[o][(c,ky,kx)] = sum_pix dY1[o][pix] * X[c][y+ky][x+kx]
-    const int n = wave * 16 + fr, nc = min(n, 74);
+    const int ent = smem[L_F1C + wave * 16 + fr];  // (kF1Col: column, bit 7 = padding lane)
+    const int nc = ent & 127;
     const int c = nc / 25, ky = (nc % 25) / 5, kx = nc % 5;
     // rows o >= 6 of A read past dY1 into other (finite) LDS data: they only feed
     // accumulator rows that are discarded, so the loads stay branch-free
@@ -1613,11 +1624,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
       for (int k = 0; k < 7; ++k) acc = mfma32(av[k], bv[k], acc);
     }
-    if (n < 75) {
+    if (ent < 128) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = 4 * fg + i;
-        if (o < 6) SLAB_PUT(SLAB_C1W + o * 75 + n, acc[i]);
+        if (o < 6) SLAB_PUT(SLAB_C1W + o * 75 + nc, acc[i]);
       }
     }
   }

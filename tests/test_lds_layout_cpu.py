@@ -71,3 +71,26 @@ def test_dgrad_window_reads_are_conflict_free():
                     total += cycles(a, G128, 16, 64)
                     ideal += 4
     assert total == ideal  # one LDS cycle per 16-lane group: 2112 per sample (the tid order took 4416)
+
+
+def test_conv1_wgrad_column_table():
+    """lenet_fused.hip kF1Col (phase F's conv1 weight gradient, column of lane fr of wave w):
+    every one of the 75 columns exactly once, padding lanes flagged, the kernel's table equal
+    to tools/lds_banks.py's, and its B reads (R1 records) at <= 4.8 LDS cycles per wave-
+    instruction on average against 8 in column order."""
+    import re
+
+    from lds_banks import F1COL, wgrad1
+
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels",
+                            "lenet_fused.hip")).read()
+    body = re.search(r"kF1Col\[80\] = \{([^}]*)\}", src).group(1)
+    assert [int(v) for v in body.split(",")] == F1COL
+    assert sorted(v for v in F1COL if v < 128) == list(range(75))
+    assert all(0 <= v - 128 < 75 for v in F1COL if v >= 128)
+
+    def avg(gen):
+        cs = [cycles(a, G128, 16, 64) for a in gen()]
+        return sum(cs) / len(cs)
+
+    assert avg(wgrad1("B")) <= 4.8 and avg(wgrad1("B", table=False)) == 8.0

@@ -130,14 +130,18 @@ def wgrad2():
             yield b
 
 
-def wgrad1(which):
+# lenet_fused.hip kF1Col: phase F's column of lane fr of wave w (bit 7: padding lane)
+F1COL = [73, 39, 201, 19, 35, 65, 56, 42, 30, 27, 59, 33, 38, 3, 25, 62, 74, 20, 17, 0, 57, 23, 72, 36, 13, 53, 10, 4, 22, 202, 18, 34, 54, 182, 67, 41, 68, 28, 2, 71, 31, 11, 55, 15, 40, 6, 9, 58, 49, 51, 37, 177, 43, 44, 12, 63, 21, 26, 24, 14, 60, 61, 48, 64, 50, 7, 70, 47, 46, 69, 45, 1, 8, 16, 32, 5, 66, 29, 178, 52]
+
+
+def wgrad1(which, table=True):
     def gen():
         for w in range(5):
             for k in range(28):
                 a = []
                 for l in lanes:
                     n = w * 16 + fr(l)
-                    nc = min(n, 74)
+                    nc = F1COL[n] & 127 if table else min(n, 74)
                     c, ky, kx = nc // 25, (nc % 25) // 5, nc % 5
                     if which == "A":
                         a.append(fr(l) * 1824 + fg(l) * 16 + k * 64)
@@ -186,5 +190,6 @@ if __name__ == "__main__":
     report("E  conv2 wgrad A/B (DY2, R2)", wgrad2)
     report("F  conv1 wgrad A (DY1 rows)", wgrad1("A"))
     report("F  conv1 wgrad B (R1 records)", wgrad1("B"))
+    report("F  conv1 wgrad B, column order", wgrad1("B", table=False))
     report("A/F R1 record build (write)", r1_write(False), "w128")
     report("E  R3 record build (write)", r3_write, "w128")
