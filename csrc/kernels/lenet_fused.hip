@@ -76,8 +76,10 @@ static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
 // REGA sub-layout during the conv backward (fc1 weights are dead after the MLP dgrad)
 constexpr int A_R3 = 0;                     // bf16x8 records [16][18][16 (14 used)] of padded dY2 73,728
-constexpr int A_DY2 = 73728;                // bf16 [16][10][16]                                 5,120
-constexpr int A_DP1 = A_DY2 + 5120;         // f32 [6][196]                                      4,704
+constexpr int A_DY2 = 73728;                // bf16 [16][10][16], channel stride DY2_CS          5,632
+constexpr int DY2_CS = 176;                 //   (elements = 22 x 16 B: the conv2-wgrad A reads are conflict-free,
+                                            //   4 LDS cycles per read instead of 8 at 160 - tools/lds_banks.py)
+constexpr int A_DP1 = A_DY2 + 16 * DY2_CS * 2;  // f32 [6][196]                                  4,704
 constexpr int A_RS = A_DP1 + 4704;          // f32 [16][10] dY2 row sums (conv2 bias grad)         640
 constexpr int A_DY1 = 0;                    // bf16 [6] x 1824 B (28 rows x 64 B + 32 B pad)    10,944
 constexpr int DY1_CH = 1824;                //   channel stride 456 dwords (= 8 mod 64): conv1-wgrad A reads conflict-free
@@ -1365,7 +1367,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (!PERS && btrace) stamps[16 + 4 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   // ============ phase E: conv2 backward =================================================
   // dY2 = unpool(dA0) masked by ReLU is materialised by rows, branch-free, twice:
-  //  * DY2 [16][10][16]: A operand of the conv2 weight gradient (8 pixels per lane),
+  //  * DY2 [16][10][16] (channel stride DY2_CS): A operand of the conv2 weight gradient (8 pixels per lane),
   //  * R3  [16][18][14] window records of dY2 zero-padded by 4 in x (y rows 4..13; the y
   //    padding rows are skipped by the consumer, never stored): A operand of
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
@@ -1405,7 +1407,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
         const int x = cc - 4;
         v[cc] = (x >= 0 && x < 10 && cd[x >> 1] == (yb | (x & 1))) ? da[x >> 1] : 0.f;
       }
-      bf16x8* drow = reinterpret_cast<bf16x8*>(DY2 + (o * 10 + y) * 16);
+      bf16x8* drow = reinterpret_cast<bf16x8*>(DY2 + o * DY2_CS + y * 16);
       if (half == 0) {
 #pragma unroll
         for (int xr = 0; xr < 7; ++xr) {
@@ -1495,7 +1497,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
     for (int sk = 0; sk < 5; ++sk) {
       const int y = 2 * sk + (fg >> 1), x0 = 8 * (fg & 1);
-      av[sk] = *reinterpret_cast<const bf16x8*>(DY2 + (fr * 10 + y) * 16 + x0);
+      av[sk] = *reinterpret_cast<const bf16x8*>(DY2 + fr * DY2_CS + y * 16 + x0);
     }
     for (int nt = nt_begin; nt < nt_end; nt += 2) {
       const bool two = nt + 1 < nt_end;

@@ -124,7 +124,7 @@ def wgrad2():
                 nc = min(n, 149)
                 c, ky, kx = nc // 25, (nc % 25) // 5, nc % 5
                 y, x0 = 2 * sk + (fg(l) >> 1), 8 * (fg(l) & 1)
-                a.append(64512 + 2 * ((fr(l) * 10 + y) * 16 + x0))
+                a.append(64512 + 2 * (fr(l) * 176 + y * 16 + x0))  # (DY2_CS = 176)
                 b.append(REGB + ((c * 14 + y + ky) * 13 + x0 + kx) * 16)
             yield a
             yield b
