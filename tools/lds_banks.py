@@ -51,13 +51,15 @@ def r1b(row, x):
 
 
 def phaseB():
-    for t in range(49):
+    # conv1 over output-pixel pairs (lenet_fused.hip phase B a_index): 25 tiles x 4 K-steps;
+    # A-row fr = (window wl = fr >> 1 of the tile, output row dy = fr & 1)
+    for t in range(25):
         for sk in range(4):
             a = []
             for l in lanes:
-                wi, pi = fr(l) >> 2, fr(l) & 3
-                q = 4 * t + wi
-                y, x = 2 * (q // 14) + (pi >> 1), 2 * (q % 14) + (pi & 1)
+                wl, dy = fr(l) >> 1, fr(l) & 1
+                q = min(8 * t + wl, 195)
+                y, x = 2 * (q // 14) + dy, 2 * (q % 14)
                 pr = min(4 * sk + fg(l), 14)
                 a.append(REGB + ((pr // 5 * 32 + y + pr % 5) * 29 + x) * 16)
             yield a
