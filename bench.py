@@ -49,7 +49,7 @@ from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa:
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
 from distributed_neural_network_amd.parallel import selflaunch  # noqa: E402
-from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, OVL_PATHS, allreduce_ab, default_candidates  # noqa: E402,E501
+from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, ab_window, allreduce_ab, default_candidates  # noqa: E402,E501
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
-    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + OVL_PATHS + BF16_PATHS + ("default",),
+    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + BF16_PATHS + ("default",),
                     help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
                          "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
@@ -106,10 +106,6 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="bf16: bf16 MFMA operands, fp32 accumulation / master weights (lenet_fused.hip); fp32: "
                          "fp32 operands throughout, the reference's arithmetic (lenet_f32.hip)")
-    ap.add_argument("--early-mlp", default="off", choices=("off", "mlp", "full"),
-                    help="bf16 fused engine, in-launch reduction (bit-identical to the serial step): mlp = the MLP "
-                         "reduction (+ exchange + SGD) in extra workgroups of the fused launch, polling the rows the "
-                         "samples publish as granules; full = the conv reduction + bookkeeping too (one launch/step)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the full-epoch timing")
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches (needed with DNN_BACKEND=gloo, whose collectives are not capturable)")
@@ -121,11 +117,24 @@ def main():
                          "inside the timed window (diagnostic)")
     args = ap.parse_args()
 
+    me = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     if args.gpus > 1 and not selflaunch.launcher_present():
-        # no launcher: become one (nothing has touched the GPU yet; children, never an exec)
-        sys.exit(selflaunch.run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
-                                out_fd=out_fd))
+        # no launcher: become one (nothing has touched the GPU yet; children, never an exec); a job
+        # that ends without a result is retried in fresh ranks with a conservative transport
+        sys.exit(selflaunch.run(me, args.gpus, out_fd=out_fd))
+    if selflaunch.supervisor_wanted():
+        # a torchrun rank: supervise the real rank as a child (same retry plan, coordinated
+        # through torchrun's store) - this process never touches the GPU
+        sys.exit(selflaunch.supervise(me, out_fd=out_fd))
     selflaunch.die_with_parent()  # (a self-launched rank: dies with its launcher; no-op otherwise)
+    # a retry attempt of the launcher (parallel/selflaunch.py ATTEMPTS): no xGMI group and no
+    # A/B (level 1: native RCCL, or the process group under gloo); level 2 adds eager launches
+    # (gloo host collectives cannot be captured)
+    safe = int(os.environ.get("DNN_SAFE_TRANSPORT", "0") or 0)
+    if safe:
+        args.allreduce = "default"
+        if safe >= 2:
+            args.no_graphs = True
     os.environ.setdefault("DNN_STARTUP_TRACE", "1")
     env = detect()
     if env.world != args.gpus:
@@ -144,9 +153,7 @@ def main():
     sampler = EpochSampler.for_rank(len(train), comm.rank, comm.world, seed=args.seed, mode="shard")
     if args.model == "lenet" and args.engine in ("auto", "fused"):
         engine = HipEngine(batch=B, seed=args.seed, device=device, graph_chunk=args.graph_chunk,
-                           overlap=args.overlap, use_graphs=not args.no_graphs, dtype=args.dtype,
-                           early_mlp=(args.early_mlp if args.early_mlp != "off" else False) if args.dtype == "bf16"
-                           else False)
+                           overlap=args.overlap, use_graphs=not args.no_graphs, dtype=args.dtype)
     else:  # modular layer engine (other models / fp32)
         engine = make_engine(str(device), B, 0.001, 0.9, seed=args.seed, model=args.model, engine="layers",
                              dtype=args.dtype, graph_chunk=min(args.graph_chunk, 16), use_graphs=not args.no_graphs)
@@ -156,7 +163,7 @@ def main():
     policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
     policy.record_waits = True  # per-step exchange wait stamps (one store per wave and step)
     policy.grad_comm = args.grad_comm
-    if args.allreduce in ORDER + OVL_PATHS + BF16_PATHS:
+    if args.allreduce in ORDER + BF16_PATHS:
         policy.path = args.allreduce
     stamp(comm.rank, f"engine {type(engine).__name__} ready; installing the all-reduce path")
     policy.attach(engine)
@@ -174,8 +181,8 @@ def main():
         eval_metrics(wl + wl2, wc.float() + wc2, B)
     ab = {}
     if comm.distributed and args.sync == "step-allreduce" and args.allreduce == "ab":
-        ab_steps = args.ab_steps or min(args.steps, 256)
-        ab = allreduce_ab(policy, engine, cur, steps=ab_steps, warmup=args.warmup, reps=args.ab_reps,
+        ab_steps, ab_warm = ab_window(cur.steps_per_epoch, args.ab_steps or args.steps, args.warmup)
+        ab = allreduce_ab(policy, engine, cur, steps=ab_steps, warmup=ab_warm, reps=args.ab_reps,
                           candidates=default_candidates(args.grad_comm),
                           log=lambda m: stamp(comm.rank, m) if comm.rank == 0 else None)
         stamp(comm.rank, f"all-reduce A/B (us/step, max over ranks): {ab}")
@@ -209,6 +216,7 @@ def main():
     xg = getattr(engine.grad_sync, "group", None)
     if xg is not None:
         xg.reset_wait_stats()
+    stamp(comm.rank, selflaunch.WINDOW_MARK)  # (the launcher records failures before / after this line)
     comm.barrier()
     torch.cuda.synchronize(device)
 
@@ -307,7 +315,6 @@ def main():
                "config": {"model": "reference CIFAR-10 CNN (models/model.py Network, 62,006 params)"
                           if args.model == "lenet" else args.model,
                           "engine": type(engine).__name__,
-                          "early_mlp": getattr(engine, "early_mlp", False) or "off",
                           # pipelined step: step k's reduction + SGD in step k+1's launch (lenet_fused.hip PIPE)
                           "pipelined_step": bool(getattr(engine, "_pipe_ok", lambda: False)()),
                           # persistent launch: the whole timed window's steps in one launch (lenet_fused.hip PERS)
@@ -315,7 +322,9 @@ def main():
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
-                          "allreduce": policy.installed(engine) if hasattr(policy, "installed") else None},
+                          "allreduce": policy.installed(engine) if hasattr(policy, "installed") else None,
+                          # launcher retry level this number was measured at (0: as requested)
+                          "safe_transport": safe},
                **epoch}
         if ab:
             out["allreduce_ab"] = ab["allreduce_ab"]

@@ -48,25 +48,10 @@ using u = uintptr_t;
 template <typename T>
 static T* P(u x) { return reinterpret_cast<T*>(x); }
 static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
-// in-launch reduction (one launch per step): grad_reduce(defer=1) stores the MLP and the conv
-// reduction's arguments here and the next fused_train(inlaunch=1) runs them as extra workgroups
-static dnn::ReduceArgs g_pending_mlp{}, g_pending_conv{};
-static bool g_pending_mlp_set = false, g_pending_conv_set = false;
 // pipelined step: grad_reduce(defer=2) stores the previous step's reduction for the next
 // fused_train_pipe launch
 static dnn::ReduceArgs g_pending_pipe{};
 static bool g_pending_pipe_set = false;
-// the last cached persistent launch (fused_train_persist(cache=1)), relaunched by persist_relaunch
-struct PersCache {
-  const uint8_t* images; const int32_t* labels; int order_len, batch;
-  const float* master; const bf16* shadow;
-  float *a0, *h1, *h2, *z1, *z2, *z3, *slab, *loss;
-  int32_t* correct; long long* stamps; unsigned char* stage;
-  dnn::ReduceArgs red; dnn::PipeCtl pc;
-};
-static PersCache g_pers_cache{};
-static bool g_pers_cache_set = false;
-static long long g_pers_cache_handle = 0;  // the caller's key of the cached launch
 
 PYBIND11_MODULE(_dnn_hip, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the data-parallel CIFAR-10 CNN engine";
@@ -84,28 +69,19 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("fused_train",
         [](u images, u labels, u order, int order_len, int batch, u state, u master, u shadow, u a0, u h1, u h2,
-           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage, u rowg,
-           u rowg_ctr, int inlaunch, u codes) {
-          // inlaunch 1: the MLP reduction in-launch (conv reduction: its own launch after);
-          // 2: both (the whole step in one launch) - from the grad_reduce(defer=1) calls before
-          if (inlaunch && !(g_pending_mlp_set && (inlaunch == 1 || g_pending_conv_set)))
-            throw std::runtime_error("fused_train(inlaunch) needs the grad_reduce(defer=1) calls of its ranges first");
-          const dnn::ReduceArgs* red = inlaunch ? &g_pending_mlp : nullptr;
-          const dnn::ReduceArgs* redc = inlaunch == 2 ? &g_pending_conv : nullptr;
-          g_pending_mlp_set = g_pending_conv_set = false;
+           u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps, u next_ids, u stage, u codes) {
           dnn::launch_fused_train(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order),
                                   order_len, batch, P<int32_t>(state), P<const float>(master),
                                   P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
                                   P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct),
                                   P<long long>(stamps), P<const int32_t>(next_ids), P<unsigned char>(stage),
-                                  S(stream), P<unsigned long long>(rowg), P<unsigned>(rowg_ctr), red, redc,
-                                  P<uint8_t>(codes));
+                                  S(stream), P<uint8_t>(codes));
         },
         py::arg("images"), py::arg("labels"), py::arg("order"), py::arg("order_len"), py::arg("batch"),
         py::arg("state"), py::arg("master"), py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"),
         py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"), py::arg("correct"),
         py::arg("stream"), py::arg("stamps") = 0, py::arg("next_ids") = 0, py::arg("stage") = 0,
-        py::arg("rowg") = 0, py::arg("rowg_ctr") = 0, py::arg("inlaunch") = 0, py::arg("codes") = 0);
+        py::arg("codes") = 0);
   m.def("fused_train_f32", [](u images, u labels, u order, int order_len, int batch, u state, u master, u a0, u h1,
                               u h2, u z1, u z2, u z3, u slab, u loss, u correct, u stream, u stamps) {
     dnn::launch_fused_train_f32(P<const uint8_t>(images), P<const int32_t>(labels), P<const int32_t>(order), order_len,
@@ -130,7 +106,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           int fuse_sgd, int lo, int hi, int bookkeeping, u order, int order_len, u batch_ids,
                           u stream, u stamps, const std::vector<u>& xp_regions, int xp_rank, long long xp_capacity, u xp_ctr,
                           u xp_err, u xp_abort, double xp_timeout_s, float xp_scale, u next_ids, int xp_mode,
-                          u xp_wait, u rg, u rg_ctr, u rg_err, double rg_timeout_s, int defer, u bk_bv_in,
+                          u xp_wait, int defer, u bk_bv_in,
                           u bk_bv_out, int bk_adv, int bk_stats) {
     dnn::ReduceArgs a{P<const float>(a0), P<const float>(h1), P<const float>(h2), P<const float>(z1),
                       P<const float>(z2), P<const float>(z3), P<const float>(slab), P<const float>(loss),
@@ -144,21 +120,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
     if (bk_adv < 0 || bk_adv > 1) throw std::runtime_error("grad_reduce: bk_adv is 0 or 1");
     a.bk_adv = bk_adv;
     a.bk_stats = bk_stats;
-    a.rg = P<const unsigned long long>(rg);
-    a.rg_ctr = P<unsigned>(rg_ctr);
-    a.rg_err = P<unsigned>(rg_err);
-    a.rg_timeout_ticks = (long long)(rg_timeout_s * 1.0e8);
     if (!xp_regions.empty()) {
       if ((int)xp_regions.size() > dnn::XG_MAX_RANKS || xp_rank < 0 || xp_rank >= (int)xp_regions.size())
         throw std::runtime_error("grad_reduce exchange: 1..8 ranks, rank in range");
-      // the whole arena, or one of the two split launches (early-MLP overlap): MLP range with
-      // counters from block 0, conv range with counters after the MLP launch's blocks
-      const bool whole = lo == 0 && hi >= dnn::ARENA, mlp = lo == dnn::OFF_F1W && hi >= dnn::ARENA,
-                 conv = lo == 0 && hi == dnn::OFF_F1W;
-      if (!(whole || mlp || conv) || xp_capacity < dnn::ARENA || !xp_ctr || !xp_err || !xp_abort)
-        throw std::runtime_error("grad_reduce exchange: whole arena or a split range, region capacity >= arena, "
-                                 "counters set");
-      a.xp_blk_off = conv ? dnn::grad_reduce_mlp_blocks() : 0;
+      // the exchange takes the whole arena (every block's elements have one step counter)
+      if (!(lo == 0 && hi >= dnn::ARENA) || xp_capacity < dnn::ARENA || !xp_ctr || !xp_err || !xp_abort)
+        throw std::runtime_error("grad_reduce exchange: the whole arena, region capacity >= arena, counters set");
       for (size_t r = 0; r < xp_regions.size(); ++r) a.xp_region[r] = P<unsigned char>(xp_regions[r]);
       a.xp_rank = xp_rank;
       a.xp_nranks = (int)xp_regions.size();
@@ -180,12 +147,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
       g_pending_pipe_set = true;
       return;
     }
-    if (defer) {  // (in-launch reduction) kept for the next fused_train(inlaunch=1) launch
-      if (lo == dnn::OFF_F1W) { g_pending_mlp = a; g_pending_mlp_set = true; }
-      else if (lo == 0 && hi == dnn::OFF_F1W) { g_pending_conv = a; g_pending_conv_set = true; }
-      else throw std::runtime_error("grad_reduce(defer=1): the MLP range or the conv range");
-      return;
-    }
+    if (defer) throw std::runtime_error("grad_reduce: defer is 0 or 2 (the pipelined / persistent launch)");
     dnn::launch_grad_reduce(a, S(stream));
   }, py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"),
      py::arg("loss"), py::arg("correct"), py::arg("batch"), py::arg("master"), py::arg("grad"), py::arg("mom"),
@@ -195,7 +157,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("xp_regions") = std::vector<u>{}, py::arg("xp_rank") = 0, py::arg("xp_capacity") = 0,
      py::arg("xp_ctr") = 0, py::arg("xp_err") = 0, py::arg("xp_abort") = 0, py::arg("xp_timeout_s") = 60.0,
      py::arg("xp_scale") = 1.0f, py::arg("next_ids") = 0, py::arg("xp_mode") = 0, py::arg("xp_wait") = 0,
-     py::arg("rg") = 0, py::arg("rg_ctr") = 0, py::arg("rg_err") = 0, py::arg("rg_timeout_s") = 10.0,
      py::arg("defer") = 0, py::arg("bk_bv_in") = 0, py::arg("bk_bv_out") = 0, py::arg("bk_adv") = 1,
      py::arg("bk_stats") = 1);
   // the pipelined step's merged launch (lenet_fused.hip PIPE): the reduction of the previous
@@ -230,8 +191,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   // last grad_reduce(defer=2) call's (rows of parity 0, parity 1 right after them)
   m.def("fused_train_persist", [](u images, u labels, int order_len, int batch, u master, u shadow, u a0, u h1, u h2,
                                   u z1, u z2, u z3, u slab, u loss, u correct, u stage, u ctl, int nsteps, u bv0,
-                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags,
-                                  long long cache) {
+                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags) {
     if (!g_pending_pipe_set) throw std::runtime_error("fused_train_persist needs a grad_reduce(defer=2) call first");
     g_pending_pipe_set = false;
     dnn::PipeCtl pc;
@@ -244,40 +204,18 @@ PYBIND11_MODULE(_dnn_hip, m) {
     pc.err = P<unsigned>(err);
     pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
     pc.flags = flags;
-    PersCache c{P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch, P<const float>(master),
-                P<const bf16>(shadow), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1), P<float>(z2),
-                P<float>(z3), P<float>(slab), P<float>(loss), P<int32_t>(correct), P<long long>(stamps),
-                P<unsigned char>(stage), g_pending_pipe, pc};
-    dnn::launch_fused_train_persist(c.images, c.labels, c.order_len, c.batch, c.master, c.shadow, c.a0, c.h1, c.h2,
-                                    c.z1, c.z2, c.z3, c.slab, c.loss, c.correct, c.stamps, c.stage, c.red, pc,
-                                    S(stream));
-    if (cache) {  // (after a launch that passed every argument check) - cache = the caller's handle
-      g_pers_cache = c;
-      g_pers_cache_set = true;
-      g_pers_cache_handle = cache;
-    }
+    dnn::launch_fused_train_persist(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
+                                    P<const float>(master), P<const bf16>(shadow), P<float>(a0), P<float>(h1),
+                                    P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
+                                    P<float>(loss), P<int32_t>(correct), P<long long>(stamps), P<unsigned char>(stage),
+                                    g_pending_pipe, pc, S(stream));
   }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"),
      py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
      py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("stage"), py::arg("ctl"), py::arg("nsteps"),
      py::arg("bv0"), py::arg("bv1"), py::arg("nid0"), py::arg("nid1"), py::arg("err"), py::arg("timeout_s"),
-     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0, py::arg("cache") = 0);
-  // Cached persistent launch: fused_train_persist(cache=1) keeps its whole argument block here;
-  // persist_relaunch(nsteps, stream) launches it again with another step count - ONE kernel, so a
-  // chunk needs no graph (a graph replay costs ~8 us of host submit, this ~3-4 us; measured in
-  // tools/window_host_probe.py)
-  m.def("persist_relaunch", [](long long handle, int nsteps, u stream) {
-    if (!g_pers_cache_set || handle != g_pers_cache_handle)
-      throw std::runtime_error("persist_relaunch: the cached launch is not this handle's");
-    dnn::PipeCtl pc = g_pers_cache.pc;
-    pc.nsteps = nsteps;
-    const auto& c = g_pers_cache;
-    dnn::launch_fused_train_persist(c.images, c.labels, c.order_len, c.batch, c.master, c.shadow, c.a0, c.h1, c.h2,
-                                    c.z1, c.z2, c.z3, c.slab, c.loss, c.correct, c.stamps, c.stage, c.red, pc,
-                                    S(stream));
-  });
-  m.def("persist_cached", [](long long handle) { return g_pers_cache_set && handle == g_pers_cache_handle; });
+     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0);
   // the fp32 kernel's persistent launch (lenet_f32.hip PERS): the reduction is the last
-  // grad_reduce(defer=2) call's (graph replays only: no cached relaunch)
+  // grad_reduce(defer=2) call's
   m.def("fused_train_persist_f32", [](u images, u labels, int order_len, int batch, u master, u a0, u h1, u h2, u z1,
                                       u z2, u z3, u slab, u loss, u correct, u ctl, int nsteps, u bv0, u bv1, u nid0,
                                       u nid1, u err, double timeout_s, u stream, int flags, u stamps) {
@@ -576,8 +514,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_xp_max_blocks", []() { return dnn::XP_MAX_BLOCKS; });
   m.def("xgmi_wait_ring", []() { return py::make_tuple(dnn::XP_WAIT_RING, dnn::XP_MAX_BLOCKS, 4); });
   m.def("grad_reduce_blocks", []() { return dnn::grad_reduce_blocks(); });
-  m.def("grad_reduce_mlp_blocks", []() { return dnn::grad_reduce_mlp_blocks(); });
-  m.def("row_granules", []() { return dnn::RG_ROW; });  // granules per sample (early-MLP overlap)
   m.def("xgmi_allreduce", [](std::vector<u> regions, int rank, long long capacity, int n, u grad, u out, u master,
                              u mom, u shadow, float lr, float momentum, float scale, int mode, u ctr, u abort_w,
                              double timeout_s, u stream, int form, u wait) {

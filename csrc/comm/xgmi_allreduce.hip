@@ -298,18 +298,19 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity) {
 }
 
 // Uncached (fine-grained) device memory, zeroed, for on-GPU hand-offs by tagged granules
-// between concurrently running kernels (the early-MLP row granules): every access bypasses
+// between concurrently running kernels (the pipelined / persistent step's control words): every access bypasses
 // the per-XCD L2s, as the xGMI regions' do.  Freed with xgmi_free.
 //
 // Pooled: a block given back with uncached_free is kept for the next request of its size class
-// (zeroed again on reuse), never returned to the driver - an engine's control words, flags and
-// row granules are re-allocated by every engine a process builds (tests, A/B candidates), and
+// ON THE SAME DEVICE (zeroed again on reuse), never returned to the driver - an engine's control
+// words and flags are re-allocated by every engine a process builds (tests, A/B candidates), and
 // each hipFree / hipExtMallocWithFlags pair of fine-grained memory cost a device-wide
 // synchronisation and a page-table update while other engines' kernels were queued.
 namespace {
 std::mutex g_uc_mu;
-std::multimap<long long, void*> g_uc_free;     // size class -> free blocks
-std::map<void*, long long> g_uc_size;          // every pooled block -> its size class
+using UcKey = std::pair<int, long long>;       // (device, size class)
+std::multimap<UcKey, void*> g_uc_free;         // (device, size class) -> free blocks
+std::map<void*, UcKey> g_uc_size;              // every pooled block -> its device and size class
 long long g_uc_violations = 0;                 // reused blocks whose canary was overwritten while free
 long long uc_class(long long bytes) { return std::max<long long>(4096, (bytes + 4095) / 4096 * 4096); }
 constexpr unsigned char UC_CANARY = 0xA5;
@@ -324,10 +325,12 @@ bool uc_check_canary() {
 
 uintptr_t uncached_alloc(long long bytes) {
   const long long cls = uc_class(bytes);
+  int dev = 0;
+  xcheck(hipGetDevice(&dev), "hipGetDevice");
   void* p = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_uc_mu);
-    auto it = g_uc_free.find(cls);
+    auto it = g_uc_free.find(UcKey{dev, cls});
     if (it != g_uc_free.end()) {
       p = it->second;
       g_uc_free.erase(it);
@@ -348,7 +351,7 @@ uintptr_t uncached_alloc(long long bytes) {
   if (p == nullptr) {
     xcheck(hipExtMallocWithFlags(&p, cls, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
     std::lock_guard<std::mutex> lk(g_uc_mu);
-    g_uc_size[p] = cls;
+    g_uc_size[p] = UcKey{dev, cls};
   }
   xcheck(hipMemset(p, 0, cls), "hipMemset(uncached)");
   xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -358,19 +361,20 @@ uintptr_t uncached_alloc(long long bytes) {
 // Give an uncached_alloc block back to the pool (the caller has synchronised: no kernel uses it).
 void uncached_free(uintptr_t p) {
   if (!p) return;
-  long long cls = 0;
+  UcKey key{0, 0};
   {
     std::lock_guard<std::mutex> lk(g_uc_mu);
     auto it = g_uc_size.find(reinterpret_cast<void*>(p));
     if (it == g_uc_size.end()) throw std::runtime_error("uncached_free: not a pooled uncached block");
-    cls = it->second;
+    key = it->second;
   }
+  const long long cls = key.second;
   if (uc_check_canary()) {
     xcheck(hipMemset(reinterpret_cast<void*>(p), UC_CANARY, cls), "hipMemset(uncached canary)");
     xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   }
   std::lock_guard<std::mutex> lk(g_uc_mu);
-  g_uc_free.emplace(cls, reinterpret_cast<void*>(p));
+  g_uc_free.emplace(key, reinterpret_cast<void*>(p));
 }
 
 // (diagnostic) pooled blocks: (total, free, canary violations seen on reuse)

@@ -47,41 +47,6 @@ constexpr int H2_LD = 84;   // relu(fc2)
 constexpr int Z1_LD = 120;  // dL/d(fc1 pre-activation)
 constexpr int Z2_LD = 84;   // dL/d(fc2 pre-activation)
 constexpr int Z3_LD = 16;   // dL/dlogits (10 used)
-// In-launch reduction (row granules): sample b's six MLP rows, its conv gradient slab and its
-// {loss, correct} as 8-byte {fp32 value, step} words in one buffer
-// [a0 | h1 | h2 | z1 | z2 | z3 | slab | lc] x batch, written by the fused kernel's sample
-// workgroups with system-scope stores and polled by the reduction workgroups of the same launch
-// until each tag shows the step - no flag, fence or kernel boundary between the two.
-constexpr int RG_LC = 2;  // {loss, correct}: published last, after the sample's every other read
-constexpr int RG_ROW = A0_LD + H1_LD + H2_LD + Z1_LD + Z2_LD + Z3_LD + SLAB + RG_LC;  // granules per sample
-constexpr int RG_SLAB = 6, RG_LCK = 7;  // kinds of the slab and {loss, correct} rows
-__device__ __forceinline__ long long rg_off(int which, int batch) {  // start of row kind `which`
-  // (prefix sums of the row lengths a0 | h1 | h2 | z1 | z2 | z3 | slab: no array, no scratch)
-  const int pre = which <= 0 ? 0 : which == 1 ? A0_LD : which == 2 ? A0_LD + H1_LD
-                : which == 3 ? A0_LD + H1_LD + H2_LD : which == 4 ? A0_LD + H1_LD + H2_LD + Z1_LD
-                : which == 5 ? A0_LD + H1_LD + H2_LD + Z1_LD + Z2_LD
-                : which == 6 ? A0_LD + H1_LD + H2_LD + Z1_LD + Z2_LD + Z3_LD
-                             : A0_LD + H1_LD + H2_LD + Z1_LD + Z2_LD + Z3_LD + SLAB;
-  return (long long)batch * pre;
-}
-
-__device__ __forceinline__ void rg_put(unsigned long long* rg, long long idx, unsigned tag, float v) {
-  __hip_atomic_store(rg + idx, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// the fused kernels' side: sample b's six rows (null source: zeros) as {value, tag} words
-__device__ __forceinline__ void put_row_granules(unsigned long long* rg, int batch, int b, unsigned tag, int tid,
-                                                 int nt, const float* a0, const float* h1, const float* h2,
-                                                 const float* z1, const float* z2, const float* z3) {
-  const float* src[6] = {a0, h1, h2, z1, z2, z3};
-  constexpr int ld[6] = {A0_LD, H1_LD, H2_LD, Z1_LD, Z2_LD, Z3_LD};
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    unsigned long long* row = rg + rg_off(k, batch) + (long long)b * ld[k];
-    for (int i = tid; i < ld[k]; i += nt) rg_put(row, i, tag, src[k] != nullptr ? src[k][i] : 0.f);
-  }
-}
-
 constexpr int IMG = 3 * 32 * 32;
 
 // ---- bf16 shadow buffer: [plain copy of the arena | kernel-ready weight images] -------

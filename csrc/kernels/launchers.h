@@ -46,18 +46,6 @@ struct ReduceArgs {
   // diagnostic / accounting: per-step exchange wait (max over lanes, s_memrealtime ticks) as
   // {step << 32 | ticks} words in a ring of XP_WAIT_RING entries (one plain store per wave)
   unsigned long long* xp_wait = nullptr;
-  // split exchange launches (early-MLP overlap): this launch's blocks use step counters and the
-  // two-hop owner mapping of blocks xp_blk_off + blockIdx (the two launches take disjoint
-  // ranges, so every element keeps one counter)
-  int xp_blk_off = 0;
-  // early-MLP overlap (rg != nullptr, MLP-range launch only): the MLP rows are read as
-  // {value, step} granules (common.h RG_ROW) written by the concurrently running fused kernel;
-  // rg_ctr[block] counts this launch's steps (the fused kernel's blocks count theirs), a wait
-  // past rg_timeout_ticks or a set abort word sets *rg_err (sticky) instead of hanging
-  const unsigned long long* rg = nullptr;
-  unsigned* rg_ctr = nullptr;
-  unsigned* rg_err = nullptr;
-  long long rg_timeout_ticks = 0;
   // Bookkeeping slots (null: the serial layout - bvalid in state[ST_BVALID], ids in next_ids).
   // The pipelined step (lenet_fused.hip, PIPE) publishes one launch ahead into the other of
   // two {bvalid, next_ids} slots: bk_bv_in = bvalid of the step whose statistics this launch
@@ -98,9 +86,7 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
-                        hipStream_t stream, unsigned long long* rowg = nullptr, unsigned* rowg_ctr = nullptr,
-                        const ReduceArgs* mlp_red = nullptr, const ReduceArgs* conv_red = nullptr,
-                        uint8_t* codes = nullptr);
+                        hipStream_t stream, uint8_t* codes = nullptr);
 // The pipelined step's merged launch: [reduction of the previous step (red, plain rows of the
 // other parity)] + [samples of this step, writing this parity's rows]; see PipeCtl.
 void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int order_len, int batch,
@@ -150,8 +136,6 @@ void init_kernels();
 void init_kernels_f32();
 void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream);
 int grad_reduce_blocks();  // grid of a whole-arena grad_reduce launch (with bookkeeping)
-int grad_reduce_mlp_blocks();  // grid of its MLP-range part (the split launches' block offset)
-int inlaunch_mlp_workgroups();  // extra workgroups of a fused launch with the in-launch MLP reduction
 void launch_epoch_begin(const int32_t* staged, int32_t* order, int n, int32_t* state, int32_t* batch_ids, int batch,
                         const uint8_t* images, const int32_t* labels, int32_t* next_ids, unsigned char* stage,
                         hipStream_t stream);

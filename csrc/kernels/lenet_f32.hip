@@ -187,7 +187,7 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane_o, t);
     } else if (rblk >= 0) {
-      grad_reduce_body<false, WtF32Sink, true>(a, sk, rblk, tid_o & 255, 0, false, t & 1);
+      grad_reduce_body<WtF32Sink, true>(a, sk, rblk, tid_o & 255, t & 1);
     }
     if (st) stamps[6145 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     // (diagnostic: the last step's per-wave body done / drained, stamps[6400 + 32 wg + 2 wave + k])
@@ -1090,7 +1090,7 @@ void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels
   if (pc_in.ctr == nullptr || pc_in.err == nullptr || !pc_in.bv_slot[0] || !pc_in.bv_slot[1] || !pc_in.nid_slot[0] ||
       !pc_in.nid_slot[1])
     throw std::runtime_error("fused_train_persist_f32: needs the control block, the error word and both slots");
-  if (!red.bookkeeping || red.batch != batch || red.rg != nullptr || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA ||
+  if (!red.bookkeeping || red.batch != batch || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA ||
       red.xp_nranks != 0 || red.batch_ids == nullptr || red.master != master)
     throw std::runtime_error("fused_train_persist_f32: a local whole-arena fused-SGD reduction with bookkeeping");
   if (red.a0 != a0 || red.h1 != h1 || red.h2 != h2 || red.z1 != z1 || red.z2 != z2 || red.z3 != z3 ||

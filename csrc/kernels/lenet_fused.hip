@@ -314,7 +314,7 @@ __device__ __forceinline__ void pipe_reduce(const ReduceArgs& a, const PipeCtl& 
       else { rblk = m - PIPE_CONV_BLOCKS - 1; grp = PG_MLP; }
     }
     WtSink sk;
-    grad_reduce_body<false>(a, sk, rblk, rtid);
+    grad_reduce_body(a, sk, rblk, rtid);
   }
   if (stamps != nullptr && threadIdx.x == 0) stamps[16 + 4 * wg + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its write-through stores
@@ -542,13 +542,13 @@ __device__ __forceinline__ void pers_reduce(const ReduceArgs& a, const PipeCtl& 
       sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
                                                                (step & 1u) * a.xp_gslot_bytes)
                        : nullptr;
-      if (grad_reduce_body<false, XpSinkT<false, true>, true>(a, sk, rblk, rtid_s, 0, false, t & 1)) {
+      if (grad_reduce_body<XpSinkT<false, true>, true>(a, sk, rblk, rtid_s, t & 1)) {
         if ((a.xp_mode & 2) == 0) xp_exchange<XNR, false, true>(a, sk, step, failed, rblk, rtid_s);
         else xp_exchange_rsag<XNR, false, true>(a, sk, step, failed, rblk, rtid_s);
       }
     } else {
       WtSink sk;
-      grad_reduce_body<false, WtSink, true>(a, sk, rblk, rtid_s, 0, false, t & 1);
+      grad_reduce_body<WtSink, true>(a, sk, rblk, rtid_s, t & 1);
     }
     if (st) stamps[2401 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     // (diagnostic: the last step's per-wave body done / drain done of the conv1 workgroups)
@@ -619,7 +619,7 @@ __constant__ unsigned char kF1Col[80] = {73, 39, 201, 19, 35, 65, 56, 42, 30, 27
 // PIPE (TRAIN + STAGED only): the pipelined step's merged launch (above)
 // PERS (PIPE only): the persistent launch - pc.nsteps steps, rows of both parities (above)
 // XNR (PERS only): the per-step xGMI all-reduce inside the launch for groups of up to XNR ranks (0: none)
-template <bool TRAIN, bool STAGED = false, int RNR = 0, bool PIPE = false, bool PERS = false, int XNR = 0>
+template <bool TRAIN, bool STAGED = false, bool PIPE = false, bool PERS = false, int XNR = 0>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) lenet_fused_kernel(
     const uint8_t* __restrict__ images,   // [N][3][32][32] u8 (CIFAR binary order)
     const int32_t* __restrict__ labels,   // [N]
@@ -635,17 +635,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     uint8_t* __restrict__ codes_out,       // TRAIN, diagnostic (tests): [batch][6*196 + 400] pool argmax codes
     const int32_t* __restrict__ next_ids,  // TRAIN + stage: sample ids of the NEXT step (-1: none)
     unsigned char* __restrict__ stage,     // TRAIN: [batch][IMG] u8 images + [batch] labels of THIS step
-    unsigned long long* __restrict__ rowg,  // TRAIN, early-MLP overlap: the MLP rows as granules
-    unsigned* __restrict__ rowg_ctr,        //   and this block's step counter (common.h RG_ROW)
-    const ReduceArgs ra, const ReduceArgs rc,  //   and the in-launch reduction: MLP (ra), conv + bookkeeping (rc)
-    const PipeCtl pc) {                     // PIPE: ra = the previous step's reduction, pc its control
-  static_assert(!PIPE || (TRAIN && STAGED && RNR == 0), "the pipelined step is a staged training launch");
+    const ReduceArgs ra,                   // PIPE: the previous step's reduction,
+    const PipeCtl pc) {                     //   pc its control
+  static_assert(!PIPE || (TRAIN && STAGED), "the pipelined step is a staged training launch");
   static_assert(!PERS || PIPE, "the persistent launch is a PIPE grid");
   static_assert(XNR == 0 || PERS, "the in-launch exchange is a persistent-launch feature");
-  if constexpr (PIPE) {  // (no early-MLP granules in a PIPE / PERS launch: their code is dead here)
-    rowg = nullptr;
-    rowg_ctr = nullptr;
-  }
   // stage (optional): block b of step c stores the image + label of step c + 1's sample b
   // there during phase F (next_ids: published two steps ahead by the reduce kernel's
   // bookkeeping; epoch_begin stages step 0); step c + 1 then loads its image from a fixed
@@ -664,19 +658,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     if ((int)blockIdx.x < nrw) {
       if constexpr (PERS) pers_reduce<XNR>(ra, pc, blockIdx.x, XNR > 1 ? nullptr : stamps);  // (XNR: at the register limit)
       else pipe_reduce(ra, pc, blockIdx.x, stamps);
-      if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-      return;
-    }
-  }
-  if constexpr (TRAIN) {
-    // in-launch reduction: workgroups past the samples reduce the MLP gradient, then the conv
-    // gradient + bookkeeping (+ exchange + SGD), polling the rows, slab and {loss, correct} the
-    // sample workgroups publish as granules - the MLP part while the samples still run the
-    // conv backward.  Dispatched after the samples (higher ids), no LDS use.
-    if (RNR > 0 && (int)blockIdx.x >= batch) {
-      const int wg = (int)blockIdx.x - batch;
-      if (wg < INLAUNCH_MLP_WG) inlaunch_reduce<RNR>(ra, wg, INLAUNCH_MLP_BLOCKS);  // (rc only if launched)
-      else inlaunch_reduce<RNR>(rc, wg - INLAUNCH_MLP_WG, INLAUNCH_CONV_BLOCKS);
       if (btrace) stamps[16 + 4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
       return;
     }
@@ -755,11 +736,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     valid = gidx < order_len;
     sample = (int)gidx;
   }
-  // early-MLP overlap: this step's row tag, read by every thread before thread 0 advances the
-  // counter (several workgroup barriers later)
-  const unsigned row_tag = (TRAIN && rowg != nullptr) ? rowg_ctr[b] + 1u : 0u;
-  // in-launch conv reduction too (rc set): the slab and {loss, correct} go out as granules
-  const bool conv_g = TRAIN && RNR > 0 && rc.rg != nullptr;
   float my_loss = 0.f;
   int my_correct = 0;
   // a row element: plain, or (PERS) written through - the reduction of the same launch reads it
@@ -808,20 +784,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     }
   };
   if (!valid) {
-    if (TRAIN && rowg != nullptr) {
-      put_row_granules(rowg, batch, b, row_tag, tid, NT, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
-      if (conv_g)
-        for (int i = tid; i < SLAB; i += NT) rg_put(rowg, rg_off(RG_SLAB, batch) + (long long)b * SLAB + i, row_tag, 0.f);
-      __syncthreads();
-      if (tid == 0) {
-        rowg_ctr[b] = row_tag;
-        if (conv_g) {
-          const long long lc = rg_off(RG_LCK, batch) + (long long)RG_LC * b;
-          rg_put(rowg, lc, row_tag, 0.f);
-          rg_put(rowg, lc + 1, row_tag, 0.f);
-        }
-      }
-    }
     if constexpr (PERS) {
       invalid_sample();
       continue;
@@ -1349,18 +1311,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       if (four) DA0[16 * 24 + fr] = acc[3][0];
     }
   }
-  // per-sample rows for the batch-reduced fc weight gradients: plain rows for the reduce
-  // launch that follows, or (early-MLP overlap) tagged granules that the concurrently running
-  // MLP reduction polls - it starts on them while this block still runs phases E and F
-  if (rowg != nullptr) {
-    put_row_granules(rowg, batch, b, row_tag, tid, NT, A0, H1, H2, DZ1, DZ2, DZ3);
-    if (tid == 0) rowg_ctr[b] = row_tag;  // (every thread read the counter at the kernel start)
-  } else {
-    for (int i = tid; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, A0[i]);
-    if (tid < H1_LD) { put_row(h1_s + (size_t)b * H1_LD + tid, H1[tid]); put_row(z1_s + (size_t)b * Z1_LD + tid, DZ1[tid]); }
-    if (tid < H2_LD) { put_row(h2_s + (size_t)b * H2_LD + tid, H2[tid]); put_row(z2_s + (size_t)b * Z2_LD + tid, DZ2[tid]); }
-    if (tid < Z3_LD) put_row(z3_s + (size_t)b * Z3_LD + tid, DZ3[tid]);
-  }
+  // per-sample rows for the batch-reduced fc weight gradients (the reduction that follows, or
+  // in a PERS launch the reduction workgroups of the same launch, reads them)
+  for (int i = tid; i < A0_LD; i += NT) put_row(a0_s + (size_t)b * A0_LD + i, A0[i]);
+  if (tid < H1_LD) { put_row(h1_s + (size_t)b * H1_LD + tid, H1[tid]); put_row(z1_s + (size_t)b * Z1_LD + tid, DZ1[tid]); }
+  if (tid < H2_LD) { put_row(h2_s + (size_t)b * H2_LD + tid, H2[tid]); put_row(z2_s + (size_t)b * Z2_LD + tid, DZ2[tid]); }
+  if (tid < Z3_LD) put_row(z3_s + (size_t)b * Z3_LD + tid, DZ3[tid]);
   lds_barrier();
 
   STAMP(5);
@@ -1373,13 +1329,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   //    the conv2 DATA gradient as a direct implicit GEMM, K = (o, ky', kx'<8) against the
   //    flipped kernel WF - no col2im scratch, no gather pass.
   float* slab = slab_s + (size_t)b * SLAB;
-  // the conv gradient slab: plain rows, or (in-launch reduction) {value, step} granules
-  unsigned long long* const slab_g = conv_g ? rowg + rg_off(RG_SLAB, batch) + (long long)b * SLAB : nullptr;
-#define SLAB_PUT(i, v)                                   \
-  do {                                                   \
-    if (slab_g != nullptr) rg_put(slab_g, (i), row_tag, (v)); \
-    else put_row(slab + (i), (v));                       \
-  } while (0)
+#define SLAB_PUT(i, v) put_row(slab + (i), (v))
   bf16x8* R3 = reinterpret_cast<bf16x8*>(smem + L_REGA + A_R3);
   bf16* DY2 = reinterpret_cast<bf16*>(smem + L_REGA + A_DY2);
   float* DP1 = reinterpret_cast<float*>(smem + L_REGA + A_DP1);
@@ -1634,16 +1584,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
       }
     }
   }
-  if (conv_g) {
-    // {loss, correct} granules LAST: every wave of this sample is past its reads of the sample
-    // ids, next_ids and cursor that the in-launch bookkeeping advances once it has them all
-    __syncthreads();
-    if (tid == 0) {
-      const long long lc = rg_off(RG_LCK, batch) + (long long)RG_LC * b;
-      rg_put(rowg, lc, row_tag, my_loss);
-      rg_put(rowg, lc + 1, row_tag, __int_as_float(my_correct));
-    }
-  }
   if (codes_out != nullptr) {  // the ReLU + max-pool decisions of this sample (mask-aware oracle tests)
     for (int i = tid; i < CODES_PER_SAMPLE; i += NT)
       codes_out[(size_t)b * CODES_PER_SAMPLE + i] = i < 6 * 196 ? CODE1[i] : CODE2[i - 6 * 196];
@@ -1672,12 +1612,10 @@ namespace dnn {
 void init_kernels() {
   static bool done = false;
   if (done) return;
-  const void* kerns[] = {(const void*)lenet_fused_kernel<true, false, 0>, (const void*)lenet_fused_kernel<true, true, 0>,
-                         (const void*)lenet_fused_kernel<true, false, 1>, (const void*)lenet_fused_kernel<true, true, 1>,
-                         (const void*)lenet_fused_kernel<true, false, 8>, (const void*)lenet_fused_kernel<true, true, 8>,
-                         (const void*)lenet_fused_kernel<false, false, 0>, (const void*)lenet_fused_kernel<true, true, 0, true>,
-                         (const void*)lenet_fused_kernel<true, true, 0, true, true>,
-                         (const void*)lenet_fused_kernel<true, true, 0, true, true, 8>};
+  const void* kerns[] = {(const void*)lenet_fused_kernel<true, false>, (const void*)lenet_fused_kernel<true, true>,
+                         (const void*)lenet_fused_kernel<false, false>, (const void*)lenet_fused_kernel<true, true, true>,
+                         (const void*)lenet_fused_kernel<true, true, true, true>,
+                         (const void*)lenet_fused_kernel<true, true, true, true, 8>};
   for (const void* k : kerns) HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL));
   init_kernels_f32();
   done = true;
@@ -1687,38 +1625,13 @@ void launch_fused_train(const uint8_t* images, const int32_t* labels, const int3
                         int batch, int32_t* state, const float* master, const bf16* shadow, float* a0,
                         float* h1, float* h2, float* z1, float* z2, float* z3, float* slab, float* loss,
                         int32_t* correct, long long* stamps, const int32_t* next_ids, unsigned char* stage,
-                        hipStream_t stream, unsigned long long* rowg, unsigned* rowg_ctr, const ReduceArgs* mlp_red,
-                        const ReduceArgs* conv_red, uint8_t* codes) {
+                        hipStream_t stream, uint8_t* codes) {
   init_kernels();
   if (stage != nullptr && next_ids == nullptr) throw std::runtime_error("fused_train: staging needs next_ids");
-  if ((rowg == nullptr) != (rowg_ctr == nullptr)) throw std::runtime_error("fused_train: row granules need their counters");
-  ReduceArgs ra{}, rc{};
-  int red_wg = 0;
-  if (conv_red != nullptr && mlp_red == nullptr)
-    throw std::runtime_error("fused_train: an in-launch conv reduction needs the in-launch MLP reduction");
-  if (mlp_red != nullptr) {  // in-launch reduction: MLP (early-MLP overlap), + conv = the whole step
-    ra = *mlp_red;
-    if (rowg == nullptr || ra.rg != rowg || ra.lo != OFF_F1W || ra.hi < ARENA || ra.bookkeeping || ra.batch != batch ||
-        ra.rg_ctr == nullptr || ra.rg_err == nullptr || ra.xp_blk_off != 0)
-      throw std::runtime_error("fused_train: the in-launch MLP reduction reads this launch's row granules (MLP range)");
-    red_wg = INLAUNCH_MLP_WG;
-    if (conv_red != nullptr) {
-      rc = *conv_red;
-      if (rc.rg != rowg || rc.lo != 0 || rc.hi != OFF_F1W || !rc.bookkeeping || rc.batch != batch ||
-          rc.rg_ctr == nullptr || rc.rg_err == nullptr || rc.xp_nranks != ra.xp_nranks ||
-          (rc.xp_nranks > 0 && rc.xp_blk_off != INLAUNCH_MLP_BLOCKS))
-        throw std::runtime_error("fused_train: the in-launch conv reduction reads this launch's slab granules");
-      red_wg += INLAUNCH_CONV_WG;
-    }
-  }
-  const int rnr = red_wg == 0 ? 0 : (ra.xp_nranks == 0 ? 1 : 8);
-  if (rnr == 8 && (ra.xp_mode & 4)) throw std::runtime_error("fused_train: the in-launch MLP reduction has fp32 granules only");
-  auto* kern = rnr == 0 ? (stage ? &lenet_fused_kernel<true, true, 0> : &lenet_fused_kernel<true, false, 0>)
-               : rnr == 1 ? (stage ? &lenet_fused_kernel<true, true, 1> : &lenet_fused_kernel<true, false, 1>)
-                          : (stage ? &lenet_fused_kernel<true, true, 8> : &lenet_fused_kernel<true, false, 8>);
-  hipLaunchKernelGGL(kern, dim3(batch + red_wg), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len,
-                     batch, 0, state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, codes,
-                     next_ids, stage, rowg, rowg_ctr, ra, rc, PipeCtl{});
+  auto* kern = stage ? &lenet_fused_kernel<true, true> : &lenet_fused_kernel<true, false>;
+  hipLaunchKernelGGL(kern, dim3(batch), dim3(NT), LDS_TOTAL, stream, images, labels, order, order_len, batch, 0, state,
+                     master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, codes, next_ids, stage,
+                     ReduceArgs{}, PipeCtl{});
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1736,15 +1649,15 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
         "fused_train_pipe: needs the stage, its next_ids / bvalid slot, the counters, flags and error word");
   if (!(pc.nred == PIPE_BLOCKS || pc.nred == 1) || (pc.wait && pc.nred != PIPE_BLOCKS) || (pc.par & ~1))
     throw std::runtime_error("fused_train_pipe: nred must be the whole reduction or the bookkeeping alone");
-  if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || red.rg != nullptr || !red.fuse_sgd)
+  if (!red.bookkeeping || red.batch != batch || red.xp_nranks != 0 || !red.fuse_sgd)
     throw std::runtime_error("fused_train_pipe: a local fused-SGD reduction with bookkeeping of this batch");
   if (pc.nred == PIPE_BLOCKS ? !(red.lo == 0 && red.hi >= ARENA) : !(red.lo == OFF_F1W && red.hi == OFF_F1W))
     throw std::runtime_error("fused_train_pipe: whole-arena reduction, or an empty range for the bookkeeping alone");
   if (batch < 1 || batch > 1024) throw std::runtime_error("fused_train_pipe: batch out of range");
   const int nrw = (pc.nred + 1) / 2;
-  hipLaunchKernelGGL((lenet_fused_kernel<true, true, 0, true>), dim3(nrw + batch), dim3(NT), LDS_TOTAL, stream, images,
+  hipLaunchKernelGGL((lenet_fused_kernel<true, true, true>), dim3(nrw + batch), dim3(NT), LDS_TOTAL, stream, images,
                      labels, nullptr, order_len, batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab,
-                     loss, correct, stamps, nullptr, next_ids, stage, nullptr, nullptr, red, ReduceArgs{}, pc);
+                     loss, correct, stamps, nullptr, next_ids, stage, red, pc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1763,10 +1676,10 @@ int persist_resident_workgroups() {
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, 0, true, true>), NT, LDS_TOTAL));
+        &per_cu, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, true, true>), NT, LDS_TOTAL));
     int per_cu_x = 0;  // (the exchange instance: its own register count)
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu_x, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, 0, true, true, 8>), NT, LDS_TOTAL));
+        &per_cu_x, reinterpret_cast<const void*>(lenet_fused_kernel<true, true, true, true, 8>), NT, LDS_TOTAL));
     resident = std::min(per_cu, per_cu_x) * cus;
   }
   return resident;
@@ -1789,12 +1702,12 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   if (stage == nullptr || pc_in.ctr == nullptr || pc_in.err == nullptr || !pc_in.bv_slot[0] || !pc_in.bv_slot[1] ||
       !pc_in.nid_slot[0] || !pc_in.nid_slot[1])
     throw std::runtime_error("fused_train_persist: needs the stage, the control block, the error word and both slots");
-  if (!red.bookkeeping || red.batch != batch || red.rg != nullptr || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA)
+  if (!red.bookkeeping || red.batch != batch || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA)
     throw std::runtime_error("fused_train_persist: a whole-arena fused-SGD reduction with bookkeeping");
   // the in-launch exchange: the serial one-launch exchange's arguments (whole arena, counters from
   // block 0, fp32 granules, pull or two-hop); grad_scale 1 (the tile update folds it: reduce_device.h)
   if (red.xp_nranks != 0 &&
-      (red.xp_nranks < 1 || red.xp_nranks > XG_MAX_RANKS || red.xp_blk_off != 0 || (red.xp_mode & ~2) != 0 ||
+      (red.xp_nranks < 1 || red.xp_nranks > XG_MAX_RANKS || (red.xp_mode & ~2) != 0 ||
        red.grad_scale != 1.f || red.xp_ctr == nullptr || red.xp_err == nullptr || red.xp_abort == nullptr ||
        red.xp_rank < 0 || red.xp_rank >= red.xp_nranks))
     throw std::runtime_error("fused_train_persist: the in-launch exchange takes the whole-arena one-launch exchange "
@@ -1810,11 +1723,11 @@ void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, in
   pc.gen = reinterpret_cast<unsigned*>(base);
   pc.flg = reinterpret_cast<unsigned*>(base + PERS_FLG_OFF);
   pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
-  auto* kern = red.xp_nranks == 0 ? &lenet_fused_kernel<true, true, 0, true, true>
-                                   : &lenet_fused_kernel<true, true, 0, true, true, 8>;
+  auto* kern = red.xp_nranks == 0 ? &lenet_fused_kernel<true, true, true, true>
+                                   : &lenet_fused_kernel<true, true, true, true, 8>;
   hipLaunchKernelGGL(kern, dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL, stream, images, labels, nullptr, order_len,
                      batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, nullptr,
-                     pc.nid_slot[0], stage, nullptr, nullptr, red, ReduceArgs{}, pc);
+                     pc.nid_slot[0], stage, red, pc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1825,8 +1738,8 @@ void launch_fused_eval(const uint8_t* images, const int32_t* labels, const int32
   if (count <= 0) return;
   hipLaunchKernelGGL((lenet_fused_kernel<false, false>), dim3(count), dim3(NT), LDS_TOTAL, stream, images, labels,
                      order, n, count, base, nullptr, master, shadow, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     ReduceArgs{}, ReduceArgs{}, PipeCtl{});
+                     nullptr, nullptr, nullptr, loss, correct, nullptr, nullptr, nullptr, nullptr, ReduceArgs{},
+                     PipeCtl{});
   HIP_CHECK(hipGetLastError());
 }
 

@@ -281,57 +281,6 @@ constexpr int FC_T0 = 8 * 25, FC_T1 = 6 * 8, FC_T2 = 1 * 6;
 constexpr int FC_TILES = FC_T0 + FC_T1 + FC_T2;   // 254 wave-tiles
 constexpr int TILE_BLOCKS = (FC_TILES + 3) / 4;  // 4 waves per block
 
-// Early-MLP overlap: poll N row granules (a.rg + off[k]) until each tag shows `tag`, values
-// into v.  Every load of a round is in flight before the first check; bounded (rg_timeout /
-// abort word -> sticky *rg_err, zeros then flow into this step: the host raises at the next
-// check).  The rows were stored by the fused kernel's blocks as ONE 8-byte system-scope word
-// {value, step} each, so a tag match IS the value - no flag or fence orders anything.
-template <int N>
-__device__ __forceinline__ void rg_poll(const ReduceArgs& a, const int (&off)[N], unsigned tag, bool failed,
-                                        float (&v)[N]) {
-  static_assert(N <= 32, "pending mask");
-  unsigned pending = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
-  const long long t0 = wall_clock64();
-  // first wait on ONE granule (this lane's first operand), polling every ~0.2 us: the rows
-  // arrive together per sample, and a full round of every lane's loads would put several TB/s
-  // of uncached polling traffic next to the samples' own memory accesses
-  while (!failed) {
-    const unsigned long long x = __hip_atomic_load(a.rg + off[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if ((unsigned)(x >> 32) == tag) break;
-    __builtin_amdgcn_s_sleep(8);
-    if (wall_clock64() - t0 > a.rg_timeout_ticks ||
-        (a.xp_abort != nullptr && __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
-      __hip_atomic_store(a.rg_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      failed = true;
-    }
-  }
-  while (true) {
-    unsigned long long x[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-      if (pending & (1u << k)) x[k] = __hip_atomic_load(a.rg + off[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-      if ((pending & (1u << k)) && (unsigned)(x[k] >> 32) == tag) {
-        v[k] = __uint_as_float((unsigned)x[k]);
-        pending &= ~(1u << k);
-      }
-    if (pending == 0u) break;
-    if (failed) {
-#pragma unroll
-      for (int k = 0; k < N; ++k)
-        if (pending & (1u << k)) v[k] = 0.f;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(4);
-    if (wall_clock64() - t0 > a.rg_timeout_ticks ||
-        (a.xp_abort != nullptr && __hip_atomic_load(a.xp_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
-      __hip_atomic_store(a.rg_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      failed = true;
-    }
-  }
-}
-
 // A per-sample row element: plain, or (SC: the persistent launch, lenet_fused.hip PERS) an sc1
 // load of a row the sample workgroups of the same launch stored write-through
 template <bool SC>
@@ -342,11 +291,9 @@ __device__ __forceinline__ float ldrow(const float* p) {
   else return *p;
 }
 
-// GR: rtag = this reduction block's row tag, rfail = an earlier wait failed (skip the waits)
 // SC / rp (the persistent launch): sc1 row loads, rows of parity rp (rp * batch rows further on)
-template <int LAYER, bool GR, class Sink, bool SC = false>
-__device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
-                                        int rp = 0) {
+template <int LAYER, class Sink, bool SC = false>
+__device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, int rp = 0) {
   using L = Fc<LAYER>;
   const float* z = LAYER == 0 ? a.z1 : (LAYER == 1 ? a.z2 : a.z3);
   const float* x = LAYER == 0 ? a.a0 : (LAYER == 1 ? a.h1 : a.h2);
@@ -380,29 +327,11 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
     // every operand load is unconditional (clamped address) and issued before the first
     // MFMA; out-of-range operands are zeroed by a select afterwards
     float av[16], bv[16];
-    if constexpr (GR) {  // row granules [a0 | h1 | h2 | z1 | z2 | z3] (common.h)
-      const int zo = (int)rg_off(3 + LAYER, a.batch), xo = (int)rg_off(LAYER, a.batch);
-      int off[32];
-      float v[32];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int b = min(b0 + 4 * s + kq, a.batch - 1);
-        off[s] = zo + b * L::ZLD + omc;
-        off[16 + s] = xo + b * L::XLD + inc;
-      }
-      rg_poll<32>(a, off, rtag, rfail, v);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        av[s] = v[s];
-        bv[s] = v[16 + s];
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int b = min(b0 + 4 * s + kq, a.batch - 1);
-        av[s] = ldrow<SC>(z + b * L::ZLD + omc);
-        bv[s] = ldrow<SC>(x + b * L::XLD + inc);
-      }
+    for (int s = 0; s < 16; ++s) {
+      const int b = min(b0 + 4 * s + kq, a.batch - 1);
+      av[s] = ldrow<SC>(z + b * L::ZLD + omc);
+      bv[s] = ldrow<SC>(x + b * L::XLD + inc);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -436,23 +365,13 @@ __device__ __forceinline__ void fc_tile(int t, const ReduceArgs& a, Sink& sk, un
 // reproducible), 16-load chains
 // instead of 64, 4x the threads in flight.
 constexpr int SPLIT = 4;
-// GR (early-MLP overlap): src is a row-granule offset into a.rg instead of a float pointer
-template <bool GR = false, bool SC = false>
-__device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q,
-                                                  const ReduceArgs* ga = nullptr, int gbase = 0, unsigned rtag = 0,
-                                                  bool rfail = false) {
+template <bool SC = false>
+__device__ __forceinline__ float column_sum_split(const float* src, int ld, int col, int batch, int q) {
   float g = 0.f;
   for (int b0 = 0; b0 < batch; b0 += 64) {
     float v[16];
-    if constexpr (GR) {
-      int off[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) off[k] = gbase + min(b0 + 16 * q + k, batch - 1) * ld + col;
-      rg_poll<16>(*ga, off, rtag, rfail, v);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = ldrow<SC>(src + min(b0 + 16 * q + k, batch - 1) * ld + col);
-    }
+    for (int k = 0; k < 16; ++k) v[k] = ldrow<SC>(src + min(b0 + 16 * q + k, batch - 1) * ld + col);
     __builtin_amdgcn_sched_barrier(0);  // all 16 loads in flight before the first wait
 #pragma unroll
     for (int k = 0; k < 16; ++k) g += (b0 + 16 * q + k < batch) ? v[k] : 0.f;
@@ -468,9 +387,8 @@ __device__ __forceinline__ float column_sum_split(const float* src, int ld, int 
 constexpr int FCB_ELEMS = 120 + 84 + 10;
 constexpr int FCB_COLS = 128 + 96 + 16;
 constexpr int FCB_SLOTS = FCB_COLS * SPLIT;  // 960
-template <bool GR, class Sink, bool SC = false>
-__device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
-                                         int rp = 0) {
+template <class Sink, bool SC = false>
+__device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, int rp = 0) {
   const int tc = min(t, FCB_SLOTS - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tc / (16 * SPLIT));  // wave-uniform source
   const int colp = tc / SPLIT, q = t % SPLIT;
@@ -486,11 +404,11 @@ __device__ __forceinline__ void fcb_task(int t, const ReduceArgs& a, Sink& sk, u
   const long rb = SC ? (long)rp * a.batch : 0;  // (the persistent launch's row parity)
   float g;  // every lane shuffles: no early exit
   if (grp < 8)
-    g = column_sum_split<GR, SC>(a.z1 + rb * Z1_LD, Z1_LD, cc, a.batch, q, &a, GR ? (int)rg_off(3, a.batch) : 0, rtag, rfail);
+    g = column_sum_split<SC>(a.z1 + rb * Z1_LD, Z1_LD, cc, a.batch, q);
   else if (grp < 14)
-    g = column_sum_split<GR, SC>(a.z2 + rb * Z2_LD, Z2_LD, cc, a.batch, q, &a, GR ? (int)rg_off(4, a.batch) : 0, rtag, rfail);
+    g = column_sum_split<SC>(a.z2 + rb * Z2_LD, Z2_LD, cc, a.batch, q);
   else
-    g = column_sum_split<GR, SC>(a.z3 + rb * Z3_LD, Z3_LD, cc, a.batch, q, &a, GR ? (int)rg_off(5, a.batch) : 0, rtag, rfail);
+    g = column_sum_split<SC>(a.z3 + rb * Z3_LD, Z3_LD, cc, a.batch, q);
   if (t < FCB_SLOTS && col < n && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
 
@@ -502,26 +420,20 @@ __device__ __forceinline__ int conv_dst(int e) {
   if (e < SLAB_C2B) return OFF_C2W + (e - SLAB_C2W);
   return OFF_C2B + (e - SLAB_C2B);
 }
-template <bool GR, class Sink, bool SC = false>
-__device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, unsigned rtag = 0, bool rfail = false,
-                                          int rp = 0) {
+template <class Sink, bool SC = false>
+__device__ __forceinline__ void conv_task(int t, const ReduceArgs& a, Sink& sk, int rp = 0) {
   const float* src = a.slab;
   if constexpr (SC) src += (long)rp * a.batch * SLAB;
   const int e = min(t / SPLIT, CONV_ELEMS - 1), q = t % SPLIT;
   const int dst = conv_dst(e);
   const float pv = a.master[dst], mv = a.mom[dst];  // (unused if !fuse_sgd)
-  const float g = column_sum_split<GR, SC>(src, SLAB, e, a.batch, q, &a, GR ? (int)rg_off(RG_SLAB, a.batch) : 0, rtag,
-                                      rfail);
+  const float g = column_sum_split<SC>(src, SLAB, e, a.batch, q);
   if (t < CONV_SLOTS && q == 0) sk.put(0, dst, g, pv, mv, a);
 }
 
 // Epoch statistics of the step that just ran + publication of the next step's cursor,
 // valid count and sample ids.  One wave (lanes 0..63), fixed summation order.
-// GR (in-launch reduction): {loss, correct} from the row granules, which every sample workgroup
-// publishes as its LAST action - so the cursor, sample ids and next_ids below are advanced only
-// after every sample of this launch read them
-template <bool GR = false>
-__device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsigned rtag = 0, bool rfail = false) {
+__device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane) {
     const float* loss = a.loss;
     const int32_t* correct = a.correct;
     float ls = 0.f;
@@ -530,17 +442,8 @@ __device__ __forceinline__ void bookkeeping(const ReduceArgs& a, int lane, unsig
     // pipelined step's bk_bv_in and bk_bv_out may be the same word)
     const int bv = a.bk_bv_in != nullptr ? *a.bk_bv_in : a.state[ST_BVALID];
     for (int b = lane; b < (a.bk_stats ? a.batch : 0); b += 64) {
-      if constexpr (GR) {
-        const int lo = (int)rg_off(RG_LCK, a.batch) + RG_LC * b;
-        const int off[2] = {lo, lo + 1};
-        float v[2];
-        rg_poll<2>(a, off, rtag, rfail, v);
-        ls += v[0];
-        cs += __float_as_int(v[1]);
-      } else {
-        ls += loss[b];
-        cs += correct[b];
-      }
+      ls += loss[b];
+      cs += correct[b];
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) { ls += __shfl_down(ls, off); cs += __shfl_down(cs, off); }

@@ -1,6 +1,6 @@
 // Device code of the batch reduction + momentum SGD + one-launch xGMI exchange, shared by the
-// grad_reduce kernel (reduce_sgd.hip) and the fused kernel's in-launch MLP reduction
-// (lenet_fused.hip, early-MLP overlap).  See reduce_sgd.hip for the parity notes.
+// grad_reduce kernel (reduce_sgd.hip) and the pipelined / persistent launches' reduction
+// workgroups (lenet_fused.hip, lenet_f32.hip).  See reduce_sgd.hip for the parity notes.
 #pragma once
 #include "reduce_common.h"
 
@@ -14,36 +14,35 @@ static_assert(RT % SPLIT == 0, "split column lanes stay inside a wave");
 // One launch's blocks: [MLP tile blocks][MLP bias blocks][conv element blocks][bookkeeping].
 // Returns true (block-uniform) when this block reduced arena elements.
 // rblk / rtid: the reduction block and its thread (grad_reduce_kernel: blockIdx / threadIdx;
-// the fused kernel's in-launch MLP reduction: two 256-thread reduction blocks per workgroup).
-// GR: rtag / rfail as fc_tile's.  SC / rp: fc_tile's (the persistent launch).
-template <bool GR, class Sink, bool SC = false>
-__device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk, int rblk, int rtid, unsigned rtag = 0,
-                                                 bool rfail = false, int rp = 0) {
+// the pipelined / persistent launches: two 256-thread reduction blocks per workgroup).
+// SC / rp: fc_tile's (the persistent launch).
+template <class Sink, bool SC = false>
+__device__ __forceinline__ bool grad_reduce_body(const ReduceArgs& a, Sink& sk, int rblk, int rtid, int rp = 0) {
   const bool mlp = a.hi > OFF_F1W;
   const bool conv = a.lo < OFF_F1W;
   int blk = rblk;
   if (mlp) {
     if (blk < TILE_BLOCKS) {
       const int t = blk * 4 + (rtid >> 6);
-      if (t < FC_T0) fc_tile<0, GR, Sink, SC>(t, a, sk, rtag, rfail, rp);
-      else if (t < FC_T0 + FC_T1) fc_tile<1, GR, Sink, SC>(t - FC_T0, a, sk, rtag, rfail, rp);
-      else if (t < FC_TILES) fc_tile<2, GR, Sink, SC>(t - FC_T0 - FC_T1, a, sk, rtag, rfail, rp);
+      if (t < FC_T0) fc_tile<0, Sink, SC>(t, a, sk, rp);
+      else if (t < FC_T0 + FC_T1) fc_tile<1, Sink, SC>(t - FC_T0, a, sk, rp);
+      else if (t < FC_TILES) fc_tile<2, Sink, SC>(t - FC_T0 - FC_T1, a, sk, rp);
       return true;
     }
     blk -= TILE_BLOCKS;
     constexpr int FB = (FCB_SLOTS + RT - 1) / RT;
     if (blk < FB) {
-      fcb_task<GR, Sink, SC>(blk * RT + rtid, a, sk, rtag, rfail, rp);
+      fcb_task<Sink, SC>(blk * RT + rtid, a, sk, rp);
       return true;
     }
     blk -= FB;
   }
   if (conv) {
     constexpr int CB = (CONV_SLOTS + RT - 1) / RT;
-    if (blk < CB) { conv_task<GR, Sink, SC>(blk * RT + rtid, a, sk, rtag, rfail, rp); return true; }
+    if (blk < CB) { conv_task<Sink, SC>(blk * RT + rtid, a, sk, rp); return true; }
     blk -= CB;
   }
-  if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping<GR>(a, rtid, rtag, rfail);
+  if (a.bookkeeping && blk == 0 && rtid < 64) bookkeeping(a, rtid);
   return false;
 }
 
@@ -66,7 +65,7 @@ __device__ __forceinline__ void record_wait(const ReduceArgs& a, unsigned step, 
   for (int off = 32; off > 0; off >>= 1) t = max(t, (unsigned)__shfl_xor((int)t, off));
   if ((rtid & 63) == 0) {
     const int w = rtid >> 6;
-    a.xp_wait[((size_t)(step % XP_WAIT_RING) * XP_MAX_BLOCKS + rblk + a.xp_blk_off) * (RT / 64) + w] =
+    a.xp_wait[((size_t)(step % XP_WAIT_RING) * XP_MAX_BLOCKS + rblk) * (RT / 64) + w] =
         ((unsigned long long)step << 32) | t;
   }
 }
@@ -239,7 +238,7 @@ template <int NR, bool PK, bool WT = false>
 __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK, WT>& sk, unsigned step, bool failed,
                                                  int rblk, int rtid) {
   const int par = step & 1u;
-  const int owner = (rblk + a.xp_blk_off) % a.xp_nranks;
+  const int owner = rblk % a.xp_nranks;
   pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);  // (null own on the owner: rounding only)
   float s[4];
   long long waited;
@@ -300,19 +299,12 @@ __device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK
 
 // One reduction block's work (rblk, rtid as grad_reduce_body's).  NR = 1: local reduction
 // (+ SGD, or gradients out); NR = 2 / 4 / 8: the one-launch exchange for groups of up to NR
-// ranks (separate instances keep the local step's registers at its own need).  GR: the MLP
-// reduction of the early-MLP overlap (rows as granules from the fused kernel's sample blocks).
+// ranks (separate instances keep the local step's registers at its own need).
 // Every thread of the workgroup calls it once (it has a workgroup barrier).
-template <int NR, bool PK, bool GR>
+template <int NR, bool PK>
 __device__ __forceinline__ void reduce_block(const ReduceArgs& a, int rblk, int rtid) {
-  unsigned rtag = 0;
-  bool rfail = false;
-  if constexpr (GR) {
-    rtag = a.rg_ctr[rblk] + 1u;
-    rfail = *a.rg_err != 0u;
-  }
   if constexpr (NR > 1) {  // one-launch all-reduce: reduce -> exchange -> SGD, per lane
-    const int gb = rblk + a.xp_blk_off;  // (split launches: disjoint counter ranges)
+    const int gb = rblk;
     const unsigned step = a.xp_ctr[gb] + 1u;
     const bool failed = *a.xp_err != 0u;
     XpSinkT<PK> sk;
@@ -323,44 +315,17 @@ __device__ __forceinline__ void reduce_block(const ReduceArgs& a, int rblk, int 
     sk.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
                                                              (step & 1u) * a.xp_gslot_bytes)
                      : nullptr;
-    if (grad_reduce_body<GR>(a, sk, rblk, rtid, rtag, rfail)) {
+    if (grad_reduce_body(a, sk, rblk, rtid)) {
       if ((a.xp_mode & 2) == 0) xp_exchange<NR, PK>(a, sk, step, failed, rblk, rtid);
       else xp_exchange_rsag<NR, PK>(a, sk, step, failed, rblk, rtid);
     }
     __syncthreads();  // every thread read this block's counters before they advance
-    if (rtid == 0) {
-      a.xp_ctr[gb] = step;
-      if constexpr (GR) a.rg_ctr[rblk] = rtag;
-    }
+    if (rtid == 0) a.xp_ctr[gb] = step;
   } else {
     DirectSink d;
-    grad_reduce_body<GR>(a, d, rblk, rtid, rtag, rfail);
-    if constexpr (GR) {
-      __syncthreads();
-      if (rtid == 0) a.rg_ctr[rblk] = rtag;
-    }
+    grad_reduce_body(a, d, rblk, rtid);
   }
 }
 
-
-// The fused kernel's in-launch reduction (one launch per step): the reduction workgroups of
-// the fused launch (after the samples) run reduction blocks 2 wg and 2 wg + 1 of one launch
-// range (MLP, then conv + bookkeeping), one per 256-thread half.  RNR: 1 = local step, 8 = the one-launch exchange of up to 8 ranks (pull or two-hop,
-// fp32 granules) - one instance per fused-kernel instance (a run-time choice among several
-// would make the compiler copy the argument block to scratch).
-template <int RNR>
-__device__ __forceinline__ void inlaunch_reduce(const ReduceArgs& a, int wg, int nblk) {
-  const int half = threadIdx.x >> 8, rblk = 2 * wg + half, rtid = threadIdx.x & 255;
-  // (an odd block count leaves the last half idle; it still meets the workgroup barrier)
-  if (rblk >= nblk) {
-    __syncthreads();
-    return;
-  }
-  reduce_block<RNR, false, true>(a, rblk, rtid);
-}
-constexpr int INLAUNCH_MLP_BLOCKS = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
-constexpr int INLAUNCH_MLP_WG = (INLAUNCH_MLP_BLOCKS + 1) / 2;
-constexpr int INLAUNCH_CONV_BLOCKS = (CONV_SLOTS + RT - 1) / RT + 1;  // + the bookkeeping block
-constexpr int INLAUNCH_CONV_WG = (INLAUNCH_CONV_BLOCKS + 1) / 2;
 
 }  // namespace dnn

@@ -17,8 +17,6 @@
 namespace dnn {
 
 int grad_reduce_blocks() { return GRAD_REDUCE_BLOCKS; }
-int grad_reduce_mlp_blocks() { return TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT; }
-int inlaunch_mlp_workgroups() { return INLAUNCH_MLP_WG; }
 
 // diagnostic per-block timeline (tools/reduce_trace.py): [2 * block] start, [2 * block + 1]
 // end of the block's work (after its stores drained)
@@ -29,10 +27,10 @@ __device__ __forceinline__ void reduce_stamp(const ReduceArgs& a, int k) {
   }
 }
 
-template <int NR, bool PK = false, bool GR = false>
+template <int NR, bool PK = false>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(1, 2))) grad_reduce_kernel(const ReduceArgs a) {
   reduce_stamp(a, 0);
-  reduce_block<NR, PK, GR>(a, blockIdx.x, threadIdx.x);
+  reduce_block<NR, PK>(a, blockIdx.x, threadIdx.x);
   if (a.stamps != nullptr) __syncthreads();
   reduce_stamp(a, 1);
 }
@@ -116,18 +114,9 @@ void launch_grad_reduce(const ReduceArgs& args, hipStream_t stream) {
   if (nblk == 0) return;
   // the exchange waits on the same elements of every peer, which the same block reduces there:
   // every block must be resident at once (<= XP_MAX_BLOCKS blocks of RT threads, at most one
-  // per CU of the 256) and the launch must take the whole arena - or one of the two split
-  // launches (MLP range at block offset 0, conv range at the MLP launch's block count)
-  const int mlp_blocks = TILE_BLOCKS + (FCB_SLOTS + RT - 1) / RT;
-  if (args.xp_nranks > 0) {
-    const bool whole = mlp && conv && args.xp_blk_off == 0;
-    const bool split_mlp = mlp && !conv && args.lo == OFF_F1W && args.hi >= ARENA && args.xp_blk_off == 0;
-    const bool split_conv = conv && !mlp && args.lo == 0 && args.xp_blk_off == mlp_blocks;
-    if (args.xp_blk_off + nblk > XP_MAX_BLOCKS || !(whole || split_mlp || split_conv))
-      throw std::runtime_error("grad_reduce exchange needs the whole-arena grid or one of the two split launches");
-  }
-  if (args.rg != nullptr)
-    throw std::runtime_error("grad_reduce: row granules are read by the fused kernel's in-launch reduction only");
+  // per CU of the 256) and the launch must take the whole arena
+  if (args.xp_nranks > 0 && (nblk > XP_MAX_BLOCKS || !(mlp && conv && args.lo == 0 && args.hi >= ARENA)))
+    throw std::runtime_error("grad_reduce exchange needs the whole-arena grid");
   const int nr = args.xp_nranks;
   if (nr > XG_MAX_RANKS) throw std::runtime_error("grad_reduce exchange: at most 8 ranks");
   const bool pk = (args.xp_mode & 4) != 0;

@@ -269,14 +269,44 @@ def train_steps_bf16(master: torch.Tensor, images_u8: torch.Tensor, labels: torc
     return p, m, losses
 
 
+def decisions_fp32(weights: torch.Tensor, master: torch.Tensor, images_u8: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """The plain fp32 forward's OWN decisions (no rounding anywhere): the ReLU + max-pool codes of
+    both convolutions (``_codes_from_pool``, the kernel's code format) and the fc ReLU masks."""
+    w = LAYOUT.views(weights.detach().float().cpu())
+    bm = LAYOUT.views(master.detach().float().cpu())
+    x = normalize_u8(images_u8.cpu())
+    c1 = F.conv2d(x, w["conv1.weight"], bm["conv1.bias"])
+    p1, i1 = F.max_pool2d_with_indices(F.relu(c1), 2, 2)
+    c2 = F.conv2d(p1, w["conv2.weight"], bm["conv2.bias"])
+    p2, i2 = F.max_pool2d_with_indices(F.relu(c2), 2, 2)
+    h1 = F.relu(F.linear(p2.flatten(1), w["fc1.weight"], bm["fc1.bias"]))
+    h2 = F.relu(F.linear(h1, w["fc2.weight"], bm["fc2.bias"]))
+    return {"codes": torch.cat([_codes_from_pool(p1, i1, 28), _codes_from_pool(p2, i2, 10)], 1),
+            "h1": h1 > 0, "h2": h2 > 0}
+
+
+def decision_flips(a: Dict[str, torch.Tensor], b: Dict[str, torch.Tensor]) -> tuple[int, int, torch.Tensor]:
+    """(decisions that differ, decisions compared, per-sample count of differing decisions) between
+    two decision sets (``decisions_fp32`` / the bf16 emulation's codes + fc masks)."""
+    per = ((a["codes"] != b["codes"]).sum(1) + (a["h1"] != b["h1"]).sum(1) + (a["h2"] != b["h2"]).sum(1))
+    total = a["codes"].shape[1] + a["h1"].shape[1] + a["h2"].shape[1]
+    return int(per.sum()), total * int(per.numel()), per
+
+
 def train_steps_fp32_masked(master: torch.Tensor, images_u8: torch.Tensor, labels: torch.Tensor, order, batch: int,
-                            steps: int, lr: float, momentum: float):
+                            steps: int, lr: float, momentum: float, flips: list | None = None):
     """The fp32 reference arithmetic over ``steps`` steps, MASK-AWARE: every step's ReLU / max-pool
     decisions are those of the bf16 trajectory (``train_steps_bf16``, run alongside from the same
     start), every operand and accumulator stays fp32 (``per_sample_outputs_masked`` on the fp32
     master).  A near-tie that bf16 operands flip then cannot turn rounding noise into an O(1)
     change of one sample's gradient, so the bf16 kernel's trajectory can be held to bf16 precision
-    of fp32 (~1e-2).  Returns (fp32 master, momentum, per-step mean losses)."""
+    of fp32 (SURVEY §4: ~1e-2).  Returns (fp32 master, momentum, per-step mean losses).
+
+    ``flips`` (optional list): per step, how often the plain fp32 forward's OWN decisions on this
+    trajectory's parameters differ from the bf16 trajectory's (the kernel's) - (decisions flipped,
+    decisions compared, samples with a flip, samples): the steps' mask-aware gradients equal the
+    plain fp32 ones on every sample without a flip, so the pair (flip counts, mask-aware error)
+    bounds the plain fp32 comparison (VERDICT r5 weak #6)."""
     pe = master.detach().float().cpu().clone()
     p32 = pe.clone()
     me, m32 = torch.zeros_like(pe), torch.zeros_like(pe)
@@ -291,6 +321,10 @@ def train_steps_fp32_masked(master: torch.Tensor, images_u8: torch.Tensor, label
         emu = per_sample_outputs_bf16(pe.bfloat16(), pe, images_u8[idx], labels[idx], n)
         f32 = per_sample_outputs_masked(p32, p32, images_u8[idx], labels[idx], emu["codes"], emu["h1"] > 0,
                                         emu["h2"] > 0, n)
+        if flips is not None:
+            own = decisions_fp32(p32, p32, images_u8[idx])
+            d, tot, per = decision_flips(own, {"codes": emu["codes"], "h1": emu["h1"] > 0, "h2": emu["h2"] > 0})
+            flips.append((d, tot, int((per > 0).sum()), n))
         for p, m, rows in ((pe, me, emu), (p32, m32, f32)):
             g = reduce_rows(rows) * mask
             m.copy_((momentum * m.double() + g.double()).float())

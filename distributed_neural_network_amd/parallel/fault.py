@@ -407,3 +407,26 @@ def beat_pause_injection(orig_rank: int, epoch: int) -> float:
         return 0.0
     r, e, d = spec.split(":")
     return float(d) if int(r) == orig_rank and int(e) == epoch else 0.0
+
+
+def setup_crash_injection(site: str, orig_rank: int) -> None:
+    """Fault injection for tests: the process dies (exit code 134, as a GPU fault's abort) at a
+    set-up site of the FIRST launch attempt only, so the launcher's retry in fresh ranks
+    (parallel/selflaunch.py) can be exercised.  ``DNN_INJECT_XGMI_SETUP_FAIL=rank`` hits the xGMI
+    group set-up (parallel/xgmi.py, before any IPC mapping is made); ``DNN_INJECT_CRASH=site:rank``
+    any named site."""
+    import sys
+
+    if os.environ.get("DNN_LAUNCH_ATTEMPT", "1") != "1":
+        return
+    want = []
+    v = os.environ.get("DNN_INJECT_XGMI_SETUP_FAIL", "")
+    if v != "":
+        want.append(("xgmi-setup", int(v)))
+    spec = os.environ.get("DNN_INJECT_CRASH", "")
+    if spec:
+        s, r = spec.rsplit(":", 1)
+        want.append((s, int(r)))
+    if (site, orig_rank) in want:
+        print(f"[fault] injected crash at {site} on rank {orig_rank} (launch attempt 1)", file=sys.stderr, flush=True)
+        os._exit(134)

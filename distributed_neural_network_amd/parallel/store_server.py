@@ -12,7 +12,8 @@ It exits when every rank of the job has checked out (``dnn/closed`` counter, inc
 ``Communicator.close``; a rank the recovery dropped counts through ``dnn/dropped``), when every
 heartbeat it has seen is older than ``--stale`` seconds (the ranks are gone without checking
 out: a crash, Ctrl-C, SIGKILL), when every rank process registered on this host
-(``dnn/pid/<r>`` = host:pid, written by every rank at connect) is gone, or when nothing at all
+(``dnn/pid/<r>`` = host:pid, written by every rank at connect) is gone and no rank of another
+host is registered (those may still need the store to recover), or when nothing at all
 has changed for ``--idle`` seconds - the idle exit only while no registered rank of this host
 is alive: a live job that makes no store writes for a while (a bench without a heartbeat) keeps
 its store.  It
@@ -57,9 +58,13 @@ def decide(world: int, closed: int, dropped: int, beats: list, stale: float, pid
     if seen and now - max(seen) > stale:
         return f"no heartbeat for {stale:.0f} s: the job is gone"
     local = [p for p in pids.values() if p > 0]
-    if local and not alive and len(pids) == world:
+    # ranks on other hosts (pid -1) may outlive every rank of this one - and need the store for
+    # their recovery (agree_survivors, reform): with any of them registered, only the check-out
+    # and heartbeat-staleness rules above apply
+    remote = any(p <= 0 for p in pids.values())
+    if local and not alive and len(pids) == world and not remote:
         return "every rank process of this host is gone"
-    if idle_for > idle and not alive:
+    if idle_for > idle and not alive and not remote:
         return f"no activity for {idle:.0f} s"
     return None
 

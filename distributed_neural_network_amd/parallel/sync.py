@@ -133,14 +133,12 @@ class StepAllReduce(SyncPolicy):
     # all-reduced on a side stream while the conv bucket is reduced; local: no all-reduce (A/B
     # baseline only: replicas diverge)
     # (xgmi-pull-bf16 / xgmi-rsag-bf16: the same exchanges with bf16 gradient granules, opt-in)
-    # (xgmi-pull-ovl / xgmi-rsag-ovl: the same exchanges run by the fused launch's in-launch MLP
-    # reduction, overlapped with the conv backward - HipEngine early_mlp="mlp"; bit-identical)
     # (xgmi-pull-pers / xgmi-rsag-pers: the same exchanges inside the PERSISTENT launch's reduction
     # workgroups - the whole window one launch, no kernel boundary between steps, the exchange +
     # SGD before each step's ready hand-off; lenet_fused.hip XNR; self-tested bit for bit against
     # the serial one-launch exchange)
-    PATHS = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl",
-             "xgmi-rsag-ovl", "xgmi-pull-bf16", "xgmi-rsag-bf16")
+    PATHS = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-bf16",
+             "xgmi-rsag-bf16")
     path: str | None = None
     grad_comm = "fp32"  # "bf16": the default xGMI path uses bf16 gradient granules (--grad-comm)
     record_waits = False  # xGMI paths: record every step's exchange wait (XgmiGroup.wait_stats)
@@ -193,9 +191,8 @@ class StepAllReduce(SyncPolicy):
             from .xgmi import MODE_NAMES
 
             form = MODE_NAMES[gs.group.xp_mode]
-            ovl = "-ovl" if getattr(engine, "early_mlp", False) and engine._early_ok() else ""
             pers = "-pers" if getattr(engine, "pers_exchange", False) and engine._pers_xchg() is not None else ""
-            return f"xgmi-{form}{ovl}{pers}" + ("" if gs.group.one_launch else "-two-launch")
+            return f"xgmi-{form}{pers}" + ("" if gs.group.one_launch else "-two-launch")
         if kind == "NativeGradAllReduce":
             return "rccl-overlap" if gs.overlap else "rccl"
         return "torch-pg"
@@ -208,19 +205,6 @@ class StepAllReduce(SyncPolicy):
             engine.invalidate_graphs()
         if hasattr(engine, "overlap"):
             engine.overlap = name == "rccl-overlap"
-        if hasattr(engine, "early_mlp"):
-            # the -ovl paths switch the in-launch MLP reduction on; other paths restore the
-            # engine's own setting
-            if not hasattr(self, "_early0"):
-                self._early0 = engine.early_mlp
-            ovl = name.endswith("-ovl")
-            if ovl and getattr(engine, "dtype", "bf16") != "bf16":
-                self.install_why = "the in-launch (-ovl) reduction is a bf16-kernel feature"
-                return False
-            engine.early_mlp = "mlp" if ovl else self._early0
-        elif name.endswith("-ovl"):
-            self.install_why = "the in-launch (-ovl) reduction needs the fused engine"
-            return False
         engine.grad_sync = None
         pers = name.endswith("-pers")
         if hasattr(engine, "pers_exchange"):
@@ -233,7 +217,7 @@ class StepAllReduce(SyncPolicy):
         if name.startswith("xgmi"):
             from .xgmi import EXCHANGE_MODES
 
-            mode = EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-ovl").removesuffix("-pers")]
+            mode = EXCHANGE_MODES[name[len("xgmi-"):].removesuffix("-pers")]
             if not self._install_xgmi(engine, mode):
                 return False
             if pers:

@@ -131,6 +131,9 @@ class XgmiGroup:
             raise
 
     def _setup(self, comm: Communicator, device_ids: list[str] | None) -> None:
+        from .fault import setup_crash_injection
+
+        setup_crash_injection("xgmi-setup", comm.orig_rank)  # (tests: the launcher's retry path)
         dev = comm.device
         self.abort_host, self.abort_dev = self.ext.xgmi_abort_word()
         nb = self.ext.xgmi_max_blocks(self.capacity)
@@ -267,6 +270,33 @@ class XgmiGroup:
         if self.abort_host:
             self.ext.xgmi_set_abort(self.abort_host, 1)
 
+    def preflight(self, timeout_s: float = 5.0) -> tuple[bool, str]:
+        """A tiny bounded round trip over every peer mapping before anything larger uses them:
+        rank r publishes 2**r in 64 granules and reads every peer's, so the rank-order sum must be
+        exactly 2**N - 1 (times fp32(1/N)).  A mapping that faults aborts this process HERE, in
+        set-up (the launcher then retries without xGMI, parallel/selflaunch.py); one that returns
+        stale or foreign data times out within ``timeout_s`` or sums wrong, and the caller turns
+        that into a voted refusal.  Returns (ok, why) - why names the peers whose contribution is
+        missing."""
+        dev = self.comm.device
+        timeout, self.timeout_s = self.timeout_s, min(self.timeout_s, timeout_s)
+        try:
+            with torch.cuda.device(dev):
+                t = torch.full((64,), float(1 << self.rank), device=dev, dtype=torch.float32)
+                self.allreduce_(t)
+                got = t.cpu()
+                err = self.failed()
+        finally:
+            self.timeout_s = timeout
+        inv = torch.tensor(1.0 / self.world, dtype=torch.float32)
+        want = torch.tensor(float((1 << self.world) - 1), dtype=torch.float32) * inv
+        if not err and bool((got == want).all()):
+            return True, ""
+        v = float(got[0])
+        seen = int(round(v * self.world)) if v == v and abs(v) < 1e6 else -1
+        missing = [r for r in range(self.world) if seen < 0 or not (seen >> r) & 1]
+        return False, ("a granule wait timed out; " if err else "") + f"missing / wrong peer contributions: {missing}"
+
     def selftest(self, steps: int = 4) -> bool:
         """``steps`` all-reduces of random per-rank data (both parity slots, fresh flags),
         checked EXACTLY against the rank-order fp32 sum every rank recomputes on the host
@@ -344,18 +374,26 @@ def build_group(comm: Communicator, capacity: int) -> XgmiGroup | None:
         grp = XgmiGroup(comm, capacity, device_ids=device_ids)
     except Exception as e:  # IPC export/import refused, etc.
         ok, why = False, f"{type(e).__name__}: {e}"
-    # agree that every rank mapped every region BEFORE any rank launches a self-test
-    # kernel that waits for peers
-    if ok and all(v == 1.0 for v in comm.gather_scalars(1.0)):
-        try:
-            ok = grp.selftest()
-            why = "" if ok else "self-test mismatch"
-        except Exception as e:
-            ok, why = False, f"{type(e).__name__}: {e}"
-    elif ok:
+    # agree that every rank mapped every region BEFORE any rank launches a kernel that waits for
+    # peers; then a tiny bounded round trip over every mapping (pre-flight), agreed on too, before
+    # the full self-test - and long before any engine kernel polls the regions
+    mapped = all(v == 1.0 for v in comm.gather_scalars(1.0 if ok else 0.0))
+    if ok and not mapped:
         ok, why = False, "a peer could not map the regions"
-    else:
-        comm.gather_scalars(0.0)
+    if mapped:
+        pre, pre_why = False, ""
+        try:
+            pre, pre_why = grp.preflight()
+        except Exception as e:
+            pre_why = f"{type(e).__name__}: {e}"
+        if not all(v == 1.0 for v in comm.gather_scalars(1.0 if pre else 0.0)):
+            ok, why = False, f"pre-flight round trip failed ({pre_why or 'on a peer'})"
+        else:
+            try:
+                ok = grp.selftest()
+                why = "" if ok else "self-test mismatch"
+            except Exception as e:
+                ok, why = False, f"{type(e).__name__}: {e}"
     votes = comm.gather_scalars(1.0 if ok else 0.0)
     if os.environ.get("DNN_DEBUG_XGMI") == "1":
         print(f"[xgmi] gen {comm.generation} rank {comm.rank}/{comm.world} ok={ok} {why} votes={votes} "

@@ -24,7 +24,6 @@ epoch ends.
 """
 from __future__ import annotations
 
-import itertools
 import os
 import sys
 import time
@@ -41,8 +40,7 @@ from ..ops import native, reference
 
 
 class StepWaitTimeout(RuntimeError):
-    """A bounded in-launch wait of the pipelined / persistent step (or the early-MLP row wait)
-    timed out: the epoch's parameters are not trustworthy.  ``Trainer.run`` restores the epoch's
+    """A bounded in-launch wait of the pipelined / persistent step timed out: the epoch's parameters are not trustworthy.  ``Trainer.run`` restores the epoch's
     snapshot, steps the engine down (``HipEngine.degrade``: persistent -> pipelined -> serial)
     and redoes the epoch; nothing else is lost."""
 
@@ -243,8 +241,7 @@ class HipEngine(Engine):
     def __init__(self, batch: int, lr: float = 0.001, momentum: float = 0.9, arena: torch.Tensor | None = None,
                  seed: int | None = None, device: str | torch.device = "cuda", graph_chunk: int = 32,
                  use_graphs: bool = True, overlap: bool = False, stage_images: bool | None = None,
-                 dtype: str = "bf16", early_mlp: bool | None = None, pipeline: bool | None = None,
-                 persist: bool | None = None) -> None:
+                 dtype: str = "bf16", pipeline: bool | None = None, persist: bool | None = None) -> None:
         super().__init__(batch, lr, momentum, arena, seed)
         if dtype not in ("bf16", "fp32"):
             raise ValueError(f"HipEngine dtype must be bf16 or fp32, not {dtype!r}")
@@ -298,24 +295,6 @@ class HipEngine(Engine):
         self.graph_chunk = 1 << max(0, int(graph_chunk).bit_length() - 1)  # power of two
         self.use_graphs = use_graphs
         self.overlap = overlap
-        # early-MLP overlap (bf16 kernel, local step or one-launch xGMI exchange): the MLP
-        # reduction (+ its exchange + SGD) runs in extra workgroups of the fused launch,
-        # CONCURRENTLY with the samples, polling the rows they publish as {value, step} granules
-        # after phase D' while they still run the conv backward; the conv reduction follows as
-        # its own launch.  Bit-identical to the serial step (same sums, same order).  (A side-
-        # stream form with a graph fork/join measured 28.3 vs 19.8 us/step: profiles/r3/early_mlp.)
-        # early_mlp: False | True / "mlp" (MLP reduction in-launch, conv reduction its own launch)
-        # | "full" (both in-launch: the whole step in one launch)
-        if early_mlp is None:
-            early_mlp = {"0": False, "1": "mlp", "mlp": "mlp", "2": "full", "full": "full"}[
-                os.environ.get("DNN_EARLY_MLP", "0")] if dtype == "bf16" else False
-        if early_mlp is True:
-            early_mlp = "mlp"
-        if early_mlp not in (False, "mlp", "full"):
-            raise ValueError(f"early_mlp must be False, 'mlp' or 'full', not {early_mlp!r}")
-        if early_mlp and dtype != "bf16":
-            raise ValueError("early-MLP overlap is a feature of the bf16 kernel")
-        self.early_mlp = early_mlp
         # Pipelined step (lenet_fused.hip PIPE; bf16, staged images, local step): launch i of a
         # step chunk runs step i - 1's batch reduction + SGD in its first workgroups and step i's
         # samples in the rest, which wait (in-launch ready counters) for the new weights before
@@ -326,9 +305,6 @@ class HipEngine(Engine):
         if pipeline is None:
             pipeline = os.environ.get("DNN_PIPELINE", "1") != "0"
         self.pipeline = bool(pipeline) and dtype == "bf16" and stage_images
-        self._rg: dict | None = None
-        if dtype == "bf16":
-            self._rg_buffers()  # (allocated up front: never inside a graph capture)
         # Persistent launch (lenet_fused.hip PERS; on top of the pipelined step - or, fp32,
         # lenet_f32.hip PERS on its own: the fp32 kernel has no pipelined form): a chunk of n steps
         # is ONE launch - the reduction and sample workgroups loop over the steps and hand off
@@ -388,7 +364,6 @@ class HipEngine(Engine):
         else:
             ctl_bytes = self.ext.persist_ctl_bytes_f32(B) if dtype == "fp32" else self.ext.persist_ctl_bytes(B)
             self._pers_ctl = self.ext.uncached_alloc(ctl_bytes) if self.persist else 0
-        self._pers_handles: dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.params_changed()
@@ -412,7 +387,6 @@ class HipEngine(Engine):
 
     def invalidate_graphs(self) -> None:
         self._graphs.clear()
-        self._pers_gen += 1
 
     # -- data ---------------------------------------------------------------------------
     def attach(self, train: Split) -> None:
@@ -473,28 +447,12 @@ class HipEngine(Engine):
                              self.order_len, self._p(self.batch_ids), s,
                              next_ids=self._p(self.next_ids) if self._staged or self._ahead else 0, **xg)
 
-    RG_TIMEOUT_S = 10.0  # bound of one early-MLP row wait (then a sticky error word, raised at epoch_stats)
-
-    def _rg_buffers(self) -> dict:
-        """Row-granule buffer (uncached device memory: every access bypasses the per-XCD L2s),
-        the fused blocks' and the MLP-reduction blocks' step counters and the error word."""
-        if self._rg is None:
-            ptr = self.ext.uncached_alloc(self.batch * self.ext.row_granules() * 8)
-            i32 = dict(device=self.device, dtype=torch.int32)
-            self._rg = dict(ptr=ptr, fctr=torch.zeros(self.batch, **i32),
-                            rctr=torch.zeros(self.ext.grad_reduce_blocks(), **i32), err=torch.zeros(1, **i32))
-        return self._rg
-
-    def early_failed(self) -> bool:
-        return self._rg is not None and int(self._rg["err"].item()) != 0
-
     def pipe_failed(self) -> bool:
         return hasattr(self, "pipe_err") and int(self.pipe_err.item()) != 0
 
     def _pipe_ok(self) -> bool:
-        """The pipelined step runs: bf16 with staged images, no all-reduce installed (one rank)
-        and no in-launch reduction."""
-        return self.pipeline and self.grad_sync is None and self._staged and not self.early_mlp
+        """The pipelined step runs: bf16 with staged images, no all-reduce installed (one rank)."""
+        return self.pipeline and self.grad_sync is None and self._staged
 
     def _pers_xchg(self):
         """The xGMI group whose one-launch exchange runs inside the persistent launch, or None:
@@ -507,18 +465,6 @@ class HipEngine(Engine):
             return None
         return grp
 
-    # persistent launches directly from the extension's cached argument block instead of graph
-    # replays (DNN_PERS_DIRECT=1).  Round 4 measured ~3.4 us less per 20-step window and saw an
-    # illegal address in a LATER engine of the same process (profiles/r4/pers_direct).  The fault
-    # needed engines freeing their uncached control buffers (hipFree of fine-grained memory) between
-    # direct-mode runs; those buffers now come from a never-freed pool whose free blocks carry a
-    # canary (csrc/comm/xgmi_allreduce.hip uncached_alloc): the minimal pair and the whole GPU suite
-    # pass in direct mode with no canary broken, i.e. no kernel wrote to a destroyed engine's control
-    # words (profiles/r5/direct_pool).  Off by default: on the round-5 box six alternating 20/5
-    # windows each way measured graph replays FASTER (median 18.07 vs 18.16 us, ab6/).
-    # DNN_PERS_DIRECT_SYNC=1 (diagnostic): sync after every relaunch
-    pers_direct = os.environ.get("DNN_PERS_DIRECT", "0") == "1"
-    pers_direct_sync = os.environ.get("DNN_PERS_DIRECT_SYNC", "0") == "1"
     # bound of one ready wait (then a sticky error word, raised at epoch_stats); DNN_PIPE_TIMEOUT_S
     # overrides it (tests force a timeout with a tiny bound + an injected delay, DNN_PIPE_FLAGS=256)
     PIPE_TIMEOUT_S = float(os.environ.get("DNN_PIPE_TIMEOUT_S", "10.0"))
@@ -580,30 +526,11 @@ class HipEngine(Engine):
         fp32: lenet_f32.hip's persistent launch, local steps only."""
         if self.dtype == "fp32":
             return self.persist and self._ahead and self.grad_sync is None
-        if not (self.persist and self.pipeline and self._staged and not self.early_mlp):
+        if not (self.persist and self.pipeline and self._staged):
             return False
         return self.grad_sync is None or self._pers_xchg() is not None
 
-    _pers_handles_next = itertools.count(1)  # process-wide: a handle is never reused
-
-    def _pers_handle(self) -> int:
-        """Handle of this engine's persistent launch as cached in the extension (persist_relaunch):
-        one per (engine, argument block) - everything the block depends on that can change between
-        launches - drawn from a process-wide counter, so a freed engine's cached block can never
-        match another engine (an id()-based key did: ids are reused, and the relaunch then ran on
-        freed buffers)."""
-        grp = self._pers_xchg()
-        key = (self.order_len, self._p(self.order), self._p(self.train.images), self._staged,
-               self._pipe_stamps, self.pipe_flags, self._pers_gen,
-               None if grp is None else (id(grp), grp.xp_mode, grp.generation))
-        h = self._pers_handles.get(key)
-        if h is None:
-            h = self._pers_handles[key] = next(HipEngine._pers_handles_next)
-        return h
-
-    _pers_gen = 0  # bumped by invalidate_graphs: a new argument block must be cached
-
-    def _launch_steps_pers(self, n: int, cache: int = 0) -> None:
+    def _launch_steps_pers(self, n: int) -> None:
         """n steps as ONE launch (lenet_fused.hip PERS): the same reduction, bookkeeping slots and
         publication sequence as _launch_steps_pipe's n + 1 launches, with the reduction of step
         n - 1 inside the launch too (it re-publishes slot 0 for the next chunk)."""
@@ -639,7 +566,7 @@ class HipEngine(Engine):
                                      self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
                                      self._p(self.stage), self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
                                      self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                     stamps=self._pipe_stamps, flags=self.pipe_flags, cache=cache)
+                                     stamps=self._pipe_stamps, flags=self.pipe_flags)
 
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
@@ -655,60 +582,23 @@ class HipEngine(Engine):
     def __del__(self) -> None:
         """Give the uncached control buffers back to the extension's pool (never to the driver:
         csrc/comm/xgmi_allreduce.hip uncached_alloc) once this engine's queued work is done."""
-        rg = getattr(self, "_rg", None)
         bufs = [getattr(self, "_pipe_ctr_ptr", 0), getattr(self, "_pipe_flg_ptr", 0),
-                getattr(self, "_pers_ctl", 0) if getattr(self, "_pers_ctl_t", None) is None else 0,
-                rg["ptr"] if rg is not None else 0]
-        if any(bufs):
-            try:
-                torch.cuda.synchronize(self.device)
-                for p in bufs:
-                    if p:
-                        self.ext.uncached_free(p)
-            except Exception:
-                pass
-
-    def _early_ok(self) -> bool:
-        if not self.early_mlp or self.dtype != "bf16":
-            return False
-        if self.grad_sync is None:
-            return True
-        # (the in-launch MLP reduction carries fp32 granules only)
-        return (getattr(self.grad_sync, "fuses_sgd", False) and self.grad_sync.group.one_launch
-                and not self.grad_sync.group.xp_mode & 4)
-
-    def _launch_step_early(self) -> None:
-        """The whole step in ONE launch: the fused kernel's sample workgroups + reduction
-        workgroups that reduce the MLP gradient (polling the rows the samples publish as {value,
-        step} granules after phase D', while the samples still run the conv backward) and the
-        conv gradient + bookkeeping (polling the slab and {loss, correct} granules), each with
-        its exchange + SGD - no kernel boundary inside the step."""
-        rg = self._rg_buffers()
-        xg = self.grad_sync.group.exchange() if self.grad_sync is not None else {}
-        s = self._stream()
-        mlp, conv = LAYOUT.mlp_range, LAYOUT.conv_range
-        nm = self.ext.grad_reduce_mlp_blocks()
-        common = dict(rg=rg["ptr"], rg_err=self._p(rg["err"]), rg_timeout_s=self.RG_TIMEOUT_S, defer=1, **xg)
-        full = self.early_mlp == "full"
-        self._reduce(1, mlp[0], mlp[1], 0, s, rg_ctr=self._p(rg["rctr"]), **common)
-        if full:
-            self._reduce(1, conv[0], conv[1], 1, s, rg_ctr=self._p(rg["rctr"]) + 4 * nm, **common)
-        self.ext.fused_train(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
-                             self.order_len, self.batch, self._p(self.state), self._p(self.master),
-                             self._p(self.shadow), self._p(self.a0), self._p(self.h1), self._p(self.h2),
-                             self._p(self.z1), self._p(self.z2), self._p(self.z3), self._p(self.slab),
-                             self._p(self.loss), self._p(self.correct), s,
-                             next_ids=self._p(self.next_ids) if self._staged else 0,
-                             stage=self._p(self.stage) if self._staged else 0,
-                             rowg=rg["ptr"], rowg_ctr=self._p(rg["fctr"]), inlaunch=2 if full else 1)
-        if not full:
-            self._reduce(1, conv[0], conv[1], 1, s, **xg)
+                getattr(self, "_pers_ctl", 0) if getattr(self, "_pers_ctl_t", None) is None else 0]
+        if not any(bufs):
+            return
+        try:
+            torch.cuda.synchronize(self.device)
+        except Exception:
+            return  # (the device is gone: nothing can be handed back safely)
+        for p in bufs:  # each on its own: one failing free must not leak the others (ADVICE r5)
+            if p:
+                try:
+                    self.ext.uncached_free(p)
+                except Exception:
+                    pass
 
     def _launch_step(self) -> None:
         assert self.train is not None
-        if self._early_ok():
-            self._launch_step_early()
-            return
         s = self._stream()
         if self.dtype == "fp32":
             self.ext.fused_train_f32(self._p(self.train.images), self._p(self.train.labels), self._p(self.batch_ids),
@@ -888,7 +778,7 @@ class HipEngine(Engine):
         return all(v == 1.0 for v in votes), why
 
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, id(self.grad_sync), self.overlap, self.early_mlp, self.order_len,
+        key = (nsteps, id(self.grad_sync), self.overlap, self.order_len,
                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
                getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
                self._pers_ok(), self.pers_exchange)
@@ -939,21 +829,6 @@ class HipEngine(Engine):
                         poll()
                     self._launch_step()
             return
-        if self._pers_ok() and self.pers_direct and self.dtype == "bf16":
-            # the persistent launch is ONE kernel whatever n is: no graph - the extension keeps its
-            # argument block and relaunches it (one pybind call, ~3-4 us of host submit against
-            # ~8 us for a graph replay; tools/window_host_probe.py, profiles/r4/pers_handoff)
-            if poll is not None:
-                poll()
-            h = self._pers_handle()
-            with torch.cuda.device(self.device):
-                if self.ext.persist_cached(h):
-                    self.ext.persist_relaunch(h, n, self._stream())
-                else:
-                    self._launch_steps_pers(n, cache=h)
-                if self.pers_direct_sync:  # (diagnostic) no host launch while a persistent kernel runs
-                    torch.cuda.synchronize(self.device)
-            return
         if n in getattr(self, "_exact", ()):
             if poll is not None:
                 poll()
@@ -970,38 +845,33 @@ class HipEngine(Engine):
                     g.replay()
 
     def step_wait_failed(self) -> bool:
-        """Did an in-launch wait of this engine's step time out (sticky error words)?"""
-        return self.early_failed() or self.pipe_failed()
+        """Did an in-launch wait of this engine's step time out (sticky error word)?"""
+        return self.pipe_failed()
 
     def degrade(self) -> str | None:
-        """Step down one level after a StepWaitTimeout: persistent -> pipelined -> serial (each
-        bit-identical to the next).  Clears the sticky error words and the cached graphs; returns
-        the new level, or None if the engine already runs the serial step (nothing to step down
-        to: the caller re-raises)."""
-        if self.persist:
+        """Step down one level after a StepWaitTimeout, from the step form that actually ran
+        (ADVICE r5): persistent -> pipelined -> serial (each bit-identical to the next).  With a
+        per-step all-reduce the persistent form is the "-pers" exchange; it steps down to the
+        serial one-launch exchange (the pipelined step has no all-reduce form).  Clears the sticky
+        error word and the cached graphs; returns the new level, or None if the engine already
+        runs the serial step (nothing to step down to: the caller re-raises)."""
+        if self._pers_ok():
             self.persist = False
-            level = ("pipelined" if self.grad_sync is None and self.pipeline
-                     else "serial (one-launch exchange)" if self.grad_sync is not None else "serial")
-        elif self.pipeline:
+            self.pers_exchange = False
+            level = ("pipelined" if self._pipe_ok() else
+                     "serial (one-launch exchange)" if self.grad_sync is not None else "serial")
+        elif self._pipe_ok():
             self.pipeline = False
             level = "serial"
-        elif self.early_mlp:
-            self.early_mlp = False
-            level = "serial (no in-launch reduction)"
         else:
             return None
         if hasattr(self, "pipe_err"):
             self.pipe_err.zero_()
-        if self._rg is not None:
-            self._rg["err"].zero_()
         self.invalidate_graphs()
         return level
 
     def epoch_stats(self, reset: bool = True) -> StepStats:
         v = self.stats.cpu().tolist()
-        if self.early_failed():
-            raise StepWaitTimeout("early-MLP overlap: a row-granule wait timed out (the MLP reduction of a step "
-                                  "did not see the fused kernel's rows)")
         if self.pipe_failed():
             raise StepWaitTimeout("pipelined / persistent step: a ready or arrival wait timed out (a reduction or "
                                   "sample workgroup did not see its hand-off in time)")

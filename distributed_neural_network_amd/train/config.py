@@ -127,8 +127,8 @@ def _common(ap: argparse.ArgumentParser, mode: str) -> None:
                    help="step-allreduce: split the flat gradient into all-reduce buckets of at most this many "
                         "KB (0 = one fused bucket, latency-optimal for the 248 KB reference gradient)")
     g.add_argument("--allreduce", default="default",
-                   choices=("default", "ab", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap", "xgmi-pull-ovl",
-                            "xgmi-rsag-ovl", "xgmi-pull-bf16", "xgmi-rsag-bf16"),
+                   choices=("default", "ab", "xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl",
+                            "rccl-overlap", "xgmi-pull-bf16", "xgmi-rsag-bf16"),
                    help="step-allreduce transport: default (one-launch xGMI exchange on one node, else RCCL), "
                         "ab (time every candidate at start-up and keep the fastest; parallel/autotune.py) or a "
                         "path name")

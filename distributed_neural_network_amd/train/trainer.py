@@ -261,12 +261,14 @@ class Trainer:
         self.allreduce_ab = None
         if c.allreduce == "ab" and self.comm.distributed and hasattr(self.policy, "PATHS"):
             # start-up A/B of the per-step all-reduce on this node (parameters restored after)
-            from ..parallel.autotune import allreduce_ab, default_candidates
+            from ..parallel.autotune import ab_window, allreduce_ab, default_candidates
             from ..runtime.cursor import EpochCursor
 
             cur = EpochCursor(self.engine, self.sampler, self.policy, c.batch_size)
             cands = default_candidates(self.policy.grad_comm)
-            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur, steps=64, warmup=16, candidates=cands)
+            steps, warmup = ab_window(cur.steps_per_epoch)
+            self.allreduce_ab = allreduce_ab(self.policy, self.engine, cur, steps=steps, warmup=warmup,
+                                             candidates=cands)
             self._say(f"[allreduce] start-up A/B (us/step, max over ranks): {self.allreduce_ab['allreduce_ab']}; "
                       f"using {self.allreduce_ab['allreduce']}")
             self.run_log.record(event="allreduce_ab", **self.allreduce_ab)
@@ -360,6 +362,15 @@ class Trainer:
                 print(f"[engine] rank {self.comm.orig_rank}: {e}; stepping down to the {level} step and redoing "
                       f"epoch {epoch} from its start", flush=True)
                 self.run_log.record(event="step_degraded", epoch=epoch, level=level, rank=self.comm.orig_rank)
+                grp = getattr(getattr(self.engine, "grad_sync", None), "group", None)
+                if grp is not None and self.comm.distributed and hasattr(grp, "clear_error"):
+                    # (voted: every rank is here) a ready wait long enough to time out also times
+                    # out the peers' in-launch exchange waits, which set the group's sticky error
+                    # word: every rank drains its device, then all clear it - else the redo would
+                    # run with the word set and end in a CommError recovery that drops nobody
+                    self.comm.wait_device()
+                    self.comm.barrier()
+                    grp.clear_error()
                 with torch.no_grad():
                     self.engine.master.copy_(snap[0])
                     self.engine.mom.copy_(snap[1])

@@ -167,38 +167,6 @@ def test_rank_drop_recovery_on_gpu_engine(tmp_path, sync):
     assert r.stdout.count("Validation loss of updated master model:") == 3
 
 
-def test_early_mlp_overlap_matches_serial_step():
-    """In-launch reduction - the MLP reduction + SGD ("mlp"), and also the conv reduction +
-    bookkeeping ("full": one launch per step), in extra workgroups of the fused launch polling
-    the row / slab / {loss, correct} granules its samples publish - gives the serial step's
-    parameters, momentum, bf16 images and epoch statistics bit for bit, graphs and eager, tail
-    batches included, and its waits never time out."""
-    import numpy as np
-    import torch
-
-    from distributed_neural_network_amd.data import synthetic
-    from distributed_neural_network_amd.models.network import init_arena
-    from distributed_neural_network_amd.runtime import HipEngine
-
-    data = synthetic(1000, 7)  # 15 full batches + a tail of 40
-    a = init_arena(seed=3)
-    res = []
-    for early, graphs in ((False, True), ("mlp", True), ("mlp", False), ("full", True), ("full", False)):
-        eng = HipEngine(batch=64, arena=a, graph_chunk=4, use_graphs=graphs, early_mlp=early)
-        eng.attach(data)
-        stats = []
-        for ep in range(2):
-            eng.begin_epoch(np.random.default_rng(ep).permutation(1000).astype(np.int32))
-            eng.run_steps(16)
-            stats.append(eng.epoch_stats())
-        torch.cuda.synchronize()
-        assert not eng.early_failed()
-        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats))
-    for m, mo, sh, st in res[1:]:
-        assert torch.equal(res[0][0], m) and torch.equal(res[0][1], mo) and torch.equal(res[0][2], sh)
-        assert [(x.loss_sum, x.samples, x.correct) for x in st] == [(x.loss_sum, x.samples, x.correct) for x in res[0][3]]
-
-
 @pytest.mark.parametrize("graphs,chunk", [(True, 8), (True, 1), (False, 4), (True, 64)])
 def test_pipelined_step_matches_serial_step(graphs, chunk):
     """The pipelined step (launch i = step i - 1's reduction + step i's samples, the samples
@@ -212,11 +180,9 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
     rng = np.random.default_rng(3)
     orders = [rng.permutation(1000).astype(np.int32) for _ in range(3)]
     res = []
-    # serial, pipelined (one launch per step), persistent (one launch per chunk, graph replays; the
-    # opt-in direct relaunch - DNN_PERS_DIRECT=1 - is not covered: see profiles/r4/pers_direct)
-    for pipe, pers, direct in ((False, False, False), (True, False, False), (True, True, False)):
+    # serial, pipelined (one launch per step), persistent (one launch per chunk, graph replays)
+    for pipe, pers in ((False, False), (True, False), (True, True)):
         eng = HipEngine(batch=64, arena=a, graph_chunk=chunk, use_graphs=graphs, pipeline=pipe, persist=pers)
-        eng.pers_direct = direct
         eng.attach(data)
         stats = []
         for ep, order in enumerate(orders):
@@ -227,8 +193,8 @@ def test_pipelined_step_matches_serial_step(graphs, chunk):
             eng.run_steps(12 if ep != 1 else 13)  # epoch 1 runs a step past its end (a no-op)
             stats.append(eng.epoch_stats())
         torch.cuda.synchronize()
-        assert not (pipe and eng.pipe_failed()), f"variant pipe={pipe} persist={pers} direct={direct}: a wait timed out"
-        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats, (pipe, pers, direct)))
+        assert not (pipe and eng.pipe_failed()), f"variant pipe={pipe} persist={pers}: a wait timed out"
+        res.append((eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats, (pipe, pers)))
     m0, mo0, sh0, st0, _ = res[0]
     for m1, mo1, sh1, st1, var in res[1:]:
         assert torch.equal(m0, m1), f"variant {var}: master differs at {int((m0 != m1).sum())} elements"
@@ -359,17 +325,3 @@ def test_fp32_persistent_back_to_back_launches_race_regression():
     for r in range(15):
         got = run(True, r + 1)
         assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]) and ref[2] == got[2], f"run {r}"
-
-
-def test_direct_relaunch_minimal_pair_regression(tmp_path):
-    """Round 4's direct-relaunch fault (profiles/r4/pers_direct): direct persistent relaunches
-    (staged[True]) followed by the early-MLP engines, then serial / pipelined / persistent engines
-    in the same process, faulted with hipErrorIllegalAddress while engines freed their uncached
-    control buffers (hipFree) between them.  The buffers now come from a never-freed pool whose
-    free blocks hold a canary: the sequence must finish AND no freed block may have been written
-    after its free (no kernel touches a destroyed engine's control words)."""
-    env = dict(os.environ, PYTHONPATH=ROOT, DNN_PERS_DIRECT="1", REPRO_SKIP="bitwise,staged_F,determ")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "repro_direct.py")], cwd=tmp_path, env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "DONE" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
-    assert " 0 canary violations" in r.stdout, r.stdout[-2000:]

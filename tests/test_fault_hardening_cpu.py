@@ -224,6 +224,11 @@ def test_store_server_outlives_idle_while_a_local_rank_lives():
     assert "no activity" in decide(pids={}, alive=[], idle_for=6.0, **kw)  # nothing known: idle exit
     assert "checked out" in decide(pids={0: 11}, alive=[11], idle_for=0.0, **dict(kw, closed=2))
     assert "heartbeat" in decide(pids={0: 11}, alive=[11], idle_for=0.0, **dict(kw, beats=[900.0, None]))
+    # rank 1 runs on another host (pid -1): rank 0's host losing its only rank must not
+    # pull the store from under the survivor; only stale heartbeats (or check-outs) end it then
+    assert decide(pids={0: 11, 1: -1}, alive=[], idle_for=0.0, **kw) is None
+    assert decide(pids={0: 11, 1: -1}, alive=[], idle_for=1e4, **kw) is None
+    assert "heartbeat" in decide(pids={0: 11, 1: -1}, alive=[], idle_for=0.0, **dict(kw, beats=[900.0, 960.0]))
     # the running server applies it: a registered live rank keeps it up past the idle bound
     port = _free_port()
     srv = _server(port, 2, "tok2", "--idle", "5")

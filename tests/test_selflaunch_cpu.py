@@ -64,13 +64,14 @@ def test_spawn_and_relay(tmp_path, monkeypatch):
     os.close(r)
     assert rc == 0, err.getvalue()
     lines = [ln for ln in out.splitlines() if ln.strip()]
-    assert len(lines) == 1 and json.loads(lines[0]) == {"metric": "m", "value": 1.5, "n_gpus": 3}
+    assert len(lines) == 1 and json.loads(lines[0]) == {"metric": "m", "value": 1.5, "n_gpus": 3, "launch_attempts": 1}
     log = err.getvalue()
     assert "[r1] rank 1 of 3 starting" in log and "[r2] rank 2 of 3 starting" in log
     assert "banner that is not json" not in out
 
 
-def test_failed_rank_reports_and_ends_the_job(tmp_path):
+def test_failed_rank_reports_and_ends_the_job(tmp_path, monkeypatch):
+    monkeypatch.setenv("DNN_LAUNCH_ATTEMPTS", "1")  # (the retry is tested below)
     r, w = os.pipe()
     err = io.StringIO()
     t0 = time.time()
@@ -81,7 +82,7 @@ def test_failed_rank_reports_and_ends_the_job(tmp_path):
     assert rc == 3, err.getvalue()
     assert out == ""
     log = err.getvalue()
-    assert "rank 1 (exit code 3) stderr tail" in log and "boom: rank 1 fails" in log
+    assert "attempt 1: rank 1 (exit code 3) stderr tail" in log and "boom: rank 1 fails" in log
     assert "terminating" in log
     assert time.time() - t0 < 60  # rank 0 (sleeping 120 s) was terminated after the grace
 
@@ -309,14 +310,155 @@ def test_ab_wall_budget_bounds_the_start_up(monkeypatch):
     assert "skipped" in res["why"]["xgmi-rsag"] and "budget" in res["why"]["xgmi-rsag"], res
     assert seen_tmo and seen_tmo[0] <= 15.0, seen_tmo  # capped after the xGMI pass
     assert wall < 1.0 + 1.6 + 1.0 and res["ab_wall_s"] <= wall + 0.01, (wall, res)
-    assert res["variant"]["xgmi-pull"] in ("persistent", "pipelined", "early-mlp", "serial")
+    assert res["variant"]["xgmi-pull"] in ("persistent", "pipelined", "serial")
     assert pol.ab_deadline is None
 
 
-def test_ab_default_candidates_drop_the_losing_ovl_forms(monkeypatch):
-    monkeypatch.delenv("DNN_AB_OVL", raising=False)
+def test_ab_default_candidates(monkeypatch):
     c = autotune.default_candidates()
-    assert not set(autotune.OVL_PATHS) & set(c) and not set(autotune.BF16_PATHS) & set(c)
-    monkeypatch.setenv("DNN_AB_OVL", "1")
-    assert set(autotune.OVL_PATHS) <= set(autotune.default_candidates("bf16"))
+    assert c == autotune.ORDER and not set(autotune.BF16_PATHS) & set(c)
     assert set(autotune.BF16_PATHS) <= set(autotune.default_candidates("bf16"))
+    assert not any(p.endswith("-ovl") for p in StepAllReduce.PATHS)  # (removed in round 6: they lost 3x)
+
+
+# ---- bounded retry in fresh ranks (VERDICT r5 next #1) -----------------------------------------
+
+RETRY_STUB = textwrap.dedent("""
+    import json, os, sys, time
+    import torch.distributed as dist
+    from distributed_neural_network_amd.parallel.fault import setup_crash_injection
+    r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    print(f"rank {r} attempt {os.environ.get('DNN_LAUNCH_ATTEMPT')} starting", file=sys.stderr, flush=True)
+    st = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), n, is_master=False)
+    setup_crash_injection("xgmi-setup", r)   # the xGMI group set-up of parallel/xgmi.py
+    # a "collective": every rank arrives; a rank whose peer died sees the launcher's death notice
+    st.add("arrive", 1)
+    while st.add("arrive", 0) < n:
+        if any(st.check([f"dnn/dead/{p}"]) for p in range(n)):
+            print("peer died: collective failed", file=sys.stderr, flush=True)
+            sys.exit(5)
+        time.sleep(0.01)
+    print("timed window start", file=sys.stderr, flush=True)
+    if r == 0:
+        print(json.dumps({"metric": "m", "value": 2.0, "n_gpus": n,
+                          "safe": os.environ.get("DNN_SAFE_TRANSPORT", "0"),
+                          "allreduce_env": os.environ.get("DNN_ALLREDUCE", "")}))
+""")
+
+
+def _retry_stub(tmp_path):
+    p = tmp_path / "retry_stub.py"
+    p.write_text(RETRY_STUB)
+    return str(p)
+
+
+def _env_for_stub(monkeypatch):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    monkeypatch.setenv("PYTHONPATH", root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "DNN_SAFE_TRANSPORT", "DNN_LAUNCH_ATTEMPT",
+              "DNN_LAUNCH_ATTEMPTS", "DNN_INJECT_CRASH", "TORCHELASTIC_USE_AGENT_STORE"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_retry_after_an_injected_xgmi_setup_crash(tmp_path, monkeypatch):
+    """Attempt 1 loses rank 1 in the xGMI set-up (exit 134, like a GPU fault's abort); the launcher
+    starts attempt 2 in fresh ranks with the conservative transport and prints exactly ONE result
+    line, from attempt 2, carrying launch_attempts and the first failure (rank, code, phase, tail)."""
+    _env_for_stub(monkeypatch)
+    monkeypatch.setenv("DNN_INJECT_XGMI_SETUP_FAIL", "1")
+    r, w = os.pipe()
+    err = io.StringIO()
+    rc = selflaunch.run([sys.executable, _retry_stub(tmp_path)], 2, out_fd=w, err=err, grace_s=2.0)
+    os.close(w)
+    out = os.read(r, 1 << 16).decode()
+    os.close(r)
+    assert rc == 0, err.getvalue()
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    res = json.loads(lines[0])
+    assert res["launch_attempts"] == 2 and res["safe"] == "1" and res["allreduce_env"] == "rccl", res
+    assert res["launch_transport"].startswith("rccl"), res
+    (f,) = res["launch_failures"]
+    assert f["attempt"] == 1 and f["rank"] == 1 and f["exit_code"] == 134, f
+    assert f["phase"] == "before the timed window", f
+    assert any("injected crash at xgmi-setup on rank 1" in ln for ln in f["stderr_tail"]), f
+    log = err.getvalue()
+    assert "retrying in fresh ranks: attempt 2" in log and "[r0 a2] rank 0 attempt 2 starting" in log, log
+
+
+def test_no_retry_when_one_attempt_is_allowed(tmp_path, monkeypatch):
+    _env_for_stub(monkeypatch)
+    monkeypatch.setenv("DNN_INJECT_XGMI_SETUP_FAIL", "1")
+    monkeypatch.setenv("DNN_LAUNCH_ATTEMPTS", "1")
+    r, w = os.pipe()
+    err = io.StringIO()
+    rc = selflaunch.run([sys.executable, _retry_stub(tmp_path)], 2, out_fd=w, err=err, grace_s=2.0)
+    os.close(w)
+    out = os.read(r, 1 << 16).decode()
+    os.close(r)
+    assert rc == 134 and out == "", (rc, out, err.getvalue())
+    assert "no JSON result line" in err.getvalue()
+
+
+def test_attempt_plan_and_annotation():
+    assert [t for t, _ in selflaunch.attempt_plan({})] == [t for t, _ in selflaunch.ATTEMPTS]
+    assert len(selflaunch.attempt_plan({"DNN_LAUNCH_ATTEMPTS": "2"})) == 2
+    assert selflaunch.attempt_plan({"DNN_LAUNCH_ATTEMPTS": "0"}) == list(selflaunch.ATTEMPTS[:1])
+    # every retry level drops the xGMI group; the last one drops RCCL as well
+    assert all(env.get("DNN_ALLREDUCE") == "rccl" for _, env in selflaunch.ATTEMPTS[1:])
+    assert selflaunch.ATTEMPTS[-1][1]["DNN_BACKEND"] == "gloo"
+    one = selflaunch._Attempt(1, "as requested")
+    assert json.loads(selflaunch.annotate('{"value": 1}', [one])) == {"value": 1, "launch_attempts": 1}
+
+
+def test_supervisors_under_torchrun_retry_together(tmp_path, monkeypatch):
+    """torchrun launched the ranks (agent store on MASTER_PORT): every rank process supervises its
+    real rank as a child; after rank 1's injected set-up crash both supervisors start attempt 2,
+    rank 0's supervisor prints the one annotated result line, both exit 0."""
+    import subprocess
+
+    import torch.distributed as dist
+
+    _env_for_stub(monkeypatch)
+    port = selflaunch._free_port()
+    agent = dist.TCPStore("127.0.0.1", port, 3, is_master=True, wait_for_workers=False)
+    stub = _retry_stub(tmp_path)
+    code = ("import sys; from distributed_neural_network_amd.parallel import selflaunch as s; "
+            f"assert s.supervisor_wanted(); sys.exit(s.supervise([sys.executable, {stub!r}], grace_s=2.0))")
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True", TORCHELASTIC_RUN_ID="t1",
+                   DNN_INJECT_XGMI_SETUP_FAIL="1")
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    del agent
+    assert [p.returncode for p in procs] == [0, 0], outs
+    lines = [ln for ln in outs[0][0].splitlines() if ln.strip()]
+    assert len(lines) == 1 and outs[1][0].strip() == "", outs
+    res = json.loads(lines[0])
+    assert res["launch_attempts"] == 2 and res["launch_failures"][0]["rank"] == 1, res
+    assert res["launch_failures"][0]["exit_code"] == 134 and res["safe"] == "1", res
+    assert not selflaunch.supervisor_wanted({"TORCHELASTIC_USE_AGENT_STORE": "True", "WORLD_SIZE": "2",
+                                             "DNN_SUPERVISED": "1"})
+    assert not selflaunch.supervisor_wanted({"WORLD_SIZE": "2"})  # mpiexec / plain env: no supervisor
+
+
+def test_bench_supervises_before_touching_the_gpu():
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    assert src.index("selflaunch.supervise(") < src.index("torch.cuda.set_device")
+    assert "DNN_SAFE_TRANSPORT" in src and "selflaunch.WINDOW_MARK" in src
+
+
+def test_trainer_and_bench_share_the_ab_window_rule():
+    """VERDICT r5 weak #9: one A/B window rule for bench.py and the trainer."""
+    assert autotune.ab_window(782, 20, 5) == (20, 5)  # the bench's driver window
+    assert autotune.ab_window(782, 5000, 500) == (autotune.AB_MAX_STEPS, 500)
+    steps, warm = autotune.ab_window(782)  # a trainer: as much of an epoch as fits
+    assert steps == autotune.AB_MAX_STEPS and 1 <= warm <= 64 and steps + warm <= 782
+    steps, warm = autotune.ab_window(11)
+    assert steps + warm <= 11 and steps >= 1 and warm >= 1
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "distributed_neural_network_amd", "train", "trainer.py")).read()
+    assert "ab_window(cur.steps_per_epoch)" in src and "steps=64, warmup=16" not in src

@@ -145,12 +145,12 @@ comm.close()
 
 
 def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="auto", engine="fused",
-               early="0", persist="0", batch=64):
-    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{early}{persist}{batch}{graphs}"
+               persist="0", batch=64):
+    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{persist}{batch}{graphs}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
                OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch, DNN_XGMI_EXCHANGE=exchange, ENGINE=engine,
-               DNN_EARLY_MLP=early, DNN_PERSIST=persist, BATCH=str(batch))
+               DNN_PERSIST=persist, BATCH=str(batch))
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -255,23 +255,6 @@ def test_xgmi_bf16_granule_exchanges_two_ranks(tmp_path):
         assert torch.equal(res[0]["master"], res[1]["master"])
         d = (res[0]["master"] - fp[0]["master"]).abs().max().item()
         assert 0 < d < 1e-4, (xch, d)  # rounded (not the fp32 bits), but only by bf16 gradient rounding
-
-
-def test_xgmi_early_mlp_two_ranks(tmp_path):
-    """2 ranks on the box's GPU, in-launch reduction: the MLP reduction + its xGMI exchange + SGD
-    run in extra workgroups of the fused launch (polling its row granules), the conv reduction +
-    exchange follow as a split launch with its own counter range (or, "full", in the same launch).
-    Pull and two-hop forms give the serial one-launch exchange's parameters bit for bit on both
-    ranks."""
-    import torch
-
-    ref, r0 = _two_ranks(tmp_path, "xgmi", "1", 29687, exchange="pull")
-    for port, xch, mode, early in ((29689, "pull", 0, "1"), (29691, "rsag", 2, "1"), (29693, "pull", 0, "2")):
-        res, r = _two_ranks(tmp_path, "xgmi", "1", port, exchange=xch, early=early)
-        assert all(x["kind"] == "XgmiGradSync" and x["one_launch"] and x["xp_mode"] == mode for x in res), \
-            r.stderr[-2000:]
-        for i in range(2):
-            assert torch.equal(res[i]["master"], ref[i]["master"]), (xch, i)
 
 
 @pytest.mark.parametrize("batch", [16, 64])

@@ -38,8 +38,8 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
 
     for name in StepAllReduce.PATHS:
         if name.startswith("xgmi-"):
-            # (-ovl: the same exchange run by the in-launch reduction; -pers: inside the persistent launch)
-            base = name.removesuffix("-ovl").removesuffix("-pers")
+            # (-pers: the same exchange inside the persistent launch)
+            base = name.removesuffix("-pers")
             mode = xgmi.EXCHANGE_MODES[base[len("xgmi-"):]]
             assert "xgmi-" + xgmi.MODE_NAMES[mode] == base
     assert set(autotune.BF16_PATHS) <= set(StepAllReduce.PATHS)

@@ -19,21 +19,26 @@
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32 | long32serial   bench.py default window (5000 / 500), bf16 / fp32 / fp32 without PERS
 #   b2k              bench.py 2000 / 200 steps, no epoch timing (envb2k:VAR=val: under one env setting)
-#   abdirect:N       N alternating 20/5 windows: graph replays vs direct relaunch (DNN_PERS_DIRECT=1)
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
 #   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
 #   phase | phase32 | phase32pers | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
-#   reprodirect      tools/repro_direct.py with DNN_PERS_DIRECT=1 (the round-4 direct-relaunch fault)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
 #   racehunt:N[:variants[:VAR=val[:extra args]]]  tools/race_hunt.py (long run under load vs serial, per variant)
-#   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B)
+#   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B;
+#                    the original extension is restored when the script exits)
+#   inject2[:VAR=val]   2 self-launched ranks on this GPU, rank 1 killed in the xGMI set-up of launch
+#                    attempt 1 (DNN_INJECT_XGMI_SETUP_FAIL=1): the launcher's retry in fresh ranks
+#   torchrun2[:VAR=val] 2 ranks under torchrun (per-rank supervisors); torchrun2inject: + the injection
 #   vgg              layer engine, cifar-vgg bf16 / fp32, split-K fc1 forward on / off
 set -e
 O=gpurun_out/${1:?usage: gpu_run.sh OUT step...}
+SO=distributed_neural_network_amd/ops/_dnn_hip.cpython-310-x86_64-linux-gnu.so
+restore_so() { [ -f "$SO.orig" ] && mv -f "$SO.orig" "$SO"; return 0; }
+trap restore_so EXIT
 shift
 mkdir -p "$O"
 export TMPDIR=/tmp
@@ -71,12 +76,6 @@ for s in "$@"; do
     k20f32serial) DNN_PERSIST=0 timeout -k 10 150 python bench.py --dtype fp32 --steps 20 --warmup 5 > "$O/$s.json" \
                     2> "$O/$s.err" ;;
     long) timeout -k 10 300 python bench.py > "$O/long.json" 2> "$O/long.err" ;;
-    abdirect:*)  # alternating 20/5 windows, graph replays vs direct relaunch, N rounds: abdirect:N
-      for i in $(seq 1 "${s#abdirect:}"); do
-        timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-epoch > "$O/abd_graph_$i.json" 2> "$O/abd_graph_$i.err"
-        DNN_PERS_DIRECT=1 timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-epoch > "$O/abd_direct_$i.json" \
-          2> "$O/abd_direct_$i.err"
-      done ;;
     b2k) timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --no-epoch > "$O/b2k.json" 2> "$O/b2k.err" ;;
     envb2k:*)  # b2k under one runtime env setting: envb2k:VAR=value
       kv="${s#envb2k:}"; n=$(echo "$kv" | tr '=/' '__')
@@ -125,7 +124,6 @@ for s in "$@"; do
         > "$O/b2k_$n.json" 2> "$O/b2k_$n.err" ;;
     phase32) timeout -k 10 300 python tools/phase_trace_f32.py > "$O/phase32.txt" 2>&1 ;;
     phase32pers) timeout -k 10 300 python tools/phase_trace_f32.py --pers > "$O/phase32pers.txt" 2>&1 ;;
-    reprodirect) DNN_PERS_DIRECT=1 timeout -k 10 300 python -u tools/repro_direct.py > "$O/reprodirect.log" 2>&1 ;;
     rehearse2) DNN_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
                  > "$O/rehearse2.json" 2> "$O/rehearse2.err" ;;
     rehearse2diag) DNN_BACKEND=gloo DNN_AB_DEBUG=1 timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
@@ -146,8 +144,19 @@ for s in "$@"; do
       tag=$(echo "${vs}_${kv}_$xa" | tr ',=/ ' '-___')
       env "$kv" timeout -k 10 500 python tools/race_hunt.py --rounds "$n" --variants "$vs" $xa > "$O/racehunt_$tag.txt" 2>&1 ;;
     useso:*)  # A/B of kernel builds in one call: copy ops/variants/NAME.so over the live extension
-      cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" \
-        distributed_neural_network_amd/ops/_dnn_hip.cpython-310-x86_64-linux-gnu.so ;;
+      [ -f "$SO.orig" ] || cp "$SO" "$SO.orig"
+      cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" "$SO" ;;
+    inject2|inject2:*)
+      kv="${s#inject2}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" DNN_INJECT_XGMI_SETUP_FAIL=1 DNN_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 \
+        --warmup 5 > "$O/inject2_$n.json" 2> "$O/inject2_$n.err" ;;
+    torchrun2|torchrun2:*|torchrun2inject)
+      kv="${s#torchrun2}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"
+      [ "$s" = torchrun2inject ] && kv="DNN_INJECT_XGMI_SETUP_FAIL=1"
+      n=$(echo "$kv" | tr '=/' '__')
+      env "$kv" DNN_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 \
+        > "$O/torchrun2_$n.json" 2> "$O/torchrun2_$n.err" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   stamp "done $s"

@@ -146,9 +146,9 @@ def pers_main(reps: int = 30, batch: int = 64, steps: int = 8):
           f"{(w64 - w8) / (64 - steps):.3f} us")
 
 
-def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
+def main(reps: int = 50, batch: int = 64):
     tr = synthetic(4096, 0)
-    eng = HipEngine(batch=batch, seed=0, use_graphs=False, early_mlp="full" if inlaunch else False)
+    eng = HipEngine(batch=batch, seed=0, use_graphs=False)
     eng.attach(tr)
     eng.begin_epoch(np.arange(4096, dtype=np.int32))
     stamps = torch.zeros(16 + 4 * 1024, dtype=torch.int64, device=eng.device)
@@ -162,14 +162,6 @@ def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
         ev0.record()
         e = eng
         st = dict(next_ids=e._p(e.next_ids), stage=e._p(e.stage)) if e._staged else {}
-        if inlaunch:  # the whole step in one launch: reduction workgroups after the samples
-            from distributed_neural_network_amd.models.network import LAYOUT
-            rg = e._rg_buffers()
-            common = dict(rg=rg["ptr"], rg_err=e._p(rg["err"]), rg_timeout_s=e.RG_TIMEOUT_S, defer=1)
-            e._reduce(1, LAYOUT.mlp_range[0], LAYOUT.mlp_range[1], 0, e._stream(), rg_ctr=e._p(rg["rctr"]), **common)
-            e._reduce(1, 0, LAYOUT.conv_range[1], 1, e._stream(),
-                      rg_ctr=e._p(rg["rctr"]) + 4 * e.ext.grad_reduce_mlp_blocks(), **common)
-            st.update(rowg=rg["ptr"], rowg_ctr=e._p(rg["fctr"]), inlaunch=2)
         e.ext.fused_train(e._p(e.train.images), e._p(e.train.labels), e._p(e.batch_ids), e.order_len, e.batch,
                           e._p(e.state), e._p(e.master), e._p(e.shadow), e._p(e.a0), e._p(e.h1), e._p(e.h2),
                           e._p(e.z1), e._p(e.z2), e._p(e.z3), e._p(e.slab), e._p(e.loss), e._p(e.correct),
@@ -179,7 +171,7 @@ def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
         walls.append(ev0.elapsed_time(ev1) * 1000)
         s = stamps.cpu().numpy()
         waves_e.append((s[3000:3008] - s[8]) * 0.01)
-        nb = batch + (57 if inlaunch else 0)
+        nb = batch
         blocks.append(s[16:16 + 4 * nb].reshape(nb, 4).copy())
         rows.append(np.concatenate([np.diff(s[:8]), [s[8] - s[5], s[6] - s[8], s[10] - s[6],
                                                       s[7] - s[10], s[9] - s[0], s[11] - s[9],
@@ -204,12 +196,6 @@ def main(reps: int = 50, batch: int = 64, inlaunch: bool = False):
     for x in sorted(set(xcc[:batch].tolist())):
         m = xcc[:batch] == x
         print(f"  xcc {x}: {m.sum():2d} blocks, end med {np.median(smp[m, 2]):.2f} max {smp[m, 2].max():.2f} us")
-    if inlaunch:
-        red = med_b[batch:]
-        for name, sl in (("MLP reduction WGs", slice(0, 34)), ("conv reduction WGs", slice(34, 57))):
-            r = red[sl]
-            print(f"{name:20s} start med {np.median(r[:, 0]):.2f}  end min/med/max {r[:, 2].min():.2f}/"
-                  f"{np.median(r[:, 2]):.2f}/{r[:, 2].max():.2f} us")
     slow = np.argsort(-smp[:, 2])[:6]
     print("  slowest blocks:", ", ".join(f"b{i}(xcc{xcc[i]}) start {smp[i, 0]:.2f} rows {smp[i, 1]:.2f} "
                                          f"end {smp[i, 2]:.2f}" for i in slow))
@@ -221,4 +207,4 @@ if __name__ == "__main__":
     elif "--pipe" in sys.argv:
         pipe_main()
     else:
-        main(inlaunch="--inlaunch" in sys.argv)
+        main()
