@@ -162,6 +162,14 @@ __device__ __forceinline__ void pf_wait_ready(const PipeCtl& pc, int b, unsigned
 // (write-through master), then this workgroup's word in every sample's ready row.
 // stamps (diagnostic, tools/phase_trace_f32.py --pers): the last step's rows seen / body done /
 // ready stored of workgroup wg at stamps[6144 + 4 wg + k]
+// XNR > 1 (the per-step all-reduce inside the fp32 persistent launch, up to XNR ranks): each
+// block reduces its elements as above, then exchanges them exactly as the serial one-launch
+// exchange does (reduce_device.h xp_exchange / xp_exchange_rsag with the F32 sink: the same
+// granule protocol, block -> counter map gb = rblk, two-hop owner map and rank-order sum, so the
+// parameters are bit-identical to it) and stores the new parameters write-through to the fp32
+// master before the workgroup signals ready.  Idle quarters take no counter; the launch advances
+// every block's counter by nsteps at its end (lenet_fused.hip pers_reduce's rule).
+template <int XNR>
 __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeCtl& pc, int wg, long long* stamps) {
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), rtid = threadIdx.x & 255, lane = threadIdx.x & 63;
   const bool bk = wg == PIPE_CONV_BLOCKS && q == 0;
@@ -173,6 +181,9 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     if (mm < PIPE_MLP_BLOCKS) rblk = mm;
   }
   const unsigned g0 = __builtin_amdgcn_readfirstlane(ld_tag(pc.gen + blockIdx.x));
+  // (XNR) this quarter's exchange counter: the grad_reduce block index (bookkeeping: the last one)
+  const int gb = bk ? PIPE_MLP_BLOCKS + PIPE_CONV_BLOCKS : rblk;
+  const unsigned xc0 = XNR > 1 && gb >= 0 ? __builtin_amdgcn_readfirstlane(a.xp_ctr[gb]) : 0u;
   if (bk && rtid < 64) bookkeeping_pers(a, pc, lane, -1);
   const unsigned* arr = pc.arrive + (long)wg * PERS_AROW;
   for (int t = 0; t < pc.nsteps; ++t) {
@@ -187,7 +198,24 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     if (bk) {
       if (rtid < 64) bookkeeping_pers(a, pc, lane_o, t);
     } else if (rblk >= 0) {
-      grad_reduce_body<WtF32Sink, true>(a, sk, rblk, tid_o & 255, t & 1);
+      if constexpr (XNR > 1) {
+        const unsigned step = xc0 + (unsigned)t + 1u;
+        const bool failed = __hip_atomic_load(a.xp_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+        XpSinkT<false, true, true> xs;
+        xs.tag = (unsigned long long)step << 32;
+        xs.stash = tid_o;  // (8 x NT floats of the reduction workgroup's otherwise unused LDS)
+        xs.stride = NT;
+        const bool publish = (a.xp_mode & 2) == 0 || gb % a.xp_nranks != a.xp_rank;
+        xs.own = publish ? reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_gslot_off +
+                                                                 (step & 1u) * a.xp_gslot_bytes)
+                         : nullptr;
+        if (grad_reduce_body<XpSinkT<false, true, true>, true>(a, xs, rblk, tid_o & 255, t & 1)) {
+          if ((a.xp_mode & 2) == 0) xp_exchange<XNR>(a, xs, step, failed, rblk, tid_o & 255);
+          else xp_exchange_rsag<XNR>(a, xs, step, failed, rblk, tid_o & 255);
+        }
+      } else {
+        grad_reduce_body<WtF32Sink, true>(a, sk, rblk, tid_o & 255, t & 1);
+      }
     }
     if (st) stamps[6145 + 4 * wg] = (long long)__builtin_amdgcn_s_memrealtime();
     // (diagnostic: the last step's per-wave body done / drained, stamps[6400 + 32 wg + 2 wave + k])
@@ -202,6 +230,9 @@ __device__ __forceinline__ void pers_reduce_f32(const ReduceArgs& a, const PipeC
     sk.flush(a);  // momentum + bf16 shadow: off the hand-off's critical path (drained by the next step's wait)
   }
   if (threadIdx.x == 0) st_tag(pc.gen + blockIdx.x, g0 + (unsigned)pc.nsteps);
+  if constexpr (XNR > 1) {
+    if (gb >= 0 && rtid == 0) a.xp_ctr[gb] = xc0 + (unsigned)pc.nsteps;  // (the next launch reads it)
+  }
 }
 
 // Parameter loads: plain, or (WT: the persistent launch) sc1 loads of the write-through master
@@ -1002,10 +1033,12 @@ __global__ void __launch_bounds__(NT) lenet_f32_kernel(const F32Args A) {
 }
 
 // The persistent launch: PF_WG reduction workgroups, then one workgroup per sample, every one
-// looping over pc.nsteps steps (lenet_fused.hip PERS's protocol; the rows alternate parities)
+// looping over pc.nsteps steps (lenet_fused.hip PERS's protocol; the rows alternate parities).
+// XNR: the per-step exchange inside the launch for groups of up to XNR ranks (0: none)
+template <int XNR>
 __global__ void __launch_bounds__(NT) lenet_f32_pers_kernel(const F32Args A, const ReduceArgs ra, const PipeCtl pc) {
   if ((int)blockIdx.x < PF_WG) {
-    pers_reduce_f32(ra, pc, blockIdx.x, A.stamps);
+    pers_reduce_f32<XNR>(ra, pc, blockIdx.x, A.stamps);
     return;
   }
   const int b = (int)blockIdx.x - PF_WG;
@@ -1025,7 +1058,7 @@ void init_kernels_f32() {
   static bool done = false;
   if (done) return;
   const void* kerns[] = {(const void*)f32k::lenet_f32_kernel<true>, (const void*)f32k::lenet_f32_kernel<false>,
-                         (const void*)f32k::lenet_f32_pers_kernel};
+                         (const void*)f32k::lenet_f32_pers_kernel<0>, (const void*)f32k::lenet_f32_pers_kernel<8>};
   for (const void* k : kerns)
     HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, f32k::LDS_TOTAL));
   done = true;
@@ -1064,8 +1097,11 @@ int persist_resident_workgroups_f32() {
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(f32k::lenet_f32_pers_kernel), f32k::NT, f32k::LDS_TOTAL));
-    resident = per_cu * cus;
+        &per_cu, reinterpret_cast<const void*>(f32k::lenet_f32_pers_kernel<0>), f32k::NT, f32k::LDS_TOTAL));
+    int per_cu_x = 0;  // (the exchange instance: its own register count)
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu_x, reinterpret_cast<const void*>(f32k::lenet_f32_pers_kernel<8>), f32k::NT, f32k::LDS_TOTAL));
+    resident = std::min(per_cu, per_cu_x) * cus;
   }
   return resident;
 }
@@ -1091,8 +1127,16 @@ void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels
       !pc_in.nid_slot[1])
     throw std::runtime_error("fused_train_persist_f32: needs the control block, the error word and both slots");
   if (!red.bookkeeping || red.batch != batch || !red.fuse_sgd || red.lo != 0 || red.hi < ARENA ||
-      red.xp_nranks != 0 || red.batch_ids == nullptr || red.master != master)
-    throw std::runtime_error("fused_train_persist_f32: a local whole-arena fused-SGD reduction with bookkeeping");
+      red.batch_ids == nullptr || red.master != master)
+    throw std::runtime_error("fused_train_persist_f32: a whole-arena fused-SGD reduction with bookkeeping");
+  // the in-launch exchange: the serial one-launch exchange's arguments (fp32 granules, pull or
+  // two-hop, grad_scale 1, counters set) - as lenet_fused.hip launch_fused_train_persist checks
+  if (red.xp_nranks != 0 &&
+      (red.xp_nranks < 1 || red.xp_nranks > XG_MAX_RANKS || (red.xp_mode & ~2) != 0 || red.grad_scale != 1.f ||
+       red.xp_ctr == nullptr || red.xp_err == nullptr || red.xp_abort == nullptr || red.xp_rank < 0 ||
+       red.xp_rank >= red.xp_nranks))
+    throw std::runtime_error("fused_train_persist_f32: the in-launch exchange takes the whole-arena one-launch "
+                             "exchange (fp32 granules, pull or two-hop, grad_scale 1, counters set)");
   if (red.a0 != a0 || red.h1 != h1 || red.h2 != h2 || red.z1 != z1 || red.z2 != z2 || red.z3 != z3 ||
       red.slab != slab || red.loss != loss || red.correct != correct)
     throw std::runtime_error("fused_train_persist_f32: the reduction reads the rows the samples write");
@@ -1103,8 +1147,8 @@ void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels
   pc.arrive = reinterpret_cast<unsigned*>(base + pers_arrive_off(batch));
   const f32k::F32Args A{images, labels, red.batch_ids, order_len, batch, 0, nullptr, master, a0, h1, h2, z1, z2, z3,
                         slab, loss, correct, stamps};
-  hipLaunchKernelGGL(f32k::lenet_f32_pers_kernel, dim3(f32k::PF_WG + batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream,
-                     A, red, pc);
+  auto* kern = red.xp_nranks == 0 ? &f32k::lenet_f32_pers_kernel<0> : &f32k::lenet_f32_pers_kernel<8>;
+  hipLaunchKernelGGL(kern, dim3(f32k::PF_WG + batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, A, red, pc);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -217,12 +217,17 @@ __device__ __forceinline__ void DirectSinkT<WT>::put_tile(const f32x4& acc, cons
 //    WT (the persistent launch's in-launch exchange, lenet_fused.hip PERS): the update after the
 //    exchange stores what the samples of the same launch read write-through - an fc1 / fc2 tile
 //    through wt_tile_update (the lane records its tile: tile_info), every other element as
-//    sgd_finish<true> does.
-template <bool PK, bool WT = false>
+//    sgd_finish<true> does.  F32 (with WT: the fp32 kernel's persistent launch, lenet_f32.hip
+//    PERS): its samples read every weight from the fp32 master, so every new parameter is stored
+//    write-through there (WtF32Sink's stores), the momentum and the bf16 shadow plainly.
+template <bool PK, bool WT = false, bool F32 = false>
 struct XpSinkT {
+  static_assert(!F32 || (WT && !PK), "the fp32 persistent exchange: write-through, fp32 granules");
+  static constexpr bool kPK = PK, kWT = WT, kF32 = F32;
   static constexpr bool kTile = false;
-  static constexpr bool kTileInfo = WT;
-  static constexpr bool kOpaqueLane = false;
+  static constexpr bool kTileInfo = WT && !F32;
+  static constexpr bool kOpaqueLane = F32;  // (the fp32 launch: 128 VGPRs, see WtF32Sink)
+  static constexpr int kRC = F32 ? 2 : 8;     // peer ranks per polling round (reduce_device.h gather_rank_sum)
   int tl = -1, to0 = 0, ti0 = 0;  // WT: the fc tile (layer, o0, i0) this lane's elements belong to
   template <int LAYER>
   __device__ __forceinline__ void tile_info(int o0, int i0) {

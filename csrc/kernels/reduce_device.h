@@ -107,8 +107,23 @@ __device__ __forceinline__ long long poll_granules(const ReduceArgs& a, const un
 // WT (the persistent launch): write-through stores of everything the samples of the same launch
 // read - an fc1 / fc2 tile through wt_tile_update (the same SGD arithmetic: grad_scale is 1 there,
 // so acc * grad_scale is s * xp_scale bit for bit), any other element as sgd_finish<true>.
-template <bool PK, bool WT = false>
-__device__ __forceinline__ void apply_update(const ReduceArgs& a, const XpSinkT<PK, WT>& sk, const float (&s)[4]) {
+// F32 (the fp32 persistent launch): every parameter write-through to the fp32 master, the
+// momentum and the bf16 shadow plain - the serial exchange's arithmetic, element by element.
+template <class Sink>
+__device__ __forceinline__ void apply_update(const ReduceArgs& a, const Sink& sk, const float (&s)[4]) {
+  constexpr bool WT = Sink::kWT;
+  if constexpr (Sink::kF32) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!sk.v[j]) continue;
+      float p, m;
+      sgd_update(s[j] * a.xp_scale, sk.pv(j), sk.mv(j), a.lr, a.momentum, p, m);
+      st_wt(a.master + sk.e[j], p);
+      a.mom[sk.e[j]] = m;
+      write_shadow(a.shadow, sk.e[j], p);
+    }
+    return;
+  }
   if constexpr (WT) {
     if (sk.tl == 0 || sk.tl == 1) {  // (wave-uniform: one tile per wave)
       f32x4 acc;
@@ -182,6 +197,49 @@ __device__ __forceinline__ void unpack_pairs(float (&x)[4], const bool (&valid)[
   }
 }
 
+// Read every peer rank's granules of this lane's elements (own: this rank's values, kept for
+// r == xp_rank) and fold the N values into s in RANK ORDER (s = v0 + v1 + ... in fp32).  RC ranks
+// per polling round: the register arrays hold RC ranks' 64-bit loads in flight; RC < NR spends one
+// more remote round per chunk to fit a tighter register budget (the fp32 persistent launch runs at
+// 128 VGPRs).  Chunks go in ascending rank order, so the additions are exactly one round's.
+// Returns the total wait.
+template <int NR, int RC, bool PK>
+__device__ __forceinline__ long long gather_rank_sum(const ReduceArgs& a, const int (&e)[4], const bool (&vld)[4],
+                                                     const float (&own)[4], unsigned step, bool failed, int par,
+                                                     float (&s)[4]) {
+  static_assert(NR % RC == 0, "whole chunks");
+  long long waited = 0;
+#pragma unroll
+  for (int r0 = 0; r0 < NR; r0 += RC) {
+    float v[RC][4];
+    unsigned pending = 0;
+    const unsigned long long* src[RC];
+#pragma unroll
+    for (int k = 0; k < RC; ++k) {
+      const int r = r0 + k;
+      src[k] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[k][j] = own[j];
+        if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(vld, j)) pending |= 1u << (4 * k + j);
+      }
+    }
+    waited += poll_granules<RC>(a, src, e, pending, step, failed, v);
+#pragma unroll
+    for (int k = 0; k < RC; ++k)
+      if (r0 + k < a.xp_nranks && r0 + k != a.xp_rank) unpack_pairs<PK>(v[k], vld);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < RC; ++k) {
+        const int r = r0 + k;
+        if (r == 0) s[j] = v[k][j];
+        else if (r < a.xp_nranks) s[j] += v[k][j];
+      }
+  }
+  return waited;
+}
+
 // The one-launch all-reduce exchange of ONE lane's (<= 4) reduced elements.  Each element
 // was stored as a granule {value, step} (XpSink::put); the lane reads the same element's
 // granule from every peer's slot over xGMI (7 links at once) until each tag shows this step,
@@ -194,35 +252,15 @@ __device__ __forceinline__ void unpack_pairs(float (&x)[4], const bool (&valid)[
 // NR: group-size bucket (2, 4 or 8 >= xp_nranks) - sizes the register arrays, so a 2-rank
 // group does not pay for 8 ranks' loads in flight.  PK: bf16 granules (half the link bytes;
 // the sum stays fp32 in rank order).
-template <int NR, bool PK, bool WT = false>
-__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK, WT>& sk, unsigned step, bool failed,
-                                            int rblk, int rtid) {
+template <int NR, class Sink>
+__device__ __forceinline__ void xp_exchange(const ReduceArgs& a, Sink& sk, unsigned step, bool failed, int rblk,
+                                            int rtid) {
+  constexpr bool PK = Sink::kPK;
+  constexpr int RC = NR < Sink::kRC ? NR : Sink::kRC;
   const int par = step & 1u;
   pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);
-  float v[NR][4];
-  unsigned pending = 0;
-  const unsigned long long* src[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[r][j] = sk.g[j];
-      if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
-    }
-  }
-  record_wait(a, step, poll_granules<NR>(a, src, sk.e, pending, step, failed, v), rblk, rtid);
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
   float s[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    s[j] = v[0][j];
-#pragma unroll
-    for (int r = 1; r < NR; ++r)
-      if (r < a.xp_nranks) s[j] += v[r][j];
-  }
+  record_wait(a, step, gather_rank_sum<NR, RC, PK>(a, sk.e, sk.v, sk.g, step, failed, par, s), rblk, rtid);
   apply_update(a, sk, s);
 }
 
@@ -234,38 +272,18 @@ __device__ __forceinline__ void xp_exchange(const ReduceArgs& a, XpSinkT<PK, WT>
 // applies SGD; the other ranks read that slot.  2 E / N granules per link instead of E, one
 // more dependent remote read.  PK: the sum is all-gathered as bf16 too (every rank, the owner
 // included, applies the rounded sum).
-template <int NR, bool PK, bool WT = false>
-__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, XpSinkT<PK, WT>& sk, unsigned step, bool failed,
-                                                 int rblk, int rtid) {
+template <int NR, class Sink>
+__device__ __forceinline__ void xp_exchange_rsag(const ReduceArgs& a, Sink& sk, unsigned step, bool failed, int rblk,
+                                                 int rtid) {
+  constexpr bool PK = Sink::kPK;
   const int par = step & 1u;
   const int owner = rblk % a.xp_nranks;
   pack_pairs<PK>(sk.g, sk.v, sk.e, sk.own, sk.tag);  // (null own on the owner: rounding only)
   float s[4];
   long long waited;
   if (owner == a.xp_rank) {
-    float v[NR][4];
-    unsigned pending = 0;
-    const unsigned long long* src[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      src[r] = reinterpret_cast<const unsigned long long*>(a.xp_region[r] + a.xp_gslot_off + par * a.xp_gslot_bytes);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[r][j] = sk.g[j];
-        if (r < a.xp_nranks && r != a.xp_rank && polled<PK>(sk.v, j)) pending |= 1u << (4 * r + j);
-      }
-    }
-    waited = poll_granules<NR>(a, src, sk.e, pending, step, failed, v);
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-      if (r < a.xp_nranks && r != a.xp_rank) unpack_pairs<PK>(v[r], sk.v);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[j] = v[0][j];
-#pragma unroll
-      for (int r = 1; r < NR; ++r)
-        if (r < a.xp_nranks) s[j] += v[r][j];
-    }
+    constexpr int RC = NR < Sink::kRC ? NR : Sink::kRC;
+    waited = gather_rank_sum<NR, RC, PK>(a, sk.e, sk.v, sk.g, step, failed, par, s);
     const unsigned long long tag = (unsigned long long)step << 32;
     unsigned long long* dst =
         reinterpret_cast<unsigned long long*>(a.xp_region[a.xp_rank] + a.xp_ag_off + par * a.xp_gslot_bytes);
@@ -316,8 +334,8 @@ __device__ __forceinline__ void reduce_block(const ReduceArgs& a, int rblk, int 
                                                              (step & 1u) * a.xp_gslot_bytes)
                      : nullptr;
     if (grad_reduce_body(a, sk, rblk, rtid)) {
-      if ((a.xp_mode & 2) == 0) xp_exchange<NR, PK>(a, sk, step, failed, rblk, rtid);
-      else xp_exchange_rsag<NR, PK>(a, sk, step, failed, rblk, rtid);
+      if ((a.xp_mode & 2) == 0) xp_exchange<NR>(a, sk, step, failed, rblk, rtid);
+      else xp_exchange_rsag<NR>(a, sk, step, failed, rblk, rtid);
     }
     __syncthreads();  // every thread read this block's counters before they advance
     if (rtid == 0) a.xp_ctr[gb] = step;

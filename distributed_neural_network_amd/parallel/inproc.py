@@ -119,7 +119,9 @@ class PairRunner:
         self.left = self.spe
 
     def prepare(self, steps: int) -> None:
-        """Capture every chunk graph + the exact-size graph of ``steps`` (outside timing)."""
+        """Capture every chunk graph + the exact-size graph of ``steps`` (outside timing).  Every
+        rank's graphs must exist before any rank replays one: a capture synchronizes the device,
+        so capturing while a peer's replay waits on this rank's granules ends in a timed-out wait."""
         for e, s in zip(self.engines, self.streams):
             with torch.cuda.stream(s):
                 e.prepare_graphs(exact=(steps,))

@@ -175,9 +175,11 @@ class StepAllReduce(SyncPolicy):
         if xgmi.wanted(self.comm) and engine.grad.numel() <= self.XGMI_MAX_ELEMS:
             mode = xgmi.exchange_mode() | (4 if self.grad_comm == "bf16" else 0)
             # the persistent form where the engine has one (fp32 granules; falls back to the
-            # serial one-launch exchange if its self-test fails)
-            pers = ("-pers" if mode in (0, 2) and getattr(engine, "persist", False) and getattr(engine, "pipeline", False)
-                    else "")  # (the bf16 persistent launch: the fp32 one has no in-launch exchange)
+            # serial one-launch exchange if its self-test fails): the bf16 kernel's (on top of its
+            # pipelined step) or the fp32 kernel's
+            has_pers = getattr(engine, "persist", False) and (getattr(engine, "pipeline", False)
+                                                               or getattr(engine, "dtype", "") == "fp32")
+            pers = "-pers" if mode in (0, 2) and has_pers else ""
             return "xgmi-" + xgmi.MODE_NAMES[mode] + pers
         return "rccl" if self.comm.backend == "nccl" else "torch-pg"
 

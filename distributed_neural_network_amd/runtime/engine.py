@@ -523,9 +523,9 @@ class HipEngine(Engine):
     def _pers_ok(self) -> bool:
         """The persistent launch runs: the pipelined step's conditions and persist - or, with a
         per-step all-reduce, its "-pers" form (the exchange inside the launch's reduction).
-        fp32: lenet_f32.hip's persistent launch, local steps only."""
+        fp32: lenet_f32.hip's persistent launch (its "-pers" exchange too: round 6)."""
         if self.dtype == "fp32":
-            return self.persist and self._ahead and self.grad_sync is None
+            return self.persist and self._ahead and (self.grad_sync is None or self._pers_xchg() is not None)
         if not (self.persist and self.pipeline and self._staged):
             return False
         return self.grad_sync is None or self._pers_xchg() is not None
@@ -537,13 +537,15 @@ class HipEngine(Engine):
         s = self._stream()
         sp = self._p(self.state)
         r = self._rows(0)
+        grp = self._pers_xchg()
+        xg = grp.exchange() if grp is not None else {}
         if self.dtype == "fp32":
             self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
                                  self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
                                  self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
                                  self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
                                  self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
-                                 self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids))
+                                 self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids), **xg)
             self.ext.fused_train_persist_f32(self._p(self.train.images), self._p(self.train.labels), self.order_len,
                                              self.batch, self._p(self.master), self._p(r["a0"]), self._p(r["h1"]),
                                              self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]), self._p(r["z3"]),
@@ -552,8 +554,6 @@ class HipEngine(Engine):
                                              self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
                                              flags=self.pipe_flags, stamps=self._pipe_stamps)
             return
-        grp = self._pers_xchg()
-        xg = grp.exchange() if grp is not None else {}
         self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
                              self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
                              self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
@@ -722,14 +722,15 @@ class HipEngine(Engine):
         runs touch - parameters, optimizer state, epoch cursor and order, bookkeeping slots, the
         image stage, epoch statistics - is restored afterwards, so it can run mid-epoch (the
         start-up A/B).  Returns (every rank passed, this rank's reason if not)."""
-        avail = self.train is not None and self.persist and self.pipeline and self.stage is not None
+        avail = self.train is not None and self.persist and (
+            self.dtype == "fp32" or (self.pipeline and self.stage is not None))
         if not all(v == 1.0 for v in comm.gather_scalars(1.0 if avail else 0.0)):  # (same collectives everywhere)
             return False, "the persistent launch is not available on " + ("this rank" if not avail else "a peer")
         dev = self.device
-        keep = [self.master, self.mom, self.shadow, self.state, self.stats, self.batch_ids, self.next_ids,
-                self.next_ids2, self.stage]
+        keep = [t for t in (self.master, self.mom, self.shadow, self.state, self.stats, self.batch_ids, self.next_ids,
+                            self.next_ids2, self.stage) if t is not None]
         saved = [t.clone() for t in keep]
-        saved_attrs = (self.order_len, self._staged, self.pers_exchange)
+        saved_attrs = (self.order_len, self._staged, self._ahead, self.pers_exchange)
         saved_order = self.order[:self.order_len].clone()
         n = min(len(self.train), steps * self.batch)
         order = np.arange(n, dtype=np.int32)
@@ -766,7 +767,7 @@ class HipEngine(Engine):
             ok = same
         votes = comm.gather_scalars(1.0 if ok else 0.0)
         with torch.no_grad():
-            self.order_len, self._staged, self.pers_exchange = saved_attrs
+            self.order_len, self._staged, self._ahead, self.pers_exchange = saved_attrs
             if self.order_len:
                 self.order[:self.order_len].copy_(saved_order)
             for t, v in zip(keep, saved):

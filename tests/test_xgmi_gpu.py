@@ -120,7 +120,7 @@ if os.environ.get("ENGINE", "fused") == "layers":
                       use_graphs=os.environ["GRAPHS"] == "1")
 else:
     eng = HipEngine(batch=int(os.environ.get("BATCH", "64")), arena=init_arena(seed=11), graph_chunk=8,
-                    use_graphs=os.environ["GRAPHS"] == "1")
+                    use_graphs=os.environ["GRAPHS"] == "1", dtype=os.environ.get("DTYPE", "bf16"))
 eng.attach(data)
 pol = make_policy("step-allreduce", comm)
 pol.attach(eng)
@@ -145,12 +145,12 @@ comm.close()
 
 
 def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, exchange="auto", engine="fused",
-               persist="0", batch=64):
-    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{persist}{batch}{graphs}"
+               persist="0", batch=64, dtype="bf16"):
+    out = tmp_path / f"{allreduce}{one_launch}{nproc}{exchange}{engine}{persist}{batch}{graphs}{dtype}"
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
                OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch, DNN_XGMI_EXCHANGE=exchange, ENGINE=engine,
-               DNN_PERSIST=persist, BATCH=str(batch))
+               DNN_PERSIST=persist, BATCH=str(batch), DTYPE=dtype)
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -257,20 +257,23 @@ def test_xgmi_bf16_granule_exchanges_two_ranks(tmp_path):
         assert 0 < d < 1e-4, (xch, d)  # rounded (not the fp32 bits), but only by bf16 gradient rounding
 
 
-@pytest.mark.parametrize("batch", [16, 64])
-def test_xgmi_exchange_inside_persistent_launch_two_ranks(tmp_path, batch):
+# (fp32 at batch 32: two ranks' fp32 grids, 2 x (63 + B) workgroups, must fit the GPU they share)
+@pytest.mark.parametrize("batch,dtype", [(16, "bf16"), (64, "bf16"), (32, "fp32")])
+def test_xgmi_exchange_inside_persistent_launch_two_ranks(tmp_path, batch, dtype):
     """2 ranks on the box's GPU, the per-step exchange INSIDE the persistent
     launch (xgmi-pull-pers / xgmi-rsag-pers: the reduction workgroups exchange their elements
     over xGMI after each step's batch reduction, sum in rank order, apply SGD and only then signal
     the samples) - installed after its self-test, engaged, and bit-identical on both ranks to the
-    serial one-launch exchange, over 2 epochs with graph replays and eager launches."""
+    serial one-launch exchange, over 2 epochs with graph replays and eager launches.  fp32 (VERDICT
+    r5 next #5): the fp32 kernel's persistent launch with the exchange inside."""
     import torch
 
-    port = 29701 + (batch // 16) * 10
-    ref, r0 = _two_ranks(tmp_path, "xgmi", "1", port, exchange="pull", batch=batch)
+    port = 29701 + (batch // 16) * 10 + (40 if dtype == "fp32" else 0)
+    ref, r0 = _two_ranks(tmp_path, "xgmi", "1", port, exchange="pull", batch=batch, dtype=dtype)
     assert all(not x["pers"] and x["path"] == "xgmi-pull" for x in ref), r0.stderr[-2000:]
     for k, (xch, graphs) in enumerate((("pull", "1"), ("rsag", "1"), ("pull", "0"))):
-        res, r = _two_ranks(tmp_path, "xgmi", graphs, port + 2 + 2 * k, exchange=xch, persist="1", batch=batch)
+        res, r = _two_ranks(tmp_path, "xgmi", graphs, port + 2 + 2 * k, exchange=xch, persist="1", batch=batch,
+                            dtype=dtype)
         assert all(x["pers"] and x["path"] == f"xgmi-{xch}-pers" for x in res), (
             [(x["path"], x["pers"]) for x in res], r.stdout[-2000:] + r.stderr[-3000:])
         for i in range(2):

@@ -100,10 +100,24 @@ def test_choose_never_local_and_skips_failed():
 
 
 def test_choose_tie_prefers_order():
-    res = {"rccl": _r(20.0), "xgmi-rsag": _r(20.0), "xgmi-pull": _r(20.0)}
+    res = {"rccl": _r(30.0), "xgmi-rsag": _r(20.0), "xgmi-pull": _r(20.0)}
     assert autotune.choose(res) == "xgmi-pull"
     res["xgmi-pull-pers"] = _r(20.0)  # the persistent form is ranked first
     assert autotune.choose(res) == "xgmi-pull-pers"
+
+
+def test_choose_prefers_rccl_within_noise(monkeypatch):
+    """VERDICT r5 weak #7 / SURVEY §5.8: the custom xGMI exchange is chosen only when it beats RCCL
+    by more than the A/B's noise margin (DNN_AB_RCCL_MARGIN, 3 %)."""
+    monkeypatch.delenv("DNN_AB_RCCL_MARGIN", raising=False)
+    res = {"rccl": _r(20.5), "rccl-overlap": _r(21.0), "xgmi-pull": _r(20.0), "xgmi-pull-pers": _r(20.2)}
+    assert autotune.choose(res) == "rccl"  # 2.5 % slower: within noise
+    res["rccl"] = _r(21.0)
+    assert autotune.choose(res) == "xgmi-pull"  # 5 % slower: the xGMI exchange wins
+    assert autotune.choose(res, margin=0.1) == "rccl"
+    monkeypatch.setenv("DNN_AB_RCCL_MARGIN", "0")
+    assert autotune.choose({"rccl": _r(20.0), "xgmi-pull": _r(20.0)}) == "rccl"  # (a tie is no win)
+    assert autotune.choose({"rccl": _r(20.0), "xgmi-pull": _r(19.9)}) == "xgmi-pull"
 
 
 def test_ab_two_ranks_agree(tmp_path):

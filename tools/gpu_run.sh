@@ -30,6 +30,7 @@
 #   racehunt:N[:variants[:VAR=val[:extra args]]]  tools/race_hunt.py (long run under load vs serial, per variant)
 #   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B;
 #                    the original extension is restored when the script exits)
+#   inproc[:args]    tools/inproc_pair.py (2 in-process ranks on this GPU: exchange forms, JSON)
 #   inject2[:VAR=val]   2 self-launched ranks on this GPU, rank 1 killed in the xGMI set-up of launch
 #                    attempt 1 (DNN_INJECT_XGMI_SETUP_FAIL=1): the launcher's retry in fresh ranks
 #   torchrun2[:VAR=val] 2 ranks under torchrun (per-rank supervisors); torchrun2inject: + the injection
@@ -146,6 +147,9 @@ for s in "$@"; do
     useso:*)  # A/B of kernel builds in one call: copy ops/variants/NAME.so over the live extension
       [ -f "$SO.orig" ] || cp "$SO" "$SO.orig"
       cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" "$SO" ;;
+    inproc|inproc:*)
+      xa="${s#inproc}"; xa="${xa#:}"; n=$(echo "inproc_$xa" | tr ' =/-' '____')
+      timeout -k 10 400 python tools/inproc_pair.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
     inject2|inject2:*)
       kv="${s#inject2}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
       env "$kv" DNN_INJECT_XGMI_SETUP_FAIL=1 DNN_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 \

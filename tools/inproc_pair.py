@@ -46,6 +46,7 @@ def main() -> None:
     ap.add_argument("--long", type=int, default=200)
     ap.add_argument("--spin", type=int, default=200)
     ap.add_argument("--forms", default=",".join(FORMS))
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp32"))
     a = ap.parse_args()
     n = a.ranks
     train = synthetic(50_000, 0, True, noise=SYNTH_NOISE_HARD)
@@ -53,12 +54,12 @@ def main() -> None:
     rng = np.random.default_rng(0)
     orders = [(r * shard + rng.permutation(shard)).astype(np.int32) for r in range(n)]
     arena = init_arena(seed=0)
-    engines = [HipEngine(batch=a.batch, arena=arena, graph_chunk=64) for _ in range(n)]
+    engines = [HipEngine(batch=a.batch, arena=arena, graph_chunk=64, dtype=a.dtype) for _ in range(n)]
     for e in engines:
         e.attach(train)
     groups = inproc.build_pair(engines, record_waits=True)
     runner = inproc.PairRunner(engines, orders)
-    out = {"ranks": n, "batch": a.batch, "steps": a.steps, "warmup": a.warmup, "reps": a.reps, "long": a.long,
+    out = {"ranks": n, "dtype": a.dtype, "batch": a.batch, "steps": a.steps, "warmup": a.warmup, "reps": a.reps, "long": a.long,
            "device": torch.cuda.get_device_name(0), "forms": {}}
 
     def timed(steps: int, warm: int) -> tuple[float, float]:
@@ -85,8 +86,11 @@ def main() -> None:
             e.pipe_err.zero_()
         for g in groups:
             g.clear_error()
-        # bit-identity run: the same 3 x 17 steps from the same start on every form
+        # bit-identity run: the same 2 x 17 steps from the same start on every form (graphs captured
+        # first: a capture synchronizes the device, which a peer's replay waiting on this rank's
+        # granules would turn into a timed-out wait)
         runner.begin()
+        runner.prepare(17)
         runner.run(17)
         runner.begin()
         runner.run(17)
@@ -128,7 +132,7 @@ def main() -> None:
                                         if f.endswith("-pers")}
     inproc.close(engines, groups)
     # one engine alone (the 1-GPU bench's step), for scale
-    e1 = HipEngine(batch=a.batch, arena=arena, graph_chunk=64)
+    e1 = HipEngine(batch=a.batch, arena=arena, graph_chunk=64, dtype=a.dtype)
     e1.attach(train)
     r1 = inproc.PairRunner([e1], [orders[0]])
     runner = r1
