@@ -29,6 +29,8 @@ std::tuple<uintptr_t, std::string, std::string> xgmi_alloc(long long capacity);
 uintptr_t uncached_alloc(long long bytes);
 void uncached_free(uintptr_t p);
 std::tuple<long long, long long, long long> uncached_pool_stats();
+void lds_poison(unsigned pattern, hipStream_t stream);
+void lds_squat(int bytes, double spin_us, int blocks, uintptr_t bad, hipStream_t stream);
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
 std::string xgmi_device_id();
@@ -504,7 +506,27 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("xgmi_free", &dnn::xgmi_free);
   m.def("uncached_alloc", &dnn::uncached_alloc);
   m.def("uncached_free", &dnn::uncached_free);
+  // A stream with a hardware queue of its own: HIP multiplexes ordinary streams onto a few
+  // hardware queues (GPU_MAX_HW_QUEUES), in order, so two streams of one process can land on
+  // the same queue and run one after the other.  Kernels that wait for each other (the
+  // in-process exchange harness: two ranks' grids polling each other's granules) must not: a
+  // CU-masked stream (all CUs) gets a dedicated queue.  Never destroyed (parallel/inproc.py).
+  m.def("stream_create_own_queue", []() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
+      throw std::runtime_error("stream_create_own_queue: device query failed");
+    std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+    hipStream_t s = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+    return reinterpret_cast<u>(s);
+  });
   m.def("uncached_pool_stats", &dnn::uncached_pool_stats);
+  m.def("lds_poison", [](unsigned pattern, u stream) { dnn::lds_poison(pattern, S(stream)); }, py::arg("pattern"),
+        py::arg("stream"));
+  m.def("lds_squat", [](int bytes, double spin_us, int blocks, u bad, u stream) {
+    dnn::lds_squat(bytes, spin_us, blocks, bad, S(stream));
+  }, py::arg("bytes"), py::arg("spin_us"), py::arg("blocks"), py::arg("bad"), py::arg("stream"));
   m.def("xgmi_abort_word", &dnn::xgmi_abort_word);
   m.def("xgmi_set_abort", &dnn::xgmi_set_abort);
   m.def("xgmi_free_abort_word", &dnn::xgmi_free_abort_word);

@@ -70,14 +70,7 @@ constexpr int L_DA0 = L_DZ1B + 256;         // f32 [400]
 constexpr int L_IMG = L_DA0 + 1600;         // u8 [3][32][32] raw image (re-used by phase F)
 constexpr int L_MISC = L_IMG + 3072;
 constexpr int L_F1C = L_MISC + 64;          // u8 [80] phase F's conv1-wgrad column table (kF1Col)
-// PERS: the NEXT step's image + label, LDS-DMA'd by waves 5-7 while the step waits for conv1's
-// weights (DNN_PERS_NXT_DMA; phase A of the next step copies it to L_IMG)
-constexpr int L_NXT = L_F1C + 128;          // u8 [3072] image | int32 label (+ 12 B pad)
-constexpr int LDS_TOTAL = L_NXT + 3072 + 16;  // 159,520 B
-#ifndef DNN_PERS_NXT_DMA
-#define DNN_PERS_NXT_DMA 1
-#endif
-constexpr bool kNxtDma = DNN_PERS_NXT_DMA != 0;
+constexpr int LDS_TOTAL = L_F1C + 128;      // 156,432 B
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
 static_assert(B_WF + 20480 <= L_REGB_SZ, "REGB sub-layout");
 
@@ -118,16 +111,6 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
-// One lane's 4 bytes: global -> LDS [lds_base + 4 lane) (the caller masks the lanes)
-__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds_base) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
       : "memory");
@@ -886,10 +869,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   else if (tid < 58) DZ3B[10 + tid - 36] = (bf16)0.f;
   else if (tid < 70) DZ2B[84 + tid - 58] = (bf16)0.f;
   else if (tid < 78) DZ1B[120 + tid - 70] = (bf16)0.f;
-  if (PERS && kNxtDma && s > 0) {  // the image + label DMA'd into L_NXT during the previous step
-    if (tid < 192) reinterpret_cast<uint4*>(IMGS)[tid] = reinterpret_cast<const uint4*>(smem + L_NXT)[tid];
-    if (tid == 192) *reinterpret_cast<int*>(smem + L_MISC) = *reinterpret_cast<const int*>(smem + L_NXT + 3072);
-  } else if (PERS && s > 0) {  // the image + label this wave group staged in the previous step's phase F
+  if (PERS && s > 0) {  // the image + label this wave group staged in the previous step's phase F
     if (tid >= 320) reinterpret_cast<uint4*>(IMGS)[tid - 320] = carry_im;
     if (tid == 320) *reinterpret_cast<int*>(smem + L_MISC) = carry_lab;
   } else {
@@ -900,26 +880,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if (PERS) label = *reinterpret_cast<const int*>(smem + L_MISC);  // (one path for every step)
   STAMP(9);
   if (tid < 384) build_r1_part(IMGS, R1, r1_row(tid), r1_q(tid));
-  if constexpr (PERS && kNxtDma) {
-    // the NEXT step's image + label (its sample id was published two steps ahead: slot s & 1 holds
-    // step s + 1's ids from the start of this step) go to L_NXT by LDS-DMA now, in the idle time
-    // before conv1's weights are ready - no register carry, no global round trip in phase F, and
-    // nothing for the end-of-step drain to wait for (the arrival's vmcnt(0) used to wait for the
-    // id -> image -> stage chain).  Waves 5-7: 1 KB each; wave 7's lane 0 also the label.
-    if (wave >= 5) {
-      const int32_t* p = pc.nid_slot[s & 1] + b;
-      asm volatile("" : "+v"(p));
-      const int nid = __builtin_amdgcn_readfirstlane(ld_sc1(p));
-      if (nid >= 0) {
-        const uint32_t nb = __builtin_amdgcn_readfirstlane(lds_addr(smem + L_NXT) + (uint32_t)(wave - 5) * 1024u);
-        dma16(images + (size_t)nid * IMG + (wave - 5) * 1024 + lane * 16, nb);
-        if (wave == 7) {
-          const uint32_t lb = __builtin_amdgcn_readfirstlane(nb + 1024u);  // L_NXT + 3072
-          if (lane == 0) dma4(labels + nid, lb);
-        }
-      }
-    }
-  }
   unsigned c2_err = 0u, c2_v = 0u;  // (PERS, below)
   int bv_pre = batch;
   if constexpr (PIPE) {
@@ -1566,7 +1526,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
     static_assert(2 * (NT - 168) <= 768 && 768 - 2 * (NT - 168) <= 168, "R1 half-task split");
     if (tid < 768 - 2 * (NT - 168)) build_r1_half(IMGS, R1, 2 * (NT - 168) + tid);
   } else {
-    if (staged && wave >= 5 && !(PERS && kNxtDma)) {  // a vector load: the lgkmcnt(0) of the barriers does not wait for it
+    if (staged && wave >= 5) {  // a vector load: the lgkmcnt(0) of the barriers does not wait for it
       const int32_t* p = (PERS ? pc.nid_slot[s & 1] : next_ids) + b;
       asm volatile("" : "+v"(p));
       ns_next = PERS ? ld_sc1(p) : *p;
@@ -1576,7 +1536,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   }
   lds_barrier();
   STAMP(10);
-  if (staged && wave >= 5 && ns_next >= 0 && !(PERS && kNxtDma)) {
+  if (staged && wave >= 5 && ns_next >= 0) {
     const int t = tid - 320;  // 192 threads x 16 B = one image
     const uint4 v = reinterpret_cast<const uint4*>(images + (size_t)ns_next * IMG)[t];
     const int lab = t == 0 ? labels[ns_next] : 0;
@@ -1635,13 +1595,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2)))
   if constexpr (PERS) {
     pers_arrive_kind(0);  // slab + loss / correct drained: the conv workgroups go
     if (stamp) stamps[2398] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (kNxtDma && s == nsteps - 1 && tid < 192) {
-      // the launch's last step: the next LAUNCH's step 0 reads its image + label from the global
-      // stage (the DMA landed: every wave drained before the arrival's barrier) - after the
-      // arrival, so this store delays no hand-off (the kernel's end drains it)
-      stage_im[(size_t)b * (IMG / 16) + tid] = reinterpret_cast<const uint4*>(smem + L_NXT)[tid];
-      if (tid == 0) stage_lab[b] = *reinterpret_cast<const int*>(smem + L_NXT + 3072);
-    }
   }
 #undef STAMP
 #undef WSTAMP

@@ -34,6 +34,7 @@ HIP_SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "linear.hip",
     CSRC / "comm" / "xgmi_allreduce.hip",
+    CSRC / "kernels" / "diag.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"
 HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp"]

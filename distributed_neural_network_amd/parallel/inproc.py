@@ -56,6 +56,31 @@ class InprocGroup(XgmiGroup):
         self.devices = 1
 
 
+_OWN_QUEUE: dict = {}  # device index -> streams with a hardware queue of their own (never destroyed)
+
+
+def own_queue_streams(engines: list) -> list:
+    """One stream per rank, each with a HARDWARE queue of its own (a CU-masked stream over every
+    CU: csrc/bindings.cpp stream_create_own_queue).  Ordinary streams share the process' few
+    hardware queues (GPU_MAX_HW_QUEUES, 4): two ranks whose streams share one run one after the
+    other, and a rank's exchange then waits for granules its peer cannot publish until the wait
+    times out.  Which streams share a queue depends on every stream the process created before
+    (tools/inproc_stream_probe.py: one extra stream created first was enough).  The streams are
+    kept for the life of the process and handed out again: the caching allocator keeps blocks
+    of tensors allocated on a stream tied to that stream, so it must never be destroyed."""
+    dev = engines[0].device
+    pool = _OWN_QUEUE.setdefault(dev.index if dev.index is not None else torch.cuda.current_device(), [])
+    with torch.cuda.device(dev):
+        while len(pool) < len(engines):
+            pool.append(torch.cuda.ExternalStream(engines[0].ext.stream_create_own_queue(), device=dev))
+    return pool[:len(engines)]
+
+
+def release_streams(engines: list, streams: list) -> None:
+    """The ranks' work is done (the streams stay in the pool for the next harness)."""
+    torch.cuda.synchronize(engines[0].device)
+
+
 def build_pair(engines: list, mode: int = 0, timeout_s: float = 5.0, record_waits: bool = True) -> list[InprocGroup]:
     """Install an in-process exchange group of form ``mode`` (xgmi.EXCHANGE_MODES: 0 pull, 2
     two-hop) on every engine of ``engines`` (one rank each, rank = list index)."""
@@ -107,9 +132,13 @@ class PairRunner:
 
     def __init__(self, engines: list, orders: list[np.ndarray]) -> None:
         self.engines, self.orders = engines, orders
-        self.streams = [torch.cuda.Stream(e.device) for e in engines]
+        self.streams = own_queue_streams(engines)
         self.spe = engines[0].steps_per_epoch() if engines[0].order_len else None
         self.left = 0
+
+    def release(self) -> None:
+        release_streams(self.engines, self.streams)
+        self.streams = []
 
     def begin(self) -> None:
         for e, s, o in zip(self.engines, self.streams, self.orders):
@@ -154,4 +183,4 @@ class PairRunner:
         return 1e6 * wall / steps, 1e6 * gpu / steps
 
 
-__all__ = ["InprocGroup", "PairRunner", "build_pair", "close", "set_form"]
+__all__ = ["InprocGroup", "PairRunner", "build_pair", "close", "own_queue_streams", "release_streams", "set_form"]

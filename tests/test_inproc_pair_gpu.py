@@ -4,16 +4,22 @@ HipEngines, one stream each, their grids concurrently resident - no IPC, no time
 the serial one-launch exchange's parameters, momentum and bf16 images BIT FOR BIT on both
 ranks, over shuffled epochs with a tail batch, graph replays and eager launches, with no failed
 wait; and the replicas must stay identical."""
+import sys
+
 import numpy as np
 import pytest
 import torch
 
 from distributed_neural_network_amd.data import synthetic
-from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.models.network import LAYOUT, init_arena
 from distributed_neural_network_amd.parallel import inproc
 from distributed_neural_network_amd.runtime import HipEngine
 
 pytestmark = pytest.mark.gpu
+
+
+def _regions() -> dict:
+    return {k: (o, LAYOUT.numel(k)) for k, o in LAYOUT.offsets.items()}
 
 
 def _run(form: str, graphs: bool, batch: int = 64, dtype: str = "bf16"):
@@ -26,7 +32,7 @@ def _run(form: str, graphs: bool, batch: int = 64, dtype: str = "bf16"):
     groups = inproc.build_pair(engines, timeout_s=5.0)
     inproc.set_form(engines, groups, form)
     orders = [[(1000 * r + rng.permutation(1000)).astype(np.int32) for r in range(2)] for _ in range(2)]
-    streams = [torch.cuda.Stream() for _ in engines]
+    streams = inproc.own_queue_streams(engines)  # (a hardware queue per rank: parallel/inproc.py)
     stats = []
     try:
         for ep in range(2):
@@ -45,21 +51,35 @@ def _run(form: str, graphs: bool, batch: int = 64, dtype: str = "bf16"):
                         e.run_steps(k)
             torch.cuda.synchronize()
             stats.append([e.epoch_stats() for e in engines])
+            d = (engines[0].master != engines[1].master).nonzero().flatten().cpu()
+            if d.numel():  # (diagnostic: the epoch the replicas parted, per parameter tensor)
+                where = {k: int(((d >= o) & (d < o + n)).sum()) for k, (o, n) in _regions().items()}
+                print(f"{form}: epoch {ep}: replicas differ at {d.numel()} elements "
+                      f"{ {k: v for k, v in where.items() if v} }; first {d[:16].tolist()}")
+                n = LAYOUT.total
+                for r, e in enumerate(engines):  # does each rank's bf16 image still match its own master?
+                    m = e.master[:n]
+                    print(f"  rank {r}: shadow != bf16(master) at {int((e.shadow[:n] != m.to(torch.bfloat16)).sum())}; "
+                          f"master at the first split {m[d[:4]].tolist()}; "
+                          f"xp_ctr {groups[r].xp_ctr[:8].tolist()} ctr_err {int(groups[r].ctr[-1])}")
         assert not any(e.pipe_failed() for e in engines) and not any(g.failed() for g in groups), form
         return [(e.master.cpu(), e.mom.cpu(), e.shadow.cpu()) for e in engines], stats
     finally:
         inproc.close(engines, groups)
+        inproc.release_streams(engines, streams)
 
 
-@pytest.mark.parametrize("dtype,graphs", [("bf16", True), ("bf16", False), ("fp32", True), ("fp32", False)])
-def test_inproc_pers_exchange_matches_serial_exchange(dtype, graphs):
+def _check(dtype: str, graphs: bool) -> None:
     """bf16: lenet_fused.hip's persistent launch with the exchange inside (pers_reduce<XNR>); fp32
     (VERDICT r5 next #5): lenet_f32.hip's (pers_reduce_f32<XNR>, the F32 exchange sink: fp32 master
     write-through, 2 peer ranks per polling round at 128 VGPRs) - each against its own serial
     one-launch exchange."""
     batch = 64 if dtype == "bf16" else 32  # (2 x (63 + B) fp32 workgroups: both grids resident at once)
     ref, st0 = _run("xgmi-pull", graphs, batch=batch, dtype=dtype)
-    assert torch.equal(ref[0][0], ref[1][0]), "serial exchange: replicas differ"
+    bad = (ref[0][0] != ref[1][0]).nonzero().flatten()
+    assert bad.numel() == 0, \
+        f"serial exchange: replicas differ at {bad.numel()} elements, first {bad[:8].tolist()}, max |d| " \
+        f"{float((ref[0][0] - ref[1][0]).abs().max()):.3e}; losses {[[s.loss_sum for s in ep] for ep in st0]}"
     for form in ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-rsag"):
         got, st = _run(form, graphs, batch=batch, dtype=dtype)
         for r in range(2):
@@ -67,3 +87,18 @@ def test_inproc_pers_exchange_matches_serial_exchange(dtype, graphs):
                 assert torch.equal(x, y), f"{form} rank {r}: {name} differs at {int((x != y).sum())} elements"
         assert [[(s.loss_sum, s.samples) for s in ep] for ep in st] == \
             [[(s.loss_sum, s.samples) for s in ep] for ep in st0], form
+
+
+@pytest.mark.parametrize("dtype,graphs", [("bf16", True), ("bf16", False), ("fp32", True), ("fp32", False)])
+def test_inproc_pers_exchange_matches_serial_exchange(dtype, graphs):
+    """In the suite's own long-lived process: each rank's stream has a hardware queue of its own
+    (parallel/inproc.py own_queue_streams).  With ordinary pool streams the two ranks shared a
+    queue whenever the streams created earlier in the process lined them up so (6 of 11 suite
+    runs; tools/inproc_stream_probe.py: one extra stream created first failed every time) - the
+    ranks then ran one after the other and the exchange waits timed out."""
+    _check(dtype, graphs)
+
+
+if __name__ == "__main__":
+    _check(sys.argv[1], bool(int(sys.argv[2])))
+    print("ok")

@@ -9,6 +9,7 @@
 #   smoke            __graft_entry__.smoke()
 #   tests            the whole GPU suite (pytest -m gpu, per-test timeout)
 #   tests:<expr>     GPU tests selected by -k <expr>
+#   files:a,b,..     the GPU tests of tests/test_a_gpu.py, ... in that order (failed asserts do not end the call)
 #   envtests:VAR=val the whole GPU suite under one environment setting
 #   k20 | k20b       bench.py --steps 20 --warmup 5 (the driver's window), bf16
 #   k20f32           the same, --dtype fp32
@@ -31,6 +32,9 @@
 #   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B;
 #                    the original extension is restored when the script exits)
 #   inproc[:args]    tools/inproc_pair.py (2 in-process ranks on this GPU: exchange forms, JSON)
+#   inproctrace:f,.. tools/inproc_pair.py --trace (per-block waits, per-step starts of those forms)
+#   streamprobe[:a,b] tools/inproc_stream_probe.py (does the harness depend on streams created before it?)
+#   export:VAR=val   export for the later steps (their output names get _VAR)
 #   inject2[:VAR=val]   2 self-launched ranks on this GPU, rank 1 killed in the xGMI set-up of launch
 #                    attempt 1 (DNN_INJECT_XGMI_SETUP_FAIL=1): the launcher's retry in fresh ranks
 #   torchrun2[:VAR=val] 2 ranks under torchrun (per-rank supervisors); torchrun2inject: + the injection
@@ -43,6 +47,7 @@ trap restore_so EXIT
 shift
 mkdir -p "$O"
 export TMPDIR=/tmp
+USESO=""  # "_NAME" after useso:NAME (suffix of the later steps' output names)
 stamp() { echo "[gpu_run $(date +%H:%M:%S)] $*"; }
 for s in "$@"; do
   stamp "step $s"
@@ -56,6 +61,15 @@ for s in "$@"; do
              > "$O/tests_$n.log" 2>&1 ;;
     tests:*) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
              -k "${s#tests:}" > "$O/tests_k.log" 2>&1 ;;
+    export:*)  # export:VAR=val for the later steps of this call (their output names get _VAR)
+      kv="${s#export:}"; export "${kv?}"; USESO="${USESO}_${kv%%=*}" ;;
+    files:*)  # files:a,b,...: the GPU tests of tests/test_<a>_gpu.py, ... in that order (one process)
+      fs=""; for f in $(echo "${s#files:}" | tr ',' ' '); do fs="$fs tests/test_${f}_gpu.py"; done
+      n=$(echo "${s#files:}" | tr ',' '_')
+      # (exit 1 = failed assertions only: the call goes on; a crash, abort or time limit ends it)
+      rc=0; timeout -k 10 900 python -u -m pytest $fs -m gpu -v --timeout 300 --timeout-method thread \
+             > "$O/files_$n$USESO.log" 2>&1 || rc=$?
+      [ "$rc" -le 1 ] || exit "$rc" ;;
     k20|k20b) timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     k20pipe) DNN_PIPELINE=1 timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/$s.json" 2> "$O/$s.err" ;;
     longpipe) DNN_PIPELINE=1 timeout -k 10 300 python bench.py > "$O/$s.json" 2> "$O/$s.err" ;;
@@ -146,10 +160,17 @@ for s in "$@"; do
       env "$kv" timeout -k 10 500 python tools/race_hunt.py --rounds "$n" --variants "$vs" $xa > "$O/racehunt_$tag.txt" 2>&1 ;;
     useso:*)  # A/B of kernel builds in one call: copy ops/variants/NAME.so over the live extension
       [ -f "$SO.orig" ] || cp "$SO" "$SO.orig"
-      cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" "$SO" ;;
+      cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" "$SO"
+      USESO="_${s#useso:}" ;;
+    inproctrace:*)
+      f="${s#inproctrace:}"; n=$(echo "$f" | tr ',' '_')$USESO
+      timeout -k 10 300 python tools/inproc_pair.py --trace "$f" > "$O/inproctrace_$n.json" 2> "$O/inproctrace_$n.err" ;;
     inproc|inproc:*)
-      xa="${s#inproc}"; xa="${xa#:}"; n=$(echo "inproc_$xa" | tr ' =/-' '____')
+      xa="${s#inproc}"; xa="${xa#:}"; n=$(echo "inproc_$xa" | tr ' =/-' '____')$USESO
       timeout -k 10 400 python tools/inproc_pair.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
+    streamprobe|streamprobe:*)  # tools/inproc_stream_probe.py [args, spaces as commas]
+      xa=$(echo "${s#streamprobe}" | sed 's/^://; s/,/ /g'); n=$(echo "sp_$xa" | tr ' =/-' '____')$USESO
+      timeout -k 10 600 python tools/inproc_stream_probe.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
     inject2|inject2:*)
       kv="${s#inject2}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
       env "$kv" DNN_INJECT_XGMI_SETUP_FAIL=1 DNN_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 \

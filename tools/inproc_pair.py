@@ -36,6 +36,57 @@ from distributed_neural_network_amd.runtime import HipEngine  # noqa: E402
 FORMS = ("local", "xgmi-pull", "xgmi-rsag", "xgmi-pull-pers", "xgmi-rsag-pers")
 
 
+def trace(engines, groups, runner, form: str, steps: int = 64, reps: int = 5) -> dict:
+    """Diagnostic (--trace): where the exchange forms spend their time.  Per-block exchange waits
+    (the wait ring: per step, the longest wave wait of each grad_reduce block; medians over the
+    steps of block categories) and sample block 0's per-step start times on every rank (stamps,
+    s_memrealtime 100 MHz), over ``reps`` launches of ``steps`` steps."""
+    dev = engines[0].device
+    inproc.set_form(engines, groups, form)
+    bufs = [torch.zeros(4096 + 64, dtype=torch.int64, device=dev) for _ in engines]
+    for e, b in zip(engines, bufs):
+        e._pipe_stamps = b.data_ptr()
+    runner.begin()
+    runner.prepare(steps)
+    cats = {"mlp_tiles": range(0, 64), "mlp_bias": range(64, 68), "conv1": range(68, 76), "conv2": range(76, 113)}
+    out = {"form": form, "cats": {}, "step_starts": [], "skew_us": []}
+    per_cat = {k: [] for k in cats}
+    for _ in range(reps):
+        if runner.left < steps:
+            runner.begin()
+        for g in groups:
+            g.reset_wait_stats()
+        for b in bufs:
+            b.zero_()
+        runner.run(steps)
+        torch.cuda.synchronize(dev)
+        ring, nblk, waves = engines[0].ext.xgmi_wait_ring()
+        for g in groups:
+            if g.wait is None:
+                continue
+            w = g.wait.view(ring, nblk, waves).cpu()
+            st = (w >> 32) & 0xffffffff
+            tk = (w & 0xffffffff).double() / 100.0
+            newest = int(st.max())
+            for k, blks in cats.items():
+                for s_ in range(newest - steps + 2, newest + 1):  # (the launch's steps; the first skipped)
+                    m = st[s_ % ring, list(blks)] == s_
+                    if bool(m.any()):
+                        per_cat[k].append(float(torch.where(m, tk[s_ % ring, list(blks)], torch.zeros(())).max()))
+        starts = [b.cpu().numpy()[2048:2048 + steps].astype(np.float64) for b in bufs]
+        t0 = min(x[0] for x in starts)
+        out["step_starts"].append([[round((v - t0) * 0.01, 2) for v in x[:12]] for x in starts])
+        out["skew_us"].append([round(float(np.median(np.abs(starts[0] - x))) * 0.01, 2) for x in starts[1:]])
+        out["period_us"] = [round(float(np.median(np.diff(x))) * 0.01, 2) for x in starts]
+    for k, v in per_cat.items():
+        if v:
+            out["cats"][k] = {"median": round(float(np.median(v)), 2), "p90": round(float(np.quantile(v, 0.9)), 2)}
+    for e in engines:
+        e._pipe_stamps = 0
+        e.invalidate_graphs()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=2)
@@ -47,6 +98,7 @@ def main() -> None:
     ap.add_argument("--spin", type=int, default=200)
     ap.add_argument("--forms", default=",".join(FORMS))
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp32"))
+    ap.add_argument("--trace", default="", help="diagnostic: per-block waits + per-step starts of these forms")
     a = ap.parse_args()
     n = a.ranks
     train = synthetic(50_000, 0, True, noise=SYNTH_NOISE_HARD)
@@ -73,6 +125,12 @@ def main() -> None:
             gpus.append(g)
         return statistics.median(walls), statistics.median(gpus)
 
+    if a.trace:
+        res = [trace(engines, groups, runner, f) for f in a.trace.split(",")]
+        inproc.close(engines, groups)
+        runner.release()
+        print(json.dumps({"trace": res}))
+        return
     p0 = [(e.master.clone(), e.mom.clone()) for e in engines]
     finals = {}
     for form in a.forms.split(","):
@@ -131,6 +189,7 @@ def main() -> None:
         out["pers_overhead_long_us"] = {f: round(v["long_us"] - loc["long_us"], 3) for f, v in out["forms"].items()
                                         if f.endswith("-pers")}
     inproc.close(engines, groups)
+    runner.release()
     # one engine alone (the 1-GPU bench's step), for scale
     e1 = HipEngine(batch=a.batch, arena=arena, graph_chunk=64, dtype=a.dtype)
     e1.attach(train)
@@ -141,6 +200,7 @@ def main() -> None:
     r1.run(a.spin)
     w20, g20 = timed(a.steps, a.warmup)
     out["single"] = {"window_us": round(w20, 3), "window_gpu_us": round(g20, 3)}
+    r1.release()
     print(json.dumps(out))
 
 
