@@ -39,19 +39,26 @@ from typing import Callable, Optional
 
 import torch
 
-# the persistent-launch forms first: on a tie they win (no kernel boundary between steps)
-ORDER = ("xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+# The default candidates.  The exchange inside the persistent launch ("-pers") left this list in
+# round 6 (kept only if it costs <= 3 us/step over the local persistent step):
+# with two ranks resident side by side on one GPU and no time-slicing (tools/inproc_pair.py,
+# profiles/r6/inproc/) it costs 67 us/step over that step in the 20/5 window (84.6 vs 17.8) and
+# loses to the serial one-launch exchange (52.1) in every window length.  DNN_AB_PERS=1 adds it.
+ORDER = ("xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap")
+PERS_PATHS = ("xgmi-pull-pers", "xgmi-rsag-pers")
 # opt-in (--grad-comm bf16): the xGMI exchanges with bf16 gradient granules - half the link
 # bytes, lower-precision gradients, so never a candidate unless asked for
 BF16_PATHS = ("xgmi-pull-bf16", "xgmi-rsag-bf16")
-RANK = ORDER + BF16_PATHS  # tie-break order
+RANK = PERS_PATHS + ORDER + BF16_PATHS  # tie-break order (a -pers form first: no kernel boundary)
 
 
 def default_candidates(grad_comm: str = "fp32") -> tuple[str, ...]:
-    """The A/B's candidate list: ORDER, + BF16_PATHS when bf16 gradient communication was asked
-    for.  (The in-launch "-ovl" forms lost 3x in every rehearsal and were removed in round 6,
+    """The A/B's candidate list: ORDER, + PERS_PATHS first with DNN_AB_PERS=1, + BF16_PATHS when
+    bf16 gradient communication was asked for.  (The in-launch "-ovl" forms lost 3x in every rehearsal and were removed in round 6,
     profiles/r4/ab_rehearsal.)"""
     c = ORDER
+    if os.environ.get("DNN_AB_PERS") == "1":
+        c = PERS_PATHS + c
     if grad_comm == "bf16":
         c = c + BF16_PATHS
     return c
@@ -324,5 +331,5 @@ def _drop(policy, engine, name: str) -> None:
             policy.comm.native = None
 
 
-__all__ = ["AB_MAX_STEPS", "BF16_PATHS", "ORDER", "ab_window", "allreduce_ab", "budget_default", "choose",
+__all__ = ["AB_MAX_STEPS", "BF16_PATHS", "ORDER", "PERS_PATHS", "ab_window", "allreduce_ab", "budget_default", "choose",
            "default_candidates", "prepare_window", "rccl_margin", "step_variant", "window"]

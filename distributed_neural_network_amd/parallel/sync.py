@@ -17,6 +17,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import time
 
 import torch
@@ -174,12 +176,14 @@ class StepAllReduce(SyncPolicy):
                 if self.comm.backend == "nccl" else "torch-pg"
         if xgmi.wanted(self.comm) and engine.grad.numel() <= self.XGMI_MAX_ELEMS:
             mode = xgmi.exchange_mode() | (4 if self.grad_comm == "bf16" else 0)
-            # the persistent form where the engine has one (fp32 granules; falls back to the
-            # serial one-launch exchange if its self-test fails): the bf16 kernel's (on top of its
-            # pipelined step) or the fp32 kernel's
+            # the serial one-launch exchange; the exchange inside the persistent launch only with
+            # DNN_AB_PERS=1 (it lost to the serial form by 32 us/step with two ranks side by side
+            # on one GPU, profiles/r6/inproc/; parallel/autotune.py ORDER) and where the engine
+            # has that launch (fp32 granules; falls back to the serial exchange if its self-test
+            # fails): the bf16 kernel's (on top of its pipelined step) or the fp32 kernel's
             has_pers = getattr(engine, "persist", False) and (getattr(engine, "pipeline", False)
                                                                or getattr(engine, "dtype", "") == "fp32")
-            pers = "-pers" if mode in (0, 2) and has_pers else ""
+            pers = "-pers" if mode in (0, 2) and has_pers and os.environ.get("DNN_AB_PERS") == "1" else ""
             return "xgmi-" + xgmi.MODE_NAMES[mode] + pers
         return "rccl" if self.comm.backend == "nccl" else "torch-pg"
 

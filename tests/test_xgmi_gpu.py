@@ -150,7 +150,7 @@ def _two_ranks(tmp_path, allreduce, graphs, port, one_launch="1", nproc=2, excha
     out.mkdir()
     env = dict(os.environ, PYTHONPATH=ROOT, DNN_BACKEND="gloo", DNN_ALLREDUCE=allreduce, OMP_NUM_THREADS="2",
                OUT=str(out), GRAPHS=graphs, DNN_XGMI_ONE_LAUNCH=one_launch, DNN_XGMI_EXCHANGE=exchange, ENGINE=engine,
-               DNN_PERSIST=persist, BATCH=str(batch), DTYPE=dtype)
+               DNN_PERSIST=persist, DNN_AB_PERS=persist, BATCH=str(batch), DTYPE=dtype)
     script = tmp_path / "w.py"
     script.write_text(_TWO_RANK)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -228,11 +228,10 @@ def test_bench_two_ranks_xgmi(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
-    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag", "xgmi-pull-pers",
-                                                                   "xgmi-rsag-pers"), out
+    assert out["n_gpus"] == 2 and out["config"]["allreduce"] in ("xgmi-pull", "xgmi-rsag"), out
     ab = out["allreduce_ab"]
-    assert set(ab) == {"xgmi-pull-pers", "xgmi-rsag-pers", "xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"}, out
-    assert ab["xgmi-pull-pers"] is not None and out["allreduce_ab_variant"]["xgmi-pull-pers"] == "persistent", out
+    # (the -pers forms are candidates only with DNN_AB_PERS=1: parallel/autotune.py ORDER)
+    assert set(ab) == {"xgmi-pull", "xgmi-rsag", "rccl", "rccl-overlap"}, out
     assert out["ab_wall_s"] > 0, out
     assert ab["xgmi-pull"] is not None and ab["rccl"] is None and "rccl" in out["allreduce_failed"], out
     assert out["local_step_us"] > 0, out

@@ -65,7 +65,10 @@ def test_path_names_map_to_exchange_modes(monkeypatch):
     monkeypatch.setattr(xgmi, "wanted", lambda comm: True)
     monkeypatch.delenv("DNN_XGMI_EXCHANGE", raising=False)
     assert pol.default_path(_Eng()) == "xgmi-pull"
-    # an engine with the persistent launch gets the exchange inside it (fp32 granules only)
+    # the exchange inside the persistent launch is opt-in (DNN_AB_PERS=1; fp32 granules only)
+    monkeypatch.delenv("DNN_AB_PERS", raising=False)
+    assert pol.default_path(_PersEng()) == "xgmi-pull"
+    monkeypatch.setenv("DNN_AB_PERS", "1")
     assert pol.default_path(_PersEng()) == "xgmi-pull-pers"
     assert pol.default_path(_PersF32Eng()) == "xgmi-pull"
     pol.grad_comm = "bf16"
@@ -90,6 +93,18 @@ def test_choose_fastest_passing():
     res = {"local": _r(10.0), "xgmi-pull": _r(30.0), "xgmi-rsag": _r(25.0), "rccl": _r(40.0),
            "rccl-overlap": _r(None, False)}
     assert autotune.choose(res) == "xgmi-rsag"
+
+
+def test_pers_forms_are_opt_in_candidates(monkeypatch):
+    """Round 6: the exchange inside the persistent launch lost to the serial
+    one-launch exchange by tens of us/step in the in-process harness (profiles/r6/inproc/), so it
+    is an A/B candidate only with DNN_AB_PERS=1 (and then ranked first)."""
+    monkeypatch.delenv("DNN_AB_PERS", raising=False)
+    c = autotune.default_candidates()
+    assert not any(k.endswith("-pers") for k in c) and c[0] == "xgmi-pull"
+    monkeypatch.setenv("DNN_AB_PERS", "1")
+    c = autotune.default_candidates("bf16")
+    assert c[:2] == autotune.PERS_PATHS and set(autotune.BF16_PATHS) <= set(c)
 
 
 def test_choose_never_local_and_skips_failed():

@@ -20,6 +20,7 @@
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
 #   long | long32 | long32serial   bench.py default window (5000 / 500), bf16 / fp32 / fp32 without PERS
 #   b2k              bench.py 2000 / 200 steps, no epoch timing (envb2k:VAR=val: under one env setting)
+#   profk20          rocprofv3 --kernel-trace over the driver's 20/5 window (+3 diagnostic windows)
 #   prof | prof32    rocprofv3 --kernel-trace --stats over 2000 steps (bf16 / fp32)
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
@@ -33,6 +34,7 @@
 #                    the original extension is restored when the script exits)
 #   inproc[:args]    tools/inproc_pair.py (2 in-process ranks on this GPU: exchange forms, JSON)
 #   inproctrace:f,.. tools/inproc_pair.py --trace (per-block waits, per-step starts of those forms)
+#   diverge[:a,b]   tools/inproc_diverge.py (when the in-process ranks' replicas part; args comma-separated)
 #   streamprobe[:a,b] tools/inproc_stream_probe.py (does the harness depend on streams created before it?)
 #   export:VAR=val   export for the later steps (their output names get _VAR)
 #   inject2[:VAR=val]   2 self-launched ranks on this GPU, rank 1 killed in the xGMI set-up of launch
@@ -112,6 +114,9 @@ for s in "$@"; do
       db=$(find "$O/$s" -name '*.db' | head -n 1 || true)
       [ -n "$db" ] && python tools/kstats.py "$db" --steps 2200 > "$O/${s}_kernel_stats.txt" 2>&1 || true
       unset DNN_PIPELINE ;;
+    profk20)  # kernel trace of the driver's window (kernel span vs the bench's wall time per window)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$s" -o run -- \
+        python3 bench.py --steps 20 --warmup 5 --diag-windows 3 > "$O/$s.log" 2>&1 ;;
     pmc:*|pmcserial:*)
       c="${s#*:}"; n=$(echo "$c" | tr ',' '_' | cut -c1-60); pre=pmc
       [ "${s%%:*}" = pmcserial ] && { export DNN_PIPELINE=0; pre=pmcserial; }
@@ -168,6 +173,9 @@ for s in "$@"; do
     inproc|inproc:*)
       xa="${s#inproc}"; xa="${xa#:}"; n=$(echo "inproc_$xa" | tr ' =/-' '____')$USESO
       timeout -k 10 400 python tools/inproc_pair.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
+    diverge|diverge:*)  # tools/inproc_diverge.py [args, spaces as commas]: when do the in-process ranks part?
+      xa=$(echo "${s#diverge}" | sed 's/^://; s/,/ /g'); n=$(echo "dv_$xa" | tr ' =/-' '____')$USESO
+      timeout -k 10 500 python tools/inproc_diverge.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
     streamprobe|streamprobe:*)  # tools/inproc_stream_probe.py [args, spaces as commas]
       xa=$(echo "${s#streamprobe}" | sed 's/^://; s/,/ /g'); n=$(echo "sp_$xa" | tr ' =/-' '____')$USESO
       timeout -k 10 600 python tools/inproc_stream_probe.py $xa > "$O/$n.json" 2> "$O/$n.err" ;;
