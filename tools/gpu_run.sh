@@ -15,6 +15,7 @@
 #   k20f32           the same, --dtype fp32
 #   k20f32serial     the same with the fp32 persistent launch off (DNN_PERSIST=0)
 #   envk20:VAR=val   k20 with one environment setting
+#   abk20:VAR=val[,N] N alternating k20 runs: default env, then VAR=val (same-box A/B)
 #   winfit           bench --steps 10..160 with --diag-windows (wall vs event time per window)
 #   k20serial | longserial | profserial   the same with the pipelined step off (DNN_PIPELINE=0)
 #   k20pipe | longpipe | profpipe         ... and on (DNN_PIPELINE=1)
@@ -80,6 +81,14 @@ for s in "$@"; do
     envk20:*)  # the driver's window under one runtime env setting: envk20:VAR=value
       kv="${s#envk20:}"; n=$(echo "$kv" | tr '=/' '__')
       env "$kv" timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/k20_$n.json" 2> "$O/k20_$n.err" ;;
+    abk20:*)  # abk20:VAR=val[,N]: N alternating driver windows (default env, then VAR=val) - a same-box A/B
+      spec="${s#abk20:}"; kv="${spec%%,*}"; n=3; [ "$spec" != "$kv" ] && n="${spec#*,}"
+      nm=$(echo "$kv" | tr '=/' '__')
+      for i in $(seq 1 "$n"); do
+        timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/abk20_${nm}_${i}_base.json" 2> "$O/abk20_${nm}_${i}_base.err"
+        env "$kv" timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/abk20_${nm}_${i}_var.json" \
+          2> "$O/abk20_${nm}_${i}_var.err"
+      done ;;
     winfit|winfit:*)  # the window's fixed cost: bench at several step counts, wall vs GPU events per
       # window (winfit:VAR=val[,k1,k2..]: under one env setting, for the given step counts)
       spec="${s#winfit}"; spec="${spec#:}"; kv="${spec%%,*}"; ks="10 20 40 80 160"
