@@ -49,7 +49,7 @@ from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa:
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
 from distributed_neural_network_amd.parallel import selflaunch  # noqa: E402
-from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, ab_window, allreduce_ab, default_candidates  # noqa: E402,E501
+from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, PERS_PATHS, ab_window, allreduce_ab, default_candidates  # noqa: E402,E501
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="2 gradient buckets, MLP all-reduce overlapped with the conv-bucket reduction "
                          "(default: one fused bucket - the 248 KB all-reduce is latency-bound)")
-    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + BF16_PATHS + ("default",),
+    ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + PERS_PATHS + BF16_PATHS + ("default",),
                     help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
                          "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
@@ -163,7 +163,7 @@ def main():
     policy.lazy_check = True  # no per-epoch host sync; the xGMI error word is checked after the run
     policy.record_waits = True  # per-step exchange wait stamps (one store per wave and step)
     policy.grad_comm = args.grad_comm
-    if args.allreduce in ORDER + BF16_PATHS:
+    if args.allreduce in ORDER + PERS_PATHS + BF16_PATHS:
         policy.path = args.allreduce
     stamp(comm.rank, f"engine {type(engine).__name__} ready; installing the all-reduce path")
     policy.attach(engine)
