@@ -26,6 +26,7 @@
 #   pmc:<c1,c2,..>   one rocprofv3 --pmc pass over 200 bf16 steps (counters comma-separated)
 #   pmcserial:<..>   the same with the pipelined step off
 #   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
+#   floor[:A=1+B=2]  launch + synchronize floor and the 20-step window under runtime settings
 #   phase | phase32 | phase32pers | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
@@ -138,6 +139,10 @@ for s in "$@"; do
     hostprobe|hostprobe:*)  # host-side cost of the timed window (tools/window_host_probe.py); hostprobe:VAR=val
       kv="${s#hostprobe}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/' '__')
       env "$kv" timeout -k 10 200 python tools/window_host_probe.py > "$O/hostprobe_$n.json" 2> "$O/hostprobe_$n.err" ;;
+    floor|floor:*)  # tools/launch_floor_probe.py under runtime settings floor:A=1+B=2 (launch + sync floor)
+      kv="${s#floor}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/+' '___')
+      env $(echo "$kv" | tr '+' ' ') timeout -k 10 120 python tools/launch_floor_probe.py > "$O/floor_$n.json" \
+        2> "$O/floor_$n.err" ;;
     pipeflags:*)  # the pipelined step's variants: phase trace + 2000-step bench per DNN_PIPE_FLAGS value
       for f in $(echo "${s#pipeflags:}" | tr ',' ' '); do
         DNN_PIPE_FLAGS=$f timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe_f$f.txt" 2>&1

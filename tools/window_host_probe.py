@@ -73,6 +73,61 @@ def main(steps: int = 20, reps: int = 40) -> None:
         m = lambda v: round(float(np.median(v[5:])), 2)  # noqa: E731
         res[name] = {"submit": m(sub), "wall": m(wall), "gpu": m(gpu),
                      "wall_minus_gpu": round(m(wall) - m(gpu), 2)}
+
+    # the floor: the same launch + synchronize around a graph of ONE trivial kernel, and an idle
+    # synchronize - what any window pays whatever the kernel does
+    x = torch.zeros(1, device=eng.device)
+    s = torch.cuda.Stream(eng.device)
+    with torch.cuda.stream(s):
+        x.add_(1)
+        torch.cuda.synchronize()
+        tg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(tg, stream=s):
+            x.add_(1)
+    torch.cuda.synchronize()
+    idle, fw, fg = [], [], []
+    for r in range(200):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        idle.append(1e6 * (time.perf_counter() - t0))
+        ev0.record()
+        t0 = time.perf_counter()
+        tg.replay()
+        ev1.record()
+        torch.cuda.synchronize()
+        fw.append(1e6 * (time.perf_counter() - t0))
+        fg.append(1e3 * ev0.elapsed_time(ev1))
+    m = lambda v: round(float(np.median(v[20:])), 2)  # noqa: E731
+    res["idle_synchronize"] = m(idle)
+    res["trivial_graph"] = {"wall": m(fw), "gpu": m(fg)}
+
+    # the persistent launch's own fixed cost: GPU time (events) and wall per window length
+    sweep = {}
+    for n in (1, 2, 4, 8, steps):
+        eng.prepare_graphs(exact=(n,))
+        gn = eng._graph(n)
+        wall, gpu = [], []
+        for r in range(30):
+            if left < n + 1:
+                eng.begin_epoch(np.arange(50000, dtype=np.int32))
+                left = spe
+            torch.cuda.synchronize()
+            ev0.record()
+            t0 = time.perf_counter()
+            gn.replay()
+            ev1.record()
+            torch.cuda.synchronize()
+            wall.append(1e6 * (time.perf_counter() - t0))
+            gpu.append(1e3 * ev0.elapsed_time(ev1))
+            left -= n
+        sweep[n] = {"wall": round(float(np.median(wall[5:])), 2), "gpu": round(float(np.median(gpu[5:])), 2)}
+    ns = sorted(sweep)
+    a = np.polyfit(ns, [sweep[n]["gpu"] for n in ns], 1)
+    b = np.polyfit(ns, [sweep[n]["wall"] for n in ns], 1)
+    res["steps_sweep"] = {str(n): v for n, v in sweep.items()}
+    res["fit_gpu_us"] = {"per_step": round(float(a[0]), 3), "fixed": round(float(a[1]), 2)}
+    res["fit_wall_us"] = {"per_step": round(float(b[0]), 3), "fixed": round(float(b[1]), 2)}
     print(json.dumps(res))
 
 
