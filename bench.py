@@ -319,6 +319,10 @@ def main():
                           "pipelined_step": bool(getattr(engine, "_pipe_ok", lambda: False)()),
                           # persistent launch: the whole timed window's steps in one launch (lenet_fused.hip PERS)
                           "persistent_launch": bool(getattr(engine, "_pers_ok", lambda: False)()),
+                          # how that launch is issued: "direct-aql" (this process's own HSA queue,
+                          # csrc/runtime/aql_dispatch.h) or "graph" (a captured hipGraph replay)
+                          "launch": ("direct-aql" if getattr(engine, "_direct_ok", lambda: False)() else
+                                     "graph" if getattr(engine, "use_graphs", False) else "eager"),
                           "global_batch": B * comm.world, "per_gpu_batch": B, "seq_len": None,
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",

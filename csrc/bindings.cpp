@@ -12,6 +12,7 @@
 
 #include "comm/xgmi_layout.h"
 #include "kernels/launchers.h"
+#include "runtime/aql_dispatch.h"
 
 
 
@@ -193,7 +194,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   // last grad_reduce(defer=2) call's (rows of parity 0, parity 1 right after them)
   m.def("fused_train_persist", [](u images, u labels, int order_len, int batch, u master, u shadow, u a0, u h1, u h2,
                                   u z1, u z2, u z3, u slab, u loss, u correct, u stage, u ctl, int nsteps, u bv0,
-                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags) {
+                                  u bv1, u nid0, u nid1, u err, double timeout_s, u stream, u stamps, int flags,
+                                  bool direct) {
     if (!g_pending_pipe_set) throw std::runtime_error("fused_train_persist needs a grad_reduce(defer=2) call first");
     g_pending_pipe_set = false;
     dnn::PipeCtl pc;
@@ -206,16 +208,16 @@ PYBIND11_MODULE(_dnn_hip, m) {
     pc.err = P<unsigned>(err);
     pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
     pc.flags = flags;
-    dnn::launch_fused_train_persist(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
+    return dnn::launch_fused_train_persist(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
                                     P<const float>(master), P<const bf16>(shadow), P<float>(a0), P<float>(h1),
                                     P<float>(h2), P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
                                     P<float>(loss), P<int32_t>(correct), P<long long>(stamps), P<unsigned char>(stage),
-                                    g_pending_pipe, pc, S(stream));
+                                    g_pending_pipe, pc, S(stream), direct);
   }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"),
      py::arg("shadow"), py::arg("a0"), py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"),
      py::arg("slab"), py::arg("loss"), py::arg("correct"), py::arg("stage"), py::arg("ctl"), py::arg("nsteps"),
      py::arg("bv0"), py::arg("bv1"), py::arg("nid0"), py::arg("nid1"), py::arg("err"), py::arg("timeout_s"),
-     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0);
+     py::arg("stream"), py::arg("stamps") = 0, py::arg("flags") = 0, py::arg("direct") = false);
   // the fp32 kernel's persistent launch (lenet_f32.hip PERS): the reduction is the last
   // grad_reduce(defer=2) call's
   m.def("fused_train_persist_f32", [](u images, u labels, int order_len, int batch, u master, u a0, u h1, u h2, u z1,
@@ -250,6 +252,16 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("persist_max_batch", []() { return dnn::persist_max_batch(); });
   m.def("persist_resident_workgroups", []() { return dnn::persist_resident_workgroups(); });
   m.def("persist_ctl_bytes", [](int batch) { return dnn::persist_ctl_bytes(batch); });
+  // direct AQL dispatch (runtime/aql_dispatch.h): "" when this process has a queue on the device,
+  // else why not; the host-clock cost of the last direct dispatch (doorbell -> completion, whole call)
+  m.def("aql_status", [](int device) {
+    std::string why;
+    return dnn::aql_queue(device, &why) != nullptr ? std::string() : why;
+  });
+  m.def("persist_direct_run", [](int handle) { dnn::persist_direct_run(handle); }, py::arg("handle"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("aql_last_us", [](int device, bool whole) { return dnn::aql_last_us(dnn::aql_queue(device), whole); },
+        py::arg("device"), py::arg("whole") = false);
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });
   m.def("pipe_groups", []() { return dnn::pipe_groups(); });
   m.def("init", []() { dnn::init_kernels(); });

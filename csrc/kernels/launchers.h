@@ -96,10 +96,15 @@ void launch_fused_train_pipe(const uint8_t* images, const int32_t* labels, int o
                              hipStream_t stream);
 // The persistent launch: pc.nsteps steps in one launch (rows: two parities, contiguous - parity
 // 1 of each row kind right after parity 0); see PipeCtl.
-void launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,
-                                const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
-                                float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
-                                unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc, hipStream_t stream);
+// direct: do not launch; prepare the launch for this process's AQL queue (runtime/aql_dispatch.h)
+// and return its handle for persist_direct_run (-1 otherwise)
+int launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                               const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
+                               float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
+                               unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc, hipStream_t stream,
+                               bool direct = false);
+// one prepared direct launch: waits for the stream's earlier work, dispatches, waits for completion
+void persist_direct_run(int handle);
 int persist_max_batch();   // largest batch whose persistent grid is co-resident on this device
 int persist_resident_workgroups();  // workgroups of the persistent kernel resident at once (occupancy x CUs)
 int persist_ctl_bytes(int batch);  // control memory of a persistent launch (uncached)

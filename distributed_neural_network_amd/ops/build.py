@@ -37,8 +37,8 @@ HIP_SOURCES = [
     CSRC / "kernels" / "diag.hip",
 ]
 HIP_BINDING = CSRC / "bindings.cpp"
-HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp"]
-HIP_HEADERS = sorted((CSRC / "kernels").glob("*.h"))
+HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "runtime" / "aql_dispatch.cpp"]
+HIP_HEADERS = sorted((CSRC / "kernels").glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
 IO_SOURCES = [CSRC / "io" / "dataio.cpp"]
 
 
@@ -97,7 +97,7 @@ def build_hip(force: bool = False, verbose_resources: bool = False) -> Path:
         for f in [ex.submit(_run, j) for j in jobs]:
             f.result()
     tmp = target.with_suffix(".tmp.so")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-ldl"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-ldl", "-L/opt/rocm/lib", "-lhsa-runtime64"])
     os.replace(tmp, target)
     return target
 

@@ -366,6 +366,23 @@ class HipEngine(Engine):
             self._pers_ctl = self.ext.uncached_alloc(ctl_bytes) if self.persist else 0
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        # Direct AQL dispatch of the bf16 persistent launch (csrc/runtime/aql_dispatch.h; default
+        # on, DNN_AQL=0 turns it off): the kernel the graphs replay, dispatched through this
+        # process's own HSA queue with its arguments in device memory, and waited for by spinning
+        # on its completion signal - no stream, graph or interrupt in the launch + completion path
+        # (a graph of one trivial kernel costs ~20 us from replay to the synchronize's return;
+        # 20/5 windows 16.75 vs 16.95 us/step: profiles/r6/aql/).  run_steps then returns once the
+        # steps are done (synchronous), after the stream's earlier work.  Only without a per-step
+        # all-reduce: the in-launch exchange needs every rank's launch in flight together.
+        self._direct_h: dict[tuple, int] = {}
+        self.direct = False
+        self.direct_why = "off (DNN_AQL=0)"
+        if os.environ.get("DNN_AQL", "1") != "0":
+            if not (self.persist and dtype == "bf16"):
+                self.direct_why = "the bf16 persistent launch is off"
+            else:
+                why = self.ext.aql_status(dev.index if dev.index is not None else torch.cuda.current_device())
+                self.direct, self.direct_why = (why == ""), (why or "on")
         self.params_changed()
         torch.cuda.synchronize(dev)
 
@@ -387,6 +404,7 @@ class HipEngine(Engine):
 
     def invalidate_graphs(self) -> None:
         self._graphs.clear()
+        self._direct_h.clear()
 
     # -- data ---------------------------------------------------------------------------
     def attach(self, train: Split) -> None:
@@ -530,7 +548,7 @@ class HipEngine(Engine):
             return False
         return self.grad_sync is None or self._pers_xchg() is not None
 
-    def _launch_steps_pers(self, n: int) -> None:
+    def _launch_steps_pers(self, n: int, direct: bool = False) -> int:
         """n steps as ONE launch (lenet_fused.hip PERS): the same reduction, bookkeeping slots and
         publication sequence as _launch_steps_pipe's n + 1 launches, with the reduction of step
         n - 1 inside the launch too (it re-publishes slot 0 for the next chunk)."""
@@ -560,13 +578,14 @@ class HipEngine(Engine):
                              self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
                              self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
                              self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids), **xg)
-        self.ext.fused_train_persist(self._p(self.train.images), self._p(self.train.labels), self.order_len,
-                                     self.batch, self._p(self.master), self._p(self.shadow), self._p(r["a0"]),
-                                     self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]),
-                                     self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
-                                     self._p(self.stage), self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
-                                     self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                     stamps=self._pipe_stamps, flags=self.pipe_flags)
+        return self.ext.fused_train_persist(self._p(self.train.images), self._p(self.train.labels), self.order_len,
+                                            self.batch, self._p(self.master), self._p(self.shadow), self._p(r["a0"]),
+                                            self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]),
+                                            self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
+                                            self._p(r["correct"]), self._p(self.stage), self._pers_ctl, n, sp + 4,
+                                            sp + 8, self._p(self.next_ids), self._p(self.next_ids2),
+                                            self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
+                                            stamps=self._pipe_stamps, flags=self.pipe_flags, direct=direct)
 
     def _launch_steps(self, n: int) -> None:
         """n training steps' launches (what a chunk graph captures)."""
@@ -778,11 +797,28 @@ class HipEngine(Engine):
         torch.cuda.synchronize(dev)
         return all(v == 1.0 for v in votes), why
 
+    def _launch_key(self, nsteps: int) -> tuple:
+        return (nsteps, id(self.grad_sync), self.overlap, self.order_len,
+                getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
+                getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
+                self._pers_ok(), self.pers_exchange)
+
+    def _direct_ok(self) -> bool:
+        return self.direct and self.dtype == "bf16" and self.grad_sync is None and self._pers_ok()
+
+    def _direct(self, nsteps: int) -> int:
+        """The prepared direct dispatch of an nsteps persistent launch (the graph's counterpart:
+        the same launch, arguments fixed once)."""
+        key = (self._launch_key(nsteps), self._stream())
+        h = self._direct_h.get(key)
+        if h is None:
+            with torch.cuda.device(self.device):
+                h = self._launch_steps_pers(nsteps, direct=True)
+            self._direct_h[key] = h
+        return h
+
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        key = (nsteps, id(self.grad_sync), self.overlap, self.order_len,
-               getattr(getattr(self.grad_sync, "group", None), "one_launch", None),
-               getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
-               self._pers_ok(), self.pers_exchange)
+        key = self._launch_key(nsteps)
         g = self._graphs.get(key)
         if g is None:
             # Capture advances nothing: kernels are recorded, not run.  The wait before it is
@@ -807,6 +843,10 @@ class HipEngine(Engine):
         ``exact``: step counts that also get a graph of their own, so ``run_steps(n)`` for such
         an n is ONE replay instead of its power-of-two decomposition (a 20-step window: one
         graph instead of 16 + 4, ~6 us less per window; profiles/r2/window/)."""
+        if self._direct_ok():  # direct dispatches replace the graphs (run_steps takes them first)
+            for k in set(self._chunk_sizes()) | {int(k) for k in exact if 0 < int(k)}:
+                self._direct(k)
+            return
         if self.use_graphs:
             for k in self._chunk_sizes():
                 self._graph(k)
@@ -818,6 +858,12 @@ class HipEngine(Engine):
         if n <= 0:
             return
         poll = self.poll
+        if self._direct_ok():  # ONE direct dispatch, returning when the n steps are done
+            h = self._direct(n)
+            if poll is not None:
+                poll()
+            self.ext.persist_direct_run(h)
+            return
         if not self.use_graphs:
             with torch.cuda.device(self.device):
                 if self._pipe_ok() or self._pers_ok():

@@ -1,0 +1,72 @@
+"""Direct AQL dispatch of the persistent launch (csrc/runtime/aql_dispatch.h, DNN_AQL=1): the
+same kernel object through this process's own HSA queue must give the graph replays' bits."""
+import numpy as np
+import pytest
+import torch
+
+from distributed_neural_network_amd.data import synthetic
+from distributed_neural_network_amd.models.network import init_arena
+from distributed_neural_network_amd.runtime import HipEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(arena, direct):
+    eng = HipEngine(batch=64, arena=arena, graph_chunk=8)
+    if not eng.persist:
+        pytest.skip("the persistent launch is off on this device")
+    if direct:
+        why = eng.ext.aql_status(torch.cuda.current_device())
+        assert why == "", f"no AQL queue on a GPU box: {why}"
+        eng.direct = True
+    return eng
+
+
+def _run(eng, data, orders, steps):
+    eng.attach(data)
+    stats = []
+    for order in orders:
+        eng.begin_epoch(order)
+        for n in steps:
+            eng.run_steps(n)
+        stats.append(eng.epoch_stats())
+    torch.cuda.synchronize()
+    return eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats
+
+
+def test_direct_dispatch_matches_graph_replays():
+    """1-, 5- and 20-step launches, a tail batch, steps past an epoch's end, two epochs."""
+    data = synthetic(1000, 4)  # 16 steps per epoch incl. a 40-sample tail
+    a = init_arena(seed=5)
+    rng = np.random.default_rng(1)
+    orders = [rng.permutation(1000).astype(np.int32) for _ in range(2)]
+    steps = (1, 5, 20)  # 26 steps: past the epoch's end (no-op steps)
+    ref = _run(_engine(a, False), data, orders, steps)
+    eng = _engine(a, True)
+    got = _run(eng, data, orders, steps)
+    assert eng._direct_h, "the direct path did not run"
+    for x, y in zip(ref[:3], got[:3]):
+        assert torch.equal(x, y)
+    for s0, s1 in zip(ref[3], got[3]):
+        assert s0.loss_sum == s1.loss_sum and s0.correct == s1.correct and s0.samples == s1.samples == 1000
+    assert not eng.step_wait_failed()
+
+
+def test_direct_dispatch_orders_after_stream_work():
+    """A window queued right behind stream work (an epoch start, a parameter reload) must see it:
+    the direct path waits for the stream before its dispatch."""
+    data = synthetic(640, 6)
+    a = init_arena(seed=7)
+    order = np.arange(640, dtype=np.int32)
+    res = []
+    for direct in (False, True):
+        eng = _engine(a, direct)
+        eng.attach(data)
+        eng.begin_epoch(order)
+        eng.run_steps(3)
+        eng.master.mul_(0.5)  # queued stream work the next window must see
+        eng.params_changed()
+        eng.run_steps(4)
+        torch.cuda.synchronize()
+        res.append(eng.master.cpu())
+    assert torch.equal(res[0], res[1])

@@ -27,6 +27,7 @@
 #   pmcserial:<..>   the same with the pipelined step off
 #   hostprobe[:VAR=val]  host-side cost of the timed window (launch paths, sync styles)
 #   floor[:A=1+B=2]  launch + synchronize floor and the 20-step window under runtime settings
+#   aqlwin[:steps]   graph replay vs direct AQL dispatch of the persistent window (timing + bits)
 #   phase | phase32 | phase32pers | phasepipe | phasepers  per-phase timeline of the fused kernels (tools/phase_trace*.py; pipelined launch)
 #   rehearse2        2 ranks on this GPU, no torchrun: DNN_BACKEND=gloo bench.py --gpus 2 (self-launch + A/B)
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
@@ -143,6 +144,9 @@ for s in "$@"; do
       kv="${s#floor}"; kv="${kv#:}"; [ -z "$kv" ] && kv="DNN_NOTHING=0"; n=$(echo "$kv" | tr '=/+' '___')
       env $(echo "$kv" | tr '+' ' ') timeout -k 10 120 python tools/launch_floor_probe.py > "$O/floor_$n.json" \
         2> "$O/floor_$n.err" ;;
+    aqlwin|aqlwin:*)  # tools/aql_window.py: graph replay vs direct AQL dispatch windows + bits (aqlwin:FENCE)
+      f="${s#aqlwin}"; f="${f#:}"; [ -z "$f" ] && f=ss
+      DNN_AQL_FENCE=$f timeout -k 10 120 python tools/aql_window.py 20 > "$O/aqlwin_$f.json" 2> "$O/aqlwin_$f.err" ;;
     pipeflags:*)  # the pipelined step's variants: phase trace + 2000-step bench per DNN_PIPE_FLAGS value
       for f in $(echo "${s#pipeflags:}" | tr ',' ' '); do
         DNN_PIPE_FLAGS=$f timeout -k 10 300 python tools/phase_trace.py --pipe > "$O/phasepipe_f$f.txt" 2>&1
