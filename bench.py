@@ -49,7 +49,8 @@ from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa:
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
 from distributed_neural_network_amd.parallel import Communicator, detect, make_policy  # noqa: E402
 from distributed_neural_network_amd.parallel import selflaunch  # noqa: E402
-from distributed_neural_network_amd.parallel.autotune import BF16_PATHS, ORDER, PERS_PATHS, ab_window, allreduce_ab, default_candidates  # noqa: E402,E501
+from distributed_neural_network_amd.parallel.autotune import (BF16_PATHS, ORDER, PERS_PATHS, ab_window,  # noqa: E402
+                                                              allreduce_ab, default_candidates, launch_ab)
 from distributed_neural_network_amd.runtime import HipEngine, eval_metrics, make_engine  # noqa: E402
 from distributed_neural_network_amd.runtime.cursor import EpochCursor  # noqa: E402
 
@@ -91,6 +92,10 @@ def main():
     ap.add_argument("--allreduce", default="ab", choices=("ab",) + ORDER + PERS_PATHS + BF16_PATHS + ("default",),
                     help="per-step all-reduce at N > 1: ab (default) = time every candidate in the untimed "
                          "set-up and keep the fastest; a path name pins it; default = the policy's own choice")
+    ap.add_argument("--launch", default="ab", choices=("ab", "direct", "graph"),
+                    help="how the persistent window is launched (bf16 engine, no per-step all-reduce): ab "
+                         "(default) = time the direct AQL dispatch and the graph replay in the untimed set-up "
+                         "and keep the faster; direct / graph pin one")
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
                     help="bf16: the A/B also times the xGMI exchanges with bf16 gradient granules (opt-in "
                          "lower-precision gradient communication; the default path becomes its -bf16 form)")
@@ -187,6 +192,20 @@ def main():
                           log=lambda m: stamp(comm.rank, m) if comm.rank == 0 else None)
         stamp(comm.rank, f"all-reduce A/B (us/step, max over ranks): {ab}")
         cur.left = 0  # the timed run starts on a fresh epoch
+
+    # the persistent window's launch path (direct AQL dispatch vs graph replay), timed like the
+    # all-reduce A/B above with the run's own window shape (untimed; engines without a per-step
+    # all-reduce only)
+    lab = {}
+    if args.launch == "ab" and isinstance(engine, HipEngine):
+        ab_steps, ab_warm = ab_window(cur.steps_per_epoch, args.ab_steps or args.steps, args.warmup)
+        lab = launch_ab(comm, engine, cur, steps=ab_steps, warmup=ab_warm,
+                        log=lambda m: stamp(comm.rank, m) if comm.rank == 0 else None)
+        if lab:
+            stamp(comm.rank, f"launch A/B (us/step, max over ranks): {lab}")
+            cur.left = 0
+    elif args.launch == "graph" and isinstance(engine, HipEngine):
+        engine.direct = False
 
     # untimed set-up: capture every chunk graph, first-call costs of the eval path (kernel,
     # D2H, host ops), then the W warmup steps LAST, so the timed window starts on a busy,
@@ -330,6 +349,8 @@ def main():
                           # launcher retry level this number was measured at (0: as requested)
                           "safe_transport": safe},
                **epoch}
+        if lab:
+            out["launch_ab"] = lab["launch_ab"]
         if ab:
             out["allreduce_ab"] = ab["allreduce_ab"]
             out["allreduce_failed"] = ab["failed"]

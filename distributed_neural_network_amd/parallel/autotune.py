@@ -333,3 +333,52 @@ def _drop(policy, engine, name: str) -> None:
 
 __all__ = ["AB_MAX_STEPS", "BF16_PATHS", "ORDER", "PERS_PATHS", "ab_window", "allreduce_ab", "budget_default", "choose",
            "default_candidates", "prepare_window", "rccl_margin", "step_variant", "window"]
+
+
+# -- how the persistent window is launched ----------------------------------------------------
+LAUNCH_PATHS = ("direct-aql", "graph")
+
+
+def launch_margin() -> float:
+    """Relative margin within which the direct AQL dispatch is kept against a faster graph replay
+    (``DNN_LAUNCH_MARGIN``, default 0.005): its launch + completion path is the shorter one
+    (profiles/r6/aql/), so a graph win inside the A/B's noise does not count as one."""
+    return float(os.environ.get("DNN_LAUNCH_MARGIN", "0.005"))
+
+
+def launch_ab(comm, engine, cur, steps: int = 20, warmup: int = 5, rounds: int = 4, reps: int = 3,
+              spin: int = 500, log: Optional[Callable[[str], None]] = None) -> dict:
+    """Start-up A/B of the persistent window's launch path, the counterpart of ``allreduce_ab`` for
+    engines whose window runs without a per-step all-reduce (collective: every rank calls it).
+    Times the direct AQL dispatch (csrc/runtime/aql_dispatch.h) and the captured-graph replay with
+    the run's own window shape (``_measure``: the bench's bracket, max over ranks), alternating
+    over ``rounds``, keeps the faster one on ``engine`` (the direct dispatch within
+    ``launch_margin()``) and returns {"launch_ab": {path: median us/step}, "launch": winner,
+    "launch_ab_wall_s": seconds}; {} where there is nothing to choose (no AQL queue on this
+    device, another engine, the fp32 step or a per-step all-reduce installed).  Like the all-reduce
+    A/B, the first candidate runs ``spin`` untimed steps first, so no path is timed at the low
+    clocks of a GPU that sat idle through the set-up (a cold 20/5 window is ~0.3 us/step slower:
+    profiles/r6/aql/)."""
+    say = log or (lambda m: None)
+    was = bool(getattr(engine, "direct", False))
+    if not was:
+        return {}
+    if cur is not None:
+        prepare_window(engine, cur, steps, warmup)  # (an epoch begun: the step forms are decided)
+    if not getattr(engine, "_direct_ok", lambda: False)():
+        return {}
+    t_start = time.perf_counter()
+    res: dict[str, list[float]] = {p: [] for p in LAUNCH_PATHS}
+    try:
+        for rnd in range(rounds):
+            for i, p in enumerate(LAUNCH_PATHS if rnd % 2 == 0 else LAUNCH_PATHS[::-1]):
+                engine.direct = p == "direct-aql"
+                us, _ = _measure(comm, engine, cur, steps, warmup, reps, spin if rnd == 0 and i == 0 else 0)
+                res[p].append(us)
+                say(f"launch A/B {p}: {us:.3f} us/step (round {rnd})")
+    finally:
+        engine.direct = was
+    med = {p: round(statistics.median(v), 3) for p, v in res.items()}
+    winner = "direct-aql" if med["direct-aql"] <= med["graph"] * (1.0 + launch_margin()) else "graph"
+    engine.direct = winner == "direct-aql"
+    return {"launch_ab": med, "launch": winner, "launch_ab_wall_s": round(time.perf_counter() - t_start, 3)}

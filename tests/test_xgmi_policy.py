@@ -207,3 +207,45 @@ def test_pers_install_and_fallback(monkeypatch):
     assert bad.grad_sync is None and not bad.pers_exchange
     pol.attach(bad)  # default path xgmi-pull-pers -> its self-test fails (cached) -> xgmi-pull
     assert bad.grad_sync is not None and not bad.pers_exchange and grp.xp_mode == 0
+
+
+class _LaunchEngine:
+    """Stands in for a HipEngine with an AQL queue: records which launch path each window ran."""
+
+    def __init__(self, ok=True):
+        self.direct, self.ok, self.seen = True, ok, []
+
+    def _direct_ok(self):
+        return self.direct and self.ok
+
+
+def _fake_measure(times):
+    def measure(comm, engine, cur, steps, warmup, reps, spin):
+        p = "direct-aql" if engine.direct else "graph"
+        engine.seen.append((p, spin))
+        return times[p], True
+    return measure
+
+
+@pytest.mark.parametrize("direct_us, graph_us, winner", [(16.2, 16.5, "direct-aql"), (16.54, 16.5, "direct-aql"),
+                                                          (16.9, 16.5, "graph")])
+def test_launch_ab_keeps_direct_within_margin(monkeypatch, direct_us, graph_us, winner):
+    """The launch A/B times both paths alternately (spin steps only before the first window) and
+    keeps the direct dispatch unless the graph replay wins by more than launch_margin()."""
+    from distributed_neural_network_amd.parallel import autotune
+
+    monkeypatch.setattr(autotune, "_measure", _fake_measure({"direct-aql": direct_us, "graph": graph_us}))
+    eng = _LaunchEngine()
+    out = autotune.launch_ab(None, eng, None, steps=20, warmup=5, rounds=4, spin=500)
+    assert out["launch"] == winner and eng.direct == (winner == "direct-aql")
+    assert out["launch_ab"] == {"direct-aql": direct_us, "graph": graph_us}
+    assert [p for p, _ in eng.seen] == ["direct-aql", "graph", "graph", "direct-aql"] * 2
+    assert [s for _, s in eng.seen] == [500] + [0] * 7
+
+
+def test_launch_ab_without_a_direct_path_is_a_no_op(monkeypatch):
+    from distributed_neural_network_amd.parallel import autotune
+
+    monkeypatch.setattr(autotune, "_measure", _fake_measure({"direct-aql": 1.0, "graph": 2.0}))
+    eng = _LaunchEngine(ok=False)
+    assert autotune.launch_ab(None, eng, None) == {} and not eng.seen

@@ -62,6 +62,14 @@ def main(steps: int = 20, reps: int = 40) -> None:
     out["direct_dispatch_us"] = {"doorbell_to_done": round(engs["direct"].ext.aql_last_us(dev, False), 2),
                                  "whole_call": round(engs["direct"].ext.aql_last_us(dev, True), 2)}
     out["window_fixed_us_saved"] = round((out["graph"]["median"] - out["direct"]["median"]) * steps, 2)
+    # host cost of the direct branch's Python (run_steps before the dispatch), per call
+    e = engs["direct"]
+    for name, fn in (("direct_ok", e._direct_ok), ("direct_handle", lambda: e._direct(steps)),
+                     ("current_stream", e._stream), ("idle_synchronize", torch.cuda.synchronize)):
+        t0 = time.perf_counter()
+        for _ in range(2000):
+            fn()
+        out.setdefault("host_us", {})[name] = round(1e6 * (time.perf_counter() - t0) / 2000, 3)
     print(json.dumps(out))
 
 
