@@ -248,8 +248,9 @@ def main():
     if diag:
         ev[1].record()
     torch.cuda.synchronize(device)
-    comm.barrier()
-    torch.cuda.synchronize(device)
+    if comm.distributed:  # (one rank: the barrier is a no-op, and so would a second synchronize be)
+        comm.barrier()
+        torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     stamp(comm.rank, f"timed window done: {1e6 * dt / args.steps:.3f} us/step on this rank")
     if diag:

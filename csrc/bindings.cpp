@@ -222,7 +222,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   // grad_reduce(defer=2) call's
   m.def("fused_train_persist_f32", [](u images, u labels, int order_len, int batch, u master, u a0, u h1, u h2, u z1,
                                       u z2, u z3, u slab, u loss, u correct, u ctl, int nsteps, u bv0, u bv1, u nid0,
-                                      u nid1, u err, double timeout_s, u stream, int flags, u stamps) {
+                                      u nid1, u err, double timeout_s, u stream, int flags, u stamps, bool direct) {
     if (!g_pending_pipe_set) throw std::runtime_error("fused_train_persist_f32 needs a grad_reduce(defer=2) call first");
     g_pending_pipe_set = false;
     dnn::PipeCtl pc;
@@ -235,15 +235,16 @@ PYBIND11_MODULE(_dnn_hip, m) {
     pc.err = P<unsigned>(err);
     pc.timeout_ticks = (long long)(timeout_s * 1.0e8);
     pc.flags = flags;
-    dnn::launch_fused_train_persist_f32(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
-                                        P<const float>(master), P<float>(a0), P<float>(h1), P<float>(h2), P<float>(z1),
-                                        P<float>(z2), P<float>(z3), P<float>(slab), P<float>(loss),
-                                        P<int32_t>(correct), g_pending_pipe, pc, S(stream), P<long long>(stamps));
+    return dnn::launch_fused_train_persist_f32(P<const uint8_t>(images), P<const int32_t>(labels), order_len, batch,
+                                               P<const float>(master), P<float>(a0), P<float>(h1), P<float>(h2),
+                                               P<float>(z1), P<float>(z2), P<float>(z3), P<float>(slab),
+                                               P<float>(loss), P<int32_t>(correct), g_pending_pipe, pc, S(stream),
+                                               P<long long>(stamps), direct);
   }, py::arg("images"), py::arg("labels"), py::arg("order_len"), py::arg("batch"), py::arg("master"), py::arg("a0"),
      py::arg("h1"), py::arg("h2"), py::arg("z1"), py::arg("z2"), py::arg("z3"), py::arg("slab"), py::arg("loss"),
      py::arg("correct"), py::arg("ctl"), py::arg("nsteps"), py::arg("bv0"), py::arg("bv1"), py::arg("nid0"),
      py::arg("nid1"), py::arg("err"), py::arg("timeout_s"), py::arg("stream"), py::arg("flags") = 0,
-     py::arg("stamps") = 0);
+     py::arg("stamps") = 0, py::arg("direct") = false);
   m.def("persist_max_batch_f32", []() { return dnn::persist_max_batch_f32(); });
   m.def("persist_resident_workgroups_f32", []() { return dnn::persist_resident_workgroups_f32(); });
   m.def("persist_wg_f32", []() { return dnn::persist_wg_f32(); });
@@ -258,7 +259,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     std::string why;
     return dnn::aql_queue(device, &why) != nullptr ? std::string() : why;
   });
-  m.def("persist_direct_run", [](int handle) { dnn::persist_direct_run(handle); }, py::arg("handle"),
+  m.def("persist_direct_run", [](int handle) { dnn::aql_prepared_run(handle); }, py::arg("handle"),
         py::call_guard<py::gil_scoped_release>());
   m.def("aql_last_us", [](int device, bool whole) { return dnn::aql_last_us(dnn::aql_queue(device), whole); },
         py::arg("device"), py::arg("whole") = false);

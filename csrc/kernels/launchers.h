@@ -103,8 +103,7 @@ int launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int
                                float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
                                unsigned char* stage, const ReduceArgs& red, const PipeCtl& pc, hipStream_t stream,
                                bool direct = false);
-// one prepared direct launch: waits for the stream's earlier work, dispatches, waits for completion
-void persist_direct_run(int handle);
+
 int persist_max_batch();   // largest batch whose persistent grid is co-resident on this device
 int persist_resident_workgroups();  // workgroups of the persistent kernel resident at once (occupancy x CUs)
 int persist_ctl_bytes(int batch);  // control memory of a persistent launch (uncached)
@@ -126,10 +125,10 @@ void launch_fused_eval_f32(const uint8_t* images, const int32_t* labels, int n, 
 // its persistent launch (lenet_f32.hip PERS): pc.nsteps steps in one launch, the reduction
 // (red: whole arena, fused SGD, bookkeeping) in its first persist_wg_f32() workgroups; rows and
 // control block as launch_fused_train_persist's; red.batch_ids = step 0's sample ids
-void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+int launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
                                     const float* master, float* a0, float* h1, float* h2, float* z1, float* z2,
                                     float* z3, float* slab, float* loss, int32_t* correct, const ReduceArgs& red,
-                                    const PipeCtl& pc, hipStream_t stream, long long* stamps = nullptr);
+                                    const PipeCtl& pc, hipStream_t stream, long long* stamps = nullptr, bool direct = false);
 int persist_max_batch_f32();
 int persist_resident_workgroups_f32();
 int persist_wg_f32();

@@ -31,6 +31,7 @@
 //    data gradient's VALU work in the other 11;
 //  * fixed summation orders everywhere (no atomics): bitwise reproducible run to run.
 #include "pers_common.h"
+#include "runtime/aql_dispatch.h"
 
 namespace dnn {
 namespace f32k {
@@ -1112,10 +1113,19 @@ int persist_max_batch_f32() {
   return std::max(0, std::min(persist_resident_workgroups_f32() - f32k::PF_WG - PERS_MARGIN_F32, PERS_AROW));
 }
 
-void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
-                                    const float* master, float* a0, float* h1, float* h2, float* z1, float* z2,
-                                    float* z3, float* slab, float* loss, int32_t* correct, const ReduceArgs& red,
-                                    const PipeCtl& pc_in, hipStream_t stream, long long* stamps) {
+// The persistent kernel's parameter block (the kernarg segment of a direct AQL dispatch: the
+// compiler lays kernel parameters out as this struct; aql_prepare checks its size against the
+// loaded symbol's kernarg segment)
+struct F32PersKernargs {
+  f32k::F32Args A;
+  ReduceArgs ra;
+  PipeCtl pc;
+};
+
+int launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels, int order_len, int batch,
+                                   const float* master, float* a0, float* h1, float* h2, float* z1, float* z2,
+                                   float* z3, float* slab, float* loss, int32_t* correct, const ReduceArgs& red,
+                                   const PipeCtl& pc_in, hipStream_t stream, long long* stamps, bool direct) {
   init_kernels_f32();
   // the shapes the kernel assumes (checked here: a mismatch would fault or hang on the device)
   if (batch < 1 || batch > persist_max_batch_f32() || f32k::PF_WG + batch > PERS_MAX_GRID)
@@ -1148,8 +1158,16 @@ void launch_fused_train_persist_f32(const uint8_t* images, const int32_t* labels
   const f32k::F32Args A{images, labels, red.batch_ids, order_len, batch, 0, nullptr, master, a0, h1, h2, z1, z2, z3,
                         slab, loss, correct, stamps};
   auto* kern = red.xp_nranks == 0 ? &f32k::lenet_f32_pers_kernel<0> : &f32k::lenet_f32_pers_kernel<8>;
+  if (direct) {  // prepare (not launch) the same kernel object for this process's AQL queue
+    const F32PersKernargs ka{A, red, pc};
+    const double bound_s = 10.0 + 2.0 * (double)pc.timeout_ticks * 1e-8 + 2e-3 * pc.nsteps;
+    return aql_prepare(reinterpret_cast<const void*>(kern),
+                       red.xp_nranks == 0 ? "lenet_f32_pers_kernelILi0E" : "lenet_f32_pers_kernelILi8E", &ka,
+                       sizeof(ka), f32k::PF_WG + batch, f32k::NT, f32k::LDS_TOTAL, bound_s, stream);
+  }
   hipLaunchKernelGGL(kern, dim3(f32k::PF_WG + batch), dim3(f32k::NT), f32k::LDS_TOTAL, stream, A, red, pc);
   HIP_CHECK(hipGetLastError());
+  return -1;
 }
 
 }  // namespace dnn

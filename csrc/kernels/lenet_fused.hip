@@ -36,11 +36,7 @@
 //    (sched_barrier), so LDS latency is paid once per batch, not once per K-step.
 #include <algorithm>
 #include <cstddef>
-#include <map>
-#include <mutex>
 #include <string>
-#include <utility>
-#include <vector>
 
 #include "pers_common.h"
 #include "runtime/aql_dispatch.h"
@@ -1718,57 +1714,6 @@ struct PersKernargs {
 static_assert(offsetof(PersKernargs, ra) == 168 && offsetof(PersKernargs, pc) == 168 + sizeof(ReduceArgs),
               "kernel parameter layout");
 
-// Prepared direct dispatches of the persistent kernel (runtime/aql_dispatch.h): the kernel object
-// the HIP runtime loaded, resolved once, and the whole parameter block of one launch shape - the
-// AQL counterpart of a captured graph (same pointers for every replay).
-struct PersDirect {
-  AqlQueue* q;
-  AqlKernel k;
-  PersKernargs* args;  // device memory, written once (HIP's kernarg placement)
-  unsigned grid;
-  double bound_s;
-  hipStream_t stream;
-};
-static std::mutex g_direct_mu;
-static std::vector<PersDirect> g_direct;
-
-static int prepare_direct(int inst, const void* host_fn, const PersKernargs& ka, unsigned grid, double bound_s,
-                          hipStream_t stream) {
-  static const char* const names[2] = {"lenet_fused_kernelILb1ELb1ELb1ELb1ELi0E", "lenet_fused_kernelILb1ELb1ELb1ELb1ELi8E"};
-  static std::map<std::pair<int, int>, AqlKernel> kernels;
-  int dev = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  std::string why;
-  AqlQueue* q = aql_queue(dev, &why);
-  if (q == nullptr) throw std::runtime_error("fused_train_persist: no AQL queue: " + why);
-  std::lock_guard<std::mutex> lock(g_direct_mu);
-  auto it = kernels.find({dev, inst});
-  if (it == kernels.end()) it = kernels.emplace(std::make_pair(dev, inst), aql_kernel(q, host_fn, names[inst])).first;
-  if (it->second.kernarg_bytes != sizeof(PersKernargs))
-    throw std::runtime_error("fused_train_persist: the loaded kernel's kernarg segment is not the parameter block");
-  PersKernargs* dka = nullptr;  // (one small block per prepared launch shape, kept for the process)
-  HIP_CHECK(hipMalloc(&dka, sizeof(PersKernargs)));
-  HIP_CHECK(hipMemcpy(dka, &ka, sizeof(PersKernargs), hipMemcpyHostToDevice));
-  g_direct.push_back(PersDirect{q, it->second, dka, grid, bound_s, stream});
-  return (int)g_direct.size() - 1;
-}
-
-void persist_direct_run(int handle) {
-  PersDirect d;
-  {
-    std::lock_guard<std::mutex> lock(g_direct_mu);
-    if (handle < 0 || handle >= (int)g_direct.size()) throw std::runtime_error("persist_direct_run: bad handle");
-    d = g_direct[handle];
-  }
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  HIP_CHECK(hipStreamIsCapturing(d.stream, &cap));
-  if (cap != hipStreamCaptureStatusNone) throw std::runtime_error("persist_direct_run: a direct dispatch cannot be captured");
-  // the stream's earlier work (the previous window, epoch_begin, copies) must be done: the AQL
-  // queue is not ordered after it (usually idle already: one query)
-  if (hipStreamQuery(d.stream) != hipSuccess) HIP_CHECK(hipStreamSynchronize(d.stream));
-  aql_run(d.q, d.k, d.args, sizeof(PersKernargs), d.grid, NT, LDS_TOTAL, d.bound_s, true);
-}
-
 int launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int order_len, int batch,
                                const float* master, const bf16* shadow, float* a0, float* h1, float* h2, float* z1,
                                float* z2, float* z3, float* slab, float* loss, int32_t* correct, long long* stamps,
@@ -1811,8 +1756,9 @@ int launch_fused_train_persist(const uint8_t* images, const int32_t* labels, int
                     slab, loss, correct, stamps, nullptr, pc.nid_slot[0], stage, red, pc};
     // every wait of the launch is bounded (pc.timeout_ticks), so the kernel ends within nsteps bounds
     const double bound_s = 10.0 + 2.0 * (double)pc.timeout_ticks * 1e-8 + 1e-3 * pc.nsteps;
-    return prepare_direct(red.xp_nranks == 0 ? 0 : 1, reinterpret_cast<const void*>(kern), ka, PERS_WG + batch,
-                          bound_s, stream);
+    return aql_prepare(reinterpret_cast<const void*>(kern),
+                       red.xp_nranks == 0 ? "lenet_fused_kernelILb1ELb1ELb1ELb1ELi0E" : "lenet_fused_kernelILb1ELb1ELb1ELb1ELi8E",
+                       &ka, sizeof(ka), PERS_WG + batch, NT, LDS_TOTAL, bound_s, stream);
   }
   hipLaunchKernelGGL(kern, dim3(PERS_WG + batch), dim3(NT), LDS_TOTAL, stream, images, labels, nullptr, order_len,
                      batch, 0, red.state, master, shadow, a0, h1, h2, z1, z2, z3, slab, loss, correct, stamps, nullptr,

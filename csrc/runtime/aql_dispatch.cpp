@@ -269,6 +269,63 @@ void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, un
   q->last_whole_us = std::chrono::duration<double, std::micro>(t2 - t0).count();
 }
 
+namespace {
+struct Prepared {
+  AqlQueue* q;
+  AqlKernel k;
+  void* args;  // device memory, written once (HIP's kernarg placement)
+  size_t bytes;
+  unsigned grid, block, lds;
+  double timeout_s;
+  hipStream_t stream;
+};
+std::mutex g_prep_mu;
+std::vector<Prepared> g_prep;
+std::map<std::pair<int, std::string>, AqlKernel> g_kernels;
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+int aql_prepare(const void* host_fn, const char* name_part, const void* args, size_t bytes, unsigned grid_x,
+                unsigned block_x, unsigned dyn_lds, double timeout_s, hipStream_t stream) {
+  int dev = 0;
+  hip_ok(hipGetDevice(&dev), "aql_prepare: hipGetDevice");
+  std::string why;
+  AqlQueue* q = aql_queue(dev, &why);
+  if (q == nullptr) throw std::runtime_error("aql_prepare: no AQL queue: " + why);
+  std::lock_guard<std::mutex> lock(g_prep_mu);
+  auto key = std::make_pair(dev, std::string(name_part));
+  auto it = g_kernels.find(key);
+  if (it == g_kernels.end()) it = g_kernels.emplace(key, aql_kernel(q, host_fn, name_part)).first;
+  if (it->second.kernarg_bytes != bytes)
+    throw std::runtime_error("aql_prepare: " + it->second.name + " has a kernarg segment of " +
+                             std::to_string(it->second.kernarg_bytes) + " bytes, the parameter block " +
+                             std::to_string(bytes));
+  void* dargs = nullptr;  // (one small block per prepared launch shape, kept for the process)
+  hip_ok(hipMalloc(&dargs, bytes), "aql_prepare: hipMalloc");
+  hip_ok(hipMemcpy(dargs, args, bytes, hipMemcpyHostToDevice), "aql_prepare: hipMemcpy");
+  g_prep.push_back(Prepared{q, it->second, dargs, bytes, grid_x, block_x, dyn_lds, timeout_s, stream});
+  return (int)g_prep.size() - 1;
+}
+
+void aql_prepared_run(int handle) {
+  Prepared d;
+  {
+    std::lock_guard<std::mutex> lock(g_prep_mu);
+    if (handle < 0 || handle >= (int)g_prep.size()) throw std::runtime_error("aql_prepared_run: bad handle");
+    d = g_prep[handle];
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  hip_ok(hipStreamIsCapturing(d.stream, &cap), "aql_prepared_run: hipStreamIsCapturing");
+  if (cap != hipStreamCaptureStatusNone) throw std::runtime_error("aql_prepared_run: a direct dispatch cannot be captured");
+  // the stream's earlier work (the previous window, epoch_begin, copies) must be done: the AQL
+  // queue is not ordered after it (usually idle already: one query)
+  if (hipStreamQuery(d.stream) != hipSuccess) hip_ok(hipStreamSynchronize(d.stream), "aql_prepared_run: sync");
+  aql_run(d.q, d.k, d.args, d.bytes, d.grid, d.block, d.lds, d.timeout_s, true);
+}
+
 double aql_last_us(AqlQueue* q, bool whole) { return q == nullptr ? 0.0 : (whole ? q->last_whole_us : q->last_wait_us); }
 
 }  // namespace dnn

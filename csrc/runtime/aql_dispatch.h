@@ -15,6 +15,8 @@
 // checks) and HIP work after it is ordered by program order.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <cstddef>
 #include <cstdint>
 #include <string>
@@ -47,6 +49,16 @@ AqlKernel aql_kernel(AqlQueue* q, const void* host_fn, const char* name_part);
 // (HIP's own placement: a kernel that re-reads its arguments pays host-link latency otherwise).
 void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x, unsigned block_x,
              unsigned dyn_lds, double timeout_s, bool args_on_device = false);
+
+// Prepared launches (the AQL counterpart of a captured graph): the kernel object of host_fn
+// (aql_kernel on the current HIP device's queue, cached per device and name), its explicit
+// parameter block copied once into device memory (checked against the symbol's kernarg size) and
+// the launch shape.  Returns a handle for aql_prepared_run.  Throws if the device has no queue.
+int aql_prepare(const void* host_fn, const char* name_part, const void* args, size_t bytes, unsigned grid_x,
+                unsigned block_x, unsigned dyn_lds, double timeout_s, hipStream_t stream);
+// Run a prepared launch: after the stream's earlier work (one query; a synchronize if it is busy),
+// dispatch and wait for completion.  Refuses a stream that is being captured.
+void aql_prepared_run(int handle);
 
 // Host-clock microseconds of the last aql_run: doorbell -> completion seen, and the whole call.
 double aql_last_us(AqlQueue* q, bool whole = false);

@@ -120,14 +120,15 @@ def _sync(engine) -> None:
 
 def window(comm, engine, cur, steps: int) -> float:
     """One timed window exactly as bench.py times it: barrier + device sync, ``steps`` steps,
-    device sync + barrier + device sync.  Returns this rank's seconds."""
+    device sync + barrier + device sync (one rank: the device sync).  Returns this rank's seconds."""
     comm.barrier()
     _sync(engine)
     t0 = time.perf_counter()
     cur.run(steps)
     _sync(engine)
-    comm.barrier()
-    _sync(engine)
+    if comm.distributed:
+        comm.barrier()
+        _sync(engine)
     return time.perf_counter() - t0
 
 

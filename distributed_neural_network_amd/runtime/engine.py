@@ -366,7 +366,7 @@ class HipEngine(Engine):
             self._pers_ctl = self.ext.uncached_alloc(ctl_bytes) if self.persist else 0
         self.stream = torch.cuda.Stream(dev)
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
-        # Direct AQL dispatch of the bf16 persistent launch (csrc/runtime/aql_dispatch.h; default
+        # Direct AQL dispatch of the persistent launch (csrc/runtime/aql_dispatch.h; default
         # on, DNN_AQL=0 turns it off): the kernel the graphs replay, dispatched through this
         # process's own HSA queue with its arguments in device memory, and waited for by spinning
         # on its completion signal - no stream, graph or interrupt in the launch + completion path
@@ -378,8 +378,8 @@ class HipEngine(Engine):
         self.direct = False
         self.direct_why = "off (DNN_AQL=0)"
         if os.environ.get("DNN_AQL", "1") != "0":
-            if not (self.persist and dtype == "bf16"):
-                self.direct_why = "the bf16 persistent launch is off"
+            if not self.persist:
+                self.direct_why = "the persistent launch is off"
             else:
                 why = self.ext.aql_status(dev.index if dev.index is not None else torch.cuda.current_device())
                 self.direct, self.direct_why = (why == ""), (why or "on")
@@ -570,14 +570,13 @@ class HipEngine(Engine):
                                  self._p(self.mom), self._p(self.shadow), sp, self._p(self.stats), self.lr,
                                  self.momentum, 1.0, 1, 0, LAYOUT.total, 1, self._p(self.order), self.order_len,
                                  self._p(self.batch_ids), s, defer=2, next_ids=self._p(self.next_ids), **xg)
-            self.ext.fused_train_persist_f32(self._p(self.train.images), self._p(self.train.labels), self.order_len,
-                                             self.batch, self._p(self.master), self._p(r["a0"]), self._p(r["h1"]),
-                                             self._p(r["h2"]), self._p(r["z1"]), self._p(r["z2"]), self._p(r["z3"]),
-                                             self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
-                                             self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids),
-                                             self._p(self.next_ids2), self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s,
-                                             flags=self.pipe_flags, stamps=self._pipe_stamps)
-            return
+            return self.ext.fused_train_persist_f32(
+                self._p(self.train.images), self._p(self.train.labels), self.order_len, self.batch,
+                self._p(self.master), self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
+                self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]), self._p(r["correct"]),
+                self._pers_ctl, n, sp + 4, sp + 8, self._p(self.next_ids), self._p(self.next_ids2),
+                self._p(self.pipe_err), self.PIPE_TIMEOUT_S, s, flags=self.pipe_flags, stamps=self._pipe_stamps,
+                direct=direct)
         self.ext.grad_reduce(self._p(r["a0"]), self._p(r["h1"]), self._p(r["h2"]), self._p(r["z1"]),
                              self._p(r["z2"]), self._p(r["z3"]), self._p(r["slab"]), self._p(r["loss"]),
                              self._p(r["correct"]), self.batch, self._p(self.master), self._p(self.grad),
@@ -810,7 +809,7 @@ class HipEngine(Engine):
                 self._pers_ok(), self.pers_exchange)
 
     def _direct_ok(self) -> bool:
-        return self.direct and self.dtype == "bf16" and self.grad_sync is None and self._pers_ok()
+        return self.direct and self.grad_sync is None and self._pers_ok()
 
     def _direct(self, nsteps: int) -> int:
         """The prepared direct dispatch of an nsteps persistent launch (the graph's counterpart:
@@ -820,6 +819,8 @@ class HipEngine(Engine):
         if h is None:
             with torch.cuda.device(self.device):
                 h = self._launch_steps_pers(nsteps, direct=True)
+            if h is None or h < 0:
+                raise RuntimeError("the persistent launcher did not prepare a direct dispatch")
             self._direct_h[key] = h
         return h
 
@@ -865,11 +866,16 @@ class HipEngine(Engine):
             return
         poll = self.poll
         if self._direct_ok():  # ONE direct dispatch, returning when the n steps are done
-            h = self._direct(n)
-            if poll is not None:
-                poll()
-            self.ext.persist_direct_run(h)
-            return
+            try:
+                h = self._direct(n)
+            except RuntimeError as e:  # (no dispatch happened: the graphs take over)
+                self.direct, self.direct_why = False, f"preparing a direct dispatch failed: {e}"
+                print(f"[engine] {self.direct_why}; using graph replays", file=sys.stderr, flush=True)
+            else:
+                if poll is not None:
+                    poll()
+                self.ext.persist_direct_run(h)
+                return
         if not self.use_graphs:
             with torch.cuda.device(self.device):
                 if self._pipe_ok() or self._pers_ok():

@@ -11,14 +11,14 @@ from distributed_neural_network_amd.runtime import HipEngine
 pytestmark = pytest.mark.gpu
 
 
-def _engine(arena, direct):
-    eng = HipEngine(batch=64, arena=arena, graph_chunk=8)
+def _engine(arena, direct, dtype="bf16"):
+    eng = HipEngine(batch=64, arena=arena, graph_chunk=8, dtype=dtype)
     if not eng.persist:
         pytest.skip("the persistent launch is off on this device")
     if direct:
         why = eng.ext.aql_status(torch.cuda.current_device())
         assert why == "", f"no AQL queue on a GPU box: {why}"
-        eng.direct = True
+    eng.direct = direct  # (on by default: the reference side turns it off)
     return eng
 
 
@@ -34,15 +34,16 @@ def _run(eng, data, orders, steps):
     return eng.master.cpu(), eng.mom.cpu(), eng.shadow.cpu(), stats
 
 
-def test_direct_dispatch_matches_graph_replays():
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_direct_dispatch_matches_graph_replays(dtype):
     """1-, 5- and 20-step launches, a tail batch, steps past an epoch's end, two epochs."""
     data = synthetic(1000, 4)  # 16 steps per epoch incl. a 40-sample tail
     a = init_arena(seed=5)
     rng = np.random.default_rng(1)
     orders = [rng.permutation(1000).astype(np.int32) for _ in range(2)]
     steps = (1, 5, 20)  # 26 steps: past the epoch's end (no-op steps)
-    ref = _run(_engine(a, False), data, orders, steps)
-    eng = _engine(a, True)
+    ref = _run(_engine(a, False, dtype), data, orders, steps)
+    eng = _engine(a, True, dtype)
     got = _run(eng, data, orders, steps)
     assert eng._direct_h, "the direct path did not run"
     for x, y in zip(ref[:3], got[:3]):
