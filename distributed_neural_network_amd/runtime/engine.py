@@ -378,11 +378,9 @@ class HipEngine(Engine):
         self.direct = False
         self.direct_why = "off (DNN_AQL=0)"
         if os.environ.get("DNN_AQL", "1") != "0":
-            if not self.persist:
-                self.direct_why = "the persistent launch is off"
-            else:
-                why = self.ext.aql_status(dev.index if dev.index is not None else torch.cuda.current_device())
-                self.direct, self.direct_why = (why == ""), (why or "on")
+            # (the queue is created by the first prepared dispatch; if that fails - no HSA agent
+            # for the device, a refused queue - run_steps falls back to graph replays, loudly)
+            self.direct, self.direct_why = (True, "on") if self.persist else (False, "the persistent launch is off")
         self.params_changed()
         torch.cuda.synchronize(dev)
 
@@ -824,6 +822,16 @@ class HipEngine(Engine):
             self._direct_h[key] = h
         return h
 
+    def _direct_or_off(self, nsteps: int) -> int | None:
+        """_direct, or None after turning the direct path off if preparing it failed (nothing was
+        dispatched: the graph replays take over, and the reason is printed and kept in direct_why)."""
+        try:
+            return self._direct(nsteps)
+        except RuntimeError as e:
+            self.direct, self.direct_why = False, f"preparing a direct dispatch failed: {e}"
+            print(f"[engine] {self.direct_why}; using graph replays", file=sys.stderr, flush=True)
+            return None
+
     def _graph(self, nsteps: int) -> torch.cuda.CUDAGraph:
         key = self._launch_key(nsteps)
         g = self._graphs.get(key)
@@ -851,9 +859,9 @@ class HipEngine(Engine):
         an n is ONE replay instead of its power-of-two decomposition (a 20-step window: one
         graph instead of 16 + 4, ~6 us less per window; profiles/r2/window/)."""
         if self._direct_ok():  # direct dispatches replace the graphs (run_steps takes them first)
-            for k in set(self._chunk_sizes()) | {int(k) for k in exact if 0 < int(k)}:
-                self._direct(k)
-            return
+            if all(self._direct_or_off(k) is not None
+                   for k in sorted(set(self._chunk_sizes()) | {int(k) for k in exact if 0 < int(k)})):
+                return
         if self.use_graphs:
             for k in self._chunk_sizes():
                 self._graph(k)
@@ -866,12 +874,8 @@ class HipEngine(Engine):
             return
         poll = self.poll
         if self._direct_ok():  # ONE direct dispatch, returning when the n steps are done
-            try:
-                h = self._direct(n)
-            except RuntimeError as e:  # (no dispatch happened: the graphs take over)
-                self.direct, self.direct_why = False, f"preparing a direct dispatch failed: {e}"
-                print(f"[engine] {self.direct_why}; using graph replays", file=sys.stderr, flush=True)
-            else:
+            h = self._direct_or_off(n)
+            if h is not None:
                 if poll is not None:
                     poll()
                 self.ext.persist_direct_run(h)

@@ -71,3 +71,32 @@ def test_direct_dispatch_orders_after_stream_work():
         torch.cuda.synchronize()
         res.append(eng.master.cpu())
     assert torch.equal(res[0], res[1])
+
+
+class _NoDirectExt:
+    """The extension with a persistent launcher that refuses to prepare direct dispatches."""
+
+    def __init__(self, ext):
+        self._ext = ext
+
+    def __getattr__(self, name):
+        return getattr(self._ext, name)
+
+    def fused_train_persist(self, *a, direct=False, **k):
+        if direct:
+            raise RuntimeError("injected: no direct dispatch")
+        return self._ext.fused_train_persist(*a, **k)
+
+
+def test_direct_dispatch_failure_falls_back_to_graphs():
+    """A launch shape whose direct dispatch cannot be prepared runs as graph replays (same bits),
+    and the engine says why."""
+    data = synthetic(640, 8)
+    a = init_arena(seed=9)
+    order = np.arange(640, dtype=np.int32)
+    ref = _run(_engine(a, False), data, [order], (3, 4))
+    eng = _engine(a, True)
+    eng.ext = _NoDirectExt(eng.ext)
+    got = _run(eng, data, [order], (3, 4))
+    assert not eng.direct and "injected" in eng.direct_why and not eng._direct_h
+    assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
