@@ -261,6 +261,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("persist_direct_run", [](int handle) { dnn::aql_prepared_run(handle); }, py::arg("handle"),
         py::call_guard<py::gil_scoped_release>());
+  m.def("persist_direct_launch", [](int handle) { dnn::aql_prepared_launch(handle); }, py::arg("handle"));
+  m.def("persist_direct_wait", [](int handle) { dnn::aql_prepared_wait(handle); }, py::arg("handle"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("aql_last_us", [](int device, bool whole) { return dnn::aql_last_us(dnn::aql_queue(device), whole); },
         py::arg("device"), py::arg("whole") = false);
   m.def("pipe_reduce_blocks", []() { return dnn::pipe_reduce_blocks(); });

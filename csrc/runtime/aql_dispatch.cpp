@@ -120,7 +120,10 @@ class AqlQueue {
   hsa_queue_t* queue = nullptr;
   hsa_signal_t done{0};
   void* kernarg = nullptr;
-  bool broken = false;
+  bool broken = false, in_flight = false;
+  std::chrono::steady_clock::time_point t_start, t_doorbell;
+  double timeout_s = 0.0;
+  std::string name;
   unsigned acq_scope = HSA_FENCE_SCOPE_SYSTEM, rel_scope = HSA_FENCE_SCOPE_SYSTEM;
   double last_wait_us = 0.0, last_whole_us = 0.0;
   std::mutex mu;
@@ -206,21 +209,22 @@ AqlKernel aql_kernel(AqlQueue* q, const void* host_fn, const char* name_part) {
   return f.hits[0];
 }
 
-void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x, unsigned block_x,
-             unsigned dyn_lds, double timeout_s, bool args_on_device) {
-  if (q == nullptr || q->broken) throw std::runtime_error("aql_run: the queue is unusable");
-  if (k.object == 0) throw std::runtime_error("aql_run: no kernel object");
+void aql_dispatch(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x,
+                  unsigned block_x, unsigned dyn_lds, double timeout_s, bool args_on_device) {
+  if (q == nullptr || q->broken) throw std::runtime_error("aql_dispatch: the queue is unusable");
+  if (q->in_flight) throw std::runtime_error("aql_dispatch: the previous dispatch was not waited for");
+  if (k.object == 0) throw std::runtime_error("aql_dispatch: no kernel object");
   if (bytes != k.kernarg_bytes || bytes > KARG_BYTES)
-    throw std::runtime_error("aql_run: " + std::to_string(bytes) + " argument bytes for a kernarg segment of " +
+    throw std::runtime_error("aql_dispatch: " + std::to_string(bytes) + " argument bytes for a kernarg segment of " +
                              std::to_string(k.kernarg_bytes) + " (" + k.name + ")");
   if (grid_x == 0 || block_x == 0 || block_x > 1024 || k.group_static + dyn_lds > 163840)
-    throw std::runtime_error("aql_run: bad launch shape");
+    throw std::runtime_error("aql_dispatch: bad launch shape");
   std::lock_guard<std::mutex> lock(q->mu);
   using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
+  q->t_start = clk::now();
   // kernel arguments: the caller's device-resident block as it is (the kernel re-reads its arguments
   // in its loops - from system memory each of those reads crosses the host link), or a copy in
-  // this queue's host kernarg buffer (the previous dispatch completed: run() is synchronous)
+  // this queue's host kernarg buffer (the previous dispatch completed: one dispatch in flight)
   const void* karg = args;
   if (!args_on_device) {
     std::memcpy(q->kernarg, args, bytes);
@@ -254,19 +258,35 @@ void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, un
   const uint16_t setup = (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
   __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(hq->doorbell_signal, (hsa_signal_value_t)idx);
-  const auto t1 = clk::now();
-  const auto limit = t1 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(timeout_s));
+  q->t_doorbell = clk::now();
+  q->timeout_s = timeout_s;
+  q->name = k.name;
+  q->in_flight = true;
+}
+
+void aql_wait(AqlQueue* q) {
+  if (q == nullptr || !q->in_flight) return;
+  using clk = std::chrono::steady_clock;
+  const auto limit = q->t_doorbell + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(q->timeout_s));
   unsigned n = 0;
   while (hsa_signal_load_scacquire(q->done) != 0) {
     cpu_relax();
     if ((++n & 1023u) == 0 && clk::now() > limit) {
       q->broken = true;
-      throw std::runtime_error("aql_run: " + k.name + " did not complete within " + std::to_string(timeout_s) + " s");
+      q->in_flight = false;
+      throw std::runtime_error("aql_wait: " + q->name + " did not complete within " + std::to_string(q->timeout_s) + " s");
     }
   }
   const auto t2 = clk::now();
-  q->last_wait_us = std::chrono::duration<double, std::micro>(t2 - t1).count();
-  q->last_whole_us = std::chrono::duration<double, std::micro>(t2 - t0).count();
+  q->in_flight = false;
+  q->last_wait_us = std::chrono::duration<double, std::micro>(t2 - q->t_doorbell).count();
+  q->last_whole_us = std::chrono::duration<double, std::micro>(t2 - q->t_start).count();
+}
+
+void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x, unsigned block_x,
+             unsigned dyn_lds, double timeout_s, bool args_on_device) {
+  aql_dispatch(q, k, args, bytes, grid_x, block_x, dyn_lds, timeout_s, args_on_device);
+  aql_wait(q);
 }
 
 namespace {
@@ -310,7 +330,7 @@ int aql_prepare(const void* host_fn, const char* name_part, const void* args, si
   return (int)g_prep.size() - 1;
 }
 
-void aql_prepared_run(int handle) {
+void aql_prepared_launch(int handle) {
   Prepared d;
   {
     std::lock_guard<std::mutex> lock(g_prep_mu);
@@ -323,7 +343,22 @@ void aql_prepared_run(int handle) {
   // the stream's earlier work (the previous window, epoch_begin, copies) must be done: the AQL
   // queue is not ordered after it (usually idle already: one query)
   if (hipStreamQuery(d.stream) != hipSuccess) hip_ok(hipStreamSynchronize(d.stream), "aql_prepared_run: sync");
-  aql_run(d.q, d.k, d.args, d.bytes, d.grid, d.block, d.lds, d.timeout_s, true);
+  aql_dispatch(d.q, d.k, d.args, d.bytes, d.grid, d.block, d.lds, d.timeout_s, true);
+}
+
+void aql_prepared_wait(int handle) {
+  AqlQueue* q = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_prep_mu);
+    if (handle < 0 || handle >= (int)g_prep.size()) throw std::runtime_error("aql_prepared_wait: bad handle");
+    q = g_prep[handle].q;
+  }
+  aql_wait(q);
+}
+
+void aql_prepared_run(int handle) {
+  aql_prepared_launch(handle);
+  aql_prepared_wait(handle);
 }
 
 double aql_last_us(AqlQueue* q, bool whole) { return q == nullptr ? 0.0 : (whole ? q->last_whole_us : q->last_wait_us); }

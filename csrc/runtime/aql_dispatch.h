@@ -49,6 +49,10 @@ AqlKernel aql_kernel(AqlQueue* q, const void* host_fn, const char* name_part);
 // (HIP's own placement: a kernel that re-reads its arguments pays host-link latency otherwise).
 void aql_run(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x, unsigned block_x,
              unsigned dyn_lds, double timeout_s, bool args_on_device = false);
+// aql_run's halves: dispatch (returns after the doorbell) and wait (no-op if nothing is in flight)
+void aql_dispatch(AqlQueue* q, const AqlKernel& k, const void* args, size_t bytes, unsigned grid_x,
+                  unsigned block_x, unsigned dyn_lds, double timeout_s, bool args_on_device = false);
+void aql_wait(AqlQueue* q);
 
 // Prepared launches (the AQL counterpart of a captured graph): the kernel object of host_fn
 // (aql_kernel on the current HIP device's queue, cached per device and name), its explicit
@@ -59,6 +63,11 @@ int aql_prepare(const void* host_fn, const char* name_part, const void* args, si
 // Run a prepared launch: after the stream's earlier work (one query; a synchronize if it is busy),
 // dispatch and wait for completion.  Refuses a stream that is being captured.
 void aql_prepared_run(int handle);
+// The same in two halves, so host work can overlap the kernel: launch returns after the doorbell,
+// wait spins until it completed (one dispatch in flight per queue: a second launch before the
+// wait throws).  Nothing but wait orders later HIP work after the kernel.
+void aql_prepared_launch(int handle);
+void aql_prepared_wait(int handle);
 
 // Host-clock microseconds of the last aql_run: doorbell -> completion seen, and the whole call.
 double aql_last_us(AqlQueue* q, bool whole = false);

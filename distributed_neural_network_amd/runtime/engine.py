@@ -869,8 +869,13 @@ class HipEngine(Engine):
             for k in self._exact:
                 self._graph(k)
 
-    def run_steps(self, n: int) -> None:
+    def run_steps(self, n: int, host_work=None) -> None:
+        """Queue n training steps.  host_work: a host-only callable to run while they run (the
+        next epoch's shuffle): with the direct dispatch, which returns only when its steps are
+        done, it overlaps the kernel instead of following it."""
         if n <= 0:
+            if host_work is not None:
+                host_work()
             return
         poll = self.poll
         if self._direct_ok():  # ONE direct dispatch, returning when the n steps are done
@@ -878,8 +883,20 @@ class HipEngine(Engine):
             if h is not None:
                 if poll is not None:
                     poll()
-                self.ext.persist_direct_run(h)
+                if host_work is None:
+                    self.ext.persist_direct_run(h)
+                    return
+                self.ext.persist_direct_launch(h)
+                try:
+                    host_work()
+                finally:
+                    self.ext.persist_direct_wait(h)
                 return
+        self._run_steps_graphs(n, poll)
+        if host_work is not None:
+            host_work()
+
+    def _run_steps_graphs(self, n: int, poll) -> None:
         if not self.use_graphs:
             with torch.cuda.device(self.device):
                 if self._pipe_ok() or self._pers_ok():

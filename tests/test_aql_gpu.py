@@ -100,3 +100,20 @@ def test_direct_dispatch_failure_falls_back_to_graphs():
     got = _run(eng, data, [order], (3, 4))
     assert not eng.direct and "injected" in eng.direct_why and not eng._direct_h
     assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+
+
+def test_direct_dispatch_overlaps_host_work():
+    """run_steps(n, host_work): the host work runs while the dispatched steps run (launch, work,
+    wait), and the steps give the same bits."""
+    data = synthetic(640, 3)
+    a = init_arena(seed=4)
+    order = np.arange(640, dtype=np.int32)
+    res, calls = [], []
+    for direct in (False, True):
+        eng = _engine(a, direct)
+        eng.attach(data)
+        eng.begin_epoch(order)
+        eng.run_steps(6, host_work=lambda: calls.append(direct))
+        torch.cuda.synchronize()
+        res.append(eng.master.cpu())
+    assert calls == [False, True] and torch.equal(res[0], res[1])
