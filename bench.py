@@ -40,10 +40,14 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_neural_network_amd.hsa_env import DEFAULTS as HSA_DEFAULTS, apply as _hsa_env  # noqa: E402
+
+_hsa_env()  # HSA runtime defaults, before torch can start the runtime (hsa_env.py)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 from distributed_neural_network_amd.data import EpochSampler, synthetic  # noqa: E402
 from distributed_neural_network_amd.data.datasets import SYNTH_NOISE_HARD  # noqa: E402
@@ -344,6 +348,8 @@ def main():
                           "image": [3, 32, 32], "parallelism": f"dp{comm.world}", "sync": args.sync,
                           "optimizer": "SGD lr=0.001 momentum=0.9, every step",
                           "allreduce": policy.installed(engine) if hasattr(policy, "installed") else None,
+                          # the HSA runtime defaults this process ran with (distributed_neural_network_amd/hsa_env.py)
+                          "runtime_env": {k: os.environ.get(k) for k in HSA_DEFAULTS},
                           # launcher retry level this number was measured at (0: as requested)
                           "safe_transport": safe},
                **epoch}
