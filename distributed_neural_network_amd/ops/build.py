@@ -40,6 +40,7 @@ HIP_BINDING = CSRC / "bindings.cpp"
 HOST_SOURCES = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "runtime" / "aql_dispatch.cpp"]
 HIP_HEADERS = sorted((CSRC / "kernels").glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
 IO_SOURCES = [CSRC / "io" / "dataio.cpp"]
+LINK_LIBS = ["-ldl", "-L/opt/rocm/lib", "-lhsa-runtime64"]  # (RCCL is dlopen'ed; HSA: runtime/aql_dispatch)
 
 
 def _pybind_includes() -> list[str]:
@@ -97,7 +98,7 @@ def build_hip(force: bool = False, verbose_resources: bool = False) -> Path:
         for f in [ex.submit(_run, j) for j in jobs]:
             f.result()
     tmp = target.with_suffix(".tmp.so")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-ldl", "-L/opt/rocm/lib", "-lhsa-runtime64"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + objs + LINK_LIBS)
     os.replace(tmp, target)
     return target
 

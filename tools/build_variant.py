@@ -45,7 +45,7 @@ def main() -> None:
     objs.append(str(objdir / "bindings.o"))
     out = REPO / "distributed_neural_network_amd" / "ops" / "variants" / f"{a.name}.so"
     out.parent.mkdir(exist_ok=True)
-    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out)] + objs + ["-ldl"],
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(out)] + objs + B.LINK_LIBS,
                    check=True)
     print(out)
 

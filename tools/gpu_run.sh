@@ -33,6 +33,7 @@
 #   fault2 | fault4  tools/fault_bench.py -n 2|4 --share-gpu (rank-drop recovery latency)
 #   sweep:<b1,b2,..> bench.py --batch-size b for each b (2000 / 200 steps)
 #   racehunt:N[:variants[:VAR=val[:extra args]]]  tools/race_hunt.py (long run under load vs serial, per variant)
+#   abso:NAME[,N]    N alternating k20 runs: main build, then ops/variants/NAME.so (kernel A/B)
 #   useso:NAME       use distributed_neural_network_amd/ops/variants/NAME.so from here on (kernel A/B;
 #                    the original extension is restored when the script exits)
 #   inproc[:args]    tools/inproc_pair.py (2 in-process ranks on this GPU: exchange forms, JSON)
@@ -185,6 +186,16 @@ for s in "$@"; do
       [ -f "$SO.orig" ] || cp "$SO" "$SO.orig"
       cp "distributed_neural_network_amd/ops/variants/${s#useso:}.so" "$SO"
       USESO="_${s#useso:}" ;;
+    abso:*)  # abso:NAME[,N]: N alternating k20 runs, main build then ops/variants/NAME.so (kernel A/B)
+      spec="${s#abso:}"; nm="${spec%%,*}"; n=3; [ "$spec" != "$nm" ] && n="${spec#*,}"
+      [ -f "$SO.orig" ] || cp "$SO" "$SO.orig"
+      for i in $(seq 1 "$n"); do
+        cp "$SO.orig" "$SO"
+        timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/abso_${nm}_${i}_base.json" 2> "$O/abso_${nm}_${i}_base.err"
+        cp "distributed_neural_network_amd/ops/variants/$nm.so" "$SO"
+        timeout -k 10 150 python bench.py --steps 20 --warmup 5 > "$O/abso_${nm}_${i}_var.json" 2> "$O/abso_${nm}_${i}_var.err"
+      done
+      cp "$SO.orig" "$SO" ;;
     inproctrace:*)
       f="${s#inproctrace:}"; n=$(echo "$f" | tr ',' '_')$USESO
       timeout -k 10 300 python tools/inproc_pair.py --trace "$f" > "$O/inproctrace_$n.json" 2> "$O/inproctrace_$n.err" ;;
