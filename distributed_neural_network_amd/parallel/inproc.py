@@ -132,6 +132,8 @@ class PairRunner:
 
     def __init__(self, engines: list, orders: list[np.ndarray]) -> None:
         self.engines, self.orders = engines, orders
+        for e in engines:  # the engines' launches must be in flight together: no synchronous direct dispatch
+            e.direct = False
         self.streams = own_queue_streams(engines)
         self.spe = engines[0].steps_per_epoch() if engines[0].order_len else None
         self.left = 0
