@@ -41,6 +41,8 @@ import threading
 import time
 from typing import IO, Optional, Sequence
 
+from .. import hsa_env
+
 
 def launcher_present(env: Optional[dict] = None) -> bool:
     """True if a launcher already set up this process as one rank of a job."""
@@ -389,7 +391,7 @@ def run(cmd: Sequence[str], nproc: int, out_fd: int | None = None, extra_env: Op
     ``out_fd``: where rank 0's (annotated) JSON line goes (default: fd 1)."""
     err = err or sys.stderr
     t_launch = time.time()
-    base = dict(os.environ)
+    base = hsa_env.strip(dict(os.environ))  # (ranks of a multi-rank job keep the runtime's defaults)
     base.update(extra_env or {})
     ndev = visible_devices()
     print(f"[launch] {ndev} GPU(s) visible to this job (KFD topology + visibility variables)", file=err, flush=True)
@@ -496,7 +498,7 @@ def supervise(cmd: Sequence[str], out_fd: int | None = None, grace_s: float = 60
         aport = int(agent.get(f"{k}/port").decode())
         st = srv if srv is not None else dist.TCPStore(addr, aport, world + 1, is_master=False,
                                                        timeout=datetime.timedelta(seconds=600))
-        env = dict(os.environ)
+        env = hsa_env.strip(dict(os.environ))
         env.update(aenv)
         env.update(MASTER_PORT=str(aport), DNN_STORE_EXTERNAL="1", TORCHELASTIC_USE_AGENT_STORE="False",
                    DNN_SUPERVISED="1", DNN_SELF_LAUNCHED="1", DNN_LAUNCHER_PID=str(os.getpid()),

@@ -25,3 +25,17 @@ def test_explicit_value_wins():
 
 def test_opt_out():
     assert _probe(DNN_HSA_DEFAULTS="0") == "None"
+
+
+def test_ranks_of_a_multi_rank_job_keep_the_runtime_defaults():
+    assert _probe(WORLD_SIZE="8") == "None"
+    assert _probe(WORLD_SIZE="1") == "1"
+
+
+def test_strip_removes_only_what_apply_set():
+    from distributed_neural_network_amd import hsa_env
+
+    env = {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1", "DNN_HSA_DEFAULTED": "HSA_ALLOCATE_QUEUE_DEV_MEM", "X": "y"}
+    assert hsa_env.strip(env) == {"X": "y"}
+    user = {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1", "X": "y"}  # set by the user: kept
+    assert hsa_env.strip(dict(user)) == user
