@@ -32,6 +32,7 @@ void uncached_free(uintptr_t p);
 std::tuple<long long, long long, long long> uncached_pool_stats();
 void lds_poison(unsigned pattern, hipStream_t stream);
 void lds_squat(int bytes, double spin_us, int blocks, uintptr_t bad, hipStream_t stream);
+bool aql_selftest(std::string* why);
 uintptr_t xgmi_open(const std::string& handle);
 void xgmi_close(uintptr_t p);
 std::string xgmi_device_id();
@@ -258,6 +259,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("aql_status", [](int device) {
     std::string why;
     return dnn::aql_queue(device, &why) != nullptr ? std::string() : why;
+  });
+  // the direct dispatch path end to end on a trivial kernel (csrc/kernels/diag.hip): "" or why not
+  m.def("aql_selftest", []() {
+    std::string why;
+    return dnn::aql_selftest(&why) ? std::string() : why;
   });
   m.def("persist_direct_run", [](int handle) { dnn::aql_prepared_run(handle); }, py::arg("handle"),
         py::call_guard<py::gil_scoped_release>());

@@ -8,8 +8,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
+
+#include "runtime/aql_dispatch.h"
 
 namespace dnn {
 
@@ -59,6 +62,53 @@ void lds_squat(int bytes, double spin_us, int blocks, uintptr_t bad, hipStream_t
                      reinterpret_cast<unsigned*>(bad));
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("lds_squat: ") + hipGetErrorString(e));
+}
+
+// aql_selftest: the direct AQL dispatch path (runtime/aql_dispatch.h) end to end on a trivial
+// kernel - the queue, the loader lookup of a HIP-loaded kernel, host kernel arguments, dynamic
+// LDS, the completion signal - with a short bound, before an engine trusts it with a launch.
+__global__ void __launch_bounds__(256) aql_probe_kernel(int* out, int base) {
+  extern __shared__ int probe_lds[];
+  probe_lds[threadIdx.x] = base + (int)blockIdx.x;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = probe_lds[255 - threadIdx.x] + 1;
+}
+
+bool aql_selftest(std::string* why) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    *why = "hipGetDevice failed";
+    return false;
+  }
+  AqlQueue* q = aql_queue(dev, why);
+  if (q == nullptr) return false;
+  constexpr int BLOCKS = 300;  // more workgroups than CUs
+  int* out = nullptr;
+  if (hipMalloc(&out, BLOCKS * sizeof(int)) != hipSuccess || hipMemset(out, 0, BLOCKS * sizeof(int)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    *why = "probe buffer allocation failed";
+    return false;
+  }
+  bool ok = true;
+  try {
+    const AqlKernel k = aql_kernel(q, reinterpret_cast<const void*>(aql_probe_kernel), "aql_probe_kernel");
+    // the explicit parameter block: the pointer, then the int - 12 bytes (no tail padding, unlike
+    // a struct of the two)
+    unsigned char args[sizeof(int*) + sizeof(int)];
+    const int base = 1000;
+    std::memcpy(args, &out, sizeof(int*));
+    std::memcpy(args + sizeof(int*), &base, sizeof(int));
+    aql_run(q, k, args, sizeof(args), BLOCKS, 256, 256 * sizeof(int), 5.0);  // host kernarg path
+    int host[BLOCKS];
+    if (hipMemcpy(host, out, sizeof(host), hipMemcpyDeviceToHost) != hipSuccess) throw std::runtime_error("copy back");
+    for (int b = 0; b < BLOCKS; ++b)
+      if (host[b] != 1000 + b + 1) throw std::runtime_error("block " + std::to_string(b) + " wrote " + std::to_string(host[b]));
+  } catch (const std::exception& e) {
+    *why = std::string("aql_selftest: ") + e.what();
+    ok = false;
+  }
+  hipFree(out);
+  return ok;
 }
 
 }  // namespace dnn

@@ -806,6 +806,8 @@ class HipEngine(Engine):
                 getattr(getattr(self.grad_sync, "group", None), "xp_mode", None), self._staged, self._pipe_ok(),
                 self._pers_ok(), self.pers_exchange)
 
+    _direct_checked: dict = {}  # device index -> the direct path passed its self-test in this process
+
     def _direct_ok(self) -> bool:
         return self.direct and self.grad_sync is None and self._pers_ok()
 
@@ -816,6 +818,12 @@ class HipEngine(Engine):
         h = self._direct_h.get(key)
         if h is None:
             with torch.cuda.device(self.device):
+                if not HipEngine._direct_checked.get(self.device.index, False):
+                    # the path end to end on a trivial kernel first (bounded: 5 s), once per device
+                    why = self.ext.aql_selftest()
+                    if why:
+                        raise RuntimeError(why)
+                    HipEngine._direct_checked[self.device.index] = True
                 h = self._launch_steps_pers(nsteps, direct=True)
             if h is None or h < 0:
                 raise RuntimeError("the persistent launcher did not prepare a direct dispatch")

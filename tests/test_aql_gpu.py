@@ -117,3 +117,10 @@ def test_direct_dispatch_overlaps_host_work():
         torch.cuda.synchronize()
         res.append(eng.master.cpu())
     assert calls == [False, True] and torch.equal(res[0], res[1])
+
+
+def test_aql_selftest_passes():
+    """The direct path end to end on a trivial kernel (host kernel arguments, dynamic LDS, more
+    workgroups than CUs): what the engine runs once per device before its first direct launch."""
+    ext = HipEngine(batch=64).ext
+    assert ext.aql_selftest() == ""
