@@ -124,7 +124,11 @@ class AqlQueue {
   std::chrono::steady_clock::time_point t_start, t_doorbell;
   double timeout_s = 0.0;
   std::string name;
-  unsigned acq_scope = HSA_FENCE_SCOPE_SYSTEM, rel_scope = HSA_FENCE_SCOPE_SYSTEM;
+  // acquire at agent scope: a dispatched kernel reads device memory only (its arguments included),
+  // which the agent-scope invalidate covers - the system scope adds host-memory coherence
+  // (15.98 vs 16.10 us/step over 6 bench pairs: profiles/r6/aql/fence/); release at system
+  // scope, so host reads and every later queue see the kernel's writes
+  unsigned acq_scope = HSA_FENCE_SCOPE_AGENT, rel_scope = HSA_FENCE_SCOPE_SYSTEM;
   double last_wait_us = 0.0, last_whole_us = 0.0;
   std::mutex mu;
 
@@ -248,9 +252,10 @@ void aql_dispatch(AqlQueue* q, const AqlKernel& k, const void* args, size_t byte
   pkt->kernarg_address = const_cast<void*>(karg);
   pkt->reserved2 = 0;
   pkt->completion_signal = q->done;
-  // system-scope acquire / release: the kernel reads what HIP kernels wrote before it and HIP
-  // work after it reads what it wrote (the packet is the only ordering between the two queues).
-  // (DNN_AQL_FENCE=<acquire><release>, each n / a / s for none / agent / system: measurement)
+  // acquire / release fences (AqlQueue: agent / system): the kernel reads what HIP kernels and
+  // copies wrote before it and HIP work after it reads what it wrote (the packet is the only
+  // ordering between the two queues).  (DNN_AQL_FENCE=<acquire><release>, each n / a / s for
+  // none / agent / system: measurement)
   const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                      (1u << HSA_PACKET_HEADER_BARRIER) |
                                      (q->acq_scope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
