@@ -216,8 +216,9 @@ def main():
     # (a host-side gap here shows up in short runs)
     cur._next_epoch()
     if isinstance(engine, HipEngine):
-        # the timed window as ONE graph replay when it fits in the current epoch (a 20-step
-        # window: one launch instead of 16 + 4; profiles/r2/window/)
+        # the timed window as ONE launch when it fits in the current epoch: a prepared direct AQL
+        # dispatch of the persistent kernel, or one exact-size graph replay (a 20-step window: one
+        # launch instead of 16 + 4; profiles/r2/window/, profiles/r6/aql/)
         engine.prepare_graphs(exact=(args.steps,) if args.steps <= min(512, cur.left - args.warmup) else ())
     else:
         engine.prepare_graphs()
